@@ -1,0 +1,403 @@
+// C ABI (include/dsocr.h).  Exceptions never cross this boundary: messages are
+// prefixed with a status tag ("EINVAL: ...") and mapped to dsocr_status.
+#include "../../../include/dsocr.h"
+
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../common/host_util.hpp"
+#include "engine.hpp"
+#include "host_ops.hpp"
+
+struct dsocr_engine {
+    std::unique_ptr<dsocr::Engine> impl;
+};
+struct dsocr_page_pixels {
+    dsocr::PagePixels px;
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+dsocr_status status_from(const std::string& msg) {
+    g_last_error = msg;
+    auto starts = [&](const char* p) { return msg.rfind(p, 0) == 0; };
+    if (starts("EINVAL")) return DSOCR_EINVAL;
+    if (starts("ENOENT")) return DSOCR_ENOENT;
+    if (starts("EDEVICE")) return DSOCR_EDEVICE;
+    if (starts("ENOMEM")) return DSOCR_ENOMEM;
+    return DSOCR_EINTERNAL;
+}
+
+template <typename F>
+dsocr_status guarded(F&& f) {
+    try {
+        f();
+        g_last_error.clear();
+        return DSOCR_OK;
+    } catch (const std::exception& e) {
+        return status_from(e.what());
+    } catch (...) {
+        return status_from("EINTERNAL: unknown error");
+    }
+}
+
+void check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("EDEVICE: ") + what + ": " + hipGetErrorString(e));
+}
+
+dsocr::GenParams to_params(const dsocr_decode_params* p) {
+    if (!p) throw std::runtime_error("EINVAL: decode params are NULL");
+    if (p->do_sample) throw std::runtime_error("EINVAL: do_sample is not supported by the MI355X engine (greedy only)");
+    if (!p->use_cache) throw std::runtime_error("EINVAL: use_cache=false is not supported (generate_without_cache)");
+    dsocr::GenParams g;
+    g.max_new = p->max_new_tokens;
+    g.rep_penalty = p->repetition_penalty;
+    g.ngram = p->no_repeat_ngram_size > 1 ? (int)p->no_repeat_ngram_size : 0;
+    g.eos = p->eos_token_id;
+    g.ignore_eos = p->ignore_eos != 0;
+    return g;
+}
+
+dsocr::GenRequest to_request(const dsocr_request& r) {
+    dsocr::GenRequest g;
+    if (!r.input_ids || r.prompt_len == 0) throw std::runtime_error("EINVAL: empty prompt");
+    g.ids.resize(r.prompt_len);
+    for (size_t i = 0; i < r.prompt_len; ++i) {
+        if (r.input_ids[i] < 0 || r.input_ids[i] > INT32_MAX) throw std::runtime_error("EINVAL: token id out of range");
+        g.ids[i] = (int)r.input_ids[i];
+    }
+    if (r.image_mask) g.mask.assign(r.image_mask, r.image_mask + r.prompt_len);
+    g.page = r.page ? &r.page->px : nullptr;
+    g.image_rows = r.image_rows;
+    g.n_image_rows = r.n_image_rows;
+    return g;
+}
+}  // namespace
+
+extern "C" {
+
+const char* dsocr_last_error(void) { return g_last_error.c_str(); }
+
+dsocr_status dsocr_engine_load(const dsocr_load_args* args, dsocr_engine** out) {
+    return guarded([&] {
+        if (!args || !out) throw std::runtime_error("EINVAL: NULL argument");
+        if (!args->config_path) throw std::runtime_error("EINVAL: config_path is required");
+        if (args->snapshot_path) throw std::runtime_error("EINVAL: .dsq snapshots are not supported yet");
+        if (args->dtype < DSOCR_F32 || args->dtype > DSOCR_BF16) throw std::runtime_error("EINVAL: bad dtype");
+        auto* e = new dsocr_engine;
+        try {
+            e->impl.reset(new dsocr::Engine(args->config_path, args->weights_path ? args->weights_path : "",
+                                            args->device_ordinal, (int)args->dtype, args->synthetic_seed));
+        } catch (...) {
+            delete e;
+            throw;
+        }
+        *out = e;
+    });
+}
+
+void dsocr_engine_free(dsocr_engine* e) { delete e; }
+
+dsocr_status dsocr_engine_info(const dsocr_engine* e, size_t* hidden, size_t* vocab, int64_t* eos, size_t* layers) {
+    return guarded([&] {
+        if (!e) throw std::runtime_error("EINVAL: NULL engine");
+        const auto& c = e->impl->cfg();
+        if (hidden) *hidden = c.lang.hidden;
+        if (vocab) *vocab = c.lang.vocab;
+        if (eos) *eos = c.lang.eos;
+        if (layers) *layers = c.lang.layers;
+    });
+}
+
+dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t w, uint32_t h, const dsocr_vision_settings* vs,
+                                dsocr_page_pixels** out) {
+    return guarded([&] {
+        if (!rgb || !vs || !out) throw std::runtime_error("EINVAL: NULL argument");
+        auto* p = new dsocr_page_pixels;
+        dsocr::PagePixels& px = p->px;
+        px.base = (int)vs->base_size;
+        px.tile = (int)vs->image_size;
+        px.crop = vs->crop_mode != 0;
+        const int gsize = px.crop ? px.base : px.tile;  // model/mod.rs:1714
+        std::vector<uint8_t> gview = dsocr::build_global_view(rgb, (int)w, (int)h, gsize);
+        px.gsize = gsize;
+        px.global_chw.resize((size_t)3 * gsize * gsize);
+        dsocr::image_to_chw(gview.data(), gsize, gsize, px.global_chw.data());
+        if (px.crop) {
+            int gw = 1, gh = 1;
+            auto tiles = dsocr::dynamic_preprocess(rgb, (int)w, (int)h, px.tile, 2, 9, &gw, &gh);
+            px.crop_w = gw;
+            px.crop_h = gh;
+            px.n_tiles = (int)tiles.size();
+            px.tiles_chw.resize((size_t)px.n_tiles * 3 * px.tile * px.tile);
+            for (int i = 0; i < px.n_tiles; ++i)
+                dsocr::image_to_chw(tiles[i].data(), px.tile, px.tile, px.tiles_chw.data() + (size_t)i * 3 * px.tile * px.tile);
+        }
+        px.n_image_tokens = dsocr::image_placeholder_count(px.base, px.tile, px.crop, px.crop_w, px.crop_h);
+        *out = p;
+    });
+}
+
+void dsocr_page_free(dsocr_page_pixels* p) { delete p; }
+
+dsocr_status dsocr_page_info(const dsocr_page_pixels* p, uint32_t* cw, uint32_t* ch, uint32_t* nt, size_t* ntok) {
+    return guarded([&] {
+        if (!p) throw std::runtime_error("EINVAL: NULL page");
+        if (cw) *cw = p->px.crop_w;
+        if (ch) *ch = p->px.crop_h;
+        if (nt) *nt = p->px.n_tiles;
+        if (ntok) *ntok = p->px.n_image_tokens;
+    });
+}
+
+dsocr_status dsocr_page_pixels_view(const dsocr_page_pixels* p, const float** g, uint32_t* gs, const float** t,
+                                    uint32_t* ts) {
+    return guarded([&] {
+        if (!p) throw std::runtime_error("EINVAL: NULL page");
+        if (g) *g = p->px.global_chw.data();
+        if (gs) *gs = p->px.gsize;
+        if (t) *t = p->px.n_tiles ? p->px.tiles_chw.data() : nullptr;
+        if (ts) *ts = p->px.tile;
+    });
+}
+
+dsocr_status dsocr_image_embeddings(dsocr_engine* e, const dsocr_page_pixels* const* pages, size_t n, float* out,
+                                    size_t cap_rows, size_t* rows_per_page) {
+    return guarded([&] {
+        if (!e || (!pages && n)) throw std::runtime_error("EINVAL: NULL argument");
+        std::vector<const dsocr::PagePixels*> ps;
+        for (size_t i = 0; i < n; ++i) ps.push_back(&pages[i]->px);
+        auto rows = e->impl->image_embeddings(ps);
+        const size_t H = e->impl->cfg().lang.hidden;
+        size_t off = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const size_t r = rows[i].size() / H;
+            if (rows_per_page) rows_per_page[i] = r;
+            if (off + r > cap_rows) throw std::runtime_error("EINVAL: output capacity too small");
+            if (out) std::memcpy(out + off * H, rows[i].data(), rows[i].size() * 4);
+            off += r;
+        }
+    });
+}
+
+dsocr_status dsocr_generate(dsocr_engine* e, const dsocr_request* req, const dsocr_decode_params* params,
+                            dsocr_stream_cb cb, void* user, int64_t* out_ids, size_t cap, size_t* n_out) {
+    return guarded([&] {
+        if (!e || !req || !out_ids || !n_out) throw std::runtime_error("EINVAL: NULL argument");
+        std::vector<dsocr::GenRequest> reqs{to_request(*req)};
+        auto r = e->impl->generate(reqs, to_params(params), cb, user);
+        if (r[0].size() > cap) throw std::runtime_error("EINVAL: output capacity too small");
+        std::memcpy(out_ids, r[0].data(), r[0].size() * sizeof(int64_t));
+        *n_out = r[0].size();
+    });
+}
+
+dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request* reqs,
+                                  const dsocr_decode_params* params, dsocr_result* results) {
+    return guarded([&] {
+        if (!e || (!reqs && n) || (!results && n)) throw std::runtime_error("EINVAL: NULL argument");
+        std::vector<dsocr::GenRequest> rq;
+        for (size_t i = 0; i < n; ++i) rq.push_back(to_request(reqs[i]));
+        auto r = e->impl->generate(rq, to_params(params), nullptr, nullptr);
+        for (size_t i = 0; i < n; ++i) {
+            results[i].status = DSOCR_OK;
+            size_t m = std::min(r[i].size(), results[i].cap);
+            if (results[i].out_ids) std::memcpy(results[i].out_ids, r[i].data(), m * sizeof(int64_t));
+            results[i].n_out = m;
+            if (m < r[i].size()) results[i].status = DSOCR_EINVAL;
+        }
+    });
+}
+
+dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t) {
+    return guarded([&] {
+        if (!e || !t) throw std::runtime_error("EINVAL: NULL argument");
+        dsocr::Timings x = e->impl->last_timings();
+        t->vision_prepare_ms = x.vision_prepare_ms;
+        t->vision_compute_ms = x.vision_compute_ms;
+        t->decode_prefill_ms = x.prefill_ms;
+        t->decode_iterative_ms = x.iterative_ms;
+        t->decode_generate_ms = x.generate_ms;
+        t->decode_steps = x.steps;
+        t->pages = x.pages;
+    });
+}
+
+// ---------------------------------------------------------------- device helpers
+dsocr_status dsocr_device_count(int* n) {
+    return guarded([&] { check_hip(hipGetDeviceCount(n), "hipGetDeviceCount"); });
+}
+dsocr_status dsocr_dev_alloc(size_t bytes, void** ptr) {
+    return guarded([&] {
+        if (hipMalloc(ptr, bytes ? bytes : 16) != hipSuccess) throw std::runtime_error("ENOMEM: hipMalloc failed");
+    });
+}
+dsocr_status dsocr_dev_free(void* ptr) {
+    return guarded([&] { check_hip(hipFree(ptr), "hipFree"); });
+}
+dsocr_status dsocr_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+    return guarded([&] { check_hip(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D"); });
+}
+dsocr_status dsocr_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+    return guarded([&] { check_hip(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H"); });
+}
+dsocr_status dsocr_dev_sync(void) {
+    return guarded([&] { check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+}
+dsocr_status dsocr_synth_bf16(const char* name, uint64_t seed, uint64_t n, uint16_t* out) {
+    return guarded([&] {
+        if (!name || (!out && n)) throw std::runtime_error("EINVAL: NULL argument");
+        dsocr::synth_bf16(name, seed, n, out);
+    });
+}
+dsocr_status dsocr_resize_bicubic(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw, uint32_t dh) {
+    return guarded([&] {
+        if (!src || !dst) throw std::runtime_error("EINVAL: NULL argument");
+        dsocr::resize_bicubic(src, (int)sw, (int)sh, dst, (int)dw, (int)dh);
+    });
+}
+
+// ---------------------------------------------------------------- kernel-level entry points
+dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias, float* C,
+                          int act, int accumulate) {
+    return guarded([&] {
+        if (K % 8) throw std::runtime_error("EINVAL: K must be a multiple of 8");
+        dsocr::GemmArgs g;
+        g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.W = W; g.ldw = K; g.wdtype = wdtype; g.bias = bias;
+        g.C = C; g.ldc = N; g.act = act; g.accumulate = accumulate;
+        dsocr::launch_gemm(g, nullptr);
+        check_hip(hipGetLastError(), "gemm launch");
+        check_hip(hipDeviceSynchronize(), "gemm");
+    });
+}
+dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const void* W, int wdtype, const float* bias, float* y,
+                          int act, int accumulate) {
+    return guarded([&] {
+        if (K % 8) throw std::runtime_error("EINVAL: K must be a multiple of 8");
+        dsocr::GemvArgs a;
+        a.M = M; a.N = N; a.K = K; a.x = x; a.ldx = K; a.W = W; a.ldw = K; a.wdtype = wdtype; a.bias = bias;
+        a.y = y; a.ldy = N; a.act = act; a.accumulate = accumulate;
+        dsocr::launch_gemv(a, nullptr);
+        check_hip(hipGetLastError(), "gemv launch");
+        check_hip(hipDeviceSynchronize(), "gemv");
+    });
+}
+dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* w, const float* b, float eps, float* y) {
+    return guarded([&] {
+        if (cols % 4) throw std::runtime_error("EINVAL: cols must be a multiple of 4");
+        dsocr::launch_layernorm(x, cols, y, cols, nullptr, rows, cols, w, b, eps, nullptr);
+        check_hip(hipDeviceSynchronize(), "layernorm");
+    });
+}
+dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w, float eps, float* y) {
+    return guarded([&] {
+        if (cols % 4) throw std::runtime_error("EINVAL: cols must be a multiple of 4");
+        dsocr::launch_rmsnorm(x, cols, y, cols, rows, cols, w, eps, nullptr);
+        check_hip(hipDeviceSynchronize(), "rmsnorm");
+    });
+}
+dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale, int causal, const float* q,
+                               const float* k, const float* v, float* o, const float* relh, const float* relw, int gh,
+                               int gw) {
+    return guarded([&] {
+        if (hd != 32 && hd != 64 && hd != 128) throw std::runtime_error("EINVAL: head_dim must be 32, 64 or 128");
+        const long C = (long)heads * hd;
+        dsocr::AttnArgs a;
+        a.q = {q, C, hd, nullptr};
+        a.k = {k, C, hd, nullptr};
+        a.v = {v, C, hd, nullptr};
+        a.o = o; a.o_row_stride = C; a.o_head_stride = hd; a.n_seq = n_seq; a.L = L; a.heads = heads;
+        a.kv_heads = heads; a.hd = hd; a.scale = scale; a.causal = causal;
+        float* rb = nullptr;
+        if (relh && relw) {
+            if (gh * gw != L) throw std::runtime_error("EINVAL: rel-pos grid does not match L");
+            check_hip(hipMalloc(&rb, sizeof(float) * (size_t)n_seq * heads * L * (gh + gw)), "hipMalloc relbias");
+            dsocr::launch_sam_relbias(q, C, n_seq, gh, gw, heads, hd, relh, relw, rb, nullptr);
+            a.relbias = rb; a.rel_h = gh; a.rel_w = gw;
+        }
+        dsocr::launch_attention(a, nullptr);
+        hipError_t e = hipDeviceSynchronize();
+        if (rb) hipFree(rb);
+        check_hip(e, "attention");
+    });
+}
+dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const void* router,
+                         const void* Wgu, const void* Wd, const void* sWgu, const void* sWd, int wdtype,
+                         int norm_topk, float scaling, float* out, int* ids_out, float* w_out) {
+    return guarded([&] {
+        if (H % 8 || I % 8 || (Is && Is % 8)) throw std::runtime_error("EINVAL: dims must be multiples of 8");
+        if (E > 256 || topk > 8 || topk > E) throw std::runtime_error("EINVAL: E <= 256 and topk <= min(8, E)");
+        const int TK = T * topk;
+        float *log, *wts, *hh, *y, *hs = nullptr, *ys = nullptr;
+        int *ids, *eoff, *arow, *apos, *iota, *deoff;
+        auto alloc = [&](void** p, size_t b) { check_hip(hipMalloc(p, b ? b : 16), "hipMalloc"); };
+        alloc((void**)&log, sizeof(float) * T * E);
+        alloc((void**)&wts, sizeof(float) * TK);
+        alloc((void**)&hh, sizeof(float) * (size_t)TK * I);
+        alloc((void**)&y, sizeof(float) * (size_t)TK * H);
+        alloc((void**)&ids, sizeof(int) * TK);
+        alloc((void**)&eoff, sizeof(int) * (E + 1));
+        alloc((void**)&arow, sizeof(int) * TK);
+        alloc((void**)&apos, sizeof(int) * TK);
+        alloc((void**)&iota, sizeof(int) * T);
+        alloc((void**)&deoff, sizeof(int) * 2);
+        std::vector<int> hi(T);
+        for (int i = 0; i < T; ++i) hi[i] = i;
+        int he[2] = {0, T};
+        check_hip(hipMemcpy(iota, hi.data(), sizeof(int) * T, hipMemcpyHostToDevice), "memcpy");
+        check_hip(hipMemcpy(deoff, he, sizeof(he), hipMemcpyHostToDevice), "memcpy");
+        dsocr::GemvArgs ra;
+        ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
+        ra.y = log; ra.ldy = E;
+        dsocr::launch_gemv(ra, nullptr);
+        dsocr::launch_router_topk(log, T, E, topk, 1, norm_topk, scaling, ids, wts, nullptr);
+        dsocr::launch_moe_group(ids, T, topk, E, eoff, arow, apos, nullptr, nullptr);
+        dsocr::MoeDecodeArgs m;
+        m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H; m.x = x; m.eoff = eoff; m.arow = arow;
+        m.Wgu = Wgu; m.Wd = Wd; m.wdtype = wdtype; m.h = hh; m.y = y; m.max_rows_per_expert = T == 1 ? 1 : 4;
+        dsocr::launch_moe_gateup_gemv(m, nullptr);
+        dsocr::launch_moe_down_gemv(m, nullptr);
+        if (sWgu && sWd && Is > 0) {
+            alloc((void**)&hs, sizeof(float) * (size_t)T * Is);
+            alloc((void**)&ys, sizeof(float) * (size_t)T * H);
+            dsocr::MoeDecodeArgs s;
+            s.T = T; s.topk = 1; s.E = 1; s.K = H; s.I = Is; s.Hout = H; s.x = x; s.eoff = deoff; s.arow = iota;
+            s.Wgu = sWgu; s.Wd = sWd; s.wdtype = wdtype; s.h = hs; s.y = ys; s.max_rows_per_expert = T;
+            dsocr::launch_moe_gateup_gemv(s, nullptr);
+            dsocr::launch_moe_down_gemv(s, nullptr);
+        }
+        dsocr::launch_moe_combine(y, apos, wts, ys, T, topk, H, out, 1, nullptr);
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess && ids_out) e = hipMemcpy(ids_out, ids, sizeof(int) * TK, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && w_out) e = hipMemcpy(w_out, wts, sizeof(float) * TK, hipMemcpyDeviceToHost);
+        for (void* p : {(void*)log, (void*)wts, (void*)hh, (void*)y, (void*)ids, (void*)eoff, (void*)arow, (void*)apos,
+                        (void*)iota, (void*)deoff, (void*)hs, (void*)ys})
+            if (p) hipFree(p);
+        check_hip(e, "moe");
+    });
+}
+dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,
+                                   int ngram, float rep_penalty, int* out_tok) {
+    return guarded([&] {
+        const int cap = 256;
+        const int rb = (int)dsocr::sample_workspace_blocks(V);
+        int *banned, *cnt, *ridx;
+        float* rval;
+        check_hip(hipMalloc(&banned, sizeof(int) * B * cap), "hipMalloc");
+        check_hip(hipMalloc(&cnt, sizeof(int) * B), "hipMalloc");
+        check_hip(hipMalloc(&ridx, sizeof(int) * B * rb), "hipMalloc");
+        check_hip(hipMalloc(&rval, sizeof(float) * B * rb), "hipMalloc");
+        dsocr::SampleArgs a;
+        a.logits = logits; a.B = B; a.V = V; a.ld = V; a.ctx = ctx; a.ctx_cap = ctx_cap; a.ctx_len = ctx_len;
+        a.ngram = ngram; a.rep_penalty = rep_penalty; a.banned = banned; a.banned_cnt = cnt; a.banned_cap = cap;
+        a.red_val = rval; a.red_idx = ridx; a.red_blocks = rb; a.out_tok = out_tok;
+        dsocr::launch_sample_greedy(a, nullptr);
+        hipError_t e = hipDeviceSynchronize();
+        hipFree(banned); hipFree(cnt); hipFree(ridx); hipFree(rval);
+        check_hip(e, "sample");
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,1161 @@
+// DeepSeek-OCR page engine (host orchestration of the gfx950 kernels).
+// Reference call stacks followed here: SURVEY §3.2-3.4; per-stage citations inline.
+#include "engine.hpp"
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "../common/host_util.hpp"
+#include "host_ops.hpp"
+
+namespace dsocr {
+
+// ============================================================================ weight source
+namespace {
+
+struct HostMat {
+    std::vector<uint16_t> data;
+    int dt = WDT_BF16;
+};
+
+struct Source {
+    std::unique_ptr<SafeTensors> st;
+    uint64_t seed = 0;
+    bool synth = false;
+    int mode = 1;  // dsocr_dtype: 0 f32, 1 f16, 2 bf16
+
+    bool has(const std::string& n) const { return synth ? synth_has(n) : st->has(n); }
+
+    static bool is_language(const std::string& n) {
+        return n.rfind("model.layers.", 0) == 0 || n.rfind("model.embed_tokens.", 0) == 0;
+    }
+    bool round16(const std::string& n) const { return mode == 1 && is_language(n); }
+
+    // exact f32 values (with the f16 rounding rule applied)
+    std::vector<float> f32(const std::string& n, size_t numel) const {
+        std::vector<float> out(numel);
+        if (synth) {
+            std::vector<uint16_t> b(numel);
+            synth_bf16(n, seed, numel, b.data());
+            for (size_t i = 0; i < numel; ++i) out[i] = bf16_to_f32(b[i]);
+        } else {
+            const StTensor& t = st->get(n);
+            if ((size_t)t.numel() != numel)
+                throw std::runtime_error("EINVAL: shape mismatch for `" + n + "`: " + std::to_string(t.numel()) +
+                                         " vs expected " + std::to_string(numel));
+            if (t.dtype == "BF16") {
+                const uint16_t* p = (const uint16_t*)t.data;
+                for (size_t i = 0; i < numel; ++i) out[i] = bf16_to_f32(p[i]);
+            } else if (t.dtype == "F16") {
+                const uint16_t* p = (const uint16_t*)t.data;
+                for (size_t i = 0; i < numel; ++i) out[i] = f16_to_f32(p[i]);
+            } else if (t.dtype == "F32") {
+                std::memcpy(out.data(), t.data, numel * 4);
+            } else {
+                throw std::runtime_error("EINVAL: unsupported dtype " + t.dtype + " for `" + n + "`");
+            }
+        }
+        if (round16(n))
+            for (auto& v : out) v = f16_to_f32(f32_to_f16_rne(v));
+        return out;
+    }
+
+    // 16-bit storage: f16 for language tensors in f16 mode (bf16 -> f16 RNE, the
+    // reference's VarBuilder F16 load), otherwise the checkpoint's own 16-bit type.
+    HostMat h16(const std::string& n, size_t numel) const {
+        HostMat m;
+        m.data.resize(numel);
+        const bool to_f16 = round16(n);
+        if (synth) {
+            synth_bf16(n, seed, numel, m.data.data());
+            if (to_f16) {
+#pragma omp parallel for schedule(static)
+                for (long i = 0; i < (long)numel; ++i) m.data[i] = f32_to_f16_rne(bf16_to_f32(m.data[i]));
+                m.dt = WDT_F16;
+            } else {
+                m.dt = WDT_BF16;
+            }
+            return m;
+        }
+        const StTensor& t = st->get(n);
+        if ((size_t)t.numel() != numel)
+            throw std::runtime_error("EINVAL: shape mismatch for `" + n + "`: " + std::to_string(t.numel()) +
+                                     " vs expected " + std::to_string(numel));
+        const uint16_t* p = (const uint16_t*)t.data;
+        if (t.dtype == "BF16") {
+            if (to_f16) {
+#pragma omp parallel for schedule(static)
+                for (long i = 0; i < (long)numel; ++i) m.data[i] = f32_to_f16_rne(bf16_to_f32(p[i]));
+                m.dt = WDT_F16;
+            } else {
+                std::memcpy(m.data.data(), p, numel * 2);
+                m.dt = WDT_BF16;
+            }
+        } else if (t.dtype == "F16") {
+            std::memcpy(m.data.data(), p, numel * 2);
+            m.dt = WDT_F16;
+        } else if (t.dtype == "F32" && to_f16) {
+            const float* f = (const float*)t.data;
+            for (size_t i = 0; i < numel; ++i) m.data[i] = f32_to_f16_rne(f[i]);
+            m.dt = WDT_F16;
+        } else {
+            throw std::runtime_error("EINVAL: matrix `" + n + "` has dtype " + t.dtype +
+                                     "; only BF16/F16 checkpoints are supported for large tensors");
+        }
+        return m;
+    }
+};
+
+std::string read_file(const std::string& p) {
+    std::ifstream f(p);
+    if (!f) throw std::runtime_error("ENOENT: cannot read config " + p);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+
+double ms_between(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+
+}  // namespace
+
+// ============================================================================ lifecycle
+void* Engine::dev_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) throw std::runtime_error("ENOMEM: hipMalloc(" + std::to_string(bytes) + ") failed");
+    allocations_.push_back(p);
+    return p;
+}
+
+void* Engine::ws(const std::string& name, size_t bytes) {
+    auto it = ws_.find(name);
+    if (it != ws_.end() && it->second.second >= bytes) return it->second.first;
+    if (capturing_) throw std::runtime_error("EINTERNAL: workspace growth during graph capture: " + name);
+    if (it != ws_.end()) {
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        HIP_CHECK(hipFree(it->second.first));
+    }
+    void* p = nullptr;
+    size_t cap = bytes + bytes / 8 + 256;
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) throw std::runtime_error("ENOMEM: workspace " + name + " (" + std::to_string(cap) + " bytes)");
+    ws_[name] = {p, cap};
+    return p;
+}
+
+Engine::Engine(const std::string& config_path, const std::string& weights_path, int device, int dtype, uint64_t seed)
+    : device_(device), dtype_(dtype) {
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) throw std::runtime_error("EDEVICE: no HIP device with ordinal " + std::to_string(device));
+    HIP_CHECK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        throw std::runtime_error(std::string("EDEVICE: device is ") + prop.gcnArchName + ", engine is built for gfx950");
+    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    cfg_ = resolve_config(Json::parse(read_file(config_path)));
+    const LangConfig& L = cfg_.lang;
+    if (L.has_lora) throw std::runtime_error("EINVAL: LoRA attention path not yet implemented");  // block.rs:452-454
+    if (L.topk_method != "greedy") throw std::runtime_error("EINVAL: MoE topk_method `" + L.topk_method + "` not yet supported (greedy only)");
+    if (L.scoring != "softmax" && L.scoring != "sigmoid") throw std::runtime_error("EINVAL: MoE scoring `" + L.scoring + "` not yet supported");
+    if (L.hidden_act != "silu" && L.hidden_act != "swish") throw std::runtime_error("EINVAL: activation `" + L.hidden_act + "` not implemented on this engine");
+    if (L.n_routed > 256) throw std::runtime_error("EINVAL: at most 256 routed experts supported");
+    if (L.topk > 8) throw std::runtime_error("EINVAL: at most 8 experts per token supported");
+    load_weights(weights_path, seed);
+    ensure_rope(4096);
+    ensure_small(64);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+Engine::~Engine() {
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& kv : ws_) (void)hipFree(kv.second.first);
+    for (void* p : allocations_) (void)hipFree(p);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Engine::ensure_small(int n) {
+    if (n <= small_cap_) return;
+    std::vector<float> ones(n, 1.f);
+    std::vector<int> iota(n);
+    for (int i = 0; i < n; ++i) iota[i] = i;
+    ones_ = (float*)dev_alloc(n * sizeof(float));
+    iota_ = (int*)dev_alloc(n * sizeof(int));
+    HIP_CHECK(hipMemcpy(ones_, ones.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(iota_, iota.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    small_cap_ = n;
+}
+
+// RoPE tables exactly as rope.rs:172-207 (f32 inv_freq, angle = pos * inv_freq, [half | half]).
+void Engine::ensure_rope(int len) {
+    if (len <= rope_cap_) return;
+    int cap = rope_cap_ > 0 ? rope_cap_ : 1;
+    while (cap < len) cap *= 2;
+    const int rd = cfg_.lang.rope_dim, half = rd / 2;
+    std::vector<float> inv(half), c((size_t)cap * rd), s((size_t)cap * rd);
+    for (int i = 0; i < half; ++i) inv[i] = 1.0f / powf(cfg_.lang.rope_theta, ((float)i * 2.0f) / (float)rd);
+    for (int p = 0; p < cap; ++p)
+        for (int i = 0; i < half; ++i) {
+            float a = (float)p * inv[i];
+            c[(size_t)p * rd + i] = c[(size_t)p * rd + half + i] = cosf(a);
+            s[(size_t)p * rd + i] = s[(size_t)p * rd + half + i] = sinf(a);
+        }
+    rope_cos_ = (float*)dev_alloc(c.size() * 4);
+    rope_sin_ = (float*)dev_alloc(s.size() * 4);
+    HIP_CHECK(hipMemcpy(rope_cos_, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(rope_sin_, s.data(), s.size() * 4, hipMemcpyHostToDevice));
+    rope_cap_ = cap;
+}
+
+// ============================================================================ loading
+void Engine::load_weights(const std::string& path, uint64_t seed) {
+    Source src;
+    src.mode = dtype_;
+    if (path.empty()) {
+        src.synth = true;
+        src.seed = seed;
+    } else {
+        src.st.reset(new SafeTensors(path));
+    }
+    auto up16 = [&](const HostMat& m) -> void* {
+        void* p = dev_alloc(m.data.size() * 2);
+        HIP_CHECK(hipMemcpy(p, m.data.data(), m.data.size() * 2, hipMemcpyHostToDevice));
+        return p;
+    };
+    auto upf = [&](const std::vector<float>& v) -> float* {
+        float* p = (float*)dev_alloc(v.size() * 4);
+        HIP_CHECK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+        return p;
+    };
+    auto vecf = [&](const std::string& n, size_t numel) -> float* { return upf(src.f32(n, numel)); };
+    auto optvec = [&](const std::string& n, size_t numel) -> float* { return src.has(n) ? vecf(n, numel) : nullptr; };
+    auto lin = [&](const std::string& pre, int N, int K, bool allow_bias) -> Lin {
+        Lin l;
+        HostMat m = src.h16(pre + ".weight", (size_t)N * K);
+        l.W = up16(m);
+        l.wdt = m.dt;
+        l.N = N;
+        l.K = K;
+        if (allow_bias && src.has(pre + ".bias")) l.b = vecf(pre + ".bias", N);
+        return l;
+    };
+    // concatenation of several [Ni][K] matrices (+ optional biases) into one [sum Ni][K]
+    auto lin_cat = [&](const std::vector<std::string>& pres, const std::vector<int>& Ns, int K) -> Lin {
+        Lin l;
+        HostMat all;
+        std::vector<float> bias;
+        bool any_bias = false;
+        int N = 0;
+        for (size_t i = 0; i < pres.size(); ++i) {
+            HostMat m = src.h16(pres[i] + ".weight", (size_t)Ns[i] * K);
+            if (i == 0) all.dt = m.dt;
+            else if (m.dt != all.dt) throw std::runtime_error("EINVAL: mixed dtypes in fused linear " + pres[i]);
+            all.data.insert(all.data.end(), m.data.begin(), m.data.end());
+            std::vector<float> b(Ns[i], 0.f);
+            if (src.has(pres[i] + ".bias")) { b = src.f32(pres[i] + ".bias", Ns[i]); any_bias = true; }
+            bias.insert(bias.end(), b.begin(), b.end());
+            N += Ns[i];
+        }
+        l.W = up16(all);
+        l.wdt = all.dt;
+        l.N = N;
+        l.K = K;
+        if (any_bias) l.b = upf(bias);
+        return l;
+    };
+    // conv [O][C][kh][kw] -> [O][kh][kw][C] (NHWC im2col order)
+    auto conv = [&](const std::string& n, int O, int C, int kh, int kw) -> Lin {
+        HostMat m = src.h16(n, (size_t)O * C * kh * kw);
+        HostMat r;
+        r.dt = m.dt;
+        r.data.resize(m.data.size());
+        for (int o = 0; o < O; ++o)
+            for (int c = 0; c < C; ++c)
+                for (int y = 0; y < kh; ++y)
+                    for (int x = 0; x < kw; ++x)
+                        r.data[(((size_t)o * kh + y) * kw + x) * C + c] = m.data[(((size_t)o * C + c) * kh + y) * kw + x];
+        Lin l;
+        l.W = up16(r);
+        l.wdt = r.dt;
+        l.N = O;
+        l.K = C * kh * kw;
+        return l;
+    };
+
+    // ---------------- SAM (vision/sam.rs:143-184)
+    const SamConfig& S = cfg_.sam;
+    const std::string sp = "model.sam_model.";
+    sam_.patch = lin(sp + "patch_embed.proj", S.dim, 3 * S.patch * S.patch, true);
+    const int tps = S.image_size / S.patch;
+    if (src.has(sp + "pos_embed")) {
+        sam_.has_pos = true;
+        sam_.pos_grid = tps;
+        std::vector<float> pos = src.f32(sp + "pos_embed", (size_t)tps * tps * S.dim);  // [1][g][g][C]
+        sam_.pos_host.resize(pos.size());
+        for (int y = 0; y < tps; ++y)
+            for (int x = 0; x < tps; ++x)
+                for (int c = 0; c < S.dim; ++c)
+                    sam_.pos_host[((size_t)c * tps + y) * tps + x] = pos[((size_t)y * tps + x) * S.dim + c];
+    }
+    const int hd = S.dim / S.heads;
+    for (int b = 0; b < S.depth; ++b) {
+        SamBlock blk;
+        const std::string bp = sp + "blocks." + std::to_string(b) + ".";
+        blk.global = S.is_global(b);
+        blk.n1 = {vecf(bp + "norm1.weight", S.dim), vecf(bp + "norm1.bias", S.dim)};
+        blk.n2 = {vecf(bp + "norm2.weight", S.dim), vecf(bp + "norm2.bias", S.dim)};
+        blk.qkv = lin(bp + "attn.qkv", 3 * S.dim, S.dim, true);
+        blk.proj = lin(bp + "attn.proj", S.dim, S.dim, true);
+        const int hid = (int)(S.dim * S.mlp_ratio);
+        std::string f1 = src.has(bp + "mlp.fc1.weight") ? "mlp.fc1" : "mlp.lin1";
+        std::string f2 = src.has(bp + "mlp.fc2.weight") ? "mlp.fc2" : "mlp.lin2";
+        blk.fc1 = lin(bp + f1, hid, S.dim, true);
+        blk.fc2 = lin(bp + f2, S.dim, hid, true);
+        blk.use_rel = src.has(bp + "attn.rel_pos_h");
+        if (blk.use_rel) {
+            const int tokens = blk.global ? tps : S.window;
+            blk.rel_len = 2 * tokens - 1;
+            blk.relh = src.f32(bp + "attn.rel_pos_h", (size_t)blk.rel_len * hd);
+            blk.relw = src.f32(bp + "attn.rel_pos_w", (size_t)blk.rel_len * hd);
+        }
+        sam_.blocks.push_back(std::move(blk));
+    }
+    sam_.neck0 = conv(sp + "neck.0.weight", S.neck, S.dim, 1, 1);
+    sam_.neck1 = {vecf(sp + "neck.1.weight", S.neck), vecf(sp + "neck.1.bias", S.neck)};
+    sam_.neck2 = conv(sp + "neck.2.weight", S.neck, S.neck, 3, 3);
+    sam_.neck3 = {vecf(sp + "neck.3.weight", S.neck), vecf(sp + "neck.3.bias", S.neck)};
+    sam_.net2 = conv(sp + "net_2.weight", S.out_ch[0], S.neck, 3, 3);
+    sam_.net3 = conv(sp + "net_3.weight", S.out_ch[1], S.out_ch[0], 3, 3);
+
+    // ---------------- CLIP (vision/clip.rs:73-88)
+    const ClipConfig& C = cfg_.clip;
+    const std::string cp = "model.vision_model.";
+    clip_.cls = vecf(cp + "embeddings.class_embedding", C.hidden);
+    clip_.pos_host = src.f32(cp + "embeddings.position_embedding.weight", (size_t)(C.seq + 1) * C.hidden);
+    clip_.pre = {vecf(cp + "pre_layrnorm.weight", C.hidden), vecf(cp + "pre_layrnorm.bias", C.hidden)};
+    for (int l = 0; l < C.layers; ++l) {
+        ClipLayer cl;
+        const std::string lp = cp + "transformer.layers." + std::to_string(l) + ".";
+        cl.ln1 = {vecf(lp + "layer_norm1.weight", C.hidden), vecf(lp + "layer_norm1.bias", C.hidden)};
+        cl.ln2 = {vecf(lp + "layer_norm2.weight", C.hidden), vecf(lp + "layer_norm2.bias", C.hidden)};
+        cl.qkv = lin(lp + "self_attn.qkv_proj", 3 * C.hidden, C.hidden, true);
+        cl.out = lin(lp + "self_attn.out_proj", C.hidden, C.hidden, true);
+        cl.fc1 = lin(lp + "mlp.fc1", C.ffn, C.hidden, true);
+        cl.fc2 = lin(lp + "mlp.fc2", C.hidden, C.ffn, true);
+        clip_.layers.push_back(cl);
+    }
+    if (C.hidden != S.out_ch[1]) throw std::runtime_error("EINVAL: CLIP width must equal SAM output channels");
+    if (C.hidden + S.out_ch[1] != cfg_.proj_in) throw std::runtime_error("EINVAL: combined hidden dims do not match projector input");
+
+    // ---------------- projector (model/mod.rs:258-390)
+    proj_ = lin("model.projector.layers", cfg_.proj_out, cfg_.proj_in, true);
+    newline_ = src.has("model.image_newline") ? vecf("model.image_newline", cfg_.proj_out)
+                                               : upf(std::vector<float>(cfg_.proj_out, 0.f));
+    separator_ = vecf("model.view_seperator", cfg_.proj_out);
+
+    // ---------------- language model (transformer/weights.rs:444-606)
+    const LangConfig& L = cfg_.lang;
+    {
+        HostMat m = src.h16("model.embed_tokens.weight", (size_t)L.vocab * L.hidden);
+        embed_ = up16(m);
+        embed_dt_ = m.dt;
+    }
+    const int H = L.hidden, KVH = L.kv_heads * L.head_dim;
+    for (int l = 0; l < L.layers; ++l) {
+        DecLayer d;
+        const std::string lp = "model.layers." + std::to_string(l) + ".";
+        d.in_norm = {vecf(lp + "input_layernorm.weight", H), nullptr};
+        d.post_norm = {vecf(lp + "post_attention_layernorm.weight", H), nullptr};
+        d.qkv = lin_cat({lp + "self_attn.q_proj", lp + "self_attn.k_proj", lp + "self_attn.v_proj"},
+                        {L.heads * L.head_dim, KVH, L.kv_heads * L.v_head_dim}, H);
+        d.o = lin(lp + "self_attn.o_proj", H, L.heads * L.v_head_dim, true);
+        d.moe = L.moe_layer(l);
+        if (!d.moe) {
+            d.gu = lin_cat({lp + "mlp.gate_proj", lp + "mlp.up_proj"}, {L.inter, L.inter}, H);
+            d.down = lin(lp + "mlp.down_proj", H, L.inter, true);
+            if (d.gu.b || d.down.b) throw std::runtime_error("EINVAL: biased dense MLP not supported");
+        } else {
+            const int E = L.n_routed, I = L.moe_inter;
+            HostMat r = src.h16(lp + "mlp.gate.weight", (size_t)E * H);
+            d.router.W = up16(r);
+            d.router.wdt = r.dt;
+            d.router.N = E;
+            d.router.K = H;
+            d.router.b = optvec(lp + "mlp.gate.e_score_correction_bias", E);
+            HostMat gu, dn;
+            gu.data.resize((size_t)E * 2 * I * H);
+            dn.data.resize((size_t)E * H * I);
+            for (int e = 0; e < E; ++e) {
+                const std::string ep = lp + "mlp.experts." + std::to_string(e) + ".";
+                HostMat g = src.h16(ep + "gate_proj.weight", (size_t)I * H);
+                HostMat u = src.h16(ep + "up_proj.weight", (size_t)I * H);
+                HostMat w = src.h16(ep + "down_proj.weight", (size_t)H * I);
+                if (src.has(ep + "gate_proj.bias") || src.has(ep + "down_proj.bias"))
+                    throw std::runtime_error("EINVAL: biased experts not supported");
+                std::copy(g.data.begin(), g.data.end(), gu.data.begin() + (size_t)e * 2 * I * H);
+                std::copy(u.data.begin(), u.data.end(), gu.data.begin() + (size_t)e * 2 * I * H + (size_t)I * H);
+                std::copy(w.data.begin(), w.data.end(), dn.data.begin() + (size_t)e * H * I);
+                gu.dt = dn.dt = g.dt;
+            }
+            d.e_gu = up16(gu);
+            d.e_d = up16(dn);
+            d.e_wdt = gu.dt;
+            if (L.n_shared > 0) {
+                const int Is = I * L.n_shared;
+                d.has_shared = true;
+                d.s_gu = lin_cat({lp + "mlp.shared_experts.gate_proj", lp + "mlp.shared_experts.up_proj"}, {Is, Is}, H);
+                d.s_d = lin(lp + "mlp.shared_experts.down_proj", H, Is, true);
+            }
+        }
+        layers_.push_back(d);
+    }
+    final_norm_ = vecf("model.norm.weight", H);  // f32 copy (model/mod.rs:1008-1014)
+    lm_head_ = lin("lm_head", L.vocab, H, false);
+}
+
+// ============================================================================ compute helpers
+void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int ldy, int act, int accumulate,
+                    const int* c_rows) {
+    if (M <= 16 && !c_rows) {
+        GemvArgs a;
+        a.M = M; a.N = l.N; a.K = l.K; a.x = x; a.ldx = ldx; a.W = l.W; a.ldw = l.K; a.wdtype = l.wdt;
+        a.bias = l.b; a.y = y; a.ldy = ldy; a.act = act; a.accumulate = accumulate;
+        launch_gemv(a, stream_);
+    } else {
+        GemmArgs g;
+        g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.wdtype = l.wdt;
+        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
+        launch_gemm(g, stream_);
+    }
+}
+
+float* Engine::sam_pos(int g) {
+    auto it = sam_.pos_dev.find(g);
+    if (it != sam_.pos_dev.end()) return it->second;
+    const int C = cfg_.sam.dim, src = sam_.pos_grid;
+    std::vector<float> r = bicubic_resize_aa(sam_.pos_host, C, src, src, g, g);  // sam.rs:982-998
+    std::vector<float> nhwc((size_t)g * g * C);
+    for (int c = 0; c < C; ++c)
+        for (int p = 0; p < g * g; ++p) nhwc[(size_t)p * C + c] = r[(size_t)c * g * g + p];
+    float* d = (float*)dev_alloc(nhwc.size() * 4);
+    HIP_CHECK(hipMemcpy(d, nhwc.data(), nhwc.size() * 4, hipMemcpyHostToDevice));
+    sam_.pos_dev[g] = d;
+    return d;
+}
+
+std::pair<float*, float*> Engine::sam_rel(SamBlock& b, int g) {
+    auto it = b.rel_dev.find(g);
+    if (it != b.rel_dev.end()) return it->second;
+    const int hd = cfg_.sam.dim / cfg_.sam.heads;
+    std::vector<float> rh = rel_pos_resize(b.relh, b.rel_len, hd, g);
+    std::vector<float> rw = rel_pos_resize(b.relw, b.rel_len, hd, g);
+    float* dh = (float*)dev_alloc(rh.size() * 4);
+    float* dw = (float*)dev_alloc(rw.size() * 4);
+    HIP_CHECK(hipMemcpy(dh, rh.data(), rh.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dw, rw.data(), rw.size() * 4, hipMemcpyHostToDevice));
+    b.rel_dev[g] = {dh, dw};
+    return {dh, dw};
+}
+
+float* Engine::clip_pos(int tokens) {
+    auto it = clip_.pos_dev.find(tokens);
+    if (it != clip_.pos_dev.end()) return it->second;
+    const ClipConfig& C = cfg_.clip;
+    std::vector<float> out;
+    if (tokens == C.seq + 1) {
+        out = clip_.pos_host;
+    } else {  // clip.rs:486-544
+        const int s = (int)std::lround(std::sqrt((double)C.seq)), t = (int)std::lround(std::sqrt((double)(tokens - 1)));
+        if (t * t != tokens - 1) throw std::runtime_error("EINVAL: clip positional table tgt tokens not square");
+        std::vector<float> grid((size_t)C.hidden * s * s);
+        for (int p = 0; p < s * s; ++p)
+            for (int c = 0; c < C.hidden; ++c) grid[(size_t)c * s * s + p] = clip_.pos_host[(size_t)(1 + p) * C.hidden + c];
+        std::vector<float> r = bicubic_resize_aa(grid, C.hidden, s, s, t, t);
+        out.resize((size_t)tokens * C.hidden);
+        std::copy(clip_.pos_host.begin(), clip_.pos_host.begin() + C.hidden, out.begin());
+        for (int p = 0; p < t * t; ++p)
+            for (int c = 0; c < C.hidden; ++c) out[(size_t)(1 + p) * C.hidden + c] = r[(size_t)c * t * t + p];
+    }
+    float* d = (float*)dev_alloc(out.size() * 4);
+    HIP_CHECK(hipMemcpy(d, out.data(), out.size() * 4, hipMemcpyHostToDevice));
+    clip_.pos_dev[tokens] = d;
+    return d;
+}
+
+// ============================================================================ vision
+// SamBackbone::forward (sam.rs:210-289) + ClipVisionModel::forward (clip.rs:98-102) +
+// build_clip_sam_tokens + ImageProjector::project (model/mod.rs:604-650, 392-444).
+float* Engine::vision_pass(const float* imgs, int n, int Spx, const std::string& out) {
+    const SamConfig& S = cfg_.sam;
+    const ClipConfig& CC = cfg_.clip;
+    const int C = S.dim, heads = S.heads, hd = C / heads;
+    if (Spx % S.patch) throw std::runtime_error("EINVAL: image dimensions must be divisible by patch size");
+    const int g = Spx / S.patch;
+    if (g % 2 || (g / 2) % 2) throw std::runtime_error("EINVAL: spatial dims cannot be evenly downsampled by stride 2");
+    const long rows = (long)n * g * g;
+    hipStream_t st = stream_;
+
+    // patch embed
+    float* cols = wsf("v_cols", (size_t)rows * 3 * S.patch * S.patch);
+    launch_patch_im2col(imgs, n, Spx, Spx, S.patch, cols, st);
+    float* x = wsf("v_x", (size_t)rows * C);
+    linear(cols, (int)rows, 3 * S.patch * S.patch, sam_.patch, x, C);
+    if (sam_.has_pos) launch_add_broadcast(x, sam_pos(g), (long)g * g, C, n, st);
+
+    // window partition maps (sam.rs:926-980)
+    const int W = S.window;
+    const int gp = g + (W - g % W) % W, nw = gp / W;
+    const long wrows = (long)n * nw * nw * W * W;
+    std::vector<int> tok2win(rows), win2tok(wrows, -1);
+    for (int b = 0; b < n; ++b)
+        for (int y = 0; y < g; ++y)
+            for (int xx = 0; xx < g; ++xx) {
+                long t = ((long)b * g + y) * g + xx;
+                long w = (((long)b * nw + y / W) * nw + xx / W) * W * W + (y % W) * W + (xx % W);
+                tok2win[t] = (int)w;
+                win2tok[w] = (int)t;
+            }
+    int* d_tok2win = upload("v_tok2win", tok2win);
+    int* d_win2tok = upload("v_win2tok", win2tok);
+    const long maxrows = std::max(rows, wrows);
+    float* xn = wsf("v_xn", (size_t)maxrows * C);
+    float* qkv = wsf("v_qkv", (size_t)maxrows * 3 * C);
+    float* ctx = wsf("v_ctx", (size_t)maxrows * C);
+    const int hid = (int)(C * S.mlp_ratio);
+    float* hbuf = wsf("v_h", (size_t)rows * hid);
+
+    for (int bi = 0; bi < S.depth; ++bi) {
+        SamBlock& blk = sam_.blocks[bi];
+        const bool win = !blk.global;
+        const int L = win ? W * W : g * g;
+        const int nseq = win ? n * nw * nw : n;
+        const long arows = (long)nseq * L;
+        if (win) {
+            HIP_CHECK(hipMemsetAsync(xn, 0, (size_t)wrows * C * 4, st));
+            launch_layernorm(x, C, xn, C, d_tok2win, (int)rows, C, blk.n1.w, blk.n1.b, 1e-6f, st);
+        } else {
+            launch_layernorm(x, C, xn, C, nullptr, (int)rows, C, blk.n1.w, blk.n1.b, 1e-6f, st);
+        }
+        linear(xn, (int)arows, C, blk.qkv, qkv, 3 * C);
+        AttnArgs a;
+        a.q = {qkv, 3L * C, hd, nullptr};
+        a.k = {qkv + C, 3L * C, hd, nullptr};
+        a.v = {qkv + 2 * C, 3L * C, hd, nullptr};
+        a.o = ctx;
+        a.o_row_stride = C;
+        a.o_head_stride = hd;
+        a.n_seq = nseq;
+        a.L = L;
+        a.heads = heads;
+        a.kv_heads = heads;
+        a.hd = hd;
+        a.scale = (float)(1.0 / std::sqrt((double)hd));
+        if (blk.use_rel) {
+            const int gg = win ? W : g;
+            auto rel = win ? std::make_pair<float*, float*>(nullptr, nullptr) : sam_rel(blk, g);
+            if (win) rel = sam_rel(blk, W);
+            float* rb = wsf("v_relbias", (size_t)nseq * heads * L * (2 * gg));
+            launch_sam_relbias(qkv, 3L * C, nseq, gg, gg, heads, hd, rel.first, rel.second, rb, st);
+            a.relbias = rb;
+            a.rel_h = gg;
+            a.rel_w = gg;
+        }
+        launch_attention(a, st);
+        // proj + residual (window_unpartition via row scatter)
+        linear(ctx, (int)arows, C, blk.proj, x, C, 0, 1, win ? d_win2tok : nullptr);
+        launch_layernorm(x, C, xn, C, nullptr, (int)rows, C, blk.n2.w, blk.n2.b, 1e-6f, st);
+        linear(xn, (int)rows, C, blk.fc1, hbuf, hid, ACT_GELU_ERF);
+        linear(hbuf, (int)rows, hid, blk.fc2, x, C, 0, 1);
+    }
+    // neck (sam.rs:503-520) in NHWC
+    const int NC = S.neck;
+    float* y = wsf("v_neck", (size_t)rows * NC);
+    linear(x, (int)rows, C, sam_.neck0, y, NC);
+    launch_layernorm(y, NC, y, NC, nullptr, (int)rows, NC, sam_.neck1.w, sam_.neck1.b, 1e-6f, st);
+    float* ncols = wsf("v_ncols", (size_t)rows * 9 * NC);
+    launch_conv_im2col_nhwc(y, n, g, g, NC, 3, 3, 1, 1, ncols, st);
+    linear(ncols, (int)rows, 9 * NC, sam_.neck2, y, NC);
+    launch_layernorm(y, NC, y, NC, nullptr, (int)rows, NC, sam_.neck3.w, sam_.neck3.b, 1e-6f, st);
+    // downsample (sam.rs:550-575)
+    const int g2 = g / 2, g4 = g / 4, c0 = S.out_ch[0], c1 = S.out_ch[1];
+    launch_conv_im2col_nhwc(y, n, g, g, NC, 3, 3, 2, 1, ncols, st);
+    float* z = wsf("v_net2", (size_t)n * g2 * g2 * c0);
+    linear(ncols, n * g2 * g2, 9 * NC, sam_.net2, z, c0);
+    float* ncols2 = wsf("v_ncols2", (size_t)n * g4 * g4 * 9 * c0);
+    launch_conv_im2col_nhwc(z, n, g2, g2, c0, 3, 3, 2, 1, ncols2, st);
+    const int Sq = g4 * g4;
+    float* sam_out = wsf("v_samout", (size_t)n * Sq * c1);
+    linear(ncols2, n * Sq, 9 * c0, sam_.net3, sam_out, c1);
+
+    // CLIP (clip.rs:165-309) on SAM features
+    const int T = Sq + 1, CH = CC.hidden, chd = CH / CC.heads;
+    const long crow = (long)n * T;
+    float* cx = wsf("c_x", (size_t)crow * CH);
+    launch_clip_embed(sam_out, clip_.cls, clip_pos(T), n, Sq, CH, cx, st);
+    launch_layernorm(cx, CH, cx, CH, nullptr, (int)crow, CH, clip_.pre.w, clip_.pre.b, 1e-5f, st);
+    float* cxn = wsf("c_xn", (size_t)crow * CH);
+    float* cqkv = wsf("c_qkv", (size_t)crow * 3 * CH);
+    float* cctx = wsf("c_ctx", (size_t)crow * CH);
+    float* ch = wsf("c_h", (size_t)crow * CC.ffn);
+    for (int l = 0; l < CC.layers; ++l) {
+        ClipLayer& cl = clip_.layers[l];
+        launch_layernorm(cx, CH, cxn, CH, nullptr, (int)crow, CH, cl.ln1.w, cl.ln1.b, 1e-5f, st);
+        linear(cxn, (int)crow, CH, cl.qkv, cqkv, 3 * CH);
+        AttnArgs a;
+        a.q = {cqkv, 3L * CH, chd, nullptr};
+        a.k = {cqkv + CH, 3L * CH, chd, nullptr};
+        a.v = {cqkv + 2 * CH, 3L * CH, chd, nullptr};
+        a.o = cctx;
+        a.o_row_stride = CH;
+        a.o_head_stride = chd;
+        a.n_seq = n;
+        a.L = T;
+        a.heads = CC.heads;
+        a.kv_heads = CC.heads;
+        a.hd = chd;
+        a.scale = (float)(1.0 / std::sqrt((double)chd));
+        launch_attention(a, st);
+        linear(cctx, (int)crow, CH, cl.out, cx, CH, 0, 1);
+        launch_layernorm(cx, CH, cxn, CH, nullptr, (int)crow, CH, cl.ln2.w, cl.ln2.b, 1e-5f, st);
+        linear(cxn, (int)crow, CH, cl.fc1, ch, CC.ffn, ACT_QUICK_GELU);
+        linear(ch, (int)crow, CC.ffn, cl.fc2, cx, CH, 0, 1);
+    }
+    // concat + projector
+    float* pre = wsf("p_pre", (size_t)n * Sq * (CH + c1));
+    launch_concat_clip_sam(cx, sam_out, n, Sq, CH, c1, pre, st);
+    float* post = wsf(out, (size_t)n * Sq * cfg_.proj_out);
+    linear(pre, n * Sq, CH + c1, proj_, post, cfg_.proj_out);
+    return post;
+}
+
+std::vector<std::vector<float>> Engine::image_embeddings(const std::vector<const PagePixels*>& pages) {
+    std::vector<std::vector<float>> result;
+    const int H = cfg_.proj_out;
+    for (const PagePixels* p : pages) {
+        // one page at a time keeps this helper simple; generate() batches pages.
+        float* gimg = upload("e_gimg", p->global_chw);
+        float* gpost = vision_pass(gimg, 1, p->gsize, "e_gpost");
+        const int gs = p->gsize / 64;
+        std::vector<float> gh((size_t)gs * gs * H);
+        HIP_CHECK(hipMemcpyAsync(gh.data(), gpost, gh.size() * 4, hipMemcpyDeviceToHost, stream_));
+        std::vector<float> lh;
+        int ls = 0;
+        if (p->n_tiles > 0) {
+            float* timg = upload("e_timg", p->tiles_chw);
+            float* lpost = vision_pass(timg, p->n_tiles, p->tile, "e_lpost");
+            ls = p->tile / 64;
+            lh.resize((size_t)p->n_tiles * ls * ls * H);
+            HIP_CHECK(hipMemcpyAsync(lh.data(), lpost, lh.size() * 4, hipMemcpyDeviceToHost, stream_));
+        }
+        HIP_CHECK(hipStreamSynchronize(stream_));
+        std::vector<float> nl(H), sp(H);
+        HIP_CHECK(hipMemcpy(nl.data(), newline_, H * 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(sp.data(), separator_, H * 4, hipMemcpyDeviceToHost));
+        std::vector<float> rows;
+        auto push = [&](const float* r) { rows.insert(rows.end(), r, r + H); };
+        if (p->n_tiles > 0) {  // format_local_tokens (model/mod.rs:677-709)
+            for (int R = 0; R < p->crop_h * ls; ++R) {
+                for (int Cc = 0; Cc < p->crop_w * ls; ++Cc) {
+                    int crop = (R / ls) * p->crop_w + (Cc / ls);
+                    push(&lh[(((size_t)crop * ls + R % ls) * ls + Cc % ls) * H]);
+                }
+                push(nl.data());
+            }
+        }
+        for (int R = 0; R < gs; ++R) {  // format_global_tokens (656-675)
+            for (int Cc = 0; Cc < gs; ++Cc) push(&gh[((size_t)R * gs + Cc) * H]);
+            push(nl.data());
+        }
+        push(sp.data());
+        result.push_back(std::move(rows));
+    }
+    return result;
+}
+
+// ============================================================================ decoder
+void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, const int* row_pos, const long* q_off,
+                                   const long* kv_off, const long* o_off, const int* seq_len, int max_len, int Lmax) {
+    const LangConfig& L = cfg_.lang;
+    DecLayer& d = layers_[l];
+    hipStream_t st = stream_;
+    const int H = L.hidden, hd = L.head_dim, KVH = L.kv_heads * hd, QKVN = d.qkv.N;
+    float* X = wsf("d_x", (size_t)T * H);
+    float* XN = wsf("d_xn", (size_t)T * H);
+    float* QKV = wsf("d_qkv", (size_t)T * QKVN);
+    float* CTX = wsf("d_ctx", (size_t)T * H);
+    const long layer_kv = (long)B * page_stride_;
+    float* kc = kc_ + (long)l * layer_kv;
+    float* vc = vc_ + (long)l * layer_kv;
+
+    launch_rmsnorm(X, H, XN, H, T, H, d.in_norm.w, L.rms_eps, st);
+    linear(XN, T, H, d.qkv, QKV, QKVN);
+    RopeKvArgs r;
+    r.qkv = QKV; r.ld = QKVN; r.rows = T; r.row_page = row_page; r.row_pos = row_pos;
+    r.heads = L.heads; r.kv_heads = L.kv_heads; r.hd = hd; r.rope_dim = L.rope_dim; r.use_mla = L.use_mla;
+    r.cos = rope_cos_; r.sin = rope_sin_; r.kc = kc; r.vc = vc; r.page_stride = page_stride_; r.head_stride = head_stride_;
+    launch_rope_kv(r, st);
+    AttnArgs a;
+    a.q = {QKV, QKVN, hd, q_off};
+    a.k = {kc, hd, head_stride_, kv_off};
+    a.v = {vc, hd, head_stride_, kv_off};
+    a.o = CTX; a.o_row_stride = H; a.o_head_stride = hd; a.o_seq_off = o_off;
+    a.n_seq = B; a.L = max_len; a.seq_len = seq_len;
+    a.heads = L.heads; a.kv_heads = L.kv_heads; a.hd = hd;
+    a.scale = (float)(1.0 / std::sqrt((double)hd));
+    a.causal = 1;
+    launch_attention(a, st);
+    (void)Lmax;
+    (void)KVH;
+    linear(CTX, T, H, d.o, X, H, 0, 1);
+    launch_rmsnorm(X, H, XN, H, T, H, d.post_norm.w, L.rms_eps, st);
+    if (!d.moe) {
+        const int I = L.inter;
+        float* G = wsf("d_g", (size_t)T * 2 * I);
+        float* HH = wsf("d_hh", (size_t)T * I);
+        linear(XN, T, H, d.gu, G, 2 * I);
+        launch_silu_mul(G, 2 * I, I, T, HH, I, st);
+        linear(HH, T, I, d.down, X, H, 0, 1);
+        return;
+    }
+    // MoE (run_moe, block.rs:1215-1395) with device-side routing
+    const int E = L.n_routed, K = L.topk, I = L.moe_inter, TK = T * K;
+    float* LOG = wsf("d_log", (size_t)T * E);
+    int* IDS = wsi("d_ids", TK);
+    float* WTS = wsf("d_wts", TK);
+    int* EOFF = wsi("d_eoff", E + 1);
+    int* AROW = wsi("d_arow", TK);
+    int* APOS = wsi("d_apos", TK);
+    linear(XN, T, H, d.router, LOG, E);
+    launch_router_topk(LOG, T, E, K, L.scoring == "softmax", L.norm_topk, L.routed_scaling, IDS, WTS, st);
+    launch_moe_group(IDS, T, K, E, EOFF, AROW, APOS, nullptr, st);
+    float* G = wsf("d_eg", (size_t)TK * 2 * I);
+    float* HH = wsf("d_ehh", (size_t)TK * I);
+    float* Y = wsf("d_ey", (size_t)TK * H);
+    GemmArgs g1;
+    g1.M = TK; g1.N = 2 * I; g1.K = H; g1.A = XN; g1.lda = H; g1.a_rows = AROW; g1.W = d.e_gu; g1.ldw = H;
+    g1.wdtype = d.e_wdt; g1.w_group_stride = (long)2 * I * H; g1.C = G; g1.ldc = 2 * I;
+    g1.group_off = EOFF; g1.groups = E; g1.max_group_rows = T;
+    launch_gemm(g1, st);
+    launch_silu_mul(G, 2 * I, I, TK, HH, I, st);
+    GemmArgs g2;
+    g2.M = TK; g2.N = H; g2.K = I; g2.A = HH; g2.lda = I; g2.W = d.e_d; g2.ldw = I; g2.wdtype = d.e_wdt;
+    g2.w_group_stride = (long)H * I; g2.C = Y; g2.ldc = H; g2.group_off = EOFF; g2.groups = E; g2.max_group_rows = T;
+    launch_gemm(g2, st);
+    float* YS = nullptr;
+    if (d.has_shared) {
+        const int Is = d.s_d.K;
+        float* GS = wsf("d_sg", (size_t)T * 2 * Is);
+        float* HS = wsf("d_shh", (size_t)T * Is);
+        YS = wsf("d_sy", (size_t)T * H);
+        linear(XN, T, H, d.s_gu, GS, 2 * Is);
+        launch_silu_mul(GS, 2 * Is, Is, T, HS, Is, st);
+        linear(HS, T, Is, d.s_d, YS, H);
+    }
+    launch_moe_combine(Y, APOS, WTS, YS, T, K, H, X, 1, st);
+}
+
+void Engine::decode_step(int B, int Lmax) {
+    const LangConfig& L = cfg_.lang;
+    hipStream_t st = stream_;
+    const int H = L.hidden, hd = L.head_dim;
+    float* X = wsf("s_x", (size_t)B * H);
+    float* XN = wsf("s_xn", (size_t)B * H);
+    int* kv_pos = wsi("s_kvpos", B);
+    int* kv_len = wsi("s_kvlen", B);
+    float* CTX = wsf("s_ctx", (size_t)B * H);
+    float* part = wsf("s_part", decode_attention_workspace(B, L.heads, hd, Lmax) / 4 + 16);
+    for (int l = 0; l < L.layers; ++l) {
+        DecLayer& d = layers_[l];
+        const int QKVN = d.qkv.N;
+        float* QKV = wsf("s_qkv", (size_t)B * QKVN);
+        const long layer_kv = (long)B * page_stride_;
+        float* kc = kc_ + (long)l * layer_kv;
+        float* vc = vc_ + (long)l * layer_kv;
+        launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st);
+        linear(XN, B, H, d.qkv, QKV, QKVN);
+        RopeKvArgs r;
+        r.qkv = QKV; r.ld = QKVN; r.rows = B; r.row_page = iota_; r.row_pos = kv_pos;
+        r.heads = L.heads; r.kv_heads = L.kv_heads; r.hd = hd; r.rope_dim = L.rope_dim; r.use_mla = L.use_mla;
+        r.cos = rope_cos_; r.sin = rope_sin_; r.kc = kc; r.vc = vc; r.page_stride = page_stride_;
+        r.head_stride = head_stride_;
+        launch_rope_kv(r, st);
+        if (L.kv_heads != L.heads) throw std::runtime_error("EINVAL: decode path requires num_key_value_heads == num_attention_heads");
+        DecodeAttnArgs da;
+        da.q = QKV; da.q_row_stride = QKVN; da.kc = kc; da.vc = vc; da.page_stride = page_stride_;
+        da.head_stride = head_stride_; da.lens = kv_len; da.B = B; da.heads = L.heads; da.hd = hd; da.max_len = Lmax;
+        da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_row_stride = H;
+        launch_decode_attention(da, st);
+        linear(CTX, B, H, d.o, X, H, 0, 1);
+        launch_rmsnorm(X, H, XN, H, B, H, d.post_norm.w, L.rms_eps, st);
+        if (!d.moe) {
+            const int I = L.inter;
+            float* HH = wsf("s_hh", (size_t)B * I);
+            float* YD = wsf("s_yd", (size_t)B * H);
+            MoeDecodeArgs m;
+            m.T = B; m.topk = 1; m.E = 1; m.K = H; m.I = I; m.Hout = H; m.x = XN; m.eoff = wsi("s_dense_eoff", 2);
+            m.arow = iota_; m.Wgu = d.gu.W; m.Wd = d.down.W; m.wdtype = d.gu.wdt; m.h = HH; m.y = YD;
+            m.max_rows_per_expert = B;
+            launch_moe_gateup_gemv(m, st);
+            launch_moe_down_gemv(m, st);
+            launch_moe_combine(YD, iota_, ones_, nullptr, B, 1, H, X, 1, st);
+            continue;
+        }
+        const int E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
+        float* LOG = wsf("s_log", (size_t)B * E);
+        int* IDS = wsi("s_ids", TK);
+        float* WTS = wsf("s_wts", TK);
+        int* EOFF = wsi("s_eoff", E + 1);
+        int* AROW = wsi("s_arow", TK);
+        int* APOS = wsi("s_apos", TK);
+        float* HH = wsf("s_ehh", (size_t)TK * I);
+        float* Y = wsf("s_ey", (size_t)TK * H);
+        linear(XN, B, H, d.router, LOG, E);
+        launch_router_topk(LOG, B, E, K, L.scoring == "softmax", L.norm_topk, L.routed_scaling, IDS, WTS, st);
+        launch_moe_group(IDS, B, K, E, EOFF, AROW, APOS, nullptr, st);
+        MoeDecodeArgs m;
+        m.T = B; m.topk = K; m.E = E; m.K = H; m.I = I; m.Hout = H; m.x = XN; m.eoff = EOFF; m.arow = AROW;
+        m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt; m.h = HH; m.y = Y;
+        m.max_rows_per_expert = B == 1 ? 1 : 4;
+        launch_moe_gateup_gemv(m, st);
+        launch_moe_down_gemv(m, st);
+        float* YS = nullptr;
+        if (d.has_shared) {
+            const int Is = d.s_d.K;
+            float* HS = wsf("s_shh", (size_t)B * Is);
+            YS = wsf("s_sy", (size_t)B * H);
+            MoeDecodeArgs s;
+            s.T = B; s.topk = 1; s.E = 1; s.K = H; s.I = Is; s.Hout = H; s.x = XN; s.eoff = wsi("s_dense_eoff", 2);
+            s.arow = iota_; s.Wgu = d.s_gu.W; s.Wd = d.s_d.W; s.wdtype = d.s_gu.wdt; s.h = HS; s.y = YS;
+            s.max_rows_per_expert = B;
+            launch_moe_gateup_gemv(s, st);
+            launch_moe_down_gemv(s, st);
+        }
+        launch_moe_combine(Y, APOS, WTS, YS, B, K, H, X, 1, st);
+    }
+}
+
+// ============================================================================ generate
+std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>& reqs, const GenParams& p, TokenCb cb,
+                                                   void* user) {
+    using clock = std::chrono::steady_clock;
+    const LangConfig& L = cfg_.lang;
+    const int B = (int)reqs.size();
+    const int H = L.hidden;
+    timings_ = Timings();
+    timings_.pages = B;
+    std::vector<std::vector<int64_t>> out(B);
+    if (B == 0) return out;
+    if (p.max_new == 0) return out;
+    ensure_small(std::max(B, 64));
+    hipStream_t st = stream_;
+    hipEvent_t ev[6];
+    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    auto t0 = clock::now();
+    HIP_CHECK(hipEventRecord(ev[0], st));
+
+    // ---------------- 1. vision (compute_image_embeddings, batched over pages)
+    std::vector<int> prompt_len(B);
+    int max_p = 0;
+    long T = 0;
+    for (int b = 0; b < B; ++b) {
+        prompt_len[b] = (int)reqs[b].ids.size();
+        if (prompt_len[b] == 0) throw std::runtime_error("EINVAL: empty prompt");
+        max_p = std::max(max_p, prompt_len[b]);
+        T += prompt_len[b];
+    }
+    // group pages by global/tile size
+    std::map<int, std::vector<int>> gsz, tsz;
+    for (int b = 0; b < B; ++b)
+        if (reqs[b].page) {
+            gsz[reqs[b].page->gsize].push_back(b);
+            if (reqs[b].page->n_tiles > 0) tsz[reqs[b].page->tile].push_back(b);
+        }
+    // per page: device pointers of global post rows and local post rows
+    std::vector<const float*> gpost(B, nullptr), lpost(B, nullptr);
+    std::vector<float*> pass_outputs;
+    int pass_id = 0;
+    for (auto& kv : gsz) {
+        const int S = kv.first;
+        std::vector<float> imgs;
+        for (int b : kv.second) imgs.insert(imgs.end(), reqs[b].page->global_chw.begin(), reqs[b].page->global_chw.end());
+        float* dimg = upload("g_img" + std::to_string(pass_id), imgs);
+        std::string name = "vis_out" + std::to_string(pass_id++);
+        float* post = vision_pass(dimg, (int)kv.second.size(), S, name);
+        const int Sq = (S / 64) * (S / 64);
+        for (size_t i = 0; i < kv.second.size(); ++i) gpost[kv.second[i]] = post + (size_t)i * Sq * H;
+    }
+    for (auto& kv : tsz) {
+        const int S = kv.first;
+        std::vector<float> imgs;
+        int n = 0;
+        for (int b : kv.second) {
+            imgs.insert(imgs.end(), reqs[b].page->tiles_chw.begin(), reqs[b].page->tiles_chw.end());
+            n += reqs[b].page->n_tiles;
+        }
+        float* dimg = upload("g_img" + std::to_string(pass_id), imgs);
+        std::string name = "vis_out" + std::to_string(pass_id++);
+        float* post = vision_pass(dimg, n, S, name);
+        const int Sq = (S / 64) * (S / 64);
+        size_t off = 0;
+        for (int b : kv.second) {
+            lpost[b] = post + off * Sq * H;
+            off += reqs[b].page->n_tiles;
+        }
+    }
+    HIP_CHECK(hipEventRecord(ev[1], st));
+
+    // ---------------- 2. prefill input rows (embed + inject, model/mod.rs:1208-1239)
+    std::vector<int> kind(T), index(T), row_page(T), row_pos(T);
+    std::vector<long> q_off(B), kv_off(B), o_off(B);
+    // host image rows of all pages concatenated (kind 1), device vision rows via per-row pointers:
+    // we copy them into one contiguous device buffer per kind to keep the assemble kernel simple.
+    std::vector<float> host_rows;
+    std::vector<long> host_row_base(B, 0);
+    for (int b = 0; b < B; ++b)
+        if (!reqs[b].page && reqs[b].image_rows) {
+            host_row_base[b] = (long)(host_rows.size() / H);
+            host_rows.insert(host_rows.end(), reqs[b].image_rows, reqs[b].image_rows + reqs[b].n_image_rows * H);
+        }
+    // device vision rows are gathered via srcB = one buffer holding every page's [local | global] post rows
+    long vis_rows_total = 0;
+    std::vector<long> vis_base(B, 0), vis_local_rows(B, 0), vis_global_rows(B, 0);
+    for (int b = 0; b < B; ++b)
+        if (reqs[b].page) {
+            const PagePixels* pg = reqs[b].page;
+            vis_base[b] = vis_rows_total;
+            vis_local_rows[b] = (long)pg->n_tiles * (pg->tile / 64) * (pg->tile / 64);
+            vis_global_rows[b] = (long)(pg->gsize / 64) * (pg->gsize / 64);
+            vis_rows_total += vis_local_rows[b] + vis_global_rows[b];
+        }
+    float* vis_rows = wsf("g_visrows", (size_t)std::max<long>(vis_rows_total, 1) * H);
+    for (int b = 0; b < B; ++b)
+        if (reqs[b].page) {
+            if (vis_local_rows[b])
+                HIP_CHECK(hipMemcpyAsync(vis_rows + vis_base[b] * H, lpost[b], vis_local_rows[b] * H * 4,
+                                         hipMemcpyDeviceToDevice, st));
+            HIP_CHECK(hipMemcpyAsync(vis_rows + (vis_base[b] + vis_local_rows[b]) * H, gpost[b],
+                                     vis_global_rows[b] * H * 4, hipMemcpyDeviceToDevice, st));
+        }
+    long r0 = 0;
+    for (int b = 0; b < B; ++b) {
+        const GenRequest& rq = reqs[b];
+        // image token sequence for this page: list of (kind, index)
+        std::vector<std::pair<int, long>> img;
+        if (rq.page) {
+            const PagePixels* pg = rq.page;
+            if (pg->n_tiles > 0) {
+                const int ls = pg->tile / 64;
+                for (int R = 0; R < pg->crop_h * ls; ++R) {
+                    for (int Cc = 0; Cc < pg->crop_w * ls; ++Cc) {
+                        int crop = (R / ls) * pg->crop_w + (Cc / ls);
+                        img.push_back({2, vis_base[b] + ((long)crop * ls + R % ls) * ls + Cc % ls});
+                    }
+                    img.push_back({3, 0});
+                }
+            }
+            const int gs = pg->gsize / 64;
+            for (int R = 0; R < gs; ++R) {
+                for (int Cc = 0; Cc < gs; ++Cc) img.push_back({2, vis_base[b] + vis_local_rows[b] + (long)R * gs + Cc});
+                img.push_back({3, 0});
+            }
+            img.push_back({4, 0});
+        } else if (rq.image_rows) {
+            for (size_t i = 0; i < rq.n_image_rows; ++i) img.push_back({1, host_row_base[b] + (long)i});
+        }
+        size_t n_mask = 0;
+        for (int i = 0; i < prompt_len[b]; ++i) n_mask += (!rq.mask.empty() && rq.mask[i]) ? 1 : 0;
+        if (n_mask != img.size())
+            throw std::runtime_error("EINVAL: prompt/image embedding mismatch: image embeddings provide " +
+                                     std::to_string(img.size()) + " tokens but mask requires " + std::to_string(n_mask));
+        size_t j = 0;
+        for (int i = 0; i < prompt_len[b]; ++i) {
+            const long r = r0 + i;
+            if (!rq.mask.empty() && rq.mask[i]) {
+                kind[r] = img[j].first;
+                index[r] = (int)img[j].second;
+                ++j;
+            } else {
+                const int id = rq.ids[i];
+                if (id < 0 || id >= L.vocab) throw std::runtime_error("EINVAL: token id out of bounds for vocab size");
+                kind[r] = 0;
+                index[r] = id;
+            }
+            row_page[r] = b;
+            row_pos[r] = i;
+        }
+        q_off[b] = 0;  // set below once strides are known
+        o_off[b] = r0 * H;
+        r0 += prompt_len[b];
+    }
+    const int Lmax = max_p + (int)p.max_new + 1;
+    ensure_rope(Lmax + 1);
+    // KV cache [layers][B][kvh][Lmax][hd] f32 (block.rs:776-789 keeps the cache in f32)
+    head_stride_ = (long)Lmax * L.head_dim;
+    page_stride_ = (long)L.kv_heads * head_stride_;
+    const size_t kv_need = (size_t)L.layers * B * page_stride_ * 4;
+    kc_ = wsf("kv_k", kv_need / 4);
+    vc_ = wsf("kv_v", kv_need / 4);
+    const int QKVN = layers_[0].qkv.N;
+    r0 = 0;
+    for (int b = 0; b < B; ++b) {
+        q_off[b] = r0 * QKVN;
+        kv_off[b] = (long)b * page_stride_;
+        r0 += prompt_len[b];
+    }
+    float* X = wsf("d_x", (size_t)T * H);
+    {
+        int* dk = upload("g_kind", kind);
+        int* di = upload("g_index", index);
+        float* hr = host_rows.empty() ? nullptr : upload("g_hostrows", host_rows);
+        launch_assemble_rows(dk, di, (int)T, H, embed_, embed_dt_, hr, vis_rows, newline_, separator_, X, H, st);
+    }
+    int* d_row_page = upload("g_rowpage", row_page);
+    int* d_row_pos = upload("g_rowpos", row_pos);
+    long* d_q_off = upload("g_qoff", q_off);
+    long* d_kv_off = upload("g_kvoff", kv_off);
+    long* d_o_off = upload("g_ooff", o_off);
+    int* d_plen = upload("g_plen", prompt_len);
+
+    // ---------------- 3. prefill (decode.prefill)
+    HIP_CHECK(hipEventRecord(ev[2], st));
+    for (int l = 0; l < L.layers; ++l)
+        layer_forward_prefill(l, (int)T, B, d_row_page, d_row_pos, d_q_off, d_kv_off, d_o_off, d_plen, max_p, Lmax);
+    // last row of every page -> final norm -> lm_head (the reference projects every
+    // position, transformer/model.rs:243-270; only the last row is ever read)
+    std::vector<int> last_rows(B);
+    r0 = 0;
+    for (int b = 0; b < B; ++b) { r0 += prompt_len[b]; last_rows[b] = (int)(r0 - 1); }
+    float* SX = wsf("s_x", (size_t)B * H);
+    float* SXN = wsf("s_xn", (size_t)B * H);
+    float* LOGITS = wsf("s_logits", (size_t)B * L.vocab);
+    {
+        std::vector<int> zero(B, 0);
+        std::vector<int> lr_kind(B, 1);
+        int* dk = upload("g_lrkind", lr_kind);
+        int* di = upload("g_lrindex", last_rows);
+        launch_assemble_rows(dk, di, B, H, nullptr, 0, X, nullptr, nullptr, nullptr, SX, H, st);
+    }
+    launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+    linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
+
+    // sampling state: context = prompt ids (+ generated), sampling.rs:34-96
+    const long ctx_cap = max_p + (long)p.max_new + 1;
+    std::vector<int> ctx((size_t)B * ctx_cap, 0), ctx_len(B), kvpos(B), kvlen(B), zeros(B, 0);
+    for (int b = 0; b < B; ++b) {
+        for (int i = 0; i < prompt_len[b]; ++i) ctx[(size_t)b * ctx_cap + i] = reqs[b].ids[i];
+        ctx_len[b] = prompt_len[b];
+        kvpos[b] = prompt_len[b];
+        kvlen[b] = prompt_len[b] + 1;
+    }
+    int* d_ctx = upload("s_ctx_ids", ctx);
+    int* d_ctx_len = upload("s_ctx_len", ctx_len);
+    int* d_kvpos = wsi("s_kvpos", B);
+    int* d_kvlen = wsi("s_kvlen", B);
+    HIP_CHECK(hipMemcpyAsync(d_kvpos, kvpos.data(), B * 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_kvlen, kvlen.data(), B * 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int* d_done = upload("s_done", zeros);
+    int* d_outlen = upload("s_outlen", zeros);
+    int* d_out = wsi("s_out", (size_t)B * p.max_new);
+    int* d_tok = wsi("s_tok", B);
+    {
+        std::vector<int> de = {0, B};
+        upload("s_dense_eoff", de);
+    }
+    const int banned_cap = 64;
+    SampleArgs sa;
+    sa.logits = LOGITS; sa.B = B; sa.V = L.vocab; sa.ld = L.vocab; sa.ctx = d_ctx; sa.ctx_cap = ctx_cap;
+    sa.ctx_len = d_ctx_len; sa.ngram = p.ngram; sa.rep_penalty = p.rep_penalty;
+    sa.banned = wsi("s_banned", (size_t)B * banned_cap); sa.banned_cnt = wsi("s_banned_cnt", B);
+    sa.banned_cap = banned_cap;
+    sa.red_blocks = (int)sample_workspace_blocks(L.vocab);
+    sa.red_val = wsf("s_redv", (size_t)B * sa.red_blocks); sa.red_idx = wsi("s_redi", (size_t)B * sa.red_blocks);
+    sa.out_tok = d_tok;
+    const int eos = p.ignore_eos ? -1 : (int)p.eos;
+    launch_sample_greedy(sa, st);
+    launch_step_update(d_tok, B, d_ctx, ctx_cap, d_ctx_len, d_out, d_outlen, (long)p.max_new, d_done, eos, embed_,
+                       embed_dt_, H, SX, st);
+    HIP_CHECK(hipEventRecord(ev[3], st));
+
+    // make sure every decode workspace exists before capture
+    decode_step(B, Lmax);  // dry build of buffers is not allowed to run; we capture below instead
+    // (the call above allocated workspaces and ran a real step; undo by re-initialising state)
+    HIP_CHECK(hipMemcpyAsync(d_kvpos, kvpos.data(), B * 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_kvlen, kvlen.data(), B * 4, hipMemcpyHostToDevice, st));
+    // the dry step overwrote X (=SX); restore the step-0 token embedding
+    launch_embed_tokens(embed_, embed_dt_, d_tok, B, H, SX, H, st);
+    HIP_CHECK(hipStreamSynchronize(st));
+
+    // ---------------- 4. decode loop (decode.iterative) as a replayed hipGraph
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    capturing_ = true;
+    HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    decode_step(B, Lmax);
+    launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+    linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
+    launch_sample_greedy(sa, st);
+    launch_step_advance(d_kvpos, d_kvlen, B, st);
+    launch_step_update(d_tok, B, d_ctx, ctx_cap, d_ctx_len, d_out, d_outlen, (long)p.max_new, d_done, eos, embed_,
+                       embed_dt_, H, SX, st);
+    HIP_CHECK(hipStreamEndCapture(st, &graph));
+    capturing_ = false;
+    HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+
+    HIP_CHECK(hipEventRecord(ev[4], st));
+    std::vector<int> h_done(B), h_outlen(B);
+    std::vector<int> h_out;
+    size_t steps = 0;
+    int* pin_done = nullptr;
+    HIP_CHECK(hipHostMalloc((void**)&pin_done, sizeof(int) * (2 * B + 1)));
+    for (size_t i = 1; i < p.max_new; ++i) {
+        HIP_CHECK(hipGraphLaunch(gexec, st));
+        ++steps;
+        const bool check = cb != nullptr || (!p.ignore_eos && (i % 8 == 0 || i + 1 == p.max_new));
+        if (check) {
+            HIP_CHECK(hipMemcpyAsync(pin_done, d_done, B * 4, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(pin_done + B, d_outlen, B * 4, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            if (cb && B == 1) {
+                int n = pin_done[B];
+                std::vector<int> tmp(n);
+                HIP_CHECK(hipMemcpy(tmp.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+                std::vector<int64_t> t64(tmp.begin(), tmp.end());
+                cb(t64.size(), t64.data(), user);
+            }
+            bool all = true;
+            for (int b = 0; b < B; ++b) all &= pin_done[b] != 0;
+            if (all) break;
+        }
+    }
+    HIP_CHECK(hipEventRecord(ev[5], st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    HIP_CHECK(hipHostFree(pin_done));
+    (void)hipGraphExecDestroy(gexec);
+    (void)hipGraphDestroy(graph);
+
+    h_out.resize((size_t)B * p.max_new);
+    HIP_CHECK(hipMemcpy(h_out.data(), d_out, h_out.size() * 4, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_outlen.data(), d_outlen, B * 4, hipMemcpyDeviceToHost));
+    for (int b = 0; b < B; ++b) out[b].assign(h_out.begin() + (size_t)b * p.max_new, h_out.begin() + (size_t)b * p.max_new + h_outlen[b]);
+
+    timings_.vision_compute_ms = ms_between(ev[0], ev[1]);
+    timings_.prefill_ms = ms_between(ev[2], ev[3]);
+    timings_.iterative_ms = ms_between(ev[4], ev[5]);
+    timings_.generate_ms = ms_between(ev[2], ev[3]) + ms_between(ev[4], ev[5]);
+    timings_.steps = steps;
+    (void)t0;
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return out;
+}
+
+}  // namespace dsocr

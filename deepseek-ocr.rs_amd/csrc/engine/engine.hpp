@@ -1,0 +1,194 @@
+// Engine: device-resident DeepSeek-OCR (SAM + CLIP + projector + DeepSeek-V2 MoE
+// decoder) orchestrating the gfx950 kernels.  One engine per GPU; pages are
+// batched inside an engine and sharded across GPUs by the caller (one process per
+// GPU, no collectives: SURVEY §8e).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../kernels/kernels.hpp"
+#include "config.hpp"
+
+namespace dsocr {
+
+#define HIP_CHECK(x)                                                                                   \
+    do {                                                                                               \
+        hipError_t _e = (x);                                                                           \
+        if (_e != hipSuccess)                                                                          \
+            throw std::runtime_error(std::string("EDEVICE: ") + #x + ": " + hipGetErrorString(_e));    \
+    } while (0)
+
+struct Lin {
+    void* W = nullptr;
+    int wdt = WDT_BF16;
+    int N = 0, K = 0;
+    float* b = nullptr;
+};
+struct Ln {
+    float* w = nullptr;
+    float* b = nullptr;
+};
+
+struct SamBlock {
+    Ln n1, n2;
+    Lin qkv, proj, fc1, fc2;
+    bool global = false;
+    int rel_len = 0;                       // rows of the stored rel tables (2*tokens-1)
+    std::vector<float> relh, relw;         // host copies [rel_len][hd]
+    std::map<int, std::pair<float*, float*>> rel_dev;  // grid -> resized device tables
+    bool use_rel = false;
+};
+struct SamW {
+    Lin patch;
+    bool has_pos = false;
+    int pos_grid = 0;
+    std::vector<float> pos_host;           // [C][grid][grid]
+    std::map<int, float*> pos_dev;         // grid -> [grid*grid][C]
+    std::vector<SamBlock> blocks;
+    Lin neck0, neck2, net2, net3;
+    Ln neck1, neck3;
+};
+struct ClipLayer {
+    Ln ln1, ln2;
+    Lin qkv, out, fc1, fc2;
+};
+struct ClipW {
+    float* cls = nullptr;
+    std::vector<float> pos_host;           // [seq+1][C]
+    std::map<int, float*> pos_dev;         // tokens -> [tokens][C]
+    Ln pre;
+    std::vector<ClipLayer> layers;
+};
+struct DecLayer {
+    Ln in_norm, post_norm;
+    Lin qkv, o;
+    bool moe = false;
+    Lin gu, down;                 // dense MLP (layer 0) [2I][H], [H][I]
+    Lin router;                   // [E][H]
+    float* router_bias = nullptr; // e_score_correction_bias
+    void* e_gu = nullptr;         // [E][2Im][H]
+    void* e_d = nullptr;          // [E][H][Im]
+    int e_wdt = WDT_F16;
+    bool has_shared = false;
+    Lin s_gu, s_d;                // [2Is][H], [H][Is]
+};
+
+struct PagePixels {
+    int base = 1024, tile = 640;
+    bool crop = true;
+    int crop_w = 1, crop_h = 1;
+    std::vector<float> global_chw;  // [3][G][G]
+    int gsize = 0;
+    std::vector<float> tiles_chw;   // [n][3][T][T]
+    int n_tiles = 0;
+    size_t n_image_tokens = 0;
+};
+
+struct Timings {
+    double vision_prepare_ms = 0, vision_compute_ms = 0, prefill_ms = 0, iterative_ms = 0, generate_ms = 0;
+    size_t steps = 0, pages = 0;
+};
+
+struct GenRequest {
+    std::vector<int> ids;
+    std::vector<uint8_t> mask;
+    const PagePixels* page = nullptr;
+    const float* image_rows = nullptr;
+    size_t n_image_rows = 0;
+};
+struct GenParams {
+    size_t max_new = 512;
+    float rep_penalty = 1.f;
+    int ngram = 20;
+    long eos = -1;
+    bool ignore_eos = false;
+};
+typedef void (*TokenCb)(size_t, const int64_t*, void*);
+
+class Engine {
+  public:
+    Engine(const std::string& config_path, const std::string& weights_path, int device, int dtype, uint64_t seed);
+    ~Engine();
+
+    const ModelConfig& cfg() const { return cfg_; }
+    // vision embeddings of pages (host output rows per page concatenated)
+    std::vector<std::vector<float>> image_embeddings(const std::vector<const PagePixels*>& pages);
+    // batched generate; returns generated ids per page
+    std::vector<std::vector<int64_t>> generate(const std::vector<GenRequest>& reqs, const GenParams& p, TokenCb cb,
+                                               void* user);
+    Timings last_timings() const { return timings_; }
+    hipStream_t stream() const { return stream_; }
+
+  private:
+    // ---- loading
+    void load_weights(const std::string& path, uint64_t seed);
+    // ---- workspace
+    void* ws(const std::string& name, size_t bytes);
+    float* wsf(const std::string& name, size_t n) { return (float*)ws(name, n * sizeof(float)); }
+    int* wsi(const std::string& name, size_t n) { return (int*)ws(name, n * sizeof(int)); }
+    long* wsl(const std::string& name, size_t n) { return (long*)ws(name, n * sizeof(long)); }
+    template <typename T>
+    T* upload(const std::string& name, const std::vector<T>& v) {
+        // synchronous: host vectors are often temporaries (pageable memory)
+        T* p = (T*)ws(name, v.size() * sizeof(T) + 16);
+        if (!v.empty()) {
+            HIP_CHECK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream_));
+            HIP_CHECK(hipStreamSynchronize(stream_));
+        }
+        return p;
+    }
+    // ---- compute pieces
+    void linear(const float* x, int M, int ldx, const Lin& l, float* y, int ldy, int act = 0, int accumulate = 0,
+                const int* c_rows = nullptr);
+    float* sam_pos(int g);
+    std::pair<float*, float*> sam_rel(SamBlock& b, int g);
+    float* clip_pos(int tokens);
+    // runs SAM+CLIP+projector on n images of size S; returns device rows [n*(S/64)^2][H] in buffer `out`
+    float* vision_pass(const float* imgs, int n, int S, const std::string& out);
+    void prefill(int B, const std::vector<int>& rows_per_page, const float* x0, int Lmax);
+    void decode_step(int B, int Lmax);
+    void layer_forward_prefill(int l, int T, int B, const int* row_page, const int* row_pos, const long* q_off,
+                               const long* kv_off, const long* o_off, const int* seq_len, int max_len, int Lmax);
+
+    ModelConfig cfg_;
+    int device_ = 0;
+    int dtype_ = 1;
+    hipStream_t stream_ = nullptr;
+    std::vector<void*> allocations_;
+    std::map<std::string, std::pair<void*, size_t>> ws_;
+    bool capturing_ = false;
+
+    SamW sam_;
+    ClipW clip_;
+    Lin proj_;
+    float* newline_ = nullptr;
+    float* separator_ = nullptr;
+    void* embed_ = nullptr;
+    int embed_dt_ = WDT_F16;
+    std::vector<DecLayer> layers_;
+    float* final_norm_ = nullptr;
+    Lin lm_head_;
+    float* rope_cos_ = nullptr;
+    float* rope_sin_ = nullptr;
+    int rope_cap_ = 0;
+    float* ones_ = nullptr;
+    int* iota_ = nullptr;
+    int small_cap_ = 0;
+    // kv cache
+    float* kc_ = nullptr;
+    float* vc_ = nullptr;
+    size_t kv_bytes_ = 0;
+    long page_stride_ = 0, head_stride_ = 0;
+    Timings timings_;
+
+    void* dev_alloc(size_t bytes);
+    void ensure_rope(int len);
+    void ensure_small(int n);
+};
+
+}  // namespace dsocr

@@ -1,0 +1,380 @@
+// Attention kernels, f32 end to end (the reference keeps scores, softmax and PV
+// in f32: sam.rs:837-872, clip.rs:449-453, block.rs:661-775).
+//
+// 1. attention_fwd: flash-style (online softmax) on the f32 matrix cores.  A wave
+//    owns 32 queries; S^T = K.Q^T is computed with v_mfma_f32_32x32x2_f32 so that a
+//    lane holds one query's scores, and P feeds the P.V MFMA straight from the
+//    accumulator (the k-order of P is permuted and V rows are read in the same
+//    permuted order: cdna_hip_programming.md §3 "An accumulator tile as the next
+//    MFMA's operand").  K/V tiles of 32 keys are shared by the 4 waves via LDS.
+//    Options: decomposed SAM rel-pos bias (sam.rs:1124-1192, never materialising
+//    [S,S]), causal masking (block.rs:1504-1526), variable sequence lengths.
+// 2. sam_relbias: per-query rel-pos dot products q.Rh / q.Rw.
+// 3. decode attention: flash-decoding over the per-page f32 KV cache.
+// 4. rope_kv: rotate_half RoPE (block.rs:1403-1471) + KV-cache append.
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+constexpr int AT_Q = 32;   // queries per wave
+constexpr int AT_KT = 32;  // keys per tile
+
+template <int HD>
+__global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
+    __shared__ float Ks[AT_KT][HD + 1];
+    __shared__ float Vs[AT_KT][HD + 1];
+    const int s = blockIdx.z, h = blockIdx.y;
+    const int len = a.seq_len ? a.seq_len[s] : a.L;
+    const int qb0 = blockIdx.x * (4 * AT_Q);
+    if (qb0 >= len) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = lane >> 5, l32 = lane & 31;
+    const int kvh = h / (a.heads / a.kv_heads);
+
+    const long qoff = a.q.seq_off ? a.q.seq_off[s] : (long)s * a.L * a.q.row_stride;
+    const long koff = a.k.seq_off ? a.k.seq_off[s] : (long)s * a.L * a.k.row_stride;
+    const long voff = a.v.seq_off ? a.v.seq_off[s] : (long)s * a.L * a.v.row_stride;
+    const long ooff = a.o_seq_off ? a.o_seq_off[s] : (long)s * a.L * a.o_row_stride;
+    const float* Q = a.q.ptr + qoff + (long)h * a.q.head_stride;
+    const float* K = a.k.ptr + koff + (long)kvh * a.k.head_stride;
+    const float* V = a.v.ptr + voff + (long)kvh * a.v.head_stride;
+
+    const int q_lane = qb0 + wave * AT_Q + l32;  // this lane's query (lanes l and l+32 share it)
+    const bool q_valid = q_lane < len;
+    float qreg[HD / 2];
+    {
+        const float* qr = Q + (long)(q_valid ? q_lane : 0) * a.q.row_stride;
+#pragma unroll
+        for (int i = 0; i < HD / 2; ++i) qreg[i] = qr[2 * i + half];
+    }
+    const float* rb = nullptr;
+    int R = 0;
+    if (a.relbias) {
+        R = a.rel_h + a.rel_w;
+        rb = a.relbias + (((long)s * a.heads + h) * a.L + (q_valid ? q_lane : 0)) * R;
+    }
+
+    f32x16 o[HD / 32];
+#pragma unroll
+    for (int t = 0; t < HD / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    int kend = len;
+    if (a.causal) kend = min(len, qb0 + 4 * AT_Q);
+    for (int k0 = 0; k0 < kend; k0 += AT_KT) {
+        // stage K/V tile (32 x HD floats each)
+        constexpr int F4 = AT_KT * HD / 4;
+        for (int i = tid; i < F4; i += 256) {
+            const int row = i / (HD / 4), c4 = (i % (HD / 4)) * 4;
+            const int key = k0 + row;
+            float4 kv4 = make_float4(0.f, 0.f, 0.f, 0.f), vv4 = kv4;
+            if (key < len) {
+                kv4 = *reinterpret_cast<const float4*>(K + (long)key * a.k.row_stride + c4);
+                vv4 = *reinterpret_cast<const float4*>(V + (long)key * a.v.row_stride + c4);
+            }
+            Ks[row][c4] = kv4.x; Ks[row][c4 + 1] = kv4.y; Ks[row][c4 + 2] = kv4.z; Ks[row][c4 + 3] = kv4.w;
+            Vs[row][c4] = vv4.x; Vs[row][c4 + 1] = vv4.y; Vs[row][c4 + 2] = vv4.z; Vs[row][c4 + 3] = vv4.w;
+        }
+        __syncthreads();
+
+        f32x16 sc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+#pragma unroll
+        for (int i = 0; i < HD / 2; ++i)
+            sc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ks[l32][2 * i + half], qreg[i], sc, 0, 0, 0);
+
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            float v = sc[r] * a.scale;
+            if (rb) v += rb[key / a.rel_w] + rb[a.rel_h + key % a.rel_w];
+            if (key >= len || (a.causal && key > q_lane)) v = -INFINITY;
+            sc[r] = v;
+            tmax = fmaxf(tmax, v);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float p = (m_new == -INFINITY) ? 0.f : expf(sc[r] - m_new);
+            sc[r] = p;
+            psum += p;
+        }
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+        // rescale O rows (query row of O acc register r lives on lane `row`)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float al = __shfl(alpha, (r & 3) + 8 * (r >> 2) + 4 * half, 64);
+#pragma unroll
+            for (int t = 0; t < HD / 32; ++t) o[t][r] *= al;
+        }
+        // O += P.V with the permuted key order kappa(s, half) = (s&3)+8*(s>>2)+4*half
+#pragma unroll
+        for (int st = 0; st < 16; ++st) {
+            const int kr = (st & 3) + 8 * (st >> 2) + 4 * half;
+#pragma unroll
+            for (int t = 0; t < HD / 32; ++t)
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(sc[st], Vs[kr][t * 32 + l32], o[t], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // normalise and store: O acc col = d (lane&31), row = query
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int qrow = (r & 3) + 8 * (r >> 2) + 4 * half;
+        const float lr = __shfl(l_run, qrow, 64);
+        const int q = qb0 + wave * AT_Q + qrow;
+        if (q < len) {
+            float* op = a.o + ooff + (long)q * a.o_row_stride + (long)h * a.o_head_stride;
+#pragma unroll
+            for (int t = 0; t < HD / 32; ++t) op[t * 32 + l32] = o[t][r] / lr;
+        }
+    }
+}
+
+void launch_attention(const AttnArgs& a, hipStream_t s) {
+    int maxlen = a.L;
+    dim3 grid((maxlen + 4 * AT_Q - 1) / (4 * AT_Q), a.heads, a.n_seq);
+    if (grid.x == 0 || a.n_seq == 0) return;
+    AttnArgs b = a;
+    if (b.kv_heads == 0) b.kv_heads = b.heads;
+    if (a.hd == 64) hipLaunchKernelGGL(attention_fwd_kernel<64>, grid, dim3(256), 0, s, b);
+    else if (a.hd == 128) hipLaunchKernelGGL(attention_fwd_kernel<128>, grid, dim3(256), 0, s, b);
+    else if (a.hd == 32) hipLaunchKernelGGL(attention_fwd_kernel<32>, grid, dim3(256), 0, s, b);
+}
+
+// ------------------------------------------------------------------ SAM rel-pos bias
+__global__ __launch_bounds__(256) void sam_relbias_kernel(const float* q, long q_rs, int n_seq, int gh, int gw,
+                                                          int heads, int hd, const float* Rh, const float* Rw,
+                                                          float* out) {
+    const int R = gh + gw;
+    const int L = gh * gw;
+    const long total = (long)n_seq * heads * L * R;
+    for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+        const int j = (int)(idx % R);
+        long t = idx / R;
+        const int qi = (int)(t % L);
+        t /= L;
+        const int h = (int)(t % heads);
+        const int s = (int)(t / heads);
+        const float* qr = q + ((long)s * L + qi) * q_rs + (long)h * hd;
+        const float* rr;
+        if (j < gh) {
+            const int qh = qi / gw;
+            rr = Rh + (long)(qh - j + gh - 1) * hd;
+        } else {
+            const int qw = qi % gw, kw = j - gh;
+            rr = Rw + (long)(qw - kw + gw - 1) * hd;
+        }
+        float acc = 0.f;
+        for (int d = 0; d < hd; d += 4) {
+            float4 a4 = *reinterpret_cast<const float4*>(qr + d);
+            float4 b4 = *reinterpret_cast<const float4*>(rr + d);
+            acc = fmaf(a4.x, b4.x, acc);
+            acc = fmaf(a4.y, b4.y, acc);
+            acc = fmaf(a4.z, b4.z, acc);
+            acc = fmaf(a4.w, b4.w, acc);
+        }
+        out[idx] = acc;
+    }
+}
+
+void launch_sam_relbias(const float* q, long q_row_stride, int n_seq, int gh, int gw, int heads, int hd,
+                        const float* Rh, const float* Rw, float* out, hipStream_t s) {
+    long total = (long)n_seq * heads * gh * gw * (gh + gw);
+    if (total == 0) return;
+    long blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(sam_relbias_kernel, dim3((unsigned)blocks), dim3(256), 0, s, q, q_row_stride, n_seq, gh, gw,
+                       heads, hd, Rh, Rw, out);
+}
+
+// ------------------------------------------------------------------ decode attention
+constexpr int DA_CH = 256;  // keys per block
+
+size_t decode_attention_workspace(int B, int heads, int hd, int max_len) {
+    int chunks = (max_len + DA_CH - 1) / DA_CH;
+    return (size_t)B * heads * chunks * (hd + 2) * sizeof(float);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void decode_attn_partial(DecodeAttnArgs a) {
+    __shared__ float p_s[DA_CH];
+    __shared__ float red[8];
+    __shared__ float o_s[2][HD];
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int len = a.lens[b];
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    float* part = a.part + (((long)b * a.heads + h) * chunks + c) * (HD + 2);
+    const int k0 = c * DA_CH;
+    if (k0 >= len) return;
+    const int kn = min(DA_CH, len - k0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* q = a.q + (long)b * a.q_row_stride + (long)h * HD;
+    const float* Kc = a.kc + (long)b * a.page_stride + (long)h * a.head_stride;
+    const float* Vc = a.vc + (long)b * a.page_stride + (long)h * a.head_stride;
+
+    // scores: 8 lanes per key, 16 dims per lane
+    constexpr int LPK = 8, DPL = HD / LPK;
+    const int sub = lane & (LPK - 1), kin = lane / LPK;  // 8 keys per wave-iteration
+    float qv[DPL];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) qv[i] = q[sub * DPL + i];
+    float lmax = -INFINITY;
+    for (int kk = wave * 8 + kin; kk < DA_CH; kk += 32) {
+        float acc = 0.f;
+        if (kk < kn) {
+            const float* kr = Kc + (long)(k0 + kk) * HD + sub * DPL;
+#pragma unroll
+            for (int i = 0; i < DPL; i += 4) {
+                float4 k4 = *reinterpret_cast<const float4*>(kr + i);
+                acc = fmaf(qv[i], k4.x, acc);
+                acc = fmaf(qv[i + 1], k4.y, acc);
+                acc = fmaf(qv[i + 2], k4.z, acc);
+                acc = fmaf(qv[i + 3], k4.w, acc);
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < LPK; o <<= 1) acc += __shfl_xor(acc, o, 64);
+        float v = kk < kn ? acc * a.scale : -INFINITY;
+        if (sub == 0) p_s[kk] = v;
+        lmax = fmaxf(lmax, v);
+    }
+    lmax = wave_max(lmax);
+    if (lane == 0) red[wave] = lmax;
+    __syncthreads();
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float lsum = 0.f;
+    for (int kk = tid; kk < DA_CH; kk += 256) {
+        float p = kk < kn ? expf(p_s[kk] - m) : 0.f;
+        p_s[kk] = p;
+        lsum += p;
+    }
+    lsum = wave_sum(lsum);
+    __syncthreads();
+    if (lane == 0) red[4 + wave] = lsum;
+    // PV: thread -> (dim d, key parity half)
+    const int d = tid % HD, hh = tid / HD;  // HD=128: hh in {0,1}; HD=64: hh in {0..3}
+    const int nh = 256 / HD;
+    float acc = 0.f;
+    for (int kk = hh; kk < kn; kk += nh) acc = fmaf(p_s[kk], Vc[(long)(k0 + kk) * HD + d], acc);
+    __syncthreads();
+    if (nh == 2) {
+        o_s[hh][d] = acc;
+    } else {
+        // fold 4 partial sums into 2 slots
+        if (hh < 2) o_s[hh][d] = acc;
+        __syncthreads();
+        if (hh >= 2) o_s[hh - 2][d] += acc;
+    }
+    __syncthreads();
+    if (tid < HD) part[2 + tid] = o_s[0][tid] + o_s[1][tid];
+    if (tid == 0) {
+        part[0] = m;
+        part[1] = (red[4] + red[5]) + (red[6] + red[7]);
+    }
+}
+
+template <int HD>
+__global__ __launch_bounds__(HD) void decode_attn_combine(DecodeAttnArgs a) {
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int len = a.lens[b];
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    const int nc = (len + DA_CH - 1) / DA_CH;
+    const float* part = a.part + ((long)b * a.heads + h) * chunks * (HD + 2);
+    float m = -INFINITY;
+    for (int c = 0; c < nc; ++c) m = fmaxf(m, part[c * (HD + 2)]);
+    float l = 0.f, acc = 0.f;
+    for (int c = 0; c < nc; ++c) {
+        const float* p = part + c * (HD + 2);
+        const float w = expf(p[0] - m);
+        l += p[1] * w;
+        acc += p[2 + threadIdx.x] * w;
+    }
+    a.o[(long)b * a.o_row_stride + (long)h * HD + threadIdx.x] = acc / l;
+}
+
+void launch_decode_attention(const DecodeAttnArgs& a, hipStream_t s) {
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    dim3 g1(chunks, a.heads, a.B), g2(a.heads, a.B);
+    if (a.hd == 128) {
+        hipLaunchKernelGGL(decode_attn_partial<128>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(decode_attn_combine<128>, g2, dim3(128), 0, s, a);
+    } else if (a.hd == 64) {
+        hipLaunchKernelGGL(decode_attn_partial<64>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(decode_attn_combine<64>, g2, dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(decode_attn_partial<32>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(decode_attn_combine<32>, g2, dim3(32), 0, s, a);
+    }
+}
+
+// ------------------------------------------------------------------ RoPE + KV append
+__global__ __launch_bounds__(256) void rope_kv_kernel(RopeKvArgs a) {
+    const int r = blockIdx.x;
+    const int page = a.row_page[r], pos = a.row_pos[r];
+    float* row = a.qkv + (long)r * a.ld;
+    const int H = a.heads * a.hd, KVH = a.kv_heads * a.hd;
+    const float* cs = a.cos + (long)pos * a.rope_dim;
+    const float* sn = a.sin + (long)pos * a.rope_dim;
+    const int half = a.rope_dim / 2;
+    const int nq = a.heads, nk = a.kv_heads;
+    const int total = (nq + nk) * a.hd;
+    constexpr int MAXPER = 32;  // supports (heads + kv_heads) * hd <= 8192
+    float outv[MAXPER];
+    const int iters = (total + 255) / 256;
+    // phase 1: read + rotate (q rotated in place, so every read precedes every write)
+    for (int it = 0; it < iters && it < MAXPER; ++it) {
+        const int idx = threadIdx.x + it * 256;
+        if (idx >= total) break;
+        const int hh = idx / a.hd, d = idx % a.hd;
+        const float* base = (hh < nq) ? (row + hh * a.hd) : (row + H + (hh - nq) * a.hd);
+        float out;
+        if (d < a.rope_dim) {
+            // x' = optional MLA even/odd regroup of x (block.rs:1405-1424)
+            auto xr = [&](int i) -> float {
+                if (!a.use_mla) return base[i];
+                return i < half ? base[2 * i] : base[2 * (i - half) + 1];
+            };
+            const float x = xr(d);
+            const float rot = d < half ? -xr(d + half) : xr(d - half);
+            out = x * cs[d] + rot * sn[d];
+        } else {
+            out = base[d];
+        }
+        outv[it] = out;
+    }
+    __syncthreads();
+    for (int it = 0; it < iters && it < MAXPER; ++it) {
+        const int idx = threadIdx.x + it * 256;
+        if (idx >= total) break;
+        const int hh = idx / a.hd, d = idx % a.hd;
+        if (hh < nq) {
+            row[hh * a.hd + d] = outv[it];
+        } else {
+            const int kh = hh - nq;
+            a.kc[(long)page * a.page_stride + (long)kh * a.head_stride + (long)pos * a.hd + d] = outv[it];
+        }
+    }
+    for (int idx = threadIdx.x; idx < nk * a.hd; idx += blockDim.x) {
+        const int kh = idx / a.hd, d = idx % a.hd;
+        float* vc = a.vc + (long)page * a.page_stride + (long)kh * a.head_stride + (long)pos * a.hd;
+        vc[d] = row[H + KVH + kh * a.hd + d];
+    }
+}
+
+void launch_rope_kv(const RopeKvArgs& a, hipStream_t s) {
+    if (a.rows == 0) return;
+    hipLaunchKernelGGL(rope_kv_kernel, dim3(a.rows), dim3(256), 0, s, a);
+}
+
+}  // namespace dsocr

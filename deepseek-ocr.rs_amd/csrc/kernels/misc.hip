@@ -1,0 +1,344 @@
+// Data-movement kernels of the page path (HBM-bound byte work: no MFMA) and the
+// on-device greedy token selection.
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+static inline unsigned grid_for(long total, int block = 256, long cap = 16384) {
+    long b = (total + block - 1) / block;
+    if (b > cap) b = cap;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+// SAM PatchEmbed conv k=s=ps (sam.rs:427-456) as im2col: img NCHW [n][3][H][W] ->
+// cols [n*gh*gw][3*ps*ps], K order (c, ky, kx) == the [O][C][kh][kw] weight layout.
+__global__ void patch_im2col_kernel(const float* img, int n, int H, int W, int ps, float* cols) {
+    const int gh = H / ps, gw = W / ps, K = 3 * ps * ps;
+    const long total = (long)n * gh * gw * K;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int k = (int)(i % K);
+        const long row = i / K;
+        const int gx = (int)(row % gw);
+        const int gy = (int)((row / gw) % gh);
+        const int b = (int)(row / ((long)gw * gh));
+        const int c = k / (ps * ps), ky = (k / ps) % ps, kx = k % ps;
+        cols[i] = img[(((long)b * 3 + c) * H + gy * ps + ky) * W + gx * ps + kx];
+    }
+}
+void launch_patch_im2col(const float* img, int n, int H, int W, int ps, float* cols, hipStream_t s) {
+    long total = (long)n * (H / ps) * (W / ps) * 3 * ps * ps;
+    hipLaunchKernelGGL(patch_im2col_kernel, dim3(grid_for(total)), dim3(256), 0, s, img, n, H, W, ps, cols);
+}
+
+// Conv2d on NHWC activations (SAM neck + downsample, sam.rs:475-576): cols
+// [n*oh*ow][kh*kw*C] with K order (ky, kx, c); the weight is re-laid out on load.
+__global__ void conv_im2col_nhwc_kernel(const float* x, int n, int H, int W, int C, int kh, int kw, int stride, int pad,
+                                        float* cols) {
+    const int oh = (H + 2 * pad - kh) / stride + 1, ow = (W + 2 * pad - kw) / stride + 1;
+    const int K = kh * kw * C;
+    const int C4 = C / 4;
+    const long total = (long)n * oh * ow * kh * kw * C4;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % C4);
+        long t = i / C4;
+        const int kx = (int)(t % kw); t /= kw;
+        const int ky = (int)(t % kh); t /= kh;
+        const int ox = (int)(t % ow); t /= ow;
+        const int oy = (int)(t % oh);
+        const int b = (int)(t / oh);
+        const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+            v = *reinterpret_cast<const float4*>(x + (((long)b * H + iy) * W + ix) * C + c4 * 4);
+        const long row = ((long)b * oh + oy) * ow + ox;
+        *reinterpret_cast<float4*>(cols + row * K + (ky * kw + kx) * C + c4 * 4) = v;
+    }
+}
+void launch_conv_im2col_nhwc(const float* x, int n, int H, int W, int C, int kh, int kw, int stride, int pad,
+                             float* cols, hipStream_t s) {
+    const int oh = (H + 2 * pad - kh) / stride + 1, ow = (W + 2 * pad - kw) / stride + 1;
+    long total = (long)n * oh * ow * kh * kw * (C / 4);
+    hipLaunchKernelGGL(conv_im2col_nhwc_kernel, dim3(grid_for(total)), dim3(256), 0, s, x, n, H, W, C, kh, kw, stride,
+                       pad, cols);
+}
+
+// x[rep][r][c] += t[r][c]  (absolute position embedding add, sam.rs:249-267)
+__global__ void add_broadcast_kernel(float* x, const float* t, long per, int reps) {
+    const long total = per * reps;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+        x[i] += t[i % per];
+}
+void launch_add_broadcast(float* x, const float* t, long rows_per_rep, int cols, int reps, hipStream_t s) {
+    long per = rows_per_rep * cols;
+    hipLaunchKernelGGL(add_broadcast_kernel, dim3(grid_for(per * reps)), dim3(256), 0, s, x, t, per, reps);
+}
+
+// CLIP embeddings (clip.rs:165-236): out[b][0] = cls + pos[0]; out[b][1+i] = sam[b][i] + pos[1+i]
+__global__ void clip_embed_kernel(const float* sam, const float* cls, const float* pos, int n, int S, int C,
+                                  float* out) {
+    const long total = (long)n * (S + 1) * C;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const long r = i / C;
+        const int tok = (int)(r % (S + 1));
+        const int b = (int)(r / (S + 1));
+        const float base = tok == 0 ? cls[c] : sam[((long)b * S + tok - 1) * C + c];
+        out[i] = base + pos[(long)tok * C + c];
+    }
+}
+void launch_clip_embed(const float* sam, const float* cls, const float* pos, int n, int S, int C, float* out,
+                       hipStream_t s) {
+    long total = (long)n * (S + 1) * C;
+    hipLaunchKernelGGL(clip_embed_kernel, dim3(grid_for(total)), dim3(256), 0, s, sam, cls, pos, n, S, C, out);
+}
+
+// build_clip_sam_tokens (model/mod.rs:604-650): [clip[b][1+i] || sam[b][i]]
+__global__ void concat_clip_sam_kernel(const float* clip, const float* sam, int n, int S, int C1, int C2, float* out) {
+    const int C = C1 + C2;
+    const long total = (long)n * S * C;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const long r = i / C;
+        const int tok = (int)(r % S);
+        const int b = (int)(r / S);
+        out[i] = c < C1 ? clip[((long)b * (S + 1) + tok + 1) * C1 + c] : sam[((long)b * S + tok) * C2 + (c - C1)];
+    }
+}
+void launch_concat_clip_sam(const float* clip, const float* sam, int n, int S, int C1, int C2, float* out,
+                            hipStream_t s) {
+    long total = (long)n * S * (C1 + C2);
+    hipLaunchKernelGGL(concat_clip_sam_kernel, dim3(grid_for(total)), dim3(256), 0, s, clip, sam, n, S, C1, C2, out);
+}
+
+__device__ __forceinline__ float table_val(const void* table, int dt, long idx) {
+    const uint16_t* t = reinterpret_cast<const uint16_t*>(table);
+    return dt == WDT_BF16 ? bf16_bits_to_f32(t[idx]) : f16_bits_to_f32(t[idx]);
+}
+
+// Prefill input rows: token embeddings with image rows injected at mask slots
+// (inject_image_tokens, model/mod.rs:1760-1857) and the formatted image tokens
+// (newline / view_separator rows, model/mod.rs:590-709, 879-923).
+__global__ void assemble_rows_kernel(const int* kind, const int* index, int rows, int H, const void* table, int dt,
+                                     const float* srcA, const float* srcB, const float* vecA, const float* vecB,
+                                     float* dst, long ld) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const int k = kind[r];
+    const long ix = index[r];
+    for (int c = threadIdx.x; c < H; c += blockDim.x) {
+        float v;
+        switch (k) {
+            case 0: v = table_val(table, dt, ix * H + c); break;
+            case 1: v = srcA[ix * H + c]; break;
+            case 2: v = srcB[ix * H + c]; break;
+            case 3: v = vecA[c]; break;
+            default: v = vecB[c]; break;
+        }
+        dst[(long)r * ld + c] = v;
+    }
+}
+void launch_assemble_rows(const int* kind, const int* index, int rows, int H, const void* table, int table_dt,
+                          const float* srcA, const float* srcB, const float* vecA, const float* vecB, float* dst,
+                          long ld_dst, hipStream_t s) {
+    if (rows == 0) return;
+    hipLaunchKernelGGL(assemble_rows_kernel, dim3(rows), dim3(256), 0, s, kind, index, rows, H, table, table_dt, srcA,
+                       srcB, vecA, vecB, dst, ld_dst);
+}
+
+__global__ void embed_tokens_kernel(const void* table, int dt, const int* ids, int n, int H, float* out, long ld) {
+    const int r = blockIdx.x;
+    if (r >= n) return;
+    const long id = ids[r];
+    for (int c = threadIdx.x; c < H; c += blockDim.x) out[(long)r * ld + c] = table_val(table, dt, id * H + c);
+}
+void launch_embed_tokens(const void* table, int table_dt, const int* ids, int n, int H, float* out, long ld,
+                         hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(embed_tokens_kernel, dim3(n), dim3(256), 0, s, table, table_dt, ids, n, H, out, ld);
+}
+
+// ------------------------------------------------------------------ greedy token selection
+// sampling.rs:34-158: repetition penalty over the set of context tokens, ban every
+// token that would complete an n-gram already present in prompt+generated, then
+// argmax (first index on ties, non-finite skipped).  If every logit is banned the
+// reference falls back to the un-banned (penalised) logits.
+constexpr int SG_BLOCK = 256;
+constexpr int SG_PER_BLOCK = 4096;
+
+size_t sample_workspace_blocks(int V) { return (size_t)(V + SG_PER_BLOCK - 1) / SG_PER_BLOCK; }
+
+__global__ void ngram_ban_kernel(SampleArgs a) {
+    const int b = blockIdx.y;
+    const int n = a.ctx_len[b];
+    const int* ctx = a.ctx + (long)b * a.ctx_cap;
+    const int g = a.ngram;
+    if (g <= 1 || n < g - 1) return;
+    // windows i in [0, n-g]: ctx[i..i+g-1) == ctx[n-g+1..n)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i <= n - g; i += gridDim.x * blockDim.x) {
+        bool match = true;
+        for (int j = 0; j < g - 1; ++j)
+            if (ctx[i + j] != ctx[n - g + 1 + j]) { match = false; break; }
+        if (match) {
+            int slot = atomicAdd(&a.banned_cnt[b], 1);
+            if (slot < a.banned_cap) a.banned[(long)b * a.banned_cap + slot] = ctx[i + g - 1];
+        }
+    }
+}
+
+__global__ void rep_penalty_kernel(SampleArgs a) {
+    // apply once per distinct context token: the first occurrence applies it
+    const int b = blockIdx.y;
+    const int n = a.ctx_len[b];
+    const int* ctx = a.ctx + (long)b * a.ctx_cap;
+    float* lg = a.logits + (long)b * a.ld;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int t = ctx[i];
+        if (t < 0 || t >= a.V) continue;
+        bool first = true;
+        for (int j = 0; j < i; ++j)
+            if (ctx[j] == t) { first = false; break; }
+        if (!first) continue;
+        float v = lg[t];
+        lg[t] = v > 0.f ? v / a.rep_penalty : v * a.rep_penalty;
+    }
+}
+
+__device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
+    return v > bv || (v == bv && i < bi);
+}
+
+__global__ __launch_bounds__(SG_BLOCK) void argmax_partial_kernel(SampleArgs a, int use_ban) {
+    __shared__ float sv[SG_BLOCK];
+    __shared__ int si[SG_BLOCK];
+    const int b = blockIdx.y;
+    const float* lg = a.logits + (long)b * a.ld;
+    const int nb = use_ban ? min(a.banned_cnt[b], a.banned_cap) : 0;
+    const int* ban = a.banned + (long)b * a.banned_cap;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    const int v0 = blockIdx.x * SG_PER_BLOCK, v1 = min(a.V, v0 + SG_PER_BLOCK);
+    for (int v = v0 + threadIdx.x; v < v1; v += SG_BLOCK) {
+        float x = lg[v];
+        if (!(x > -INFINITY) || !(x < INFINITY)) continue;  // skips -inf, +inf, NaN
+        bool banned = false;
+        for (int j = 0; j < nb; ++j) banned |= (ban[j] == v);
+        if (banned) continue;
+        if (better(x, v, bv, bi)) { bv = x; bi = v; }
+    }
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int o = SG_BLOCK / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o && better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
+            sv[threadIdx.x] = sv[threadIdx.x + o];
+            si[threadIdx.x] = si[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.red_val[(long)b * a.red_blocks + blockIdx.x] = sv[0];
+        a.red_idx[(long)b * a.red_blocks + blockIdx.x] = si[0];
+    }
+}
+
+__global__ __launch_bounds__(SG_BLOCK) void argmax_final_kernel(SampleArgs a) {
+    __shared__ float sv[SG_BLOCK];
+    __shared__ int si[SG_BLOCK];
+    const int b = blockIdx.x;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = threadIdx.x; j < a.red_blocks; j += SG_BLOCK) {
+        float v = a.red_val[(long)b * a.red_blocks + j];
+        int i = a.red_idx[(long)b * a.red_blocks + j];
+        if (i != 0x7fffffff && better(v, i, bv, bi)) { bv = v; bi = i; }
+    }
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int o = SG_BLOCK / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o && better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
+            sv[threadIdx.x] = sv[threadIdx.x + o];
+            si[threadIdx.x] = si[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    const bool found = si[0] != 0x7fffffff;
+    __syncthreads();
+    if (!found) {
+        // every candidate banned or non-finite: argmax of the (penalised) logits, else 0
+        const float* lg = a.logits + (long)b * a.ld;
+        bv = -INFINITY;
+        bi = 0x7fffffff;
+        for (int v = threadIdx.x; v < a.V; v += SG_BLOCK) {
+            float x = lg[v];
+            if (!(x > -INFINITY) || !(x < INFINITY)) continue;
+            if (better(x, v, bv, bi)) { bv = x; bi = v; }
+        }
+        sv[threadIdx.x] = bv;
+        si[threadIdx.x] = bi;
+        __syncthreads();
+        for (int o = SG_BLOCK / 2; o > 0; o >>= 1) {
+            if (threadIdx.x < o && better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
+                sv[threadIdx.x] = sv[threadIdx.x + o];
+                si[threadIdx.x] = si[threadIdx.x + o];
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) a.out_tok[b] = (si[0] == 0x7fffffff) ? 0 : si[0];
+}
+
+__global__ void zero_int_kernel(int* p, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
+}
+
+void launch_sample_greedy(const SampleArgs& a, hipStream_t s) {
+    SampleArgs b = a;
+    b.red_blocks = (int)sample_workspace_blocks(a.V);
+    hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(256), 0, s, a.banned_cnt, a.B);
+    if (a.rep_penalty > 0.f && fabsf(a.rep_penalty - 1.0f) > 1.1920929e-07f)
+        hipLaunchKernelGGL(rep_penalty_kernel, dim3(8, a.B), dim3(256), 0, s, b);
+    if (a.ngram > 1) hipLaunchKernelGGL(ngram_ban_kernel, dim3(8, a.B), dim3(256), 0, s, b);
+    dim3 g(b.red_blocks, a.B);
+    hipLaunchKernelGGL(argmax_partial_kernel, g, dim3(SG_BLOCK), 0, s, b, 1);
+    hipLaunchKernelGGL(argmax_final_kernel, dim3(a.B), dim3(SG_BLOCK), 0, s, b);
+}
+
+// After a token is chosen: generate loop bookkeeping (model/mod.rs:1977-2034).
+// EOS finishes a page (the EOS id itself is not emitted); finished pages keep
+// running in the batch but their context and output stop growing.
+__global__ void step_update_kernel(const int* tok, int B, int* ctx, long ctx_cap, int* ctx_len, int* out_ids,
+                                   int* out_len, long out_cap, int* done, int eos, const void* table, int dt, int H,
+                                   float* x_next) {
+    const int b = blockIdx.x;
+    const int t = tok[b];
+    if (threadIdx.x == 0 && !done[b]) {
+        if (eos >= 0 && t == eos) {
+            done[b] = 1;
+        } else {
+            const int st = out_len[b];
+            if (st < out_cap) { out_ids[(long)b * out_cap + st] = t; out_len[b] = st + 1; }
+            if (st + 1 >= out_cap) done[b] = 1;
+            const int n = ctx_len[b];
+            if (n < ctx_cap) { ctx[(long)b * ctx_cap + n] = t; ctx_len[b] = n + 1; }
+        }
+    }
+    for (int c = threadIdx.x; c < H; c += blockDim.x) x_next[(long)b * H + c] = table_val(table, dt, (long)t * H + c);
+}
+__global__ void step_advance_kernel(int* kv_pos, int* kv_len, int B) {
+    for (int b = threadIdx.x; b < B; b += blockDim.x) { kv_pos[b] += 1; kv_len[b] += 1; }
+}
+
+void launch_step_update(const int* tok, int B, int* ctx, long ctx_cap, int* ctx_len, int* out_ids, int* out_len,
+                        long out_cap, int* done, int eos, const void* table, int table_dt, int H, float* x_next,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(step_update_kernel, dim3(B), dim3(256), 0, s, tok, B, ctx, ctx_cap, ctx_len, out_ids, out_len,
+                       out_cap, done, eos, table, table_dt, H, x_next);
+}
+void launch_step_advance(int* kv_pos, int* kv_len, int B, hipStream_t s) {
+    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(256), 0, s, kv_pos, kv_len, B);
+}
+
+}  // namespace dsocr

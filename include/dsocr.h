@@ -1,0 +1,185 @@
+/*
+ * dsocr.h — C ABI of the MI355X-native DeepSeek-OCR page engine (gfx950).
+ *
+ * Drop-in boundary for the reference's `OcrEngine` (TimmyOVO/deepseek-ocr.rs,
+ * crates/core/src/inference.rs:189-209) and its loader `load_model`
+ * (crates/infer-deepseek/src/model/mod.rs:90-115).  A Rust FFI crate (or the
+ * Python mirror in deepseek-ocr.rs_amd/dsocr) binds these symbols; see
+ * INTEGRATION.md.  Plain C types only: no torch, no C++ types.
+ *
+ * Ownership: the caller owns every host buffer it passes; the engine owns its
+ * device memory.  An engine handle is Send-not-Sync like the reference engine
+ * (server/src/state.rs:22 keeps one behind a Mutex): one thread at a time.
+ * Errors: every call returns a dsocr_status; dsocr_last_error() gives the
+ * thread-local message.  DSOCR_EINVAL maps to the reference server's HTTP 400
+ * ("prompt formatting failed" / "prompt/image embedding mismatch",
+ * server/src/generation.rs:108-118), everything else to 500.
+ */
+#ifndef DSOCR_H
+#define DSOCR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    DSOCR_OK = 0,
+    DSOCR_EINVAL = 1,    /* bad arguments / prompt-image mismatch (reference: anyhow context -> 400) */
+    DSOCR_ENOENT = 2,    /* missing file or tensor */
+    DSOCR_EDEVICE = 3,   /* HIP runtime failure / no gfx950 device */
+    DSOCR_ENOMEM = 4,    /* device allocation failed */
+    DSOCR_EINTERNAL = 5  /* anything else (-> 500) */
+} dsocr_status;
+
+/* Reference `Precision` (core/src/runtime.rs:15-19).  F16 = the reference's GPU default:
+ * decoder weights rounded bf16->f16, f32 compute. */
+typedef enum { DSOCR_F32 = 0, DSOCR_F16 = 1, DSOCR_BF16 = 2 } dsocr_dtype;
+
+typedef struct dsocr_engine dsocr_engine;
+typedef struct dsocr_page_pixels dsocr_page_pixels;
+
+/* ModelLoadArgs (core/src/inference.rs:178-186). weights_path == NULL selects the
+ * deterministic synthetic checkpoint (seeded, real tensor names/shapes). */
+typedef struct {
+    const char* config_path;
+    const char* weights_path;
+    const char* snapshot_path; /* .dsq snapshot: not supported yet -> DSOCR_EINVAL */
+    int device_ordinal;
+    dsocr_dtype dtype;
+    uint64_t synthetic_seed;
+} dsocr_load_args;
+
+/* VisionSettings (core/src/inference.rs:13-18). */
+typedef struct {
+    uint32_t base_size;
+    uint32_t image_size;
+    int crop_mode;
+} dsocr_vision_settings;
+
+/* DecodeParameters (core/src/inference.rs:21-79) + generation options (model/mod.rs:177-218). */
+typedef struct {
+    size_t max_new_tokens;
+    int do_sample;               /* sampling is not on this engine's path: must be 0 */
+    double temperature;
+    double top_p;                /* <= 0 or >= 1: unset */
+    size_t top_k;                /* 0: unset */
+    float repetition_penalty;    /* 1.0: off */
+    size_t no_repeat_ngram_size; /* 0 or 1: off (reference default 20) */
+    uint64_t seed;
+    int use_cache;               /* must be 1 */
+    int64_t eos_token_id;        /* < 0: none (reference: config eos_token_id) */
+    int ignore_eos;              /* benchmark mode: always produce max_new_tokens */
+} dsocr_decode_params;
+
+/* stream callback: invoked after each generated token (model/mod.rs:1980-1982). */
+typedef void (*dsocr_stream_cb)(size_t n_generated, const int64_t* tokens, void* user);
+
+/* One page of a batched generate call. */
+typedef struct {
+    const int64_t* input_ids;      /* [prompt_len], BOS first (build_prompt_tokens) */
+    const uint8_t* image_mask;     /* [prompt_len], 1 on <image> slots; may be NULL if no image */
+    size_t prompt_len;
+    const dsocr_page_pixels* page; /* if non-NULL the vision tower runs on device for this page */
+    const float* image_rows;       /* else: host image embeddings [n_image_rows][hidden] (or NULL) */
+    size_t n_image_rows;
+} dsocr_request;
+
+typedef struct {
+    int64_t* out_ids; /* caller buffer, capacity max_new_tokens */
+    size_t cap;
+    size_t n_out;
+    dsocr_status status;
+} dsocr_result;
+
+/* Stage times of the last call, named after the reference Timer events
+ * (model/mod.rs:1871,1924,1975,2464,2498). */
+typedef struct {
+    double vision_prepare_ms;     /* vision.prepare_inputs (host, this call's pages) */
+    double vision_compute_ms;     /* vision.compute_embeddings */
+    double decode_prefill_ms;     /* decode.prefill */
+    double decode_iterative_ms;   /* decode.iterative */
+    double decode_generate_ms;    /* decode.generate */
+    size_t decode_steps;          /* decode forwards executed */
+    size_t pages;
+} dsocr_timings;
+
+/* ---- engine lifecycle (load_model, model/mod.rs:90-115; DeepseekOcrModel::load 946-1105) */
+dsocr_status dsocr_engine_load(const dsocr_load_args* args, dsocr_engine** out);
+void dsocr_engine_free(dsocr_engine* e);
+const char* dsocr_last_error(void);
+/* hidden size (image-row width), vocab, eos id, layers */
+dsocr_status dsocr_engine_info(const dsocr_engine* e, size_t* hidden, size_t* vocab, int64_t* eos_token_id,
+                               size_t* num_layers);
+
+/* ---- host preprocessing a1-a3 (build_global_view 2308-2330, dynamic_preprocess_with_params
+ *      preprocess.rs:67-138, image_to_tensor 2332-2347).  rgb: HWC uint8. */
+dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t width, uint32_t height,
+                                const dsocr_vision_settings* vs, dsocr_page_pixels** out);
+void dsocr_page_free(dsocr_page_pixels* p);
+/* crop grid (w,h), tile count, and the number of <image> slots build_image_placeholders emits */
+dsocr_status dsocr_page_info(const dsocr_page_pixels* p, uint32_t* crop_w, uint32_t* crop_h, uint32_t* n_tiles,
+                             size_t* n_image_tokens);
+/* normalised CHW f32 views: global [3][S][S], tiles [n][3][T][T] (NULL if none) */
+dsocr_status dsocr_page_pixels_view(const dsocr_page_pixels* p, const float** global_chw, uint32_t* global_size,
+                                    const float** tiles_chw, uint32_t* tile_size);
+
+/* ---- compute_image_embeddings (model/mod.rs:1276-1314): rows [n][hidden] per page,
+ *      concatenated into `out` (capacity cap_rows); rows_per_page[i] receives each count. */
+dsocr_status dsocr_image_embeddings(dsocr_engine* e, const dsocr_page_pixels* const* pages, size_t n_pages,
+                                    float* out, size_t cap_rows, size_t* rows_per_page);
+
+/* ---- generate (model/mod.rs:1870-2048), batch-1 semantics per page */
+dsocr_status dsocr_generate(dsocr_engine* e, const dsocr_request* req, const dsocr_decode_params* params,
+                            dsocr_stream_cb cb, void* user, int64_t* out_ids, size_t cap, size_t* n_out);
+/* B pages at once (vision batched, prefill batched, decode batched); each result equals dsocr_generate. */
+dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request* reqs,
+                                  const dsocr_decode_params* params, dsocr_result* results);
+dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t);
+
+/* ---- device helpers for tests / tooling (plain pointers; no torch) */
+dsocr_status dsocr_device_count(int* n);
+dsocr_status dsocr_dev_alloc(size_t bytes, void** ptr);
+dsocr_status dsocr_dev_free(void* ptr);
+dsocr_status dsocr_memcpy_h2d(void* dst, const void* src, size_t bytes);
+dsocr_status dsocr_memcpy_d2h(void* dst, const void* src, size_t bytes);
+dsocr_status dsocr_dev_sync(void);
+/* host: deterministic synthetic bf16 weights (same recipe as oracle/synth.c) */
+dsocr_status dsocr_synth_bf16(const char* name, uint64_t seed, uint64_t n, uint16_t* out);
+/* host: Pillow-exact bicubic resize (vision/resample.rs:101-160), RGB8 HWC */
+dsocr_status dsocr_resize_bicubic(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw,
+                                  uint32_t dh);
+
+/* ---- kernel-level entry points (device pointers, default stream) for parity tests */
+/* C[M][N] = act(A[M][K] . W[N][K]^T + bias) (+ C if accumulate); wdtype 0 = bf16, 1 = f16 */
+dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias, float* C,
+                          int act, int accumulate);
+dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const void* W, int wdtype, const float* bias, float* y,
+                          int act, int accumulate);
+dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* w, const float* b, float eps,
+                               float* y);
+dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w, float eps, float* y);
+/* softmax(scale * q.k^T [+ SAM decomposed rel-pos] [causal]) . v over n_seq uniform sequences of L
+ * rows; q,k,v,o are [n_seq*L][heads*hd]; relh/relw (optional) are the resized [2g-1][hd] tables of
+ * a gh x gw grid (gh*gw == L). */
+dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale, int causal, const float* q,
+                               const float* k, const float* v, float* o, const float* relh, const float* relw, int gh,
+                               int gw);
+/* Decode MoE layer (the north-star kernel chain): router GEMV + softmax top-k + grouping +
+ * grouped SwiGLU experts + shared experts + weighted combine, out[T][H] += moe(x).
+ * Wgu: [E][2I][H] (gate rows then up rows), Wd: [E][H][I], router [E][H], shared Wgu [2Is][H],
+ * shared Wd [H][Is] (shared may be NULL), all 16-bit (wdtype). */
+dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const void* router,
+                         const void* Wgu, const void* Wd, const void* sWgu, const void* sWd, int wdtype,
+                         int norm_topk, float scaling, float* out, int* topk_ids_out, float* topk_w_out);
+/* Greedy selection with repetition penalty + n-gram ban (sampling.rs:34-158) over B rows of V
+ * logits; ctx [B][ctx_cap] int32 with ctx_len[B]. */
+dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,
+                                   int ngram, float rep_penalty, int* out_tok);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSOCR_H */
