@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""DeepSeek-OCR page throughput on MI355X (BASELINE.json metric).
+
+A *step* = one pass of the page path over one batch of synthetic input: for every
+page of the batch, vision tower (SAM + CLIP + projector) -> 706-token prefill ->
+512 greedy decode tokens (EOS ignored, no_repeat_ngram_size = 20), exactly the
+reference's OcrEngine::decode work per page.  Default workload =
+BASELINE configs[1]: one 1024x1024 page per GPU per step (DeepSeek-OCR, weights
+fp16-rounded as the reference's `--dtype f16`, f32 compute).  `--pages-per-gpu 8`
+with 8 GPUs is configs[2] (batch 64, data parallel).
+
+Multi-GPU: one process per GPU (torchrun), pages sharded by index, no data-path
+collective; a CPU gloo group only provides the barrier and the max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "deepseek-ocr.rs_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
+    """The repo's CPU oracle (numpy restatement of the reference path) on rank 0's host
+    cores: bounded sample = 1 page vision + prefill + `decode_steps` decode forwards,
+    extrapolated to one full page (vision + prefill + (max_new-1) decode steps)."""
+    import numpy as np
+
+    import dsocr
+    from oracle.model import OracleModel
+    from oracle.specs import tensor_names
+    from oracle.weights import Weights, synthetic_has
+    cfg = json.load(open(dsocr.FULL_CONFIG))
+    W = Weights(seed=0, dtype="f16")
+    t = time.time()
+    for n, shape in tensor_names(cfg).items():   # materialise weights outside the timed sample
+        if synthetic_has(n):
+            W.get(n, shape)
+    log(f"[cpu] oracle weights ready in {time.time() - t:.1f}s")
+    orc = OracleModel(cfg, W)
+    img = pages[0]
+    t0 = time.time()
+    emb, _ = orc.image_embeddings(img)
+    t1 = time.time()
+    orc.dec.reset()
+    lg = orc.dec.forward(orc.prefill_embeddings(tok_ids, mask, emb))
+    t2 = time.time()
+    nxt = int(np.argmax(lg[0]))
+    for _ in range(decode_steps):
+        lg = orc.dec.forward(orc.dec.embed([nxt]))
+        nxt = int(np.argmax(lg[0]))
+    t3 = time.time()
+    per_step = (t3 - t2) / decode_steps
+    page_s = (t1 - t0) + (t2 - t1) + per_step * (max_new - 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads, "kind": "port",
+            "decode_tok_s": 1.0 / per_step,
+            "sample": f"1 synthetic 1024x1024 page: vision {t1 - t0:.2f}s + prefill {t2 - t1:.2f}s "
+                      f"({len(tok_ids)} tok) + {decode_steps} decode steps {per_step * 1e3:.0f} ms/step, "
+                      f"extrapolated to {max_new} tokens"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pages-per-gpu", type=int, default=1)
+    ap.add_argument("--max-new-tokens", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-decode-steps", type=int, default=2)
+    ap.add_argument("--roofline-iters", type=int, default=3)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # host-side barrier / max only; the data path has no collective
+
+    import numpy as np
+
+    import dsocr
+    from dsocr import DecodeParameters, ModelLoadArgs, Page, VisionSettings, build_prompt_tokens, load_model
+    from dsocr._lib import check, lib
+    from dsocr.synth import BENCH_PROMPT, SyntheticTokenizer, synthetic_page
+
+    def barrier():
+        check(lib().dsocr_dev_sync())
+        if dist is not None:
+            dist.barrier()
+
+    t_load = time.time()
+    eng = load_model(ModelLoadArgs(config_path=dsocr.FULL_CONFIG, synthetic_seed=0, dtype="f16", device=local))
+    log(f"[rank {rank}] engine loaded on hip:{local} in {time.time() - t_load:.1f}s")
+    tok = SyntheticTokenizer(eng.vocab)
+    vs = VisionSettings(1024, 640, True)
+    ppg = args.pages_per_gpu
+
+    def make_batch(step):
+        imgs, reqs = [], []
+        for i in range(ppg):
+            idx = (step * world + rank) * ppg + i
+            img = synthetic_page(idx)
+            page = Page(img, vs)
+            ids, mask = build_prompt_tokens(tok, BENCH_PROMPT, [page.n_image_tokens])
+            imgs.append(img)
+            reqs.append((ids, mask, page, None))
+        return imgs, reqs
+
+    params = DecodeParameters(max_new_tokens=args.max_new_tokens)
+    t = time.time()
+    batches = [make_batch(s) for s in range(args.warmup + args.steps)]
+    prep_ms = (time.time() - t) * 1e3 / max(1, len(batches) * ppg)
+    for s in range(args.warmup):
+        eng.generate_batch(batches[s][1], params, ignore_eos=True)
+
+    timings = []
+    barrier()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, args.warmup + args.steps):
+        out = eng.generate_batch(batches[s][1], params, ignore_eos=True)
+        assert all(len(o) == args.max_new_tokens for o in out)
+        timings.append(eng.last_timings())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    iterative_s = sum(t["decode_iterative_ms"] for t in timings) / 1e3
+    stage = {k: sum(t[k] for t in timings) / len(timings)
+             for k in ("vision_compute_ms", "decode_prefill_ms", "decode_iterative_ms")}
+    tokens_rank = args.steps * ppg * args.max_new_tokens
+    tok_s_rank = tokens_rank / iterative_s if iterative_s > 0 else 0.0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        ts = torch.tensor([tok_s_rank], dtype=torch.float64)
+        dist.all_reduce(ts, op=dist.ReduceOp.SUM)
+        tok_s = float(ts.item())
+    else:
+        tok_s = tok_s_rank
+    pages_total = args.steps * ppg * world
+    value = pages_total / elapsed
+
+    result = None
+    if rank == 0:
+        prof = eng.profile_decode_moe(args.roofline_iters)
+        achieved = prof["bytes"] / (prof["avg_us"] * 1e-6) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "moe_gateup_kernel<routed> + moe_down_kernel<routed> (decode MoE grouped GEMV)",
+                    "avg_launch_pair_us": round(prof["avg_us"], 2), "bytes_per_launch_pair": prof["bytes"],
+                    "experts_touched": prof["experts_touched"]}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            b = batches[args.warmup]
+            try:
+                cpu = cpu_baseline(b[0], b[1][0][0], b[1][0][1], args.max_new_tokens, args.cpu_decode_steps)
+            except Exception as e:  # reported, not fatal for the GPU number
+                cpu = {"value": None, "error": repr(e)}
+        result = {
+            "metric": "pages/sec + decode tok/s, DeepSeek-OCR fp16 1024px/512tok",
+            "value": round(value, 4),
+            "unit": "pages/s",
+            "decode_tok_s": round(tok_s, 1),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (fp16-rounded decoder weights, bf16 vision/lm_head weights)",
+            "data": "synthetic 1024x1024 pages + seeded synthetic weights (no checkpoint offline)",
+            "config": {"workload": "configs[1]: deepseek-ocr, 1024x1024 page, crop (2,2), 706-token prefill, "
+                                   "512 greedy tokens" if ppg == 1 else f"deepseek-ocr, {ppg} pages/GPU batch",
+                       "pages_per_gpu": ppg, "global_batch": ppg * world, "prefill_tokens": len(batches[0][1][0][0]),
+                       "max_new_tokens": args.max_new_tokens, "parallelism": f"dp{world}"},
+            "stage_ms": {k: round(v, 2) for k, v in stage.items()},
+            "host_prepare_ms_per_page": round(prep_ms, 2),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -225,6 +225,18 @@ dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t) {
     });
 }
 
+dsocr_status dsocr_profile_decode_moe(dsocr_engine* e, int iters, double* avg_us, double* bytes, double* flops,
+                                      int* experts_touched) {
+    return guarded([&] {
+        if (!e || iters <= 0) throw std::runtime_error("EINVAL: bad arguments");
+        auto p = e->impl->profile_decode_moe(iters);
+        if (avg_us) *avg_us = p.avg_us;
+        if (bytes) *bytes = p.bytes;
+        if (flops) *flops = p.flops;
+        if (experts_touched) *experts_touched = p.experts_touched;
+    });
+}
+
 // ---------------------------------------------------------------- device helpers
 dsocr_status dsocr_device_count(int* n) {
     return guarded([&] { check_hip(hipGetDeviceCount(n), "hipGetDeviceCount"); });
@@ -321,6 +333,22 @@ dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale,
         hipError_t e = hipDeviceSynchronize();
         if (rb) hipFree(rb);
         check_hip(e, "attention");
+    });
+}
+dsocr_status dsocr_k_decode_attention(int B, int heads, int hd, int max_len, float scale, const float* q,
+                                      const float* kc, const float* vc, const int* lens, float* o) {
+    return guarded([&] {
+        if (hd != 32 && hd != 64 && hd != 128) throw std::runtime_error("EINVAL: head_dim must be 32, 64 or 128");
+        float* part = nullptr;
+        check_hip(hipMalloc(&part, dsocr::decode_attention_workspace(B, heads, hd, max_len)), "hipMalloc");
+        dsocr::DecodeAttnArgs a;
+        a.q = q; a.q_row_stride = (long)heads * hd; a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd;
+        a.page_stride = (long)heads * max_len * hd; a.lens = lens; a.B = B; a.heads = heads; a.hd = hd;
+        a.max_len = max_len; a.scale = scale; a.part = part; a.o = o; a.o_row_stride = (long)heads * hd;
+        dsocr::launch_decode_attention(a, nullptr);
+        hipError_t e = hipDeviceSynchronize();
+        hipFree(part);
+        check_hip(e, "decode attention");
     });
 }
 dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const void* router,

@@ -3,6 +3,7 @@
 #include "engine.hpp"
 
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -1096,20 +1097,28 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipStreamSynchronize(st));
 
     // ---------------- 4. decode loop (decode.iterative) as a replayed hipGraph
+    // DSOCR_NO_GRAPH=1 launches the same kernels eagerly (rocprofv3 kernel tracing of
+    // graph replays is unreliable on this stack; kernel durations are unchanged).
+    const bool use_graph = !(getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0);
+    auto step_body = [&]() {
+        decode_step(B, Lmax);
+        launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+        linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
+        launch_sample_greedy(sa, st);
+        launch_step_advance(d_kvpos, d_kvlen, B, st);
+        launch_step_update(d_tok, B, d_ctx, ctx_cap, d_ctx_len, d_out, d_outlen, (long)p.max_new, d_done, eos, embed_,
+                           embed_dt_, H, SX, st);
+    };
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    capturing_ = true;
-    HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    decode_step(B, Lmax);
-    launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
-    linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
-    launch_sample_greedy(sa, st);
-    launch_step_advance(d_kvpos, d_kvlen, B, st);
-    launch_step_update(d_tok, B, d_ctx, ctx_cap, d_ctx_len, d_out, d_outlen, (long)p.max_new, d_done, eos, embed_,
-                       embed_dt_, H, SX, st);
-    HIP_CHECK(hipStreamEndCapture(st, &graph));
-    capturing_ = false;
-    HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+    if (use_graph) {
+        capturing_ = true;
+        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        step_body();
+        HIP_CHECK(hipStreamEndCapture(st, &graph));
+        capturing_ = false;
+        HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+    }
 
     HIP_CHECK(hipEventRecord(ev[4], st));
     std::vector<int> h_done(B), h_outlen(B);
@@ -1118,7 +1127,8 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     int* pin_done = nullptr;
     HIP_CHECK(hipHostMalloc((void**)&pin_done, sizeof(int) * (2 * B + 1)));
     for (size_t i = 1; i < p.max_new; ++i) {
-        HIP_CHECK(hipGraphLaunch(gexec, st));
+        if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
+        else step_body();
         ++steps;
         const bool check = cb != nullptr || (!p.ignore_eos && (i % 8 == 0 || i + 1 == p.max_new));
         if (check) {
@@ -1140,8 +1150,8 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipEventRecord(ev[5], st));
     HIP_CHECK(hipStreamSynchronize(st));
     HIP_CHECK(hipHostFree(pin_done));
-    (void)hipGraphExecDestroy(gexec);
-    (void)hipGraphDestroy(graph);
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
 
     h_out.resize((size_t)B * p.max_new);
     HIP_CHECK(hipMemcpy(h_out.data(), d_out, h_out.size() * 4, hipMemcpyDeviceToHost));
@@ -1153,9 +1163,58 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     timings_.iterative_ms = ms_between(ev[4], ev[5]);
     timings_.generate_ms = ms_between(ev[2], ev[3]) + ms_between(ev[4], ev[5]);
     timings_.steps = steps;
+    last_B_ = B;
     (void)t0;
     for (auto& e : ev) (void)hipEventDestroy(e);
     return out;
+}
+
+Engine::MoeProfile Engine::profile_decode_moe(int iters) {
+    MoeProfile prof;
+    const LangConfig& L = cfg_.lang;
+    const int B = last_B_;
+    if (B == 0 || L.n_routed == 0) throw std::runtime_error("EINVAL: run a generate() first");
+    const int E = L.n_routed, K = L.topk, I = L.moe_inter, H = L.hidden, TK = B * K;
+    hipStream_t st = stream_;
+    int* EOFF = wsi("s_eoff", E + 1);
+    std::vector<int> eoff(E + 1);
+    HIP_CHECK(hipMemcpyAsync(eoff.data(), EOFF, (E + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (int e = 0; e < E; ++e) prof.experts_touched += eoff[e + 1] > eoff[e] ? 1 : 0;
+    std::vector<hipEvent_t> evs;
+    std::vector<int> moe_layers;
+    for (int l = 0; l < L.layers; ++l)
+        if (layers_[l].moe) moe_layers.push_back(l);
+    const int n = iters * (int)moe_layers.size();
+    evs.resize(2 * n);
+    for (auto& e : evs) HIP_CHECK(hipEventCreate(&e));
+    int k = 0;
+    for (int it = 0; it < iters; ++it)
+        for (int l : moe_layers) {  // rotating over layers (~450 MB) defeats the 256 MB Infinity Cache
+            DecLayer& d = layers_[l];
+            MoeDecodeArgs m;
+            m.T = B; m.topk = K; m.E = E; m.K = H; m.I = I; m.Hout = H; m.x = wsf("s_xn", (size_t)B * H);
+            m.eoff = EOFF; m.arow = wsi("s_arow", TK); m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
+            m.h = wsf("s_ehh", (size_t)TK * I); m.y = wsf("s_ey", (size_t)TK * H);
+            m.max_rows_per_expert = B == 1 ? 1 : 4;
+            HIP_CHECK(hipEventRecord(evs[2 * k], st));
+            launch_moe_gateup_gemv(m, st);
+            launch_moe_down_gemv(m, st);
+            HIP_CHECK(hipEventRecord(evs[2 * k + 1], st));
+            ++k;
+        }
+    HIP_CHECK(hipStreamSynchronize(st));
+    double total = 0;
+    for (int i = 0; i < n; ++i) total += ms_between(evs[2 * i], evs[2 * i + 1]);
+    for (auto& e : evs) (void)hipEventDestroy(e);
+    const double wbytes = (double)prof.experts_touched * 3.0 * I * H * 2.0;  // fp16 gate+up+down of touched experts
+    const double abytes = (double)B * H * 4 + 2.0 * TK * I * 4 + (double)TK * H * 4 + (E + 1 + TK) * 4.0;
+    prof.avg_us = 1000.0 * total / n;
+    prof.bytes = wbytes + abytes;
+    prof.flops = 2.0 * TK * 3.0 * H * I;
+    prof.pairs = n;
+    prof.tokens = B;
+    return prof;
 }
 
 }  // namespace dsocr

@@ -122,6 +122,13 @@ class Engine {
     std::vector<std::vector<int64_t>> generate(const std::vector<GenRequest>& reqs, const GenParams& p, TokenCb cb,
                                                void* user);
     Timings last_timings() const { return timings_; }
+    // Replays the decode MoE grouped GEMV (routed experts, gate/up + down) of every MoE
+    // layer on the last decode step's routing, timing each launch pair with HIP events.
+    struct MoeProfile {
+        double avg_us = 0, bytes = 0, flops = 0;
+        int pairs = 0, experts_touched = 0, tokens = 0;
+    };
+    MoeProfile profile_decode_moe(int iters);
     hipStream_t stream() const { return stream_; }
 
   private:
@@ -185,6 +192,7 @@ class Engine {
     size_t kv_bytes_ = 0;
     long page_stride_ = 0, head_stride_ = 0;
     Timings timings_;
+    int last_B_ = 0;
 
     void* dev_alloc(size_t bytes);
     void ensure_rope(int len);

@@ -210,7 +210,7 @@ template <int HD>
 __global__ __launch_bounds__(256) void decode_attn_partial(DecodeAttnArgs a) {
     __shared__ float p_s[DA_CH];
     __shared__ float red[8];
-    __shared__ float o_s[2][HD];
+    __shared__ float o_s[256 / HD][HD];
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int len = a.lens[b];
     const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
@@ -262,22 +262,19 @@ __global__ __launch_bounds__(256) void decode_attn_partial(DecodeAttnArgs a) {
     lsum = wave_sum(lsum);
     __syncthreads();
     if (lane == 0) red[4 + wave] = lsum;
-    // PV: thread -> (dim d, key parity half)
-    const int d = tid % HD, hh = tid / HD;  // HD=128: hh in {0,1}; HD=64: hh in {0..3}
-    const int nh = 256 / HD;
+    // PV: thread -> (dim d, key slice hh of nh = 256/HD slices)
+    const int d = tid % HD, hh = tid / HD;
+    constexpr int NH = 256 / HD;
     float acc = 0.f;
-    for (int kk = hh; kk < kn; kk += nh) acc = fmaf(p_s[kk], Vc[(long)(k0 + kk) * HD + d], acc);
+    for (int kk = hh; kk < kn; kk += NH) acc = fmaf(p_s[kk], Vc[(long)(k0 + kk) * HD + d], acc);
+    o_s[hh][d] = acc;
     __syncthreads();
-    if (nh == 2) {
-        o_s[hh][d] = acc;
-    } else {
-        // fold 4 partial sums into 2 slots
-        if (hh < 2) o_s[hh][d] = acc;
-        __syncthreads();
-        if (hh >= 2) o_s[hh - 2][d] += acc;
+    if (tid < HD) {
+        float o = 0.f;
+#pragma unroll
+        for (int j = 0; j < NH; ++j) o += o_s[j][tid];
+        part[2 + tid] = o;
     }
-    __syncthreads();
-    if (tid < HD) part[2 + tid] = o_s[0][tid] + o_s[1][tid];
     if (tid == 0) {
         part[0] = m;
         part[1] = (red[4] + red[5]) + (red[6] + red[7]);

@@ -105,7 +105,9 @@ void launch_gemv(const GemvArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------ MoE decode (grouped GEMV)
 // grid.x = E * ceil(I / (4*RB)); wave owns RB intermediate rows i of expert e and
 // computes gate_i and up_i for every token routed to e (chunks of MT tokens).
-template <typename WT, int MT, int RB>
+// ROUTED only distinguishes the routed-expert instantiation from the dense / shared-expert one
+// (E = 1) in profiles; the code is identical.
+template <typename WT, int MT, int RB, bool ROUTED>
 __global__ __launch_bounds__(256) void moe_gateup_kernel(MoeDecodeArgs a) {
     const int units_per_e = (a.I + 4 * RB - 1) / (4 * RB);
     const int e = blockIdx.x / units_per_e;
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(256) void moe_gateup_kernel(MoeDecodeArgs a) {
     }
 }
 
-template <typename WT, int MT, int RB>
+template <typename WT, int MT, int RB, bool ROUTED>
 __global__ __launch_bounds__(256) void moe_down_kernel(MoeDecodeArgs a) {
     const int units_per_e = (a.Hout + 4 * RB - 1) / (4 * RB);
     const int e = blockIdx.x / units_per_e;
@@ -231,36 +233,40 @@ __global__ __launch_bounds__(256) void moe_down_kernel(MoeDecodeArgs a) {
     }
 }
 
-void launch_moe_gateup_gemv(const MoeDecodeArgs& a, hipStream_t s) {
+template <typename WT, int MT, bool ROUTED>
+static void moe_launch_pair_gateup(const MoeDecodeArgs& a, hipStream_t s) {
     constexpr int RB = 2;
     const int units = (a.I + 4 * RB - 1) / (4 * RB);
-    dim3 grid(a.E * units);
+    hipLaunchKernelGGL((moe_gateup_kernel<WT, MT, RB, ROUTED>), dim3(a.E * units), dim3(256), 0, s, a);
+}
+template <typename WT, int MT, bool ROUTED>
+static void moe_launch_pair_down(const MoeDecodeArgs& a, hipStream_t s) {
+    constexpr int RB = 2;
+    const int units = (a.Hout + 4 * RB - 1) / (4 * RB);
+    hipLaunchKernelGGL((moe_down_kernel<WT, MT, RB, ROUTED>), dim3(a.E * units), dim3(256), 0, s, a);
+}
+
+template <typename WT, bool ROUTED>
+static void moe_dispatch(const MoeDecodeArgs& a, hipStream_t s, bool gateup) {
     if (a.max_rows_per_expert <= 1) {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_kernel<bf16_t, 1, RB>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((moe_gateup_kernel<f16_t, 1, RB>), grid, dim3(256), 0, s, a);
+        gateup ? moe_launch_pair_gateup<WT, 1, ROUTED>(a, s) : moe_launch_pair_down<WT, 1, ROUTED>(a, s);
     } else if (a.max_rows_per_expert <= 4) {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_kernel<bf16_t, 4, RB>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((moe_gateup_kernel<f16_t, 4, RB>), grid, dim3(256), 0, s, a);
+        gateup ? moe_launch_pair_gateup<WT, 4, ROUTED>(a, s) : moe_launch_pair_down<WT, 4, ROUTED>(a, s);
     } else {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_kernel<bf16_t, 8, RB>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((moe_gateup_kernel<f16_t, 8, RB>), grid, dim3(256), 0, s, a);
+        gateup ? moe_launch_pair_gateup<WT, 8, ROUTED>(a, s) : moe_launch_pair_down<WT, 8, ROUTED>(a, s);
     }
 }
 
-void launch_moe_down_gemv(const MoeDecodeArgs& a, hipStream_t s) {
-    constexpr int RB = 2;
-    const int units = (a.Hout + 4 * RB - 1) / (4 * RB);
-    dim3 grid(a.E * units);
-    if (a.max_rows_per_expert <= 1) {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down_kernel<bf16_t, 1, RB>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((moe_down_kernel<f16_t, 1, RB>), grid, dim3(256), 0, s, a);
-    } else if (a.max_rows_per_expert <= 4) {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down_kernel<bf16_t, 4, RB>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((moe_down_kernel<f16_t, 4, RB>), grid, dim3(256), 0, s, a);
+static void moe_dispatch_all(const MoeDecodeArgs& a, hipStream_t s, bool gateup) {
+    const bool routed = a.E > 1;
+    if (a.wdtype == WDT_BF16) {
+        routed ? moe_dispatch<bf16_t, true>(a, s, gateup) : moe_dispatch<bf16_t, false>(a, s, gateup);
     } else {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down_kernel<bf16_t, 8, RB>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((moe_down_kernel<f16_t, 8, RB>), grid, dim3(256), 0, s, a);
+        routed ? moe_dispatch<f16_t, true>(a, s, gateup) : moe_dispatch<f16_t, false>(a, s, gateup);
     }
 }
+
+void launch_moe_gateup_gemv(const MoeDecodeArgs& a, hipStream_t s) { moe_dispatch_all(a, s, true); }
+void launch_moe_down_gemv(const MoeDecodeArgs& a, hipStream_t s) { moe_dispatch_all(a, s, false); }
 
 }  // namespace dsocr

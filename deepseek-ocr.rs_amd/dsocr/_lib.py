@@ -60,9 +60,9 @@ STREAM_CB = C.CFUNCTYPE(None, C.c_size_t, C.POINTER(C.c_int64), C.c_void_p)
 EXPORTS = [
     "dsocr_engine_load", "dsocr_engine_free", "dsocr_last_error", "dsocr_engine_info", "dsocr_prepare_page",
     "dsocr_page_free", "dsocr_page_info", "dsocr_page_pixels_view", "dsocr_image_embeddings", "dsocr_generate",
-    "dsocr_generate_batch", "dsocr_last_timings", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
+    "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode_moe", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
-    "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_moe",
+    "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
     "dsocr_k_sample_greedy",
 ]
 
@@ -92,6 +92,8 @@ def lib():
                                  C.POINTER(sz)]
     L.dsocr_generate_batch.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC)]
     L.dsocr_last_timings.argtypes = [vp, C.POINTER(TimingsC)]
+    L.dsocr_profile_decode_moe.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                           C.POINTER(C.c_double), C.POINTER(i32)]
     L.dsocr_device_count.argtypes = [C.POINTER(i32)]
     L.dsocr_dev_alloc.argtypes = [sz, C.POINTER(vp)]
     L.dsocr_dev_free.argtypes = [vp]
@@ -104,6 +106,7 @@ def lib():
     L.dsocr_k_layernorm.argtypes = [i32, i32, vp, vp, vp, f32, vp]
     L.dsocr_k_rmsnorm.argtypes = [i32, i32, vp, vp, f32, vp]
     L.dsocr_k_attention.argtypes = [i32, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp, vp, i32, i32]
+    L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, f32, vp, vp, vp, vp, vp]
     L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]
     L.dsocr_k_sample_greedy.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, vp]
     _lib = L

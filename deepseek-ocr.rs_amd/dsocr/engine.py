@@ -245,6 +245,11 @@ class DeepseekOcrEngine:
         check(lib().dsocr_last_timings(self._h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in TimingsC._fields_}
 
+    def profile_decode_moe(self, iters: int = 3) -> dict:
+        a, b, f, e = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+        check(lib().dsocr_profile_decode_moe(self._h, iters, C.byref(a), C.byref(b), C.byref(f), C.byref(e)))
+        return {"avg_us": a.value, "bytes": b.value, "flops": f.value, "experts_touched": e.value}
+
     # ------------------------------------------------------------------ OcrEngine::decode
     def decode(self, tokenizer, prompt: str, images: Sequence, vision: VisionSettings,
                params: DecodeParameters, stream: Optional[Callable] = None) -> DecodeOutcome:

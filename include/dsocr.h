@@ -139,6 +139,13 @@ dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request
                                   const dsocr_decode_params* params, dsocr_result* results);
 dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t);
 
+/* Roofline probe for the north-star kernel: replays the decode MoE grouped GEMV (routed
+ * gate/up + down) of every MoE layer on the last decode step's routing, HIP-event timed.
+ * avg_us: mean duration of one (gate/up, down) launch pair; bytes/flops: algorithmic
+ * traffic/work of one pair (touched experts' fp16 weights + f32 activations). */
+dsocr_status dsocr_profile_decode_moe(dsocr_engine* e, int iters, double* avg_us, double* bytes, double* flops,
+                                      int* experts_touched);
+
 /* ---- device helpers for tests / tooling (plain pointers; no torch) */
 dsocr_status dsocr_device_count(int* n);
 dsocr_status dsocr_dev_alloc(size_t bytes, void** ptr);
@@ -167,6 +174,10 @@ dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w,
 dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale, int causal, const float* q,
                                const float* k, const float* v, float* o, const float* relh, const float* relw, int gh,
                                int gw);
+/* Decode attention over a per-page f32 KV cache laid out [B][heads][max_len][hd]: for page b,
+ * o[b] = softmax(scale * q[b].K[b][:lens[b]]^T) . V[b][:lens[b]]  (q, o: [B][heads*hd]; lens on device). */
+dsocr_status dsocr_k_decode_attention(int B, int heads, int hd, int max_len, float scale, const float* q,
+                                      const float* kc, const float* vc, const int* lens, float* o);
 /* Decode MoE layer (the north-star kernel chain): router GEMV + softmax top-k + grouping +
  * grouped SwiGLU experts + shared experts + weighted combine, out[T][H] += moe(x).
  * Wgu: [E][2I][H] (gate rows then up rows), Wd: [E][H][I], router [E][H], shared Wgu [2Is][H],

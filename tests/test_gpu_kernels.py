@@ -1,0 +1,240 @@
+"""Kernel-level parity on MI355X (gfx950) through the C ABI entry points.
+
+Tolerances (f32 accumulation in a different order than the oracle's BLAS):
+  GEMM/GEMV/attention/MoE: |got - ref| <= 2e-5 * sum_k |a_k w_k| + 1e-6 (per element bound)
+  norms: 1e-5 relative.  Greedy token selection: exact.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+from _dev import Dev, bf16_round, bf16_to_f32, f16_bits
+from dsocr._lib import check, lib
+from oracle.decoder import rms_norm, select_token_id, softmax
+from oracle.vision import gelu_erf, get_rel_pos, layer_norm, sigmoid
+
+pytestmark = pytest.mark.gpu
+
+
+def _weights(rng, n, k, wdtype):
+    w = (rng.standard_normal((n, k)) * 0.05).astype(np.float32)
+    if wdtype == 0:
+        bits = bf16_round(w)
+        return bits, bf16_to_f32(bits)
+    bits = f16_bits(w)
+    return bits, bits.view(np.float16).astype(np.float32)
+
+
+def _bound(a, w):
+    return 2e-5 * (np.abs(a) @ np.abs(w).T) + 1e-6
+
+
+ACTS = {0: lambda x: x, 1: gelu_erf, 2: lambda x: sigmoid(x * np.float32(1.702)) * x,
+        3: lambda x: x / (np.float32(1) + np.exp(-x))}
+
+
+@pytest.mark.parametrize("M,N,K,wdt,act,acc", [(256, 256, 256, 0, 0, 0), (1000, 770, 768, 0, 1, 0),
+                                              (77, 130, 24, 1, 0, 1), (4096, 2304, 768, 0, 0, 0),
+                                              (300, 4096, 1024, 1, 2, 0), (129, 64, 1280, 1, 3, 1)])
+def test_gemm(gpu, M, N, K, wdt, act, acc):
+    rng = np.random.default_rng(M + N + K)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    bits, w = _weights(rng, N, K, wdt)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
+    dA, dW, dB, dC = Dev(a), Dev(bits), Dev(bias), Dev(c0)
+    check(lib().dsocr_k_gemm(M, N, K, dA.ptr, dW.ptr, wdt, dB.ptr, dC.ptr, act, acc))
+    ref = ACTS[act]((a.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias) + (c0 if acc else 0)
+    got = dC.get()
+    bound = _bound(a, w) * (2.0 if act else 1.0)
+    assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
+
+
+@pytest.mark.parametrize("M,N,K,wdt", [(1, 1280, 1280, 1), (1, 129280, 1280, 0), (3, 3840, 1280, 1),
+                                       (8, 896, 1792, 1), (16, 100, 64, 0), (21, 513, 128, 0)])
+def test_gemv(gpu, M, N, K, wdt):
+    rng = np.random.default_rng(N + K + M)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    bits, w = _weights(rng, N, K, wdt)
+    dx, dW, dy = Dev(x), Dev(bits), Dev.zeros((M, N))
+    check(lib().dsocr_k_gemv(M, N, K, dx.ptr, dW.ptr, wdt, None, dy.ptr, 0, 0))
+    ref = (x.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32)
+    assert np.all(np.abs(dy.get() - ref) <= _bound(x, w))
+
+
+@pytest.mark.parametrize("rows,cols,eps", [(4096, 768, 1e-6), (257, 1024, 1e-5), (100, 256, 1e-6)])
+def test_layernorm(gpu, rows, cols, eps):
+    rng = np.random.default_rng(rows)
+    x = (rng.standard_normal((rows, cols)) * 3 + 1).astype(np.float32)
+    w = rng.standard_normal(cols).astype(np.float32)
+    b = rng.standard_normal(cols).astype(np.float32)
+    dx, dw, db, dy = Dev(x), Dev(w), Dev(b), Dev.zeros((rows, cols))
+    check(lib().dsocr_k_layernorm(rows, cols, dx.ptr, dw.ptr, db.ptr, eps, dy.ptr))
+    ref = layer_norm(x, w, b, eps)
+    assert np.max(np.abs(dy.get() - ref)) <= 1e-5 * (1 + np.max(np.abs(ref)))
+
+
+def test_rmsnorm(gpu):
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((706, 1280)).astype(np.float32) * 0.01
+    w = (1 + rng.standard_normal(1280) * 0.05).astype(np.float32)
+    dx, dw, dy = Dev(x), Dev(w), Dev.zeros((706, 1280))
+    check(lib().dsocr_k_rmsnorm(706, 1280, dx.ptr, dw.ptr, 1e-6, dy.ptr))
+    ref = rms_norm(x, w, 1e-6)
+    assert np.max(np.abs(dy.get() - ref)) <= 1e-5 * np.max(np.abs(ref))
+
+
+def _attn_ref(q, k, v, scale, causal=False, bias=None):
+    s = (q.astype(np.float64) @ k.T.astype(np.float64)) * scale
+    if bias is not None:
+        s = s + bias
+    if causal:
+        s = s + np.triu(np.full(s.shape, -1e9), 1)
+    s = s - s.max(-1, keepdims=True)
+    p = np.exp(s)
+    p /= p.sum(-1, keepdims=True)
+    return p @ v.astype(np.float64)
+
+
+@pytest.mark.parametrize("n_seq,L,heads,hd,causal", [(2, 257, 16, 64, 0), (3, 101, 4, 32, 0), (1, 706, 10, 128, 1),
+                                                     (5, 196, 12, 64, 0), (2, 33, 2, 128, 1)])
+def test_attention(gpu, n_seq, L, heads, hd, causal):
+    rng = np.random.default_rng(L * heads)
+    C_ = heads * hd
+    q, k, v = (rng.standard_normal((n_seq * L, C_)).astype(np.float32) for _ in range(3))
+    dq, dk, dv, do = Dev(q), Dev(k), Dev(v), Dev.zeros((n_seq * L, C_))
+    scale = 1.0 / math.sqrt(hd)
+    check(lib().dsocr_k_attention(n_seq, L, heads, hd, scale, causal, dq.ptr, dk.ptr, dv.ptr, do.ptr, None, None, 0, 0))
+    got = do.get()
+    for s in range(n_seq):
+        for h in range(heads):
+            sl, hl = slice(s * L, (s + 1) * L), slice(h * hd, (h + 1) * hd)
+            ref = _attn_ref(q[sl, hl], k[sl, hl], v[sl, hl], scale, bool(causal))
+            assert np.max(np.abs(got[sl, hl] - ref)) < 2e-5, (s, h)
+
+
+@pytest.mark.parametrize("g,rel_len", [(14, 27), (16, 31), (40, 127), (64, 127)])
+def test_attention_sam_relpos(gpu, g, rel_len):
+    """SamAttention::forward with the decomposed rel-pos bias (sam.rs:804-888, 1124-1247)."""
+    rng = np.random.default_rng(g)
+    heads, hd, n_seq, L = 2, 64, 1, g * g
+    q, k, v = (rng.standard_normal((L, heads * hd)).astype(np.float32) for _ in range(3))
+    relh = rng.standard_normal((rel_len, hd)).astype(np.float32) * 0.2
+    relw = rng.standard_normal((rel_len, hd)).astype(np.float32) * 0.2
+    Rh, Rw = get_rel_pos(g, g, relh), get_rel_pos(g, g, relw)       # [g, g, hd]
+    # direct construction of the resized table from get_rel_pos: idx = qi - ki + g - 1
+    tab_h = np.zeros((2 * g - 1, hd), np.float32)
+    tab_w = np.zeros((2 * g - 1, hd), np.float32)
+    for qi in range(g):
+        for ki in range(g):
+            tab_h[qi - ki + g - 1] = Rh[qi, ki]
+            tab_w[qi - ki + g - 1] = Rw[qi, ki]
+    dq, dk, dv, do = Dev(q), Dev(k), Dev(v), Dev.zeros((L, heads * hd))
+    dh, dw = Dev(tab_h), Dev(tab_w)
+    scale = 1.0 / math.sqrt(hd)
+    check(lib().dsocr_k_attention(n_seq, L, heads, hd, scale, 0, dq.ptr, dk.ptr, dv.ptr, do.ptr, dh.ptr, dw.ptr, g, g))
+    got = do.get()
+    for h in range(heads):
+        hl = slice(h * hd, (h + 1) * hd)
+        qg = q[:, hl].reshape(g, g, hd).astype(np.float64)
+        rel_h = np.einsum("hwc,hkc->hwk", qg, Rh)
+        rel_w = np.einsum("hwc,wkc->hwk", qg, Rw)
+        bias = (rel_h[:, :, :, None] + rel_w[:, :, None, :]).reshape(L, L)
+        ref = _attn_ref(q[:, hl], k[:, hl], v[:, hl], scale, False, bias)
+        assert np.max(np.abs(got[:, hl] - ref)) < 5e-5
+
+
+@pytest.mark.parametrize("B,heads,hd,max_len", [(1, 10, 128, 1218), (3, 4, 32, 300), (5, 12, 64, 700), (2, 10, 128, 257)])
+def test_decode_attention(gpu, B, heads, hd, max_len):
+    """Decode step attention (block.rs:608-775 with past_len > 0) over the f32 cache."""
+    rng = np.random.default_rng(B * hd + max_len)
+    q = rng.standard_normal((B, heads * hd)).astype(np.float32)
+    kc = rng.standard_normal((B, heads, max_len, hd)).astype(np.float32)
+    vc = rng.standard_normal((B, heads, max_len, hd)).astype(np.float32)
+    lens = rng.integers(1, max_len + 1, B).astype(np.int32)
+    lens[0] = max_len
+    if B > 1:
+        lens[1] = 1
+    dq, dk, dv, dl, do = Dev(q), Dev(kc), Dev(vc), Dev(lens), Dev.zeros((B, heads * hd))
+    scale = 1.0 / math.sqrt(hd)
+    check(lib().dsocr_k_decode_attention(B, heads, hd, max_len, scale, dq.ptr, dk.ptr, dv.ptr, dl.ptr, do.ptr))
+    got = do.get()
+    for b in range(B):
+        for h in range(heads):
+            L = lens[b]
+            ref = _attn_ref(q[b, h * hd:(h + 1) * hd][None], kc[b, h, :L], vc[b, h, :L], scale)[0]
+            assert np.max(np.abs(got[b, h * hd:(h + 1) * hd] - ref)) < 2e-5, (b, h)
+
+
+def test_moe_decode_layer(gpu):
+    """Decode MoE (north-star kernel chain) vs the oracle's run_moe (block.rs:1215-1395)."""
+    from oracle.decoder import Decoder
+    rng = np.random.default_rng(5)
+    T, H, E, topk, I, ns = 3, 256, 16, 6, 64, 2
+    Is = I * ns
+    x = rng.standard_normal((T, H)).astype(np.float32)
+    router = f16_bits(rng.standard_normal((E, H)) * 0.1)
+    gate = [f16_bits(rng.standard_normal((I, H)) * 0.05) for _ in range(E)]
+    up = [f16_bits(rng.standard_normal((I, H)) * 0.05) for _ in range(E)]
+    down = [f16_bits(rng.standard_normal((H, I)) * 0.05) for _ in range(E)]
+    sg, su, sd = (f16_bits(rng.standard_normal(s) * 0.05) for s in [(Is, H), (Is, H), (H, Is)])
+    Wgu = np.stack([np.concatenate([gate[e], up[e]]) for e in range(E)])
+    Wd = np.stack(down)
+    sWgu = np.concatenate([sg, su])
+    out0 = rng.standard_normal((T, H)).astype(np.float32)
+    dx, dr, dgu, dd, dsgu, dsd, dout = Dev(x), Dev(router), Dev(Wgu), Dev(Wd), Dev(sWgu), Dev(sd), Dev(out0)
+    ids = np.zeros(T * topk, np.int32)
+    wts = np.zeros(T * topk, np.float32)
+    check(lib().dsocr_k_moe(T, H, E, topk, I, Is, dx.ptr, dr.ptr, dgu.ptr, dd.ptr, dsgu.ptr, dsd.ptr, 1, 0, 1.0,
+                            dout.ptr, ids.ctypes.data_as(C.c_void_p), wts.ctypes.data_as(C.c_void_p)))
+
+    f = lambda b: b.view(np.float16).astype(np.float32)
+    W = {"l.mlp.gate.weight": f(router), "l.mlp.shared_experts.gate_proj.weight": f(sg),
+         "l.mlp.shared_experts.up_proj.weight": f(su), "l.mlp.shared_experts.down_proj.weight": f(sd)}
+    for e in range(E):
+        W[f"l.mlp.experts.{e}.gate_proj.weight"] = f(gate[e])
+        W[f"l.mlp.experts.{e}.up_proj.weight"] = f(up[e])
+        W[f"l.mlp.experts.{e}.down_proj.weight"] = f(down[e])
+
+    class _W:
+        def get(self, n, shape=None):
+            return W[n.replace("model.layers.1.", "l.")]
+
+        def has(self, n):
+            return n.replace("model.layers.1.", "l.") in W
+
+    dec = Decoder.__new__(Decoder)
+    dec.W = _W()
+    dec.H = H
+
+    class _L:
+        n_routed_experts, num_experts_per_tok, moe_intermediate_size = E, topk, I
+        topk_method, scoring_func, norm_topk_prob, routed_scaling_factor, n_shared_experts = "greedy", "softmax", False, 1.0, ns
+    dec.lang = _L()
+    ref = dec.moe(1, x) + out0
+    logits = x @ f(router).T
+    order = np.argsort(-softmax(logits), axis=-1, kind="stable")[:, :topk]
+    assert np.array_equal(ids.reshape(T, topk), order)
+    assert np.max(np.abs(dout.get() - ref)) < 1e-4
+
+
+@pytest.mark.parametrize("ngram,pen", [(0, 1.0), (3, 1.0), (20, 1.0), (3, 1.3)])
+def test_sample_greedy(gpu, ngram, pen):
+    rng = np.random.default_rng(ngram)
+    B, V, cap = 3, 5000, 64
+    logits = rng.standard_normal((B, V)).astype(np.float32)
+    ctx = np.zeros((B, cap), np.int32)
+    lens = np.array([40, 25, 3], np.int32)
+    for b in range(B):
+        base = rng.integers(0, 50, 5)
+        seq = np.tile(base, 20)[: lens[b]]
+        ctx[b, : lens[b]] = seq
+        logits[b, seq] += 3.0  # make the repeated tokens the likely argmax
+    dl, dc, dn, dt = Dev(logits), Dev(ctx), Dev(lens), Dev.zeros(B, np.int32)
+    check(lib().dsocr_k_sample_greedy(B, V, dl.ptr, dc.ptr, cap, dn.ptr, ngram, pen, dt.ptr))
+    got = dt.get()
+    for b in range(B):
+        ref = select_token_id(logits[b], ctx[b, : lens[b]].tolist(), pen, ngram if ngram > 1 else None)
+        assert got[b] == ref, (b, got[b], ref)

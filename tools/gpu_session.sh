@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU session runner for gpurun: each step bounded by its own timeout; test failures
+# (pytest rc=1) do not stop the session, anything else (fault, abort, timeout) does.
+# usage: tools/gpu_session.sh <step>...   steps: kernels model_tiny model_full smoke bench bench_prof
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; echo "rc=$rc :: $*" >> gpurun_out/rc.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; return 0; }
+for step in "$@"; do
+  case $step in
+    kernels) run 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider > gpurun_out/kernels.log 2>&1 ;;
+    model_tiny) run 600 python -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider -k "tiny or eos or mask or safetensors" > gpurun_out/model_tiny.log 2>&1 ;;
+    model_full) run 900 python -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider -k "full" > gpurun_out/model_full.log 2>&1 ;;
+    gpu_all) run 1100 python -m pytest tests -q -m gpu -rf -p no:cacheprovider > gpurun_out/gpu_all.log 2>&1 ;;
+    smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
+    bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
+    bench_full) run 1100 python bench.py > gpurun_out/bench_full.log 2>&1 ;;
+    prof) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
+    *) echo "unknown step $step" >> gpurun_out/rc.log ;;
+  esac
+done
