@@ -159,13 +159,18 @@ def main():
 
     result = None
     if rank == 0:
-        prof = eng.profile_decode_moe(args.roofline_iters)
-        achieved = prof["bytes"] / (prof["avg_us"] * 1e-6) / 1e9
+        prof = eng.profile_decode(args.roofline_iters)
+        gu = prof["moe_gateup"]
+        achieved = gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "moe_gateup_kernel<routed> + moe_down_kernel<routed> (decode MoE grouped GEMV)",
-                    "avg_launch_pair_us": round(prof["avg_us"], 2), "bytes_per_launch_pair": prof["bytes"],
-                    "experts_touched": prof["experts_touched"]}
+                    "kernel": "moe_gateup2_kernel (decode MoE gate/up: routed top-6 + shared experts, one layer)",
+                    "avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
+                    "experts_touched": prof["experts_touched"],
+                    "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
+                                   "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
+                               for k in ("moe_down", "attention", "lm_head")},
+                    "kv_len": prof["kv_len"]}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             b = batches[args.warmup]

@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CLANG = os.environ.get("DSOCR_CXX", "/opt/rocm/llvm/bin/clang++")
 ARCH = "gfx950"
 
-KERNELS = ["gemm", "gemv", "moe", "norm", "attention", "misc"]
+KERNELS = ["gemm", "moe", "norm", "attention", "misc", "decode"]
 HOST = ["engine", "capi"]
 
 

@@ -225,15 +225,22 @@ dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t) {
     });
 }
 
-dsocr_status dsocr_profile_decode_moe(dsocr_engine* e, int iters, double* avg_us, double* bytes, double* flops,
-                                      int* experts_touched) {
+dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out) {
     return guarded([&] {
-        if (!e || iters <= 0) throw std::runtime_error("EINVAL: bad arguments");
-        auto p = e->impl->profile_decode_moe(iters);
-        if (avg_us) *avg_us = p.avg_us;
-        if (bytes) *bytes = p.bytes;
-        if (flops) *flops = p.flops;
-        if (experts_touched) *experts_touched = p.experts_touched;
+        if (!e || iters <= 0 || !out) throw std::runtime_error("EINVAL: bad arguments");
+        auto p = e->impl->profile_decode(iters);
+        auto cp = [](const dsocr::Engine::KernelProfile& k) {
+            dsocr_kernel_profile r;
+            r.avg_us = k.avg_us; r.bytes = k.bytes; r.flops = k.flops; r.launches = k.launches;
+            return r;
+        };
+        out->moe_gateup = cp(p.moe_gateup);
+        out->moe_down = cp(p.moe_down);
+        out->attention = cp(p.attention);
+        out->lm_head = cp(p.lm_head);
+        out->experts_touched = p.experts_touched;
+        out->tokens = p.tokens;
+        out->kv_len = p.kv_len;
     });
 }
 
@@ -284,14 +291,14 @@ dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, in
         check_hip(hipDeviceSynchronize(), "gemm");
     });
 }
-dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const void* W, int wdtype, const float* bias, float* y,
-                          int act, int accumulate) {
+dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm_w, float eps, const void* W,
+                          int wdtype, const float* bias, float* y, int act, int accumulate) {
     return guarded([&] {
         if (K % 8) throw std::runtime_error("EINVAL: K must be a multiple of 8");
-        dsocr::GemvArgs a;
+        dsocr::DecGemvArgs a;
         a.M = M; a.N = N; a.K = K; a.x = x; a.ldx = K; a.W = W; a.ldw = K; a.wdtype = wdtype; a.bias = bias;
-        a.y = y; a.ldy = N; a.act = act; a.accumulate = accumulate;
-        dsocr::launch_gemv(a, nullptr);
+        a.y = y; a.ldy = N; a.act = act; a.accumulate = accumulate; a.norm_w = norm_w; a.eps = eps;
+        dsocr::launch_dec_gemv(a, nullptr);
         check_hip(hipGetLastError(), "gemv launch");
         check_hip(hipDeviceSynchronize(), "gemv");
     });
@@ -335,95 +342,105 @@ dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale,
         check_hip(e, "attention");
     });
 }
-dsocr_status dsocr_k_decode_attention(int B, int heads, int hd, int max_len, float scale, const float* q,
-                                      const float* kc, const float* vc, const int* lens, float* o) {
+dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, int rope_dim, int max_len, float scale,
+                                      const float* qkv, const float* cos, const float* sin, float* kc, float* vc,
+                                      const int* kv_pos, float* o) {
     return guarded([&] {
         if (hd != 32 && hd != 64 && hd != 128) throw std::runtime_error("EINVAL: head_dim must be 32, 64 or 128");
+        if (kv_heads <= 0 || heads % kv_heads || rope_dim > hd || rope_dim % 2)
+            throw std::runtime_error("EINVAL: bad head / rope configuration");
         float* part = nullptr;
-        check_hip(hipMalloc(&part, dsocr::decode_attention_workspace(B, heads, hd, max_len)), "hipMalloc");
-        dsocr::DecodeAttnArgs a;
-        a.q = q; a.q_row_stride = (long)heads * hd; a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd;
-        a.page_stride = (long)heads * max_len * hd; a.lens = lens; a.B = B; a.heads = heads; a.hd = hd;
-        a.max_len = max_len; a.scale = scale; a.part = part; a.o = o; a.o_row_stride = (long)heads * hd;
-        dsocr::launch_decode_attention(a, nullptr);
+        int* cnt = nullptr;
+        check_hip(hipMalloc(&part, dsocr::dec_attn_workspace(B, heads, hd, max_len)), "hipMalloc");
+        check_hip(hipMalloc(&cnt, sizeof(int) * B * heads), "hipMalloc");
+        check_hip(hipMemset(cnt, 0, sizeof(int) * B * heads), "hipMemset");
+        dsocr::DecAttn2Args a;
+        a.qkv = qkv; a.ld = (long)(heads + 2 * kv_heads) * hd; a.kv_pos = kv_pos; a.B = B; a.heads = heads;
+        a.kv_heads = kv_heads; a.hd = hd; a.rope_dim = rope_dim; a.use_mla = 0; a.max_len = max_len;
+        a.cos = cos; a.sin = sin; a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd;
+        a.page_stride = (long)kv_heads * max_len * hd; a.scale = scale; a.part = part; a.o = o;
+        a.o_ld = (long)heads * hd; a.counters = cnt;
+        dsocr::launch_dec_attn(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
         hipFree(part);
+        hipFree(cnt);
         check_hip(e, "decode attention");
     });
 }
-dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const void* router,
-                         const void* Wgu, const void* Wd, const void* sWgu, const void* sWd, int wdtype,
-                         int norm_topk, float scaling, float* out, int* ids_out, float* w_out) {
+dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const float* norm_w,
+                         float eps, const void* router, const void* Wgu, const void* Wd, const void* sWgu,
+                         const void* sWd, int wdtype, int norm_topk, float scaling, float* out, int* ids_out,
+                         float* w_out) {
     return guarded([&] {
         if (H % 8 || I % 8 || (Is && Is % 8)) throw std::runtime_error("EINVAL: dims must be multiples of 8");
-        if (E > 256 || topk > 8 || topk > E) throw std::runtime_error("EINVAL: E <= 256 and topk <= min(8, E)");
+        if (E > 256 || topk > 8 || topk > E || T * topk > 512)
+            throw std::runtime_error("EINVAL: E <= 256, topk <= min(8, E), T*topk <= 512");
         const int TK = T * topk;
-        float *log, *wts, *hh, *y, *hs = nullptr, *ys = nullptr;
-        int *ids, *eoff, *arow, *apos, *iota, *deoff;
-        auto alloc = [&](void** p, size_t b) { check_hip(hipMalloc(p, b ? b : 16), "hipMalloc"); };
-        alloc((void**)&log, sizeof(float) * T * E);
-        alloc((void**)&wts, sizeof(float) * TK);
-        alloc((void**)&hh, sizeof(float) * (size_t)TK * I);
-        alloc((void**)&y, sizeof(float) * (size_t)TK * H);
-        alloc((void**)&ids, sizeof(int) * TK);
-        alloc((void**)&eoff, sizeof(int) * (E + 1));
-        alloc((void**)&arow, sizeof(int) * TK);
-        alloc((void**)&apos, sizeof(int) * TK);
-        alloc((void**)&iota, sizeof(int) * T);
-        alloc((void**)&deoff, sizeof(int) * 2);
-        std::vector<int> hi(T);
-        for (int i = 0; i < T; ++i) hi[i] = i;
-        int he[2] = {0, T};
-        check_hip(hipMemcpy(iota, hi.data(), sizeof(int) * T, hipMemcpyHostToDevice), "memcpy");
-        check_hip(hipMemcpy(deoff, he, sizeof(he), hipMemcpyHostToDevice), "memcpy");
-        dsocr::GemvArgs ra;
-        ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
-        ra.y = log; ra.ldy = E;
-        dsocr::launch_gemv(ra, nullptr);
-        dsocr::launch_router_topk(log, T, E, topk, 1, norm_topk, scaling, ids, wts, nullptr);
-        dsocr::launch_moe_group(ids, T, topk, E, eoff, arow, apos, nullptr, nullptr);
-        dsocr::MoeDecodeArgs m;
-        m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H; m.x = x; m.eoff = eoff; m.arow = arow;
-        m.Wgu = Wgu; m.Wd = Wd; m.wdtype = wdtype; m.h = hh; m.y = y; m.max_rows_per_expert = T == 1 ? 1 : 4;
-        dsocr::launch_moe_gateup_gemv(m, nullptr);
-        dsocr::launch_moe_down_gemv(m, nullptr);
-        if (sWgu && sWd && Is > 0) {
-            alloc((void**)&hs, sizeof(float) * (size_t)T * Is);
-            alloc((void**)&ys, sizeof(float) * (size_t)T * H);
-            dsocr::MoeDecodeArgs s;
-            s.T = T; s.topk = 1; s.E = 1; s.K = H; s.I = Is; s.Hout = H; s.x = x; s.eoff = deoff; s.arow = iota;
-            s.Wgu = sWgu; s.Wd = sWd; s.wdtype = wdtype; s.h = hs; s.y = ys; s.max_rows_per_expert = T;
-            dsocr::launch_moe_gateup_gemv(s, nullptr);
-            dsocr::launch_moe_down_gemv(s, nullptr);
+        std::vector<void*> bufs;
+        auto alloc = [&](size_t b) {
+            void* p = nullptr;
+            check_hip(hipMalloc(&p, b ? b : 16), "hipMalloc");
+            bufs.push_back(p);
+            return p;
+        };
+        dsocr::MoeRouteArgs r;
+        if (dsocr::moe_router_fused_ok(T, E, H)) {
+            r.x = x; r.norm_w = norm_w; r.eps = eps; r.router = router; r.Kdim = H; r.wdtype = wdtype;
+        } else {
+            float* log = (float*)alloc(sizeof(float) * T * E);
+            dsocr::DecGemvArgs ra;
+            ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
+            ra.y = log; ra.ldy = E; ra.norm_w = norm_w; ra.eps = eps;
+            dsocr::launch_dec_gemv(ra, nullptr);
+            r.logits = log;
         }
-        dsocr::launch_moe_combine(y, apos, wts, ys, T, topk, H, out, 1, nullptr);
+        r.T = T; r.E = E; r.topk = topk; r.softmax_scoring = 1; r.norm_topk = norm_topk;
+        r.scaling = scaling;
+        r.ids = (int*)alloc(sizeof(int) * TK); r.w = (float*)alloc(sizeof(float) * TK);
+        r.eoff = (int*)alloc(sizeof(int) * (E + 1)); r.arow = (int*)alloc(sizeof(int) * TK);
+        r.apos = (int*)alloc(sizeof(int) * TK); r.active = (int*)alloc(sizeof(int) * E);
+        r.aw = (float*)alloc(sizeof(float) * TK);
+        r.n_active = (int*)alloc(sizeof(int));
+        dsocr::launch_moe_route(r, nullptr);
+        dsocr::MoeDec2Args m;
+        m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H; m.slots = std::min(E, TK);
+        m.x = x; m.norm_w = norm_w; m.eps = eps;
+        m.eoff = r.eoff; m.arow = r.arow; m.apos = r.apos; m.ids = r.ids; m.active = r.active; m.n_active = r.n_active;
+        m.aw = r.aw; m.Wgu = Wgu; m.Wd = Wd; m.wdtype = wdtype; m.out = out;
+        m.h = (float*)alloc(sizeof(float) * (size_t)TK * I);
+        if (sWgu && sWd && Is > 0) {
+            m.Is = Is; m.sWgu = sWgu; m.sWd = sWd; m.hs = (float*)alloc(sizeof(float) * (size_t)T * Is);
+        }
+        dsocr::launch_moe_gateup2(m, nullptr);
+        dsocr::launch_moe_down2(m, nullptr);
         hipError_t e = hipDeviceSynchronize();
-        if (e == hipSuccess && ids_out) e = hipMemcpy(ids_out, ids, sizeof(int) * TK, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && w_out) e = hipMemcpy(w_out, wts, sizeof(float) * TK, hipMemcpyDeviceToHost);
-        for (void* p : {(void*)log, (void*)wts, (void*)hh, (void*)y, (void*)ids, (void*)eoff, (void*)arow, (void*)apos,
-                        (void*)iota, (void*)deoff, (void*)hs, (void*)ys})
-            if (p) hipFree(p);
+        if (e == hipSuccess && ids_out) e = hipMemcpy(ids_out, r.ids, sizeof(int) * TK, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && w_out) e = hipMemcpy(w_out, r.w, sizeof(float) * TK, hipMemcpyDeviceToHost);
+        for (void* p : bufs) (void)hipFree(p);
         check_hip(e, "moe");
     });
 }
 dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,
                                    int ngram, float rep_penalty, int* out_tok) {
     return guarded([&] {
-        const int cap = 256;
-        const int rb = (int)dsocr::sample_workspace_blocks(V);
-        int *banned, *cnt, *ridx;
+        const int rb = (int)dsocr::dec_sample_blocks(V);
+        int *ridx, *done;
         float* rval;
-        check_hip(hipMalloc(&banned, sizeof(int) * B * cap), "hipMalloc");
-        check_hip(hipMalloc(&cnt, sizeof(int) * B), "hipMalloc");
         check_hip(hipMalloc(&ridx, sizeof(int) * B * rb), "hipMalloc");
         check_hip(hipMalloc(&rval, sizeof(float) * B * rb), "hipMalloc");
-        dsocr::SampleArgs a;
-        a.logits = logits; a.B = B; a.V = V; a.ld = V; a.ctx = ctx; a.ctx_cap = ctx_cap; a.ctx_len = ctx_len;
-        a.ngram = ngram; a.rep_penalty = rep_penalty; a.banned = banned; a.banned_cnt = cnt; a.banned_cap = cap;
-        a.red_val = rval; a.red_idx = ridx; a.red_blocks = rb; a.out_tok = out_tok;
-        dsocr::launch_sample_greedy(a, nullptr);
+        check_hip(hipMalloc(&done, sizeof(int) * B), "hipMalloc");
+        check_hip(hipMemset(done, 0, sizeof(int) * B), "hipMemset");
+        dsocr::SampleArgs p;
+        p.logits = logits; p.B = B; p.V = V; p.ld = V; p.ctx = ctx; p.ctx_cap = ctx_cap; p.ctx_len = ctx_len;
+        p.rep_penalty = rep_penalty;
+        dsocr::launch_rep_penalty(p, nullptr);
+        dsocr::DecSampleArgs a;  // selection only: no bookkeeping buffers
+        a.logits = logits; a.B = B; a.V = V; a.ld = V; a.ctx = const_cast<int*>(ctx); a.ctx_cap = ctx_cap;
+        a.ctx_len = const_cast<int*>(ctx_len); a.ngram = ngram; a.red_val = rval; a.red_idx = ridx;
+        a.out_tok = out_tok; a.done = done;
+        dsocr::launch_dec_sample(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
-        hipFree(banned); hipFree(cnt); hipFree(ridx); hipFree(rval);
+        hipFree(ridx); hipFree(rval); hipFree(done);
         check_hip(e, "sample");
     });
 }

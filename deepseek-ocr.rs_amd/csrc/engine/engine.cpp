@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <sstream>
 
 #include "../common/host_util.hpp"
@@ -427,10 +428,10 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
 void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int ldy, int act, int accumulate,
                     const int* c_rows) {
     if (M <= 16 && !c_rows) {
-        GemvArgs a;
+        DecGemvArgs a;
         a.M = M; a.N = l.N; a.K = l.K; a.x = x; a.ldx = ldx; a.W = l.W; a.ldw = l.K; a.wdtype = l.wdt;
         a.bias = l.b; a.y = y; a.ldy = ldy; a.act = act; a.accumulate = accumulate;
-        launch_gemv(a, stream_);
+        launch_dec_gemv(a, stream_);
     } else {
         GemmArgs g;
         g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.wdtype = l.wdt;
@@ -765,83 +766,111 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
 }
 
 void Engine::decode_step(int B, int Lmax) {
+    // One token for each of B pages: 8 launches per layer (decode.hip).  For B <= 2 the
+    // RMSNorms are fused into the consuming GEMV / expert kernels (x normalised on the fly).
     const LangConfig& L = cfg_.lang;
     hipStream_t st = stream_;
     const int H = L.hidden, hd = L.head_dim;
+    const bool fuse_norm = B <= 2;
     float* X = wsf("s_x", (size_t)B * H);
     float* XN = wsf("s_xn", (size_t)B * H);
     int* kv_pos = wsi("s_kvpos", B);
-    int* kv_len = wsi("s_kvlen", B);
     float* CTX = wsf("s_ctx", (size_t)B * H);
-    float* part = wsf("s_part", decode_attention_workspace(B, L.heads, hd, Lmax) / 4 + 16);
+    float* part = wsf("s_part", dec_attn_workspace(B, L.heads, hd, Lmax) / 4 + 16);
+    if (L.heads % L.kv_heads) throw std::runtime_error("EINVAL: num_attention_heads must be a multiple of num_key_value_heads");
     for (int l = 0; l < L.layers; ++l) {
         DecLayer& d = layers_[l];
         const int QKVN = d.qkv.N;
         float* QKV = wsf("s_qkv", (size_t)B * QKVN);
         const long layer_kv = (long)B * page_stride_;
-        float* kc = kc_ + (long)l * layer_kv;
-        float* vc = vc_ + (long)l * layer_kv;
-        launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st);
-        linear(XN, B, H, d.qkv, QKV, QKVN);
-        RopeKvArgs r;
-        r.qkv = QKV; r.ld = QKVN; r.rows = B; r.row_page = iota_; r.row_pos = kv_pos;
-        r.heads = L.heads; r.kv_heads = L.kv_heads; r.hd = hd; r.rope_dim = L.rope_dim; r.use_mla = L.use_mla;
-        r.cos = rope_cos_; r.sin = rope_sin_; r.kc = kc; r.vc = vc; r.page_stride = page_stride_;
-        r.head_stride = head_stride_;
-        launch_rope_kv(r, st);
-        if (L.kv_heads != L.heads) throw std::runtime_error("EINVAL: decode path requires num_key_value_heads == num_attention_heads");
-        DecodeAttnArgs da;
-        da.q = QKV; da.q_row_stride = QKVN; da.kc = kc; da.vc = vc; da.page_stride = page_stride_;
-        da.head_stride = head_stride_; da.lens = kv_len; da.B = B; da.heads = L.heads; da.hd = hd; da.max_len = Lmax;
-        da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_row_stride = H;
-        launch_decode_attention(da, st);
-        linear(CTX, B, H, d.o, X, H, 0, 1);
-        launch_rmsnorm(X, H, XN, H, B, H, d.post_norm.w, L.rms_eps, st);
+        // attention: [norm] qkv -> rope + append + flash-decoding -> o_proj + residual
+        DecGemvArgs g;
+        g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
+        g.y = QKV; g.ldy = QKVN;
+        if (fuse_norm) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
+        else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
+        launch_dec_gemv(g, st);
+        DecAttn2Args da;
+        da.qkv = QKV; da.ld = QKVN; da.kv_pos = kv_pos; da.B = B; da.heads = L.heads; da.kv_heads = L.kv_heads;
+        da.hd = hd; da.rope_dim = L.rope_dim; da.use_mla = L.use_mla; da.max_len = Lmax;
+        da.cos = rope_cos_; da.sin = rope_sin_;
+        da.kc = kc_ + (long)l * layer_kv; da.vc = vc_ + (long)l * layer_kv;
+        da.page_stride = page_stride_; da.head_stride = head_stride_;
+        da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
+        da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
+        launch_dec_attn(da, st);
+        DecGemvArgs go;
+        go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
+        go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
+        launch_dec_gemv(go, st);
+        // MLP / MoE
+        const float* mx = X;
+        const float* mnorm = d.post_norm.w;
+        if (!fuse_norm) { launch_rmsnorm(X, H, XN, H, B, H, d.post_norm.w, L.rms_eps, st); mx = XN; mnorm = nullptr; }
+        MoeDec2Args m;
+        m.T = B; m.K = H; m.Hout = H; m.x = mx; m.norm_w = mnorm; m.eps = L.rms_eps; m.out = X;
         if (!d.moe) {
-            const int I = L.inter;
-            float* HH = wsf("s_hh", (size_t)B * I);
-            float* YD = wsf("s_yd", (size_t)B * H);
-            MoeDecodeArgs m;
-            m.T = B; m.topk = 1; m.E = 1; m.K = H; m.I = I; m.Hout = H; m.x = XN; m.eoff = wsi("s_dense_eoff", 2);
-            m.arow = iota_; m.Wgu = d.gu.W; m.Wd = d.down.W; m.wdtype = d.gu.wdt; m.h = HH; m.y = YD;
-            m.max_rows_per_expert = B;
-            launch_moe_gateup_gemv(m, st);
-            launch_moe_down_gemv(m, st);
-            launch_moe_combine(YD, iota_, ones_, nullptr, B, 1, H, X, 1, st);
+            m.topk = 0; m.E = 0; m.slots = 0; m.I = 8; m.Is = L.inter;
+            m.sWgu = d.gu.W; m.sWd = d.down.W; m.wdtype = d.gu.wdt;
+            m.hs = wsf("s_hh", (size_t)B * L.inter);
+            m.n_active = wsi("s_nact", 1);
+            launch_moe_gateup2(m, st);
+            launch_moe_down2(m, st);
             continue;
         }
         const int E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
-        float* LOG = wsf("s_log", (size_t)B * E);
-        int* IDS = wsi("s_ids", TK);
-        float* WTS = wsf("s_wts", TK);
-        int* EOFF = wsi("s_eoff", E + 1);
-        int* AROW = wsi("s_arow", TK);
-        int* APOS = wsi("s_apos", TK);
-        float* HH = wsf("s_ehh", (size_t)TK * I);
-        float* Y = wsf("s_ey", (size_t)TK * H);
-        linear(XN, B, H, d.router, LOG, E);
-        launch_router_topk(LOG, B, E, K, L.scoring == "softmax", L.norm_topk, L.routed_scaling, IDS, WTS, st);
-        launch_moe_group(IDS, B, K, E, EOFF, AROW, APOS, nullptr, st);
-        MoeDecodeArgs m;
-        m.T = B; m.topk = K; m.E = E; m.K = H; m.I = I; m.Hout = H; m.x = XN; m.eoff = EOFF; m.arow = AROW;
-        m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt; m.h = HH; m.y = Y;
-        m.max_rows_per_expert = B == 1 ? 1 : 4;
-        launch_moe_gateup_gemv(m, st);
-        launch_moe_down_gemv(m, st);
-        float* YS = nullptr;
-        if (d.has_shared) {
-            const int Is = d.s_d.K;
-            float* HS = wsf("s_shh", (size_t)B * Is);
-            YS = wsf("s_sy", (size_t)B * H);
-            MoeDecodeArgs s;
-            s.T = B; s.topk = 1; s.E = 1; s.K = H; s.I = Is; s.Hout = H; s.x = XN; s.eoff = wsi("s_dense_eoff", 2);
-            s.arow = iota_; s.Wgu = d.s_gu.W; s.Wd = d.s_d.W; s.wdtype = d.s_gu.wdt; s.h = HS; s.y = YS;
-            s.max_rows_per_expert = B;
-            launch_moe_gateup_gemv(s, st);
-            launch_moe_down_gemv(s, st);
+        if (TK > 512 || E > 256 || K > 8) throw std::runtime_error("EINVAL: decode MoE supports batch*top_k <= 512, <= 256 experts, top_k <= 8");
+        MoeRouteArgs ra;
+        ra.T = B; ra.E = E; ra.topk = K; ra.softmax_scoring = L.scoring == "softmax";
+        ra.norm_topk = L.norm_topk; ra.scaling = L.routed_scaling;
+        ra.ids = wsi("s_ids", TK); ra.w = wsf("s_wts", TK); ra.eoff = wsi("s_eoff", E + 1);
+        ra.arow = wsi("s_arow", TK); ra.apos = wsi("s_apos", TK); ra.aw = wsf("s_aw", TK);
+        ra.active = wsi("s_active", E);
+        ra.n_active = wsi("s_nact", 1);
+        if (getenv("DSOCR_FUSED_ROUTER") && moe_router_fused_ok(B, E, H)) {  // one-block variant (slower on MI355X)
+            ra.x = mx; ra.norm_w = mnorm; ra.eps = L.rms_eps; ra.router = d.router.W; ra.bias = d.router.b;
+            ra.Kdim = H; ra.wdtype = d.router.wdt;
+        } else {
+            float* LOG = wsf("s_log", (size_t)B * E);
+            DecGemvArgs gr;
+            gr.M = B; gr.N = E; gr.K = H; gr.x = mx; gr.ldx = H; gr.W = d.router.W; gr.ldw = H; gr.wdtype = d.router.wdt;
+            gr.bias = d.router.b; gr.y = LOG; gr.ldy = E; gr.norm_w = mnorm; gr.eps = L.rms_eps;
+            launch_dec_gemv(gr, st);
+            ra.logits = LOG;
         }
-        launch_moe_combine(Y, APOS, WTS, YS, B, K, H, X, 1, st);
+        launch_moe_route(ra, st);
+        m.topk = K; m.E = E; m.I = I; m.slots = std::min(E, TK);
+        m.eoff = ra.eoff; m.arow = ra.arow; m.apos = ra.apos; m.ids = ra.ids; m.active = ra.active;
+        m.n_active = ra.n_active; m.aw = ra.aw;
+        m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
+        m.h = wsf("s_ehh", (size_t)TK * I);
+        if (d.has_shared) {
+            if (d.s_gu.wdt != d.e_wdt) throw std::runtime_error("EINTERNAL: shared/routed expert dtype mismatch");
+            m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is);
+        }
+        launch_moe_gateup2(m, st);
+        launch_moe_down2(m, st);
     }
+}
+
+// final norm + lm_head + greedy selection + step bookkeeping for the B decode rows in s_x
+void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
+    const LangConfig& L = cfg_.lang;
+    hipStream_t st = stream_;
+    const int H = L.hidden;
+    float* SX = wsf("s_x", (size_t)B * H);
+    DecGemvArgs g;
+    g.M = B; g.N = L.vocab; g.K = H; g.W = lm_head_.W; g.ldw = H; g.wdtype = lm_head_.wdt; g.bias = lm_head_.b;
+    g.y = const_cast<float*>(sa.logits); g.ldy = L.vocab;
+    if (B <= 2) { g.x = SX; g.ldx = H; g.norm_w = final_norm_; g.eps = L.rms_eps; }
+    else {
+        float* SXN = wsf("s_xn", (size_t)B * H);
+        launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+        g.x = SXN; g.ldx = H;
+    }
+    launch_dec_gemv(g, st);
+    launch_rep_penalty(pen, st);
+    launch_dec_sample(sa, st);
 }
 
 // ============================================================================ generate
@@ -1005,6 +1034,8 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     const size_t kv_need = (size_t)L.layers * B * page_stride_ * 4;
     kc_ = wsf("kv_k", kv_need / 4);
     vc_ = wsf("kv_v", kv_need / 4);
+    // arrival tickets of the decode-attention combine: zero here, every launch leaves them zero
+    HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     const int QKVN = layers_[0].qkv.N;
     r0 = 0;
     for (int b = 0; b < B; ++b) {
@@ -1068,31 +1099,36 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     int* d_outlen = upload("s_outlen", zeros);
     int* d_out = wsi("s_out", (size_t)B * p.max_new);
     int* d_tok = wsi("s_tok", B);
-    {
-        std::vector<int> de = {0, B};
-        upload("s_dense_eoff", de);
-    }
-    const int banned_cap = 64;
-    SampleArgs sa;
+    // penalty (applied in place to the logits when != 1) + fused greedy selection
+    SampleArgs pen;
+    pen.logits = LOGITS; pen.B = B; pen.V = L.vocab; pen.ld = L.vocab; pen.ctx = d_ctx; pen.ctx_cap = ctx_cap;
+    pen.ctx_len = d_ctx_len; pen.rep_penalty = p.rep_penalty;
+    DecSampleArgs sa;
     sa.logits = LOGITS; sa.B = B; sa.V = L.vocab; sa.ld = L.vocab; sa.ctx = d_ctx; sa.ctx_cap = ctx_cap;
-    sa.ctx_len = d_ctx_len; sa.ngram = p.ngram; sa.rep_penalty = p.rep_penalty;
-    sa.banned = wsi("s_banned", (size_t)B * banned_cap); sa.banned_cnt = wsi("s_banned_cnt", B);
-    sa.banned_cap = banned_cap;
-    sa.red_blocks = (int)sample_workspace_blocks(L.vocab);
+    sa.ctx_len = d_ctx_len; sa.ngram = p.ngram;
+    sa.red_blocks = (int)dec_sample_blocks(L.vocab);
     sa.red_val = wsf("s_redv", (size_t)B * sa.red_blocks); sa.red_idx = wsi("s_redi", (size_t)B * sa.red_blocks);
-    sa.out_tok = d_tok;
-    const int eos = p.ignore_eos ? -1 : (int)p.eos;
-    launch_sample_greedy(sa, st);
-    launch_step_update(d_tok, B, d_ctx, ctx_cap, d_ctx_len, d_out, d_outlen, (long)p.max_new, d_done, eos, embed_,
-                       embed_dt_, H, SX, st);
+    sa.out_tok = d_tok; sa.out_ids = d_out; sa.out_len = d_outlen; sa.out_cap = (long)p.max_new; sa.done = d_done;
+    sa.eos = p.ignore_eos ? -1 : (int)p.eos;
+    sa.table = embed_; sa.table_dt = embed_dt_; sa.H = H; sa.x_next = SX; sa.kv_pos = d_kvpos; sa.kv_len = d_kvlen;
+    // the fused selection kernel advances the KV position; after the prefill the first
+    // decode position must be P, so start one behind
+    launch_rep_penalty(pen, st);
+    {
+        std::vector<int> pm1(B), lm1(B);
+        for (int b = 0; b < B; ++b) { pm1[b] = kvpos[b] - 1; lm1[b] = kvlen[b] - 1; }
+        HIP_CHECK(hipMemcpyAsync(d_kvpos, pm1.data(), B * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d_kvlen, lm1.data(), B * 4, hipMemcpyHostToDevice, st));
+        launch_dec_sample(sa, st);
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
     HIP_CHECK(hipEventRecord(ev[3], st));
 
-    // make sure every decode workspace exists before capture
-    decode_step(B, Lmax);  // dry build of buffers is not allowed to run; we capture below instead
-    // (the call above allocated workspaces and ran a real step; undo by re-initialising state)
+    // make sure every decode workspace exists before capture: a dry step allocates them
+    // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
+    decode_step(B, Lmax);
     HIP_CHECK(hipMemcpyAsync(d_kvpos, kvpos.data(), B * 4, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_kvlen, kvlen.data(), B * 4, hipMemcpyHostToDevice, st));
-    // the dry step overwrote X (=SX); restore the step-0 token embedding
     launch_embed_tokens(embed_, embed_dt_, d_tok, B, H, SX, H, st);
     HIP_CHECK(hipStreamSynchronize(st));
 
@@ -1102,12 +1138,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     const bool use_graph = !(getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0);
     auto step_body = [&]() {
         decode_step(B, Lmax);
-        launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
-        linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
-        launch_sample_greedy(sa, st);
-        launch_step_advance(d_kvpos, d_kvlen, B, st);
-        launch_step_update(d_tok, B, d_ctx, ctx_cap, d_ctx_len, d_out, d_outlen, (long)p.max_new, d_done, eos, embed_,
-                           embed_dt_, H, SX, st);
+        decode_head(B, sa, pen);
     };
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
@@ -1164,56 +1195,118 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     timings_.generate_ms = ms_between(ev[2], ev[3]) + ms_between(ev[4], ev[5]);
     timings_.steps = steps;
     last_B_ = B;
+    last_Lmax_ = Lmax;
     (void)t0;
     for (auto& e : ev) (void)hipEventDestroy(e);
     return out;
 }
 
-Engine::MoeProfile Engine::profile_decode_moe(int iters) {
-    MoeProfile prof;
+Engine::DecodeProfile Engine::profile_decode(int iters) {
+    DecodeProfile prof;
     const LangConfig& L = cfg_.lang;
-    const int B = last_B_;
-    if (B == 0 || L.n_routed == 0) throw std::runtime_error("EINVAL: run a generate() first");
-    const int E = L.n_routed, K = L.topk, I = L.moe_inter, H = L.hidden, TK = B * K;
+    const int B = last_B_, Lmax = last_Lmax_;
+    if (B == 0 || Lmax == 0) throw std::runtime_error("EINVAL: run a generate() first");
+    const int H = L.hidden, hd = L.head_dim;
     hipStream_t st = stream_;
-    int* EOFF = wsi("s_eoff", E + 1);
-    std::vector<int> eoff(E + 1);
-    HIP_CHECK(hipMemcpyAsync(eoff.data(), EOFF, (E + 1) * 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    for (int e = 0; e < E; ++e) prof.experts_touched += eoff[e + 1] > eoff[e] ? 1 : 0;
-    std::vector<hipEvent_t> evs;
+    std::vector<int> kvpos(B);
+    HIP_CHECK(hipMemcpy(kvpos.data(), wsi("s_kvpos", B), B * 4, hipMemcpyDeviceToHost));
+    // the replays re-run the last decoded position (pos - 1): its K/V slot is rewritten with the same values
+    std::vector<int> pm1(B);
+    long keys = 0;
+    for (int b = 0; b < B; ++b) { pm1[b] = std::max(0, kvpos[b] - 1); keys += pm1[b] + 1; }
+    int* d_pos = wsi("p_kvpos", B);
+    HIP_CHECK(hipMemcpy(d_pos, pm1.data(), B * 4, hipMemcpyHostToDevice));
+    prof.tokens = B;
+    prof.kv_len = pm1[0] + 1;
+    auto timed = [&](KernelProfile& kp, int n, const std::function<void(int)>& body) {
+        std::vector<hipEvent_t> evs(2 * n);
+        for (auto& e : evs) HIP_CHECK(hipEventCreate(&e));
+        for (int i = 0; i < n; ++i) {
+            HIP_CHECK(hipEventRecord(evs[2 * i], st));
+            body(i);
+            HIP_CHECK(hipEventRecord(evs[2 * i + 1], st));
+        }
+        HIP_CHECK(hipStreamSynchronize(st));
+        double total = 0;
+        for (int i = 0; i < n; ++i) total += ms_between(evs[2 * i], evs[2 * i + 1]);
+        for (auto& e : evs) (void)hipEventDestroy(e);
+        kp.avg_us = 1000.0 * total / n;
+        kp.launches = n;
+    };
     std::vector<int> moe_layers;
     for (int l = 0; l < L.layers; ++l)
         if (layers_[l].moe) moe_layers.push_back(l);
-    const int n = iters * (int)moe_layers.size();
-    evs.resize(2 * n);
-    for (auto& e : evs) HIP_CHECK(hipEventCreate(&e));
-    int k = 0;
-    for (int it = 0; it < iters; ++it)
-        for (int l : moe_layers) {  // rotating over layers (~450 MB) defeats the 256 MB Infinity Cache
+    if (!moe_layers.empty()) {
+        const int E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
+        std::vector<int> eoff(E + 1);
+        HIP_CHECK(hipMemcpy(eoff.data(), wsi("s_eoff", E + 1), (E + 1) * 4, hipMemcpyDeviceToHost));
+        for (int e = 0; e < E; ++e) prof.experts_touched += eoff[e + 1] > eoff[e] ? 1 : 0;
+        const float* Xc = wsf("s_x", (size_t)B * H);
+        // replay on a scratch copy of the residual stream so the engine state is untouched
+        float* Xs = wsf("p_x", (size_t)B * H);
+        HIP_CHECK(hipMemcpyAsync(Xs, Xc, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
+        auto args = [&](int l) {
             DecLayer& d = layers_[l];
-            MoeDecodeArgs m;
-            m.T = B; m.topk = K; m.E = E; m.K = H; m.I = I; m.Hout = H; m.x = wsf("s_xn", (size_t)B * H);
-            m.eoff = EOFF; m.arow = wsi("s_arow", TK); m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
-            m.h = wsf("s_ehh", (size_t)TK * I); m.y = wsf("s_ey", (size_t)TK * H);
-            m.max_rows_per_expert = B == 1 ? 1 : 4;
-            HIP_CHECK(hipEventRecord(evs[2 * k], st));
-            launch_moe_gateup_gemv(m, st);
-            launch_moe_down_gemv(m, st);
-            HIP_CHECK(hipEventRecord(evs[2 * k + 1], st));
-            ++k;
-        }
-    HIP_CHECK(hipStreamSynchronize(st));
-    double total = 0;
-    for (int i = 0; i < n; ++i) total += ms_between(evs[2 * i], evs[2 * i + 1]);
-    for (auto& e : evs) (void)hipEventDestroy(e);
-    const double wbytes = (double)prof.experts_touched * 3.0 * I * H * 2.0;  // fp16 gate+up+down of touched experts
-    const double abytes = (double)B * H * 4 + 2.0 * TK * I * 4 + (double)TK * H * 4 + (E + 1 + TK) * 4.0;
-    prof.avg_us = 1000.0 * total / n;
-    prof.bytes = wbytes + abytes;
-    prof.flops = 2.0 * TK * 3.0 * H * I;
-    prof.pairs = n;
-    prof.tokens = B;
+            MoeDec2Args m;
+            m.T = B; m.K = H; m.Hout = H; m.x = Xs; m.norm_w = B <= 2 ? d.post_norm.w : nullptr; m.eps = L.rms_eps;
+            m.out = Xs; m.topk = K; m.E = E; m.I = I; m.slots = std::min(E, TK);
+            m.eoff = wsi("s_eoff", E + 1); m.arow = wsi("s_arow", TK); m.apos = wsi("s_apos", TK);
+            m.ids = wsi("s_ids", TK); m.active = wsi("s_active", E); m.n_active = wsi("s_nact", 1);
+            m.aw = wsf("s_aw", TK); m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
+            m.h = wsf("s_ehh", (size_t)TK * I);
+            if (d.has_shared) { m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is); }
+            return m;
+        };
+        const int n = iters * (int)moe_layers.size();
+        // rotating over the layers (~55 MB each) defeats the 256 MB Infinity Cache
+        timed(prof.moe_gateup, n, [&](int i) { launch_moe_gateup2(args(moe_layers[i % moe_layers.size()]), st); });
+        timed(prof.moe_down, n, [&](int i) { launch_moe_down2(args(moe_layers[i % moe_layers.size()]), st); });
+        const DecLayer& d0 = layers_[moe_layers[0]];
+        const double Is = d0.has_shared ? d0.s_d.K : 0;
+        const double touched = (double)prof.experts_touched;
+        prof.moe_gateup.bytes = (touched * 2.0 * I + 2.0 * Is) * H * 2.0   // fp16 gate+up rows
+                                + (double)B * H * 4 + (double)(TK * I + B * Is) * 4;  // x in, h out
+        prof.moe_gateup.flops = 2.0 * (TK * 2.0 * I + B * 2.0 * Is) * H;
+        prof.moe_down.bytes = (touched * I + Is) * H * 2.0 + (double)(TK * I + B * Is) * 4 + 2.0 * B * H * 4;
+        prof.moe_down.flops = 2.0 * (TK * (double)I + B * Is) * H;
+    }
+    {
+        const int QKVN = layers_[0].qkv.N;
+        float* part = wsf("s_part", dec_attn_workspace(B, L.heads, hd, Lmax) / 4 + 16);
+        float* CTX = wsf("p_ctx", (size_t)B * H);
+        const int n = iters * L.layers;
+        timed(prof.attention, n, [&](int i) {
+            const int l = i % L.layers;
+            DecAttn2Args da;
+            da.qkv = wsf("s_qkv", (size_t)B * QKVN); da.ld = QKVN; da.kv_pos = d_pos; da.B = B; da.heads = L.heads;
+            da.kv_heads = L.kv_heads; da.hd = hd; da.rope_dim = L.rope_dim; da.use_mla = L.use_mla; da.max_len = Lmax;
+            da.cos = rope_cos_; da.sin = rope_sin_;
+            da.kc = kc_ + (long)l * B * page_stride_; da.vc = vc_ + (long)l * B * page_stride_;
+            da.page_stride = page_stride_; da.head_stride = head_stride_;
+            da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
+            da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
+            launch_dec_attn(da, st);
+        });
+        // K and V of every attended key (f32 cache) + q/k/v row + context out
+        prof.attention.bytes = (double)keys * L.kv_heads * hd * 4.0 * 2.0 + (double)B * (QKVN + H) * 4.0;
+        prof.attention.flops = 4.0 * keys * L.heads * hd;
+    }
+    {
+        float* LG = wsf("p_logits", (size_t)B * L.vocab);
+        const float* SX = wsf("s_x", (size_t)B * H);
+        float* SXN = wsf("p_xn", (size_t)B * H);
+        if (B > 2) launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+        timed(prof.lm_head, iters, [&](int) {
+            DecGemvArgs g;
+            g.M = B; g.N = L.vocab; g.K = H; g.W = lm_head_.W; g.ldw = H; g.wdtype = lm_head_.wdt; g.bias = lm_head_.b;
+            g.y = LG; g.ldy = L.vocab;
+            if (B <= 2) { g.x = SX; g.ldx = H; g.norm_w = final_norm_; g.eps = L.rms_eps; }
+            else { g.x = SXN; g.ldx = H; }
+            launch_dec_gemv(g, st);
+        });
+        prof.lm_head.bytes = (double)L.vocab * H * 2.0 + (double)B * (L.vocab + H) * 4.0;
+        prof.lm_head.flops = 2.0 * B * (double)L.vocab * H;
+    }
     return prof;
 }
 

@@ -124,11 +124,15 @@ class Engine {
     Timings last_timings() const { return timings_; }
     // Replays the decode MoE grouped GEMV (routed experts, gate/up + down) of every MoE
     // layer on the last decode step's routing, timing each launch pair with HIP events.
-    struct MoeProfile {
+    struct KernelProfile {
         double avg_us = 0, bytes = 0, flops = 0;
-        int pairs = 0, experts_touched = 0, tokens = 0;
+        int launches = 0;
     };
-    MoeProfile profile_decode_moe(int iters);
+    struct DecodeProfile {
+        KernelProfile moe_gateup, moe_down, attention, lm_head;
+        int experts_touched = 0, tokens = 0, kv_len = 0;
+    };
+    DecodeProfile profile_decode(int iters);
     hipStream_t stream() const { return stream_; }
 
   private:
@@ -159,6 +163,7 @@ class Engine {
     float* vision_pass(const float* imgs, int n, int S, const std::string& out);
     void prefill(int B, const std::vector<int>& rows_per_page, const float* x0, int Lmax);
     void decode_step(int B, int Lmax);
+    void decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen);
     void layer_forward_prefill(int l, int T, int B, const int* row_page, const int* row_pos, const long* q_off,
                                const long* kv_off, const long* o_off, const int* seq_len, int max_len, int Lmax);
 
@@ -193,6 +198,7 @@ class Engine {
     long page_stride_ = 0, head_stride_ = 0;
     Timings timings_;
     int last_B_ = 0;
+    int last_Lmax_ = 0;
 
     void* dev_alloc(size_t bytes);
     void ensure_rope(int len);

@@ -10,8 +10,8 @@
 //    Options: decomposed SAM rel-pos bias (sam.rs:1124-1192, never materialising
 //    [S,S]), causal masking (block.rs:1504-1526), variable sequence lengths.
 // 2. sam_relbias: per-query rel-pos dot products q.Rh / q.Rw.
-// 3. decode attention: flash-decoding over the per-page f32 KV cache.
-// 4. rope_kv: rotate_half RoPE (block.rs:1403-1471) + KV-cache append.
+// 3. rope_kv: rotate_half RoPE (block.rs:1403-1471) + KV-cache append (prefill rows;
+//    the decode step fuses both into dec_attn_kernel, decode.hip).
 #include "dev_common.hpp"
 #include "kernels.hpp"
 
@@ -196,123 +196,6 @@ void launch_sam_relbias(const float* q, long q_row_stride, int n_seq, int gh, in
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(sam_relbias_kernel, dim3((unsigned)blocks), dim3(256), 0, s, q, q_row_stride, n_seq, gh, gw,
                        heads, hd, Rh, Rw, out);
-}
-
-// ------------------------------------------------------------------ decode attention
-constexpr int DA_CH = 256;  // keys per block
-
-size_t decode_attention_workspace(int B, int heads, int hd, int max_len) {
-    int chunks = (max_len + DA_CH - 1) / DA_CH;
-    return (size_t)B * heads * chunks * (hd + 2) * sizeof(float);
-}
-
-template <int HD>
-__global__ __launch_bounds__(256) void decode_attn_partial(DecodeAttnArgs a) {
-    __shared__ float p_s[DA_CH];
-    __shared__ float red[8];
-    __shared__ float o_s[256 / HD][HD];
-    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int len = a.lens[b];
-    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
-    float* part = a.part + (((long)b * a.heads + h) * chunks + c) * (HD + 2);
-    const int k0 = c * DA_CH;
-    if (k0 >= len) return;
-    const int kn = min(DA_CH, len - k0);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float* q = a.q + (long)b * a.q_row_stride + (long)h * HD;
-    const float* Kc = a.kc + (long)b * a.page_stride + (long)h * a.head_stride;
-    const float* Vc = a.vc + (long)b * a.page_stride + (long)h * a.head_stride;
-
-    // scores: 8 lanes per key, 16 dims per lane
-    constexpr int LPK = 8, DPL = HD / LPK;
-    const int sub = lane & (LPK - 1), kin = lane / LPK;  // 8 keys per wave-iteration
-    float qv[DPL];
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) qv[i] = q[sub * DPL + i];
-    float lmax = -INFINITY;
-    for (int kk = wave * 8 + kin; kk < DA_CH; kk += 32) {
-        float acc = 0.f;
-        if (kk < kn) {
-            const float* kr = Kc + (long)(k0 + kk) * HD + sub * DPL;
-#pragma unroll
-            for (int i = 0; i < DPL; i += 4) {
-                float4 k4 = *reinterpret_cast<const float4*>(kr + i);
-                acc = fmaf(qv[i], k4.x, acc);
-                acc = fmaf(qv[i + 1], k4.y, acc);
-                acc = fmaf(qv[i + 2], k4.z, acc);
-                acc = fmaf(qv[i + 3], k4.w, acc);
-            }
-        }
-#pragma unroll
-        for (int o = 1; o < LPK; o <<= 1) acc += __shfl_xor(acc, o, 64);
-        float v = kk < kn ? acc * a.scale : -INFINITY;
-        if (sub == 0) p_s[kk] = v;
-        lmax = fmaxf(lmax, v);
-    }
-    lmax = wave_max(lmax);
-    if (lane == 0) red[wave] = lmax;
-    __syncthreads();
-    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    float lsum = 0.f;
-    for (int kk = tid; kk < DA_CH; kk += 256) {
-        float p = kk < kn ? expf(p_s[kk] - m) : 0.f;
-        p_s[kk] = p;
-        lsum += p;
-    }
-    lsum = wave_sum(lsum);
-    __syncthreads();
-    if (lane == 0) red[4 + wave] = lsum;
-    // PV: thread -> (dim d, key slice hh of nh = 256/HD slices)
-    const int d = tid % HD, hh = tid / HD;
-    constexpr int NH = 256 / HD;
-    float acc = 0.f;
-    for (int kk = hh; kk < kn; kk += NH) acc = fmaf(p_s[kk], Vc[(long)(k0 + kk) * HD + d], acc);
-    o_s[hh][d] = acc;
-    __syncthreads();
-    if (tid < HD) {
-        float o = 0.f;
-#pragma unroll
-        for (int j = 0; j < NH; ++j) o += o_s[j][tid];
-        part[2 + tid] = o;
-    }
-    if (tid == 0) {
-        part[0] = m;
-        part[1] = (red[4] + red[5]) + (red[6] + red[7]);
-    }
-}
-
-template <int HD>
-__global__ __launch_bounds__(HD) void decode_attn_combine(DecodeAttnArgs a) {
-    const int h = blockIdx.x, b = blockIdx.y;
-    const int len = a.lens[b];
-    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
-    const int nc = (len + DA_CH - 1) / DA_CH;
-    const float* part = a.part + ((long)b * a.heads + h) * chunks * (HD + 2);
-    float m = -INFINITY;
-    for (int c = 0; c < nc; ++c) m = fmaxf(m, part[c * (HD + 2)]);
-    float l = 0.f, acc = 0.f;
-    for (int c = 0; c < nc; ++c) {
-        const float* p = part + c * (HD + 2);
-        const float w = expf(p[0] - m);
-        l += p[1] * w;
-        acc += p[2 + threadIdx.x] * w;
-    }
-    a.o[(long)b * a.o_row_stride + (long)h * HD + threadIdx.x] = acc / l;
-}
-
-void launch_decode_attention(const DecodeAttnArgs& a, hipStream_t s) {
-    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
-    dim3 g1(chunks, a.heads, a.B), g2(a.heads, a.B);
-    if (a.hd == 128) {
-        hipLaunchKernelGGL(decode_attn_partial<128>, g1, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(decode_attn_combine<128>, g2, dim3(128), 0, s, a);
-    } else if (a.hd == 64) {
-        hipLaunchKernelGGL(decode_attn_partial<64>, g1, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(decode_attn_combine<64>, g2, dim3(64), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(decode_attn_partial<32>, g1, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(decode_attn_combine<32>, g2, dim3(32), 0, s, a);
-    }
 }
 
 // ------------------------------------------------------------------ RoPE + KV append

@@ -1,0 +1,1010 @@
+// Fused decode-step kernels (B pages x 1 token).  One decode step of the reference
+// (model/mod.rs:1977-2034 -> block.rs:124-191 x 12 -> lm_head -> select_token_id)
+// becomes 7 launches per layer instead of 15:
+//   dec_gemv (RMSNorm fused) -> dec_attn (RoPE + KV append + flash-decoding + combine)
+//   -> dec_gemv (o_proj + residual) -> dec_gemv (router, norm fused)
+//   -> moe_route (softmax top-k + grouping, one block) -> moe_gateup2 (routed + shared)
+//   -> moe_down2 (routed + shared + weighted combine + residual)
+// Every reduction keeps the reference's f32 order where it is observable
+// (top-k weighted sum in top-k order, then + shared, then the residual add).
+#include <algorithm>
+#include <stdexcept>
+
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+// ------------------------------------------------------------------ helpers
+// Dynamic LDS of the GEMV-type kernels: [XS_RED floats of row partial sums][M][K staged rows].
+constexpr int XS_RED = 128;  // >= M * (blockDim / 64)
+
+// Block-wide: stage M rows of x (row m = rows ? rows[m] : m, stride ldx) into LDS, RMS-normalised
+// when nw != null (rms_norm_slow, block.rs:24-29: x / sqrt(mean(x^2) + eps) * w).  Every
+// thread of the block must call it (two barriers).
+__device__ __forceinline__ void stage_rows(const float* x, long ldx, const int* rows, int M, int K, const float* nw,
+                                           float eps, float* smem) {
+    float* red = smem;
+    float* xs = smem + XS_RED;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwv = blockDim.x >> 6;
+    const int step = blockDim.x * 4;
+    if (nw) {
+        for (int m = 0; m < M; ++m) {
+            const float* xr = x + (long)(rows ? rows[m] : m) * ldx;
+            float q = 0.f;
+            for (int k = tid * 4; k < K; k += step) {
+                const float4 v = *reinterpret_cast<const float4*>(xr + k);
+                q += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+            }
+            q = wave_sum(q);
+            if (lane == 0) red[m * nwv + wave] = q;
+        }
+        __syncthreads();
+    }
+    for (int m = 0; m < M; ++m) {
+        const float* xr = x + (long)(rows ? rows[m] : m) * ldx;
+        float den = 1.f;
+        if (nw) {
+            float q = 0.f;
+            for (int w = 0; w < nwv; ++w) q += red[m * nwv + w];
+            den = sqrtf(q / (float)K + eps);
+        }
+        for (int k = tid * 4; k < K; k += step) {
+            float4 v = *reinterpret_cast<const float4*>(xr + k);
+            if (nw) {
+                const float4 w = *reinterpret_cast<const float4*>(nw + k);
+                v.x = (v.x / den) * w.x;
+                v.y = (v.y / den) * w.y;
+                v.z = (v.z / den) * w.z;
+                v.w = (v.w / den) * w.w;
+            }
+            *reinterpret_cast<float4*>(xs + m * K + k) = v;
+        }
+    }
+    __syncthreads();
+}
+
+// 8 consecutive f32 (LDS or global) into registers
+__device__ __forceinline__ void ld_x8(const float* xs, float* o) {
+    const float4 a = *reinterpret_cast<const float4*>(xs);
+    const float4 b = *reinterpret_cast<const float4*>(xs + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+static size_t stage_bytes(int M, int K) { return sizeof(float) * (XS_RED + (size_t)M * K); }
+constexpr size_t STAGE_LDS_MAX = 64 * 1024;
+
+// ------------------------------------------------------------------ dec_gemv
+// y[m][n] (+)= act(sum_k xn[m][k] W[n][k] + b[n]); xn = rmsnorm(x) if norm_w else x.
+// A wave owns RB rows.  Every lane issues its 16-byte weight loads for the first U*64
+// chunks BEFORE the block stages x through LDS, so the HBM latency of the weight
+// stream overlaps the norm prologue; K <= 64*U*8 is a single batch.
+template <typename WT, int MT, int RB, int U>
+__global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
+    extern __shared__ float smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = (blockIdx.x * 4 + wave) * RB;
+    const bool active = n0 < a.N;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    uint4 wq[U][RB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int n = min(n0 + r, a.N - 1);
+            wq[u][r] = (active && c < chunks) ? ldg_nt16(W + (long)n * a.ldw + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    stage_rows(a.x, a.ldx, nullptr, a.M, a.K, a.norm_w, a.eps, smem);
+    if (!active) return;
+    const float* xs = smem + XS_RED;
+    float acc[RB][MT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+    for (int base = 0;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = base + u * 64 + lane;
+            if (c < chunks) {
+                float w8[RB][8];
+#pragma unroll
+                for (int r = 0; r < RB; ++r) unpack8<WT>(wq[u][r], w8[r]);
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    if (m < a.M) {
+                        float xv[8];
+                        ld_x8(xs + m * a.K + (c << 3), xv);
+#pragma unroll
+                        for (int r = 0; r < RB; ++r)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) acc[r][m] = fmaf(xv[j], w8[r][j], acc[r][m]);
+                    }
+                }
+            }
+        }
+        base += 64 * U;
+        if (base >= chunks) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = base + u * 64 + lane;
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const int n = min(n0 + r, a.N - 1);
+                wq[u][r] = c < chunks ? ldg_nt16(W + (long)n * a.ldw + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            float v = wave_sum(acc[r][m]);
+            const int n = n0 + r;
+            if (lane == 0 && m < a.M && n < a.N) {
+                v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
+                float* yp = a.y + (long)m * a.ldy + n;
+                if (a.accumulate) v = *yp + v;
+                *yp = v;
+            }
+        }
+}
+
+template <typename WT, int MT>
+static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
+    const size_t lds = stage_bytes(a.M, a.K);
+    // small N: one row per wave so the whole matrix is in flight at once; large N: RB rows per wave
+    if (a.N <= 16384) {
+        constexpr int RB = 1;
+        hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
+    } else {
+        constexpr int RB = MT <= 2 ? 4 : 2;
+        hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
+    }
+}
+template <typename WT>
+static void dec_gemv_dispatch(const DecGemvArgs& a, hipStream_t s) {
+    if (a.M <= 1) dec_gemv_rb<WT, 1>(a, s);
+    else if (a.M <= 2) dec_gemv_rb<WT, 2>(a, s);
+    else if (a.M <= 4) dec_gemv_rb<WT, 4>(a, s);
+    else if (a.M <= 8) dec_gemv_rb<WT, 8>(a, s);
+    else dec_gemv_rb<WT, 16>(a, s);
+}
+void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
+    if (a.M == 0 || a.N == 0) return;
+    // rows per launch: <= 16 and the staged rows must fit the 64 KB dynamic LDS window
+    const int per = (int)std::min<size_t>(16, (STAGE_LDS_MAX - sizeof(float) * XS_RED) / (sizeof(float) * a.K));
+    if (per < 1) throw std::runtime_error("EINVAL: dec_gemv K too large for LDS staging");
+    for (int m0 = 0; m0 < a.M; m0 += per) {
+        DecGemvArgs p = a;
+        p.M = std::min(per, a.M - m0);
+        p.x = a.x + (long)m0 * a.ldx;
+        p.y = a.y + (long)m0 * a.ldy;
+        if (a.wdtype == WDT_BF16) dec_gemv_dispatch<bf16_t>(p, s);
+        else dec_gemv_dispatch<f16_t>(p, s);
+    }
+}
+
+// ------------------------------------------------------------------ decode attention
+// grid (chunks of 64 keys, heads, B).  The token being decoded sits at pos = kv_pos[b]:
+// q and k are rotated here (rotate_half RoPE, block.rs:1403-1471), the block owning
+// chunk pos/64 appends k,v to the f32 cache (block.rs:776-789) and uses them directly.
+// Each block issues its K and V cache loads first, then builds q; the block that
+// arrives last for a (page, head) merges the chunk partials (flash-decoding combine)
+// with one agent-scope release / acquire (cdna_hip_programming.md §5 split-K recipe).
+constexpr int DA2_CH = 64;
+
+__device__ __forceinline__ float rope_elem(const float* base, int d, int hd, int rd, int mla, const float* cs,
+                                           const float* sn) {
+    if (d >= rd) return base[d];
+    const int half = rd / 2;
+    auto xr = [&](int i) -> float {
+        if (!mla) return base[i];
+        return i < half ? base[2 * i] : base[2 * (i - half) + 1];
+    };
+    const float x = xr(d);
+    const float rot = d < half ? -xr(d + half) : xr(d - half);
+    return x * cs[d] + rot * sn[d];
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
+    constexpr int DPL = HD / 4;                                  // dims per lane when scoring (4 lanes / key)
+    constexpr int DG = HD / 4, KG = 256 / DG, KPG = DA2_CH / KG;  // PV: float4 dim groups x key groups
+    __shared__ float qs[HD];
+    __shared__ float knew[HD];
+    __shared__ float vnew[HD];
+    __shared__ float p_s[DA2_CH];
+    __shared__ float red[8];
+    __shared__ int last_s;
+    __shared__ float4 o_s[384];  // P.V partials; reused by the combine (m, l per chunk + per-group sums)
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int pos = a.kv_pos[b];
+    const int len = pos + 1;
+    const int k0 = c * DA2_CH;
+    if (k0 >= len) return;
+    const int kn = min(DA2_CH, len - k0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kvh = h / (a.heads / a.kv_heads);
+    float* Kc = a.kc + (long)b * a.page_stride + (long)kvh * a.head_stride;
+    float* Vc = a.vc + (long)b * a.page_stride + (long)kvh * a.head_stride;
+    // 1. cache loads for this thread's keys (the slot at pos is replaced by the new k / v below)
+    const int key = wave * 16 + (lane >> 2), sub = lane & 3;
+    float4 kreg[DPL / 4];
+    {
+        const bool ok = key < kn && k0 + key != pos;
+        const float4* kp = reinterpret_cast<const float4*>(Kc + (long)(k0 + key) * HD + sub * DPL);
+#pragma unroll
+        for (int i = 0; i < DPL / 4; ++i) kreg[i] = ok ? kp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int dg = tid % DG, kg = tid / DG;
+    float4 vreg[KPG];
+#pragma unroll
+    for (int j = 0; j < KPG; ++j) {
+        const int kk = k0 + kg * KPG + j;
+        vreg[j] = (kg * KPG + j < kn && kk != pos) ? *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // 2. rotated q (and the new k, v in the owning chunk)
+    const float* row = a.qkv + (long)b * a.ld;
+    const float* cs = a.cos + (long)pos * a.rope_dim;
+    const float* sn = a.sin + (long)pos * a.rope_dim;
+    const bool own = pos >= k0 && pos < k0 + DA2_CH;
+    if (tid < HD) {
+        qs[tid] = rope_elem(row + h * HD, tid, HD, a.rope_dim, a.use_mla, cs, sn);
+        if (own) {
+            const float* kr = row + a.heads * HD + kvh * HD;
+            const float* vr = row + (a.heads + a.kv_heads) * HD + kvh * HD;
+            const float kv = rope_elem(kr, tid, HD, a.rope_dim, a.use_mla, cs, sn);
+            const float vv = vr[tid];
+            knew[tid] = kv;
+            vnew[tid] = vv;
+            if (h == kvh * (a.heads / a.kv_heads)) {  // one writer per kv head
+                Kc[(long)pos * HD + tid] = kv;
+                Vc[(long)pos * HD + tid] = vv;
+            }
+        }
+    }
+    __syncthreads();
+    // 3. scores: wave w owns keys w*16 .. w*16+15
+    {
+        float acc = 0.f;
+        if (key < kn) {
+            if (k0 + key == pos) {
+#pragma unroll
+                for (int i = 0; i < DPL; ++i) acc = fmaf(qs[sub * DPL + i], knew[sub * DPL + i], acc);
+            } else {
+#pragma unroll
+                for (int i = 0; i < DPL / 4; ++i) {
+                    acc = fmaf(qs[sub * DPL + 4 * i + 0], kreg[i].x, acc);
+                    acc = fmaf(qs[sub * DPL + 4 * i + 1], kreg[i].y, acc);
+                    acc = fmaf(qs[sub * DPL + 4 * i + 2], kreg[i].z, acc);
+                    acc = fmaf(qs[sub * DPL + 4 * i + 3], kreg[i].w, acc);
+                }
+            }
+        }
+        acc += __shfl_xor(acc, 1, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        const float sc = key < kn ? acc * a.scale : -INFINITY;
+        if (sub == 0) p_s[key] = sc;
+        const float mw = wave_max(sc);
+        if (lane == 0) red[wave] = mw;
+    }
+    __syncthreads();
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (tid < DA2_CH) {
+        const float p = tid < kn ? expf(p_s[tid] - m) : 0.f;
+        p_s[tid] = p;
+        const float l = wave_sum(p);
+        if (tid == 0) red[4] = l;
+    }
+    __syncthreads();
+    // 4. P.V over this thread's KPG keys
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (own) {
+#pragma unroll
+        for (int j = 0; j < KPG; ++j)
+            if (k0 + kg * KPG + j == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < KPG; ++j) {
+        const float p = p_s[kg * KPG + j];
+        o.x = fmaf(p, vreg[j].x, o.x);
+        o.y = fmaf(p, vreg[j].y, o.y);
+        o.z = fmaf(p, vreg[j].z, o.z);
+        o.w = fmaf(p, vreg[j].w, o.w);
+    }
+    o_s[tid] = o;
+    __syncthreads();
+    const int chunks = (a.max_len + DA2_CH - 1) / DA2_CH;
+    float* part0 = a.part + ((long)b * a.heads + h) * chunks * (HD + 2);
+    float* part = part0 + (long)c * (HD + 2);
+    if (tid < DG) {
+        float4 t = o_s[tid];
+        for (int g = 1; g < KG; ++g) {
+            const float4 u = o_s[g * DG + tid];
+            t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        *reinterpret_cast<float4*>(part + 2 + tid * 4) = t;
+    }
+    if (tid == 0) {
+        part[0] = m;
+        part[1] = red[4];
+    }
+    // 5. arrival ticket; the last chunk block of (b, h) merges every partial
+    const int nc = (len + DA2_CH - 1) / DA2_CH;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int* cnt = a.counters + (long)b * a.heads + h;
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == nc - 1;
+        if (last) {
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    // every partial of (b, h) is loaded in parallel: chunk maxima / sums into LDS, then each
+    // of the 256/HD thread groups folds a strided subset of the chunks for its dim
+    float* ms = reinterpret_cast<float*>(o_s);
+    float* ls = ms + 512;
+    float* accp = ms + 1024;
+    float* lp = ms + 1280;
+    for (int cc = tid; cc < nc; cc += 256) {
+        ms[cc] = part0[cc * (HD + 2)];
+        ls[cc] = part0[cc * (HD + 2) + 1];
+    }
+    __syncthreads();
+    float mm = -INFINITY;
+    for (int cc = 0; cc < nc; ++cc) mm = fmaxf(mm, ms[cc]);
+    constexpr int KS = 256 / HD;
+    const int dim = tid % HD, grp = tid / HD;
+    float l = 0.f, acc = 0.f;
+#pragma unroll 4
+    for (int cc = grp; cc < nc; cc += KS) {
+        const float w = expf(ms[cc] - mm);
+        l += ls[cc] * w;
+        acc += part0[cc * (HD + 2) + 2 + dim] * w;
+    }
+    accp[grp * HD + dim] = acc;
+    lp[grp * HD + dim] = l;
+    __syncthreads();
+    if (tid < HD) {
+        float at = 0.f, lt = 0.f;
+#pragma unroll
+        for (int g = 0; g < KS; ++g) { at += accp[g * HD + tid]; lt += lp[g * HD + tid]; }
+        a.o[(long)b * a.o_ld + (long)h * HD + tid] = at / lt;
+    }
+}
+
+size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
+    return (size_t)B * heads * ((max_len + DA2_CH - 1) / DA2_CH) * (hd + 2) * sizeof(float);
+}
+
+void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
+    if (!a.counters) throw std::runtime_error("EINTERNAL: dec_attn needs a zeroed counter array");
+    if (a.max_len > 512 * DA2_CH) throw std::runtime_error("EINVAL: decode context longer than 32768 tokens");
+    const int chunks = (a.max_len + DA2_CH - 1) / DA2_CH;
+    dim3 g1(chunks, a.heads, a.B);
+    if (a.hd == 128) hipLaunchKernelGGL(dec_attn_kernel<128>, g1, dim3(256), 0, s, a);
+    else if (a.hd == 64) hipLaunchKernelGGL(dec_attn_kernel<64>, g1, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(dec_attn_kernel<32>, g1, dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ MoE routing (one block)
+// softmax (or sigmoid) + greedy top-k (stable, block.rs:1271-1301) per token, then
+// grouping: eoff[E+1], arow/apos/aw by sorted position, and the compact list of active
+// experts (block.rs:1303-1324 sorts on the host; here one block does it in LDS).
+constexpr int RT_MAXT = 64;  // tokens per routing block
+
+struct RouteLds {
+    int ids[RT_MAXT * 8];
+    float w[RT_MAXT * 8];
+    int cnt[257];
+    int cur[257];
+};
+
+// top-k of one token's E logits (lg in LDS or global) by one wave
+__device__ __forceinline__ void route_token(const MoeRouteArgs& a, const float* lg, int t, RouteLds& L) {
+    const int lane = threadIdx.x & 63, E = a.E, K = a.topk;
+    float sc[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = lane + 64 * j;
+        sc[j] = e < E ? lg[e] : -INFINITY;
+        mx = fmaxf(mx, sc[j]);
+    }
+    if (a.softmax_scoring) {
+        mx = wave_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = lane + 64 * j;
+            sc[j] = e < E ? expf(sc[j] - mx) : 0.f;
+            sum += sc[j];
+        }
+        sum = wave_sum(sum);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[j] = (lane + 64 * j) < E ? sc[j] / sum : -INFINITY;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[j] = (lane + 64 * j) < E ? 1.0f / (1.0f + expf(-sc[j])) : -INFINITY;
+    }
+    float picked[8];
+    float wsum = 0.f;
+    for (int k = 0; k < K; ++k) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = lane + 64 * j;
+            if (e < E && (sc[j] > bv || (sc[j] == bv && e < bi))) { bv = sc[j]; bi = e; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (lane + 64 * j == bi) sc[j] = -INFINITY;
+        picked[k] = bv;
+        wsum += bv;
+        if (lane == 0) { L.ids[t * K + k] = bi; a.ids[t * K + k] = bi; }
+    }
+    if (lane == 0)
+        for (int k = 0; k < K; ++k) {
+            float v = picked[k];
+            if (K > 1 && a.norm_topk) v = v / (wsum + 1e-20f);
+            if (a.scaling != 1.0f) v = v * a.scaling;
+            a.w[t * K + k] = v;
+            L.w[t * K + k] = v;
+        }
+}
+
+// block-wide grouping of L.ids (T*topk assignments) by expert; call after a barrier
+__device__ __forceinline__ void group_assignments(const MoeRouteArgs& a, RouteLds& L) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nt = blockDim.x;
+    const int E = a.E, n = a.T * a.topk;
+    for (int i = tid; i < n; i += nt) atomicAdd(&L.cnt[L.ids[i]], 1);
+    __syncthreads();
+    if (wave == 0) {  // exclusive scan of the E counts + active-expert compaction, 4 experts per lane
+        int c[4], local = 0, al = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = lane * 4 + j;
+            c[j] = e < E ? L.cnt[e] : 0;
+            local += c[j];
+            al += c[j] > 0;
+        }
+        int incl = local, ai = al;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64), z = __shfl_up(ai, o, 64);
+            if (lane >= o) { incl += y; ai += z; }
+        }
+        int acc = incl - local, ap = ai - al;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = lane * 4 + j;
+            if (e < E) {
+                L.cnt[e] = acc;
+                acc += c[j];
+                if (c[j] > 0) a.active[ap++] = e;
+            }
+        }
+        if (lane == 63) { L.cnt[E] = incl; *a.n_active = ai; }
+    }
+    __syncthreads();
+    for (int e = tid; e <= E; e += nt) a.eoff[e] = L.cnt[e];
+    for (int i = tid; i < n; i += nt) {
+        const int e = L.ids[i];
+        const int p = L.cnt[e] + atomicAdd(&L.cur[e], 1);
+        a.arow[p] = i / a.topk;
+        a.apos[i] = p;
+        a.aw[p] = L.w[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void moe_route_kernel(MoeRouteArgs a) {
+    __shared__ RouteLds L;
+    const int wave = threadIdx.x >> 6;
+    for (int e = threadIdx.x; e <= a.E; e += 256) { L.cnt[e] = 0; L.cur[e] = 0; }
+    for (int t = wave; t < a.T; t += 4) route_token(a, a.logits + (long)t * a.E, t, L);
+    __syncthreads();
+    group_assignments(a, L);
+}
+
+// One block of 1024 threads: [RMSNorm] + router logits + top-k + grouping (T <= 8 tokens).
+// Router weights (E x K, 164 KB at E = 64) are streamed by 16 waves, R expert rows per
+// wave per batch, the first batch issued before the norm prologue.
+template <typename WT, int U, int R>
+__device__ __forceinline__ void load_rows(uint4 (&q)[U][R], const WT* W, int e0, int E, int K, int base, int lane) {
+    const int chunks = K >> 3;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = base + u * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = min(e0 + r, E - 1);
+            q[u][r] = (e0 < E && c < chunks) ? ldg_nt16(W + (long)e * K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+}
+
+constexpr int RT_FUSED_MAXT = 8;
+
+template <typename WT, int MT>
+__global__ __launch_bounds__(1024) void moe_router_kernel(MoeRouteArgs a) {
+    extern __shared__ float smem[];
+    __shared__ RouteLds L;
+    __shared__ float lg_s[RT_FUSED_MAXT * 256];
+    constexpr int R = 2, U = 3;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int E = a.E, K = a.Kdim, T = a.T;
+    const WT* W = reinterpret_cast<const WT*>(a.router);
+    const int chunks = K >> 3;
+    for (int e = tid; e <= E; e += 1024) { L.cnt[e] = 0; L.cur[e] = 0; }
+    uint4 q[U][R];
+    int e0 = wave * R;
+    load_rows<WT, U, R>(q, W, e0, E, K, 0, lane);
+    stage_rows(a.x, K, nullptr, T, K, a.norm_w, a.eps, smem);
+    const float* xs = smem + XS_RED;
+    for (; e0 < E; e0 += 16 * R) {
+        float acc[R][MT];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[r][t] = 0.f;
+        for (int base = 0;;) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = base + u * 64 + lane;
+                if (c >= chunks) continue;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    float w8[8];
+                    unpack8<WT>(q[u][r], w8);
+#pragma unroll
+                    for (int t = 0; t < MT; ++t) {
+                        if (t < T) {
+                            float xv[8];
+                            ld_x8(xs + t * K + (c << 3), xv);
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) acc[r][t] = fmaf(xv[j], w8[j], acc[r][t]);
+                        }
+                    }
+                }
+            }
+            base += 64 * U;
+            if (base >= chunks) break;
+            load_rows<WT, U, R>(q, W, e0, E, K, base, lane);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const float v = wave_sum(acc[r][t]);
+                const int e = e0 + r;
+                if (lane == 0 && t < T && e < E) lg_s[t * E + e] = v + (a.bias ? a.bias[e] : 0.f);
+            }
+        if (e0 + 16 * R < E) load_rows<WT, U, R>(q, W, e0 + 16 * R, E, K, 0, lane);
+    }
+    __syncthreads();
+    for (int t = wave; t < T; t += 16) route_token(a, lg_s + t * E, t, L);
+    __syncthreads();
+    group_assignments(a, L);
+}
+
+bool moe_router_fused_ok(int T, int E, int K) {
+    return T <= RT_FUSED_MAXT && E <= 256 && stage_bytes(T, K) <= 48 * 1024;
+}
+
+void launch_moe_route(const MoeRouteArgs& a, hipStream_t s) {
+    if (a.T > RT_MAXT || a.E > 256 || a.topk > 8) throw std::runtime_error("EINVAL: routing supports T <= 64, E <= 256, top_k <= 8");
+    if (a.router) {
+        if (!moe_router_fused_ok(a.T, a.E, a.Kdim)) throw std::runtime_error("EINTERNAL: fused router out of range");
+        const size_t lds = stage_bytes(a.T, a.Kdim);
+        const dim3 g(1), bl(1024);
+        if (a.wdtype == WDT_BF16) {
+            if (a.T == 1) hipLaunchKernelGGL((moe_router_kernel<bf16_t, 1>), g, bl, lds, s, a);
+            else if (a.T == 2) hipLaunchKernelGGL((moe_router_kernel<bf16_t, 2>), g, bl, lds, s, a);
+            else if (a.T <= 4) hipLaunchKernelGGL((moe_router_kernel<bf16_t, 4>), g, bl, lds, s, a);
+            else hipLaunchKernelGGL((moe_router_kernel<bf16_t, 8>), g, bl, lds, s, a);
+        } else {
+            if (a.T == 1) hipLaunchKernelGGL((moe_router_kernel<f16_t, 1>), g, bl, lds, s, a);
+            else if (a.T == 2) hipLaunchKernelGGL((moe_router_kernel<f16_t, 2>), g, bl, lds, s, a);
+            else if (a.T <= 4) hipLaunchKernelGGL((moe_router_kernel<f16_t, 4>), g, bl, lds, s, a);
+            else hipLaunchKernelGGL((moe_router_kernel<f16_t, 8>), g, bl, lds, s, a);
+        }
+    } else {
+        hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(256), 0, s, a);
+    }
+}
+
+// ------------------------------------------------------------------ MoE gate/up (routed + shared)
+// blocks [0, slots*units_r): routed expert active[s] (rows I); the rest: the shared
+// experts (rows Is, all T tokens).  h = silu(x.Wg) * (x.Wu) with x = rmsnorm(X) staged in
+// LDS; routed rows are pre-multiplied by their routing weight (aw, sorted order) so that
+// the down kernel reduces every expert of a token into ONE accumulator.
+template <typename WT, int MT>
+__global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
+    extern __shared__ float smem[];
+    constexpr int RB = 2, U = 3;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
+    const int bid = blockIdx.x;
+    const WT* Wg;
+    const WT* Wu;
+    int rows_I, u, p0, cnt;
+    float* hout;
+    const int* rowmap;
+    if (bid < a.slots * units_r) {
+        const int s = bid / units_r;
+        if (s >= *a.n_active) return;
+        const int e = a.active[s];
+        u = bid % units_r;
+        rows_I = a.I;
+        Wg = reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
+        Wu = Wg + (long)a.I * a.K;
+        p0 = a.eoff[e];
+        cnt = a.eoff[e + 1] - p0;
+        hout = a.h;
+        rowmap = a.arow;
+    } else {
+        if (!a.sWgu) return;
+        u = bid - a.slots * units_r;
+        rows_I = a.Is;
+        Wg = reinterpret_cast<const WT*>(a.sWgu);
+        Wu = Wg + (long)a.Is * a.K;
+        p0 = 0;
+        cnt = a.T;
+        hout = a.hs;
+        rowmap = nullptr;
+    }
+    const int i0 = (u * 4 + wave) * RB;
+    const bool active = i0 < rows_I;
+    const int chunks = a.K >> 3;
+    const float* xs = smem + XS_RED;
+    for (int t0 = 0; t0 < cnt; t0 += MT) {
+        const int tn = min(MT, cnt - t0);
+        uint4 qg[U][RB], qu[U][RB];
+#pragma unroll
+        for (int uu = 0; uu < U; ++uu) {
+            const int c = uu * 64 + lane;
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const int i = min(i0 + r, rows_I - 1);
+                const bool ok = active && c < chunks;
+                qg[uu][r] = ok ? ldg_nt16(Wg + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                qu[uu][r] = ok ? ldg_nt16(Wu + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+        if (t0 > 0) __syncthreads();  // previous group's LDS rows fully consumed
+        if (rowmap) stage_rows(a.x, a.K, rowmap + p0 + t0, tn, a.K, a.norm_w, a.eps, smem);
+        else stage_rows(a.x + (long)t0 * a.K, a.K, nullptr, tn, a.K, a.norm_w, a.eps, smem);
+        if (!active) continue;
+        float ag[RB][MT], au[RB][MT];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) { ag[r][m] = 0.f; au[r][m] = 0.f; }
+        for (int base = 0;;) {
+#pragma unroll
+            for (int uu = 0; uu < U; ++uu) {
+                const int c = base + uu * 64 + lane;
+                if (c >= chunks) continue;
+                float wg[RB][8], wu[RB][8];
+#pragma unroll
+                for (int r = 0; r < RB; ++r) { unpack8<WT>(qg[uu][r], wg[r]); unpack8<WT>(qu[uu][r], wu[r]); }
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    if (m < tn) {
+                        float xv[8];
+                        ld_x8(xs + m * a.K + (c << 3), xv);
+#pragma unroll
+                        for (int r = 0; r < RB; ++r)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                ag[r][m] = fmaf(xv[j], wg[r][j], ag[r][m]);
+                                au[r][m] = fmaf(xv[j], wu[r][j], au[r][m]);
+                            }
+                    }
+                }
+            }
+            base += 64 * U;
+            if (base >= chunks) break;
+#pragma unroll
+            for (int uu = 0; uu < U; ++uu) {
+                const int c = base + uu * 64 + lane;
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const int i = min(i0 + r, rows_I - 1);
+                    qg[uu][r] = c < chunks ? ldg_nt16(Wg + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                    qu[uu][r] = c < chunks ? ldg_nt16(Wu + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const float gs = wave_sum(ag[r][m]);
+                const float us = wave_sum(au[r][m]);
+                const int i = i0 + r;
+                if (lane == 0 && m < tn && i < rows_I) {
+                    float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
+                    if (rowmap) hv = hv * a.aw[p0 + t0 + m];
+                    hout[(long)(p0 + t0 + m) * rows_I + i] = hv;
+                }
+            }
+    }
+}
+
+// ------------------------------------------------------------------ MoE down + combine + residual
+// A wave owns output row j of every token: v = sum_k h~[apos(t,k)] . Wd_{e_k}[j]
+// (h~ already carries w_k) + hs[t] . Wsd[j];  X[t][j] += v.  All routed and shared
+// weight loads of a token are issued before the first FMA.
+template <typename WT>
+__global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int j = blockIdx.x * 4 + wave;
+    if (j >= a.Hout) return;
+    const int K = a.topk;
+    const int ch_r = K > 0 ? (a.I >> 3) : 0, ch_s = a.sWd ? (a.Is >> 3) : 0;
+    const WT* Ws = reinterpret_cast<const WT*>(a.sWd) + (long)j * a.Is;
+    for (int t = 0; t < a.T; ++t) {
+        float acc = 0.f;
+        const float* hs = a.hs + (long)t * a.Is;
+        for (int br = 0, bs = 0; br < ch_r || bs < ch_s; br += 128, bs += 256) {
+            uint4 qr[8][2], qs[4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k < K) {
+                    const int e = a.ids[t * K + k];
+                    const WT* Wd = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + j) * a.I;
+#pragma unroll
+                    for (int uu = 0; uu < 2; ++uu) {
+                        const int c = br + uu * 64 + lane;
+                        qr[k][uu] = c < ch_r ? ldg_nt16(Wd + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                    }
+                }
+            }
+#pragma unroll
+            for (int uu = 0; uu < 4; ++uu) {
+                const int c = bs + uu * 64 + lane;
+                qs[uu] = c < ch_s ? ldg_nt16(Ws + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k < K) {
+                    const float* hp = a.h + (long)a.apos[t * K + k] * a.I;
+#pragma unroll
+                    for (int uu = 0; uu < 2; ++uu) {
+                        const int c = br + uu * 64 + lane;
+                        if (c < ch_r) {
+                            float hv[8], w8[8];
+                            ld_x8(hp + (c << 3), hv);
+                            unpack8<WT>(qr[k][uu], w8);
+#pragma unroll
+                            for (int jj = 0; jj < 8; ++jj) acc = fmaf(hv[jj], w8[jj], acc);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int uu = 0; uu < 4; ++uu) {
+                const int c = bs + uu * 64 + lane;
+                if (c < ch_s) {
+                    float hv[8], w8[8];
+                    ld_x8(hs + (c << 3), hv);
+                    unpack8<WT>(qs[uu], w8);
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) acc = fmaf(hv[jj], w8[jj], acc);
+                }
+            }
+        }
+        const float v = wave_sum(acc);
+        if (lane == 0) {
+            float* xp = a.out + (long)t * a.Hout + j;
+            *xp = *xp + v;
+        }
+    }
+}
+
+void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
+    constexpr int RB = 2;
+    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
+    const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
+    dim3 grid(a.slots * units_r + units_s);
+    const int mt = a.T == 1 ? 1 : (a.T <= 4 ? 4 : 8);
+    const size_t lds = stage_bytes(mt, a.K);
+    if (lds > STAGE_LDS_MAX) throw std::runtime_error("EINVAL: moe_gateup2 hidden size too large for LDS staging");
+    if (a.wdtype == WDT_BF16) {
+        if (mt == 1) hipLaunchKernelGGL((moe_gateup2_kernel<bf16_t, 1>), grid, dim3(256), lds, s, a);
+        else if (mt == 4) hipLaunchKernelGGL((moe_gateup2_kernel<bf16_t, 4>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((moe_gateup2_kernel<bf16_t, 8>), grid, dim3(256), lds, s, a);
+    } else {
+        if (mt == 1) hipLaunchKernelGGL((moe_gateup2_kernel<f16_t, 1>), grid, dim3(256), lds, s, a);
+        else if (mt == 4) hipLaunchKernelGGL((moe_gateup2_kernel<f16_t, 4>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((moe_gateup2_kernel<f16_t, 8>), grid, dim3(256), lds, s, a);
+    }
+}
+void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
+    if (a.topk > 8) throw std::runtime_error("EINVAL: moe_down2 supports top_k <= 8");
+    dim3 grid((a.Hout + 3) / 4);
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down2_kernel<bf16_t>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((moe_down2_kernel<f16_t>), grid, dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ sampling (fused)
+// argmax over the vocabulary with the no-repeat-ngram ban evaluated inside each block
+// (sampling.rs:141-158), then one block per page finalises: fallback, EOS / output /
+// context bookkeeping, next-step embedding and the KV position advance.
+constexpr int SP_BLOCK = 256;
+constexpr int SP_PER_BLOCK = 2048;  // 8 logits per thread, all loaded before the first compare
+size_t dec_sample_blocks(int V) { return (size_t)(V + SP_PER_BLOCK - 1) / SP_PER_BLOCK; }
+
+__device__ __forceinline__ bool sp_better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
+
+// (value, index) argmax over the block (first index on ties); result in sv[0] / si[0]
+__device__ __forceinline__ void block_argmax(float bv, int bi, float* sv, int* si) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (sp_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { sv[wave] = bv; si[wave] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+            if (sp_better(sv[w], si[w], bv, bi)) { bv = sv[w]; bi = si[w]; }
+        sv[0] = bv;
+        si[0] = bi;
+    }
+    __syncthreads();
+}
+
+template <bool LDSCTX>
+__global__ __launch_bounds__(SP_BLOCK) void dec_argmax_partial_kernel(DecSampleArgs a) {
+    extern __shared__ int ctx_s[];  // the page's context, staged once per block (LDSCTX)
+    __shared__ float sv[SP_BLOCK];
+    __shared__ int si[SP_BLOCK];
+    __shared__ unsigned ban[SP_PER_BLOCK / 32];  // banned-token bitmap of this block's vocab range
+    const int b = blockIdx.y;
+    const float* lg = a.logits + (long)b * a.ld;
+    const int v0 = blockIdx.x * SP_PER_BLOCK, v1 = min(a.V, v0 + SP_PER_BLOCK);
+    // this block's logits first (independent loads in flight during the n-gram scan)
+    constexpr int PER = SP_PER_BLOCK / SP_BLOCK;
+    float xv[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int v = v0 + threadIdx.x + j * SP_BLOCK;
+        xv[j] = v < v1 ? lg[v] : -INFINITY;
+    }
+    for (int i = threadIdx.x; i < SP_PER_BLOCK / 32; i += SP_BLOCK) ban[i] = 0u;
+    const int n = a.ctx_len[b], g = a.ngram;
+    const int* ctx = a.ctx + (long)b * a.ctx_cap;
+    const bool use_ban = g > 1 && n >= g - 1;
+    if (LDSCTX && use_ban)
+        for (int i = threadIdx.x; i < n; i += SP_BLOCK) ctx_s[i] = ctx[i];
+    __syncthreads();
+    const int* cx = LDSCTX ? ctx_s : ctx;
+    if (use_ban) {
+        for (int i = threadIdx.x; i <= n - g; i += SP_BLOCK) {
+            const int t = cx[i + g - 1];
+            if (t < v0 || t >= v1) continue;
+            bool match = true;
+            for (int jj = 0; jj < g - 1; ++jj)
+                if (cx[i + jj] != cx[n - g + 1 + jj]) { match = false; break; }
+            if (match) atomicOr(&ban[(t - v0) >> 5], 1u << ((t - v0) & 31));
+        }
+    }
+    __syncthreads();
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int v = v0 + threadIdx.x + j * SP_BLOCK;
+        const float x = xv[j];
+        if (v >= v1 || !(x > -INFINITY) || !(x < INFINITY)) continue;
+        if (ban[(v - v0) >> 5] & (1u << ((v - v0) & 31))) continue;
+        if (sp_better(x, v, bv, bi)) { bv = x; bi = v; }
+    }
+    block_argmax(bv, bi, sv, si);
+    if (threadIdx.x == 0) {
+        a.red_val[(long)b * a.red_blocks + blockIdx.x] = sv[0];
+        a.red_idx[(long)b * a.red_blocks + blockIdx.x] = si[0];
+    }
+}
+
+__global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArgs a) {
+    __shared__ float sv[SP_BLOCK];
+    __shared__ int si[SP_BLOCK];
+    __shared__ int tok_s;
+    const int b = blockIdx.x;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = threadIdx.x; j < a.red_blocks; j += SP_BLOCK) {
+        float v = a.red_val[(long)b * a.red_blocks + j];
+        int i = a.red_idx[(long)b * a.red_blocks + j];
+        if (i != 0x7fffffff && sp_better(v, i, bv, bi)) { bv = v; bi = i; }
+    }
+    block_argmax(bv, bi, sv, si);
+    const bool found = si[0] != 0x7fffffff;
+    __syncthreads();
+    if (!found) {  // everything banned / non-finite: argmax of the penalised logits, else 0
+        const float* lg = a.logits + (long)b * a.ld;
+        bv = -INFINITY;
+        bi = 0x7fffffff;
+        for (int v = threadIdx.x; v < a.V; v += SP_BLOCK) {
+            float x = lg[v];
+            if (!(x > -INFINITY) || !(x < INFINITY)) continue;
+            if (sp_better(x, v, bv, bi)) { bv = x; bi = v; }
+        }
+        sv[threadIdx.x] = bv;
+        si[threadIdx.x] = bi;
+        __syncthreads();
+        for (int o = SP_BLOCK / 2; o > 0; o >>= 1) {
+            if (threadIdx.x < o && sp_better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
+                sv[threadIdx.x] = sv[threadIdx.x + o];
+                si[threadIdx.x] = si[threadIdx.x + o];
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        const int t = si[0] == 0x7fffffff ? 0 : si[0];
+        tok_s = t;
+        a.out_tok[b] = t;
+        if (a.out_ids && !a.done[b]) {
+            if (a.eos >= 0 && t == a.eos) {
+                a.done[b] = 1;
+            } else {
+                const int st = a.out_len[b];
+                if (st < a.out_cap) { a.out_ids[(long)b * a.out_cap + st] = t; a.out_len[b] = st + 1; }
+                if (st + 1 >= a.out_cap) a.done[b] = 1;
+                const int n = a.ctx_len[b];
+                if (n < a.ctx_cap) { a.ctx[(long)b * a.ctx_cap + n] = t; a.ctx_len[b] = n + 1; }
+            }
+        }
+        if (a.kv_pos) {
+            a.kv_pos[b] += 1;
+            a.kv_len[b] += 1;
+        }
+    }
+    __syncthreads();
+    if (!a.table) return;
+    const int t = tok_s;
+    const uint16_t* tab = reinterpret_cast<const uint16_t*>(a.table);
+    for (int c = threadIdx.x; c < a.H; c += SP_BLOCK) {
+        const uint32_t bits = tab[(long)t * a.H + c];
+        a.x_next[(long)b * a.H + c] = a.table_dt == WDT_BF16 ? bf16_bits_to_f32(bits) : f16_bits_to_f32(bits);
+    }
+}
+
+void launch_dec_sample(const DecSampleArgs& a0, hipStream_t s) {
+    DecSampleArgs a = a0;
+    a.red_blocks = (int)dec_sample_blocks(a.V);
+    if (a.ctx_cap <= 16384)
+        hipLaunchKernelGGL(dec_argmax_partial_kernel<true>, dim3(a.red_blocks, a.B), dim3(SP_BLOCK),
+                           sizeof(int) * a.ctx_cap, s, a);
+    else
+        hipLaunchKernelGGL(dec_argmax_partial_kernel<false>, dim3(a.red_blocks, a.B), dim3(SP_BLOCK), 0, s, a);
+    hipLaunchKernelGGL(dec_sample_final_kernel, dim3(a.B), dim3(SP_BLOCK), 0, s, a);
+}
+
+}  // namespace dsocr

@@ -32,42 +32,7 @@ struct GemmArgs {
 };
 void launch_gemm(const GemmArgs& g, hipStream_t s);
 
-// ------------------------------------------------------------------ skinny linear (gemv.hip)
-// y[m][n] = act(sum_k x[m][k] W[n][k] + bias[n]) (+ y) for M <= 16 rows.
-struct GemvArgs {
-    int M = 0, N = 0, K = 0;
-    const float* x = nullptr;
-    int ldx = 0;
-    const void* W = nullptr;
-    int ldw = 0;
-    int wdtype = WDT_F16;
-    const float* bias = nullptr;
-    float* y = nullptr;
-    int ldy = 0;
-    int act = 0;
-    int accumulate = 0;
-};
-void launch_gemv(const GemvArgs& a, hipStream_t s);
-
-// Grouped SwiGLU experts for decode (moe.hip).  Assignment list sorted by expert:
-// expert e owns sorted positions [eoff[e], eoff[e+1]); arow[p] = token row of x.
-//   h[p][i] = silu(x[arow[p]] . Wg_e[i]) * (x[arow[p]] . Wu_e[i])     (W_gu_e = [gate; up], [2I][K])
-//   y[p][j] = h[p] . Wd_e[j]                                           (W_d_e = [Hout][I])
-struct MoeDecodeArgs {
-    int T = 0, topk = 0, E = 0, K = 0, I = 0, Hout = 0;
-    const float* x = nullptr;  // [T][K]
-    const int* eoff = nullptr; // [E+1]
-    const int* arow = nullptr; // [T*topk]
-    const void* Wgu = nullptr; // E x [2I][K]
-    const void* Wd = nullptr;  // E x [Hout][I]
-    int wdtype = WDT_F16;
-    float* h = nullptr;        // [T*topk][I]
-    float* y = nullptr;        // [T*topk][Hout]
-    int max_rows_per_expert = 16;
-};
-void launch_moe_gateup_gemv(const MoeDecodeArgs& a, hipStream_t s);
-void launch_moe_down_gemv(const MoeDecodeArgs& a, hipStream_t s);
-
+// ------------------------------------------------------------------ MoE prefill helpers (moe.hip)
 // Router: scores = softmax(logits) (or sigmoid), greedy top-k (descending, stable),
 // optional renormalise + scaling (block.rs:1254-1301).
 void launch_router_topk(const float* logits, int T, int E, int topk, int softmax_scoring, int norm_topk,
@@ -109,20 +74,6 @@ void launch_attention(const AttnArgs& a, hipStream_t s);
 // SAM decomposed rel-pos: out[s][h][q][kh] = q . Rh[qh-kh+gh-1], out[..][gh+kw] = q . Rw[qw-kw+gw-1]
 void launch_sam_relbias(const float* q, long q_row_stride, int n_seq, int gh, int gw, int heads, int hd,
                         const float* Rh, const float* Rw, float* out, hipStream_t s);
-// Decode attention over the per-page f32 KV cache (flash-decoding, split over keys).
-struct DecodeAttnArgs {
-    const float* q = nullptr;  long q_row_stride = 0;   // [B][heads*hd]
-    const float* kc = nullptr; const float* vc = nullptr;
-    long page_stride = 0, head_stride = 0;              // cache [B][H][Lmax][hd]
-    const int* lens = nullptr;                          // keys per page (device)
-    int B = 0, heads = 0, hd = 0, max_len = 0;
-    float scale = 1.f;
-    float* part = nullptr;                              // workspace
-    float* o = nullptr; long o_row_stride = 0;
-};
-void launch_decode_attention(const DecodeAttnArgs& a, hipStream_t s);
-size_t decode_attention_workspace(int B, int heads, int hd, int max_len);
-
 // RoPE (rotate_half, optional MLA reorder) on q,k inside a fused qkv buffer and KV-cache append.
 struct RopeKvArgs {
     float* qkv = nullptr; long ld = 0; int rows = 0;
@@ -148,22 +99,89 @@ void launch_assemble_rows(const int* kind, const int* index, int rows, int H, co
                           long ld_dst, hipStream_t s);
 void launch_embed_tokens(const void* table, int table_dt, const int* ids, int n, int H, float* out, long ld,
                          hipStream_t s);
-// Greedy token selection with repetition penalty + no-repeat-ngram ban (sampling.rs:34-158).
+// Repetition penalty over the context tokens (sampling.rs:34-96), in place on the logits.
 struct SampleArgs {
     float* logits = nullptr; int B = 0, V = 0; long ld = 0;
     const int* ctx = nullptr; long ctx_cap = 0; const int* ctx_len = nullptr;
-    int ngram = 0; float rep_penalty = 1.f;
-    int* banned = nullptr; int* banned_cnt = nullptr; int banned_cap = 0;
-    float* red_val = nullptr; int* red_idx = nullptr; int red_blocks = 0;
-    int* out_tok = nullptr;
+    float rep_penalty = 1.f;
 };
-void launch_sample_greedy(const SampleArgs& a, hipStream_t s);
-size_t sample_workspace_blocks(int V);
-// Per-step bookkeeping: record the token (EOS finishes the page), grow the
-// context, embed it as the next step's input; then advance KV positions.
-void launch_step_update(const int* tok, int B, int* ctx, long ctx_cap, int* ctx_len, int* out_ids, int* out_len,
-                        long out_cap, int* done, int eos, const void* table, int table_dt, int H, float* x_next,
-                        hipStream_t s);
-void launch_step_advance(int* kv_pos, int* kv_len, int B, hipStream_t s);
+void launch_rep_penalty(const SampleArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ fused decode step (decode.hip)
+// Skinny linear with the preceding RMSNorm fused (norm_w != null: x is normalised on the fly).
+struct DecGemvArgs {
+    int M = 0, N = 0, K = 0;
+    const float* x = nullptr;
+    int ldx = 0;
+    const void* W = nullptr;
+    int ldw = 0;
+    int wdtype = WDT_F16;
+    const float* bias = nullptr;
+    float* y = nullptr;
+    int ldy = 0;
+    int act = 0;
+    int accumulate = 0;
+    const float* norm_w = nullptr;
+    float eps = 0.f;
+};
+void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s);
+// RoPE on q / new k + KV-cache append + flash-decoding over 64-key chunks + combine.
+struct DecAttn2Args {
+    const float* qkv = nullptr; long ld = 0;           // [B][(heads + 2 kv_heads) * hd]
+    const int* kv_pos = nullptr;                        // position of the token being decoded
+    int B = 0, heads = 0, kv_heads = 0, hd = 0, rope_dim = 0, use_mla = 0, max_len = 0;
+    const float* cos = nullptr; const float* sin = nullptr;
+    float* kc = nullptr; float* vc = nullptr; long page_stride = 0, head_stride = 0;
+    float scale = 1.f;
+    float* part = nullptr;
+    int* counters = nullptr;                            // [B][heads] arrival tickets, zero between launches
+    float* o = nullptr; long o_ld = 0;
+};
+void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
+size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
+// Router top-k + grouping in one block (T <= 64, E <= 256, top_k <= 8).  With `router` set
+// the block also computes the logits of rmsnorm(x) (T <= 8, see moe_router_fused_ok).
+struct MoeRouteArgs {
+    const float* logits = nullptr;
+    const float* x = nullptr; const float* norm_w = nullptr; float eps = 0.f;
+    const void* router = nullptr; const float* bias = nullptr; int Kdim = 0; int wdtype = WDT_F16;
+    int T = 0, E = 0, topk = 0, softmax_scoring = 1, norm_topk = 0;
+    float scaling = 1.f;
+    int* ids = nullptr; float* w = nullptr;
+    int* eoff = nullptr; int* arow = nullptr; int* apos = nullptr;
+    float* aw = nullptr;            // routing weight by sorted position
+    int* active = nullptr; int* n_active = nullptr;
+};
+void launch_moe_route(const MoeRouteArgs& a, hipStream_t s);
+bool moe_router_fused_ok(int T, int E, int K);
+// Routed experts + shared experts (gate/up: one launch; down + weighted combine + residual: one launch).
+struct MoeDec2Args {
+    int T = 0, topk = 0, E = 0, K = 0, I = 0, Is = 0, Hout = 0, slots = 0;
+    const float* x = nullptr;       // [T][K] (pre-norm residual stream if norm_w)
+    const float* norm_w = nullptr; float eps = 0.f;
+    const int* eoff = nullptr; const int* arow = nullptr; const int* apos = nullptr; const int* ids = nullptr;
+    const int* active = nullptr; const int* n_active = nullptr;
+    const float* aw = nullptr;      // routing weight by sorted position (folded into h)
+    const void* Wgu = nullptr; const void* Wd = nullptr;    // routed: E x [2I][K], E x [Hout][I]
+    const void* sWgu = nullptr; const void* sWd = nullptr;  // shared / dense: [2Is][K], [Hout][Is]
+    int wdtype = WDT_F16;
+    float* h = nullptr; float* hs = nullptr;
+    float* out = nullptr;           // [T][Hout], += combined
+};
+void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
+void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
+// Greedy selection (ngram ban evaluated in-kernel) + step bookkeeping + KV advance.
+struct DecSampleArgs {
+    const float* logits = nullptr; int B = 0, V = 0; long ld = 0;
+    int* ctx = nullptr; long ctx_cap = 0; int* ctx_len = nullptr;
+    int ngram = 0;
+    float* red_val = nullptr; int* red_idx = nullptr; int red_blocks = 0;
+    int* out_tok = nullptr; int* out_ids = nullptr; int* out_len = nullptr; long out_cap = 0;
+    int* done = nullptr; int eos = -1;
+    const void* table = nullptr; int table_dt = 0; int H = 0; float* x_next = nullptr;
+    int* kv_pos = nullptr; int* kv_len = nullptr;
+};
+void launch_dec_sample(const DecSampleArgs& a, hipStream_t s);
+size_t dec_sample_blocks(int V);
 
 }  // namespace dsocr

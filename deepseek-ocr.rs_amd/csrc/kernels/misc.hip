@@ -159,34 +159,9 @@ void launch_embed_tokens(const void* table, int table_dt, const int* ids, int n,
     hipLaunchKernelGGL(embed_tokens_kernel, dim3(n), dim3(256), 0, s, table, table_dt, ids, n, H, out, ld);
 }
 
-// ------------------------------------------------------------------ greedy token selection
-// sampling.rs:34-158: repetition penalty over the set of context tokens, ban every
-// token that would complete an n-gram already present in prompt+generated, then
-// argmax (first index on ties, non-finite skipped).  If every logit is banned the
-// reference falls back to the un-banned (penalised) logits.
-constexpr int SG_BLOCK = 256;
-constexpr int SG_PER_BLOCK = 4096;
-
-size_t sample_workspace_blocks(int V) { return (size_t)(V + SG_PER_BLOCK - 1) / SG_PER_BLOCK; }
-
-__global__ void ngram_ban_kernel(SampleArgs a) {
-    const int b = blockIdx.y;
-    const int n = a.ctx_len[b];
-    const int* ctx = a.ctx + (long)b * a.ctx_cap;
-    const int g = a.ngram;
-    if (g <= 1 || n < g - 1) return;
-    // windows i in [0, n-g]: ctx[i..i+g-1) == ctx[n-g+1..n)
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i <= n - g; i += gridDim.x * blockDim.x) {
-        bool match = true;
-        for (int j = 0; j < g - 1; ++j)
-            if (ctx[i + j] != ctx[n - g + 1 + j]) { match = false; break; }
-        if (match) {
-            int slot = atomicAdd(&a.banned_cnt[b], 1);
-            if (slot < a.banned_cap) a.banned[(long)b * a.banned_cap + slot] = ctx[i + g - 1];
-        }
-    }
-}
-
+// ------------------------------------------------------------------ repetition penalty
+// sampling.rs:34-96: every distinct context token's logit is divided (>0) or multiplied
+// (<=0) by the penalty once.  Selection itself is dec_argmax_partial / dec_sample_final (decode.hip).
 __global__ void rep_penalty_kernel(SampleArgs a) {
     // apply once per distinct context token: the first occurrence applies it
     const int b = blockIdx.y;
@@ -205,140 +180,9 @@ __global__ void rep_penalty_kernel(SampleArgs a) {
     }
 }
 
-__device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
-    return v > bv || (v == bv && i < bi);
-}
-
-__global__ __launch_bounds__(SG_BLOCK) void argmax_partial_kernel(SampleArgs a, int use_ban) {
-    __shared__ float sv[SG_BLOCK];
-    __shared__ int si[SG_BLOCK];
-    const int b = blockIdx.y;
-    const float* lg = a.logits + (long)b * a.ld;
-    const int nb = use_ban ? min(a.banned_cnt[b], a.banned_cap) : 0;
-    const int* ban = a.banned + (long)b * a.banned_cap;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    const int v0 = blockIdx.x * SG_PER_BLOCK, v1 = min(a.V, v0 + SG_PER_BLOCK);
-    for (int v = v0 + threadIdx.x; v < v1; v += SG_BLOCK) {
-        float x = lg[v];
-        if (!(x > -INFINITY) || !(x < INFINITY)) continue;  // skips -inf, +inf, NaN
-        bool banned = false;
-        for (int j = 0; j < nb; ++j) banned |= (ban[j] == v);
-        if (banned) continue;
-        if (better(x, v, bv, bi)) { bv = x; bi = v; }
-    }
-    sv[threadIdx.x] = bv;
-    si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int o = SG_BLOCK / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o && better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
-            sv[threadIdx.x] = sv[threadIdx.x + o];
-            si[threadIdx.x] = si[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        a.red_val[(long)b * a.red_blocks + blockIdx.x] = sv[0];
-        a.red_idx[(long)b * a.red_blocks + blockIdx.x] = si[0];
-    }
-}
-
-__global__ __launch_bounds__(SG_BLOCK) void argmax_final_kernel(SampleArgs a) {
-    __shared__ float sv[SG_BLOCK];
-    __shared__ int si[SG_BLOCK];
-    const int b = blockIdx.x;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int j = threadIdx.x; j < a.red_blocks; j += SG_BLOCK) {
-        float v = a.red_val[(long)b * a.red_blocks + j];
-        int i = a.red_idx[(long)b * a.red_blocks + j];
-        if (i != 0x7fffffff && better(v, i, bv, bi)) { bv = v; bi = i; }
-    }
-    sv[threadIdx.x] = bv;
-    si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int o = SG_BLOCK / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o && better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
-            sv[threadIdx.x] = sv[threadIdx.x + o];
-            si[threadIdx.x] = si[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    const bool found = si[0] != 0x7fffffff;
-    __syncthreads();
-    if (!found) {
-        // every candidate banned or non-finite: argmax of the (penalised) logits, else 0
-        const float* lg = a.logits + (long)b * a.ld;
-        bv = -INFINITY;
-        bi = 0x7fffffff;
-        for (int v = threadIdx.x; v < a.V; v += SG_BLOCK) {
-            float x = lg[v];
-            if (!(x > -INFINITY) || !(x < INFINITY)) continue;
-            if (better(x, v, bv, bi)) { bv = x; bi = v; }
-        }
-        sv[threadIdx.x] = bv;
-        si[threadIdx.x] = bi;
-        __syncthreads();
-        for (int o = SG_BLOCK / 2; o > 0; o >>= 1) {
-            if (threadIdx.x < o && better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
-                sv[threadIdx.x] = sv[threadIdx.x + o];
-                si[threadIdx.x] = si[threadIdx.x + o];
-            }
-            __syncthreads();
-        }
-    }
-    if (threadIdx.x == 0) a.out_tok[b] = (si[0] == 0x7fffffff) ? 0 : si[0];
-}
-
-__global__ void zero_int_kernel(int* p, int n) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
-}
-
-void launch_sample_greedy(const SampleArgs& a, hipStream_t s) {
-    SampleArgs b = a;
-    b.red_blocks = (int)sample_workspace_blocks(a.V);
-    hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(256), 0, s, a.banned_cnt, a.B);
+void launch_rep_penalty(const SampleArgs& a, hipStream_t s) {
     if (a.rep_penalty > 0.f && fabsf(a.rep_penalty - 1.0f) > 1.1920929e-07f)
-        hipLaunchKernelGGL(rep_penalty_kernel, dim3(8, a.B), dim3(256), 0, s, b);
-    if (a.ngram > 1) hipLaunchKernelGGL(ngram_ban_kernel, dim3(8, a.B), dim3(256), 0, s, b);
-    dim3 g(b.red_blocks, a.B);
-    hipLaunchKernelGGL(argmax_partial_kernel, g, dim3(SG_BLOCK), 0, s, b, 1);
-    hipLaunchKernelGGL(argmax_final_kernel, dim3(a.B), dim3(SG_BLOCK), 0, s, b);
-}
-
-// After a token is chosen: generate loop bookkeeping (model/mod.rs:1977-2034).
-// EOS finishes a page (the EOS id itself is not emitted); finished pages keep
-// running in the batch but their context and output stop growing.
-__global__ void step_update_kernel(const int* tok, int B, int* ctx, long ctx_cap, int* ctx_len, int* out_ids,
-                                   int* out_len, long out_cap, int* done, int eos, const void* table, int dt, int H,
-                                   float* x_next) {
-    const int b = blockIdx.x;
-    const int t = tok[b];
-    if (threadIdx.x == 0 && !done[b]) {
-        if (eos >= 0 && t == eos) {
-            done[b] = 1;
-        } else {
-            const int st = out_len[b];
-            if (st < out_cap) { out_ids[(long)b * out_cap + st] = t; out_len[b] = st + 1; }
-            if (st + 1 >= out_cap) done[b] = 1;
-            const int n = ctx_len[b];
-            if (n < ctx_cap) { ctx[(long)b * ctx_cap + n] = t; ctx_len[b] = n + 1; }
-        }
-    }
-    for (int c = threadIdx.x; c < H; c += blockDim.x) x_next[(long)b * H + c] = table_val(table, dt, (long)t * H + c);
-}
-__global__ void step_advance_kernel(int* kv_pos, int* kv_len, int B) {
-    for (int b = threadIdx.x; b < B; b += blockDim.x) { kv_pos[b] += 1; kv_len[b] += 1; }
-}
-
-void launch_step_update(const int* tok, int B, int* ctx, long ctx_cap, int* ctx_len, int* out_ids, int* out_len,
-                        long out_cap, int* done, int eos, const void* table, int table_dt, int H, float* x_next,
-                        hipStream_t s) {
-    hipLaunchKernelGGL(step_update_kernel, dim3(B), dim3(256), 0, s, tok, B, ctx, ctx_cap, ctx_len, out_ids, out_len,
-                       out_cap, done, eos, table, table_dt, H, x_next);
-}
-void launch_step_advance(int* kv_pos, int* kv_len, int B, hipStream_t s) {
-    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(256), 0, s, kv_pos, kv_len, B);
+        hipLaunchKernelGGL(rep_penalty_kernel, dim3(8, a.B), dim3(256), 0, s, a);
 }
 
 }  // namespace dsocr

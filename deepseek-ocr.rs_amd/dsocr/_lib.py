@@ -54,13 +54,22 @@ class TimingsC(C.Structure):
                 ("decode_generate_ms", C.c_double), ("decode_steps", C.c_size_t), ("pages", C.c_size_t)]
 
 
+class KernelProfileC(C.Structure):
+    _fields_ = [("avg_us", C.c_double), ("bytes", C.c_double), ("flops", C.c_double), ("launches", C.c_int)]
+
+
+class DecodeProfileC(C.Structure):
+    _fields_ = [("moe_gateup", KernelProfileC), ("moe_down", KernelProfileC), ("attention", KernelProfileC),
+                ("lm_head", KernelProfileC), ("experts_touched", C.c_int), ("tokens", C.c_int), ("kv_len", C.c_int)]
+
+
 STREAM_CB = C.CFUNCTYPE(None, C.c_size_t, C.POINTER(C.c_int64), C.c_void_p)
 
 # every symbol include/dsocr.h declares (tests check the library exports all of them)
 EXPORTS = [
     "dsocr_engine_load", "dsocr_engine_free", "dsocr_last_error", "dsocr_engine_info", "dsocr_prepare_page",
     "dsocr_page_free", "dsocr_page_info", "dsocr_page_pixels_view", "dsocr_image_embeddings", "dsocr_generate",
-    "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode_moe", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
+    "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
     "dsocr_k_sample_greedy",
@@ -92,8 +101,7 @@ def lib():
                                  C.POINTER(sz)]
     L.dsocr_generate_batch.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC)]
     L.dsocr_last_timings.argtypes = [vp, C.POINTER(TimingsC)]
-    L.dsocr_profile_decode_moe.argtypes = [vp, i32, C.POINTER(C.c_double), C.POINTER(C.c_double),
-                                           C.POINTER(C.c_double), C.POINTER(i32)]
+    L.dsocr_profile_decode.argtypes = [vp, i32, C.POINTER(DecodeProfileC)]
     L.dsocr_device_count.argtypes = [C.POINTER(i32)]
     L.dsocr_dev_alloc.argtypes = [sz, C.POINTER(vp)]
     L.dsocr_dev_free.argtypes = [vp]
@@ -102,12 +110,12 @@ def lib():
     L.dsocr_synth_bf16.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, vp]
     L.dsocr_resize_bicubic.argtypes = [vp, u32, u32, vp, u32, u32]
     L.dsocr_k_gemm.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32]
-    L.dsocr_k_gemv.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32]
+    L.dsocr_k_gemv.argtypes = [i32, i32, i32, vp, vp, f32, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_layernorm.argtypes = [i32, i32, vp, vp, vp, f32, vp]
     L.dsocr_k_rmsnorm.argtypes = [i32, i32, vp, vp, f32, vp]
     L.dsocr_k_attention.argtypes = [i32, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp, vp, i32, i32]
-    L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, f32, vp, vp, vp, vp, vp]
-    L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]
+    L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, vp]
+    L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]
     L.dsocr_k_sample_greedy.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, vp]
     _lib = L
     return L

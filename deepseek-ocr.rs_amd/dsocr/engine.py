@@ -245,10 +245,17 @@ class DeepseekOcrEngine:
         check(lib().dsocr_last_timings(self._h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in TimingsC._fields_}
 
-    def profile_decode_moe(self, iters: int = 3) -> dict:
-        a, b, f, e = C.c_double(), C.c_double(), C.c_double(), C.c_int()
-        check(lib().dsocr_profile_decode_moe(self._h, iters, C.byref(a), C.byref(b), C.byref(f), C.byref(e)))
-        return {"avg_us": a.value, "bytes": b.value, "flops": f.value, "experts_touched": e.value}
+    def profile_decode(self, iters: int = 3) -> dict:
+        """HIP-event timings + algorithmic bytes of the dominant decode kernels (see dsocr.h)."""
+        from ._lib import DecodeProfileC
+        p = DecodeProfileC()
+        check(lib().dsocr_profile_decode(self._h, iters, C.byref(p)))
+        out = {}
+        for k in ("moe_gateup", "moe_down", "attention", "lm_head"):
+            kp = getattr(p, k)
+            out[k] = {"avg_us": kp.avg_us, "bytes": kp.bytes, "flops": kp.flops, "launches": kp.launches}
+        out.update(experts_touched=p.experts_touched, tokens=p.tokens, kv_len=p.kv_len)
+        return out
 
     # ------------------------------------------------------------------ OcrEngine::decode
     def decode(self, tokenizer, prompt: str, images: Sequence, vision: VisionSettings,

@@ -139,12 +139,26 @@ dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request
                                   const dsocr_decode_params* params, dsocr_result* results);
 dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t);
 
-/* Roofline probe for the north-star kernel: replays the decode MoE grouped GEMV (routed
- * gate/up + down) of every MoE layer on the last decode step's routing, HIP-event timed.
- * avg_us: mean duration of one (gate/up, down) launch pair; bytes/flops: algorithmic
- * traffic/work of one pair (touched experts' fp16 weights + f32 activations). */
-dsocr_status dsocr_profile_decode_moe(dsocr_engine* e, int iters, double* avg_us, double* bytes, double* flops,
-                                      int* experts_touched);
+/* Decode-kernel profile (bench roofline): replays the dominant decode kernels of the
+ * last generate() call on its final routing / KV state, each timed with HIP events on
+ * the engine stream.  avg_us = mean duration of one launch; bytes / flops = algorithmic
+ * HBM traffic / work of one launch (fp16 weights touched + f32 activations / KV reads). */
+typedef struct dsocr_kernel_profile {
+    double avg_us;
+    double bytes;
+    double flops;
+    int launches;
+} dsocr_kernel_profile;
+typedef struct dsocr_decode_profile {
+    dsocr_kernel_profile moe_gateup;  /* moe_gateup2_kernel: routed + shared gate/up, one MoE layer */
+    dsocr_kernel_profile moe_down;    /* moe_down2_kernel: routed + shared down + combine + residual */
+    dsocr_kernel_profile attention;   /* dec_attn_kernel + combine: one layer, all pages */
+    dsocr_kernel_profile lm_head;     /* dec_gemv over the 129280 x 1280 lm_head */
+    int experts_touched;              /* routed experts active in the replayed step (per layer, summed / layers) */
+    int tokens;                       /* pages in the batch */
+    int kv_len;                       /* keys attended by page 0 */
+} dsocr_decode_profile;
+dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out);
 
 /* ---- device helpers for tests / tooling (plain pointers; no torch) */
 dsocr_status dsocr_device_count(int* n);
@@ -163,8 +177,10 @@ dsocr_status dsocr_resize_bicubic(const uint8_t* src, uint32_t sw, uint32_t sh, 
 /* C[M][N] = act(A[M][K] . W[N][K]^T + bias) (+ C if accumulate); wdtype 0 = bf16, 1 = f16 */
 dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias, float* C,
                           int act, int accumulate);
-dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const void* W, int wdtype, const float* bias, float* y,
-                          int act, int accumulate);
+/* Decode linear (transformer/block.rs attention / MLP projections at seq_len 1): y[M][N] =
+ * act(xn . W^T + bias) (+ y), xn = rmsnorm(x; norm_w, eps) when norm_w != NULL (block.rs:24-29), else x. */
+dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm_w, float eps, const void* W,
+                          int wdtype, const float* bias, float* y, int act, int accumulate);
 dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* w, const float* b, float eps,
                                float* y);
 dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w, float eps, float* y);
@@ -174,15 +190,20 @@ dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w,
 dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale, int causal, const float* q,
                                const float* k, const float* v, float* o, const float* relh, const float* relw, int gh,
                                int gw);
-/* Decode attention over a per-page f32 KV cache laid out [B][heads][max_len][hd]: for page b,
- * o[b] = softmax(scale * q[b].K[b][:lens[b]]^T) . V[b][:lens[b]]  (q, o: [B][heads*hd]; lens on device). */
-dsocr_status dsocr_k_decode_attention(int B, int heads, int hd, int max_len, float scale, const float* q,
-                                      const float* kc, const float* vc, const int* lens, float* o);
-/* Decode MoE layer (the north-star kernel chain): router GEMV + softmax top-k + grouping +
- * grouped SwiGLU experts + shared experts + weighted combine, out[T][H] += moe(x).
+/* Decode attention step (block.rs:608-789 at seq_len 1, rope block.rs:1403-1471): for page b the
+ * token at position pos = kv_pos[b] has its q / k rotated (cos/sin tables [max_len][rope_dim]), k and v
+ * appended to the f32 cache [B][kv_heads][max_len][hd] at pos, then
+ * o[b] = softmax(scale * q.K[:pos+1]^T) . V[:pos+1].  qkv: [B][(heads + 2 kv_heads) * hd]; o: [B][heads*hd]. */
+dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, int rope_dim, int max_len, float scale,
+                                      const float* qkv, const float* cos, const float* sin, float* kc, float* vc,
+                                      const int* kv_pos, float* o);
+/* Decode MoE layer (the north-star kernel chain, block.rs:1215-1395): [RMSNorm] + router GEMV +
+ * softmax top-k + grouping + grouped SwiGLU experts + shared experts + weighted combine,
+ * out[T][H] += moe(xn), xn = rmsnorm(x; norm_w, eps) if norm_w != NULL else x.
  * Wgu: [E][2I][H] (gate rows then up rows), Wd: [E][H][I], router [E][H], shared Wgu [2Is][H],
  * shared Wd [H][Is] (shared may be NULL), all 16-bit (wdtype). */
-dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const void* router,
+dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const float* norm_w,
+                         float eps, const void* router,
                          const void* Wgu, const void* Wd, const void* sWgu, const void* sWd, int wdtype,
                          int norm_topk, float scaling, float* out, int* topk_ids_out, float* topk_w_out);
 /* Greedy selection with repetition penalty + n-gram ban (sampling.rs:34-158) over B rows of V

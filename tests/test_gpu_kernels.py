@@ -52,16 +52,23 @@ def test_gemm(gpu, M, N, K, wdt, act, acc):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
-@pytest.mark.parametrize("M,N,K,wdt", [(1, 1280, 1280, 1), (1, 129280, 1280, 0), (3, 3840, 1280, 1),
-                                       (8, 896, 1792, 1), (16, 100, 64, 0), (21, 513, 128, 0)])
-def test_gemv(gpu, M, N, K, wdt):
+@pytest.mark.parametrize("M,N,K,wdt,norm", [(1, 1280, 1280, 1, True), (1, 129280, 1280, 0, True),
+                                            (2, 3840, 1280, 1, True), (3, 3840, 1280, 1, False),
+                                            (8, 896, 1792, 1, False), (16, 100, 64, 0, False),
+                                            (21, 513, 128, 0, True), (1, 64, 1280, 1, True), (4, 9000, 256, 0, False)])
+def test_gemv(gpu, M, N, K, wdt, norm):
+    """Decode linear (dec_gemv) with the optional fused RMSNorm prologue (block.rs:24-29)."""
     rng = np.random.default_rng(N + K + M)
     x = rng.standard_normal((M, K)).astype(np.float32)
     bits, w = _weights(rng, N, K, wdt)
-    dx, dW, dy = Dev(x), Dev(bits), Dev.zeros((M, N))
-    check(lib().dsocr_k_gemv(M, N, K, dx.ptr, dW.ptr, wdt, None, dy.ptr, 0, 0))
-    ref = (x.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32)
-    assert np.all(np.abs(dy.get() - ref) <= _bound(x, w))
+    nw = (1.0 + 0.05 * rng.standard_normal(K)).astype(np.float32)
+    y0 = rng.standard_normal((M, N)).astype(np.float32)
+    acc = int(M % 2 == 1)
+    dx, dW, dy, dn = Dev(x), Dev(bits), Dev(y0 if acc else np.zeros((M, N), np.float32)), Dev(nw)
+    check(lib().dsocr_k_gemv(M, N, K, dx.ptr, dn.ptr if norm else None, 1e-6, dW.ptr, wdt, None, dy.ptr, 0, acc))
+    xn = rms_norm(x, nw, 1e-6) if norm else x
+    ref = (xn.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + (y0 if acc else 0)
+    assert np.all(np.abs(dy.get() - ref) <= _bound(xn, w) + 1e-6 * np.abs(ref))
 
 
 @pytest.mark.parametrize("rows,cols,eps", [(4096, 768, 1e-6), (257, 1024, 1e-5), (100, 256, 1e-6)])
@@ -146,33 +153,53 @@ def test_attention_sam_relpos(gpu, g, rel_len):
         assert np.max(np.abs(got[:, hl] - ref)) < 5e-5
 
 
-@pytest.mark.parametrize("B,heads,hd,max_len", [(1, 10, 128, 1218), (3, 4, 32, 300), (5, 12, 64, 700), (2, 10, 128, 257)])
-def test_decode_attention(gpu, B, heads, hd, max_len):
-    """Decode step attention (block.rs:608-775 with past_len > 0) over the f32 cache."""
+@pytest.mark.parametrize("B,heads,kvh,hd,max_len", [(1, 10, 10, 128, 1218), (3, 4, 4, 32, 300),
+                                                   (5, 12, 4, 64, 700), (2, 10, 10, 128, 257), (1, 10, 10, 128, 64)])
+def test_decode_attention(gpu, B, heads, kvh, hd, max_len):
+    """Fused decode attention (block.rs:608-789 at seq_len 1): RoPE on q / new k (block.rs:1403-1471),
+    K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the f32 cache."""
+    from types import SimpleNamespace
+    from oracle.decoder import apply_rope, rope_tables
     rng = np.random.default_rng(B * hd + max_len)
-    q = rng.standard_normal((B, heads * hd)).astype(np.float32)
-    kc = rng.standard_normal((B, heads, max_len, hd)).astype(np.float32)
-    vc = rng.standard_normal((B, heads, max_len, hd)).astype(np.float32)
-    lens = rng.integers(1, max_len + 1, B).astype(np.int32)
-    lens[0] = max_len
+    qkvw = (heads + 2 * kvh) * hd
+    qkv = rng.standard_normal((B, qkvw)).astype(np.float32)
+    kc = rng.standard_normal((B, kvh, max_len, hd)).astype(np.float32)
+    vc = rng.standard_normal((B, kvh, max_len, hd)).astype(np.float32)
+    pos = rng.integers(0, max_len, B).astype(np.int32)
+    pos[0] = max_len - 1
     if B > 1:
-        lens[1] = 1
-    dq, dk, dv, dl, do = Dev(q), Dev(kc), Dev(vc), Dev(lens), Dev.zeros((B, heads * hd))
+        pos[1] = 0
+    if B > 2:
+        pos[2] = 63
+    lang = SimpleNamespace(rope_theta=10000.0)
+    cos, sin = rope_tables(lang, max_len, hd)
+    dqkv, dk, dv, dp, do = Dev(qkv), Dev(kc), Dev(vc), Dev(pos), Dev.zeros((B, heads * hd))
+    dcos, dsin = Dev(cos), Dev(sin)
     scale = 1.0 / math.sqrt(hd)
-    check(lib().dsocr_k_decode_attention(B, heads, hd, max_len, scale, dq.ptr, dk.ptr, dv.ptr, dl.ptr, do.ptr))
-    got = do.get()
+    check(lib().dsocr_k_decode_attention(B, heads, kvh, hd, hd, max_len, scale, dqkv.ptr, dcos.ptr, dsin.ptr,
+                                         dk.ptr, dv.ptr, dp.ptr, do.ptr))
+    got, gk, gv = do.get(), dk.get(), dv.get()
     for b in range(B):
+        p = pos[b]
+        cs, sn = cos[p][None], sin[p][None]
+        q = apply_rope(qkv[b, :heads * hd].reshape(heads, hd), cs, sn, False)
+        kn = apply_rope(qkv[b, heads * hd:(heads + kvh) * hd].reshape(kvh, hd), cs, sn, False)
+        vn = qkv[b, (heads + kvh) * hd:].reshape(kvh, hd)
+        assert np.max(np.abs(gk[b, :, p] - kn)) < 1e-5 and np.array_equal(gv[b, :, p], vn)
+        K = kc[b].copy(); V = vc[b].copy()
+        K[:, p] = kn; V[:, p] = vn
         for h in range(heads):
-            L = lens[b]
-            ref = _attn_ref(q[b, h * hd:(h + 1) * hd][None], kc[b, h, :L], vc[b, h, :L], scale)[0]
+            g = h // (heads // kvh)
+            ref = _attn_ref(q[h][None], K[g, :p + 1], V[g, :p + 1], scale)[0]
             assert np.max(np.abs(got[b, h * hd:(h + 1) * hd] - ref)) < 2e-5, (b, h)
 
 
-def test_moe_decode_layer(gpu):
+@pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(3, 256, 16, 6, 64, 2, False), (1, 256, 16, 6, 64, 2, True),
+                                                  (2, 1280, 64, 6, 896, 2, True), (9, 128, 8, 3, 32, 1, False)])
+def test_moe_decode_layer(gpu, T, H, E, topk, I, ns, norm):
     """Decode MoE (north-star kernel chain) vs the oracle's run_moe (block.rs:1215-1395)."""
     from oracle.decoder import Decoder
-    rng = np.random.default_rng(5)
-    T, H, E, topk, I, ns = 3, 256, 16, 6, 64, 2
+    rng = np.random.default_rng(5 + T)
     Is = I * ns
     x = rng.standard_normal((T, H)).astype(np.float32)
     router = f16_bits(rng.standard_normal((E, H)) * 0.1)
@@ -187,8 +214,13 @@ def test_moe_decode_layer(gpu):
     dx, dr, dgu, dd, dsgu, dsd, dout = Dev(x), Dev(router), Dev(Wgu), Dev(Wd), Dev(sWgu), Dev(sd), Dev(out0)
     ids = np.zeros(T * topk, np.int32)
     wts = np.zeros(T * topk, np.float32)
-    check(lib().dsocr_k_moe(T, H, E, topk, I, Is, dx.ptr, dr.ptr, dgu.ptr, dd.ptr, dsgu.ptr, dsd.ptr, 1, 0, 1.0,
-                            dout.ptr, ids.ctypes.data_as(C.c_void_p), wts.ctypes.data_as(C.c_void_p)))
+    nw = (1.0 + 0.05 * rng.standard_normal(H)).astype(np.float32)
+    dn = Dev(nw)
+    check(lib().dsocr_k_moe(T, H, E, topk, I, Is, dx.ptr, dn.ptr if norm else None, 1e-6, dr.ptr, dgu.ptr, dd.ptr,
+                            dsgu.ptr, dsd.ptr, 1, 0, 1.0, dout.ptr, ids.ctypes.data_as(C.c_void_p),
+                            wts.ctypes.data_as(C.c_void_p)))
+    if norm:
+        x = rms_norm(x, nw, 1e-6)
 
     f = lambda b: b.view(np.float16).astype(np.float32)
     W = {"l.mlp.gate.weight": f(router), "l.mlp.shared_experts.gate_proj.weight": f(sg),

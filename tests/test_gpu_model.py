@@ -84,11 +84,13 @@ def test_tiny_generate_host_rows_and_stream(tiny_engine, tiny_oracle):
     assert seen and seen[-1] == got[: len(seen[-1])]
 
 
-def test_tiny_batch_equals_single(tiny_engine):
+@pytest.mark.parametrize("n", [2, 4])
+def test_tiny_batch_equals_single(tiny_engine, n):
+    """B <= 2 runs the norm-fused decode kernels, B > 2 the separate-RMSNorm variant: same ids."""
     tok = SyntheticTokenizer(512)
     reqs, singles = [], []
     params = DecodeParameters(max_new_tokens=20)
-    for i, hw in enumerate([(300, 420), (256, 256), (500, 140), (130, 130)]):
+    for i, hw in enumerate([(300, 420), (256, 256), (500, 140), (130, 130)][:n]):
         page = Page(_img(100 + i, *hw), TINY_VS)
         ids, mask = _prompt(tok, page)
         reqs.append((ids, mask, page, None))
