@@ -383,39 +383,42 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
             bufs.push_back(p);
             return p;
         };
-        dsocr::MoeRouteArgs r;
-        if (dsocr::moe_router_fused_ok(T, E, H)) {
-            r.x = x; r.norm_w = norm_w; r.eps = eps; r.router = router; r.Kdim = H; r.wdtype = wdtype;
-        } else {
-            float* log = (float*)alloc(sizeof(float) * T * E);
-            dsocr::DecGemvArgs ra;
-            ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
-            ra.y = log; ra.ldy = E; ra.norm_w = norm_w; ra.eps = eps;
-            dsocr::launch_dec_gemv(ra, nullptr);
-            r.logits = log;
-        }
-        r.T = T; r.E = E; r.topk = topk; r.softmax_scoring = 1; r.norm_topk = norm_topk;
-        r.scaling = scaling;
-        r.ids = (int*)alloc(sizeof(int) * TK); r.w = (float*)alloc(sizeof(float) * TK);
-        r.eoff = (int*)alloc(sizeof(int) * (E + 1)); r.arow = (int*)alloc(sizeof(int) * TK);
-        r.apos = (int*)alloc(sizeof(int) * TK); r.active = (int*)alloc(sizeof(int) * E);
-        r.aw = (float*)alloc(sizeof(float) * TK);
-        r.n_active = (int*)alloc(sizeof(int));
-        dsocr::launch_moe_route(r, nullptr);
+        float* log = (float*)alloc(sizeof(float) * T * E);
+        dsocr::DecGemvArgs ra;
+        ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
+        ra.y = log; ra.ldy = E; ra.norm_w = norm_w; ra.eps = eps;
+        dsocr::launch_dec_gemv(ra, nullptr);
+        // same dispatch as Engine::moe_decode_args: slot mode for T <= 8, grouped by expert above
         dsocr::MoeDec2Args m;
-        m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H; m.slots = std::min(E, TK);
-        m.x = x; m.norm_w = norm_w; m.eps = eps;
-        m.eoff = r.eoff; m.arow = r.arow; m.apos = r.apos; m.ids = r.ids; m.active = r.active; m.n_active = r.n_active;
-        m.aw = r.aw; m.Wgu = Wgu; m.Wd = Wd; m.wdtype = wdtype; m.out = out;
+        m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H;
+        m.x = x; m.norm_w = norm_w; m.eps = eps; m.Wgu = Wgu; m.Wd = Wd; m.wdtype = wdtype; m.out = out;
         m.h = (float*)alloc(sizeof(float) * (size_t)TK * I);
+        int* ids = (int*)alloc(sizeof(int) * TK);
+        float* wts = (float*)alloc(sizeof(float) * TK);
+        m.ids = ids;
         if (sWgu && sWd && Is > 0) {
             m.Is = Is; m.sWgu = sWgu; m.sWd = sWd; m.hs = (float*)alloc(sizeof(float) * (size_t)T * Is);
+        }
+        if (T <= 8) {
+            m.slot_mode = 1; m.slots = TK; m.logits = log; m.softmax_scoring = 1; m.norm_topk = norm_topk;
+            m.scaling = scaling; m.ids_out = ids; m.w_out = wts;
+        } else {
+            dsocr::MoeRouteArgs r;
+            r.logits = log; r.T = T; r.E = E; r.topk = topk; r.softmax_scoring = 1; r.norm_topk = norm_topk;
+            r.scaling = scaling; r.ids = ids; r.w = wts;
+            r.eoff = (int*)alloc(sizeof(int) * (E + 1)); r.arow = (int*)alloc(sizeof(int) * TK);
+            r.apos = (int*)alloc(sizeof(int) * TK); r.active = (int*)alloc(sizeof(int) * E);
+            r.aw = (float*)alloc(sizeof(float) * TK); r.n_active = (int*)alloc(sizeof(int));
+            dsocr::launch_moe_route(r, nullptr);
+            m.slots = std::min(E, TK);
+            m.eoff = r.eoff; m.arow = r.arow; m.apos = r.apos; m.active = r.active; m.n_active = r.n_active;
+            m.aw = r.aw;
         }
         dsocr::launch_moe_gateup2(m, nullptr);
         dsocr::launch_moe_down2(m, nullptr);
         hipError_t e = hipDeviceSynchronize();
-        if (e == hipSuccess && ids_out) e = hipMemcpy(ids_out, r.ids, sizeof(int) * TK, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && w_out) e = hipMemcpy(w_out, r.w, sizeof(float) * TK, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && ids_out) e = hipMemcpy(ids_out, ids, sizeof(int) * TK, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && w_out) e = hipMemcpy(w_out, wts, sizeof(float) * TK, hipMemcpyDeviceToHost);
         for (void* p : bufs) (void)hipFree(p);
         check_hip(e, "moe");
     });

@@ -765,6 +765,35 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     launch_moe_combine(Y, APOS, WTS, YS, T, K, H, X, 1, st);
 }
 
+// Decode MoE arguments of layer l for B pages (shared by decode_step and profile_decode).
+// B <= 8: slot mode (gate/up blocks route themselves from s_log); else grouped by expert.
+MoeDec2Args Engine::moe_decode_args(int l, int B, const float* x, const float* norm, float* out) {
+    const LangConfig& L = cfg_.lang;
+    DecLayer& d = layers_[l];
+    const int H = L.hidden, E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
+    MoeDec2Args m;
+    m.T = B; m.K = H; m.Hout = H; m.x = x; m.norm_w = norm; m.eps = L.rms_eps; m.out = out;
+    m.topk = K; m.E = E; m.I = I;
+    m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
+    m.h = wsf("s_ehh", (size_t)TK * I);
+    m.ids = wsi("s_ids", TK);
+    if (d.has_shared) {
+        if (d.s_gu.wdt != d.e_wdt) throw std::runtime_error("EINTERNAL: shared/routed expert dtype mismatch");
+        m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is);
+    }
+    if (B <= 8) {
+        m.slot_mode = 1; m.slots = TK; m.logits = wsf("s_log", (size_t)B * E);
+        m.softmax_scoring = L.scoring == "softmax"; m.norm_topk = L.norm_topk; m.scaling = L.routed_scaling;
+        m.ids_out = wsi("s_ids", TK); m.w_out = wsf("s_wts", TK);
+        if (const char* dbg = getenv("DSOCR_DBG_GU")) m.dbg = atoi(dbg);
+    } else {
+        m.slots = std::min(E, TK);
+        m.eoff = wsi("s_eoff", E + 1); m.arow = wsi("s_arow", TK); m.apos = wsi("s_apos", TK);
+        m.aw = wsf("s_aw", TK); m.active = wsi("s_active", E); m.n_active = wsi("s_nact", 1);
+    }
+    return m;
+}
+
 void Engine::decode_step(int B, int Lmax) {
     // One token for each of B pages: 8 launches per layer (decode.hip).  For B <= 2 the
     // RMSNorms are fused into the consuming GEMV / expert kernels (x normalised on the fly).
@@ -818,35 +847,22 @@ void Engine::decode_step(int B, int Lmax) {
             launch_moe_down2(m, st);
             continue;
         }
-        const int E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
+        const int E = L.n_routed, K = L.topk, TK = B * K;
         if (TK > 512 || E > 256 || K > 8) throw std::runtime_error("EINVAL: decode MoE supports batch*top_k <= 512, <= 256 experts, top_k <= 8");
-        MoeRouteArgs ra;
-        ra.T = B; ra.E = E; ra.topk = K; ra.softmax_scoring = L.scoring == "softmax";
-        ra.norm_topk = L.norm_topk; ra.scaling = L.routed_scaling;
-        ra.ids = wsi("s_ids", TK); ra.w = wsf("s_wts", TK); ra.eoff = wsi("s_eoff", E + 1);
-        ra.arow = wsi("s_arow", TK); ra.apos = wsi("s_apos", TK); ra.aw = wsf("s_aw", TK);
-        ra.active = wsi("s_active", E);
-        ra.n_active = wsi("s_nact", 1);
-        if (getenv("DSOCR_FUSED_ROUTER") && moe_router_fused_ok(B, E, H)) {  // one-block variant (slower on MI355X)
-            ra.x = mx; ra.norm_w = mnorm; ra.eps = L.rms_eps; ra.router = d.router.W; ra.bias = d.router.b;
-            ra.Kdim = H; ra.wdtype = d.router.wdt;
-        } else {
-            float* LOG = wsf("s_log", (size_t)B * E);
-            DecGemvArgs gr;
-            gr.M = B; gr.N = E; gr.K = H; gr.x = mx; gr.ldx = H; gr.W = d.router.W; gr.ldw = H; gr.wdtype = d.router.wdt;
-            gr.bias = d.router.b; gr.y = LOG; gr.ldy = E; gr.norm_w = mnorm; gr.eps = L.rms_eps;
-            launch_dec_gemv(gr, st);
-            ra.logits = LOG;
-        }
-        launch_moe_route(ra, st);
-        m.topk = K; m.E = E; m.I = I; m.slots = std::min(E, TK);
-        m.eoff = ra.eoff; m.arow = ra.arow; m.apos = ra.apos; m.ids = ra.ids; m.active = ra.active;
-        m.n_active = ra.n_active; m.aw = ra.aw;
-        m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
-        m.h = wsf("s_ehh", (size_t)TK * I);
-        if (d.has_shared) {
-            if (d.s_gu.wdt != d.e_wdt) throw std::runtime_error("EINTERNAL: shared/routed expert dtype mismatch");
-            m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is);
+        float* LOG = wsf("s_log", (size_t)B * E);
+        DecGemvArgs gr;
+        gr.M = B; gr.N = E; gr.K = H; gr.x = mx; gr.ldx = H; gr.W = d.router.W; gr.ldw = H; gr.wdtype = d.router.wdt;
+        gr.bias = d.router.b; gr.y = LOG; gr.ldy = E; gr.norm_w = mnorm; gr.eps = L.rms_eps;
+        launch_dec_gemv(gr, st);
+        m = moe_decode_args(l, B, mx, mnorm, X);
+        if (!m.slot_mode) {  // B > 8: one block sorts the assignments by expert
+            MoeRouteArgs ra;
+            ra.logits = LOG; ra.T = B; ra.E = E; ra.topk = K; ra.softmax_scoring = L.scoring == "softmax";
+            ra.norm_topk = L.norm_topk; ra.scaling = L.routed_scaling;
+            ra.ids = const_cast<int*>(m.ids); ra.w = wsf("s_wts", TK); ra.eoff = const_cast<int*>(m.eoff);
+            ra.arow = const_cast<int*>(m.arow); ra.apos = const_cast<int*>(m.apos); ra.aw = const_cast<float*>(m.aw);
+            ra.active = const_cast<int*>(m.active); ra.n_active = const_cast<int*>(m.n_active);
+            launch_moe_route(ra, st);
         }
         launch_moe_gateup2(m, st);
         launch_moe_down2(m, st);
@@ -1218,45 +1234,37 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     HIP_CHECK(hipMemcpy(d_pos, pm1.data(), B * 4, hipMemcpyHostToDevice));
     prof.tokens = B;
     prof.kv_len = pm1[0] + 1;
+    // n back-to-back launches between two events on the engine stream: per-launch time =
+    // span / n (a single event-bracketed launch carries ~10 us of event overhead on MI355X)
     auto timed = [&](KernelProfile& kp, int n, const std::function<void(int)>& body) {
-        std::vector<hipEvent_t> evs(2 * n);
-        for (auto& e : evs) HIP_CHECK(hipEventCreate(&e));
-        for (int i = 0; i < n; ++i) {
-            HIP_CHECK(hipEventRecord(evs[2 * i], st));
-            body(i);
-            HIP_CHECK(hipEventRecord(evs[2 * i + 1], st));
-        }
-        HIP_CHECK(hipStreamSynchronize(st));
-        double total = 0;
-        for (int i = 0; i < n; ++i) total += ms_between(evs[2 * i], evs[2 * i + 1]);
-        for (auto& e : evs) (void)hipEventDestroy(e);
-        kp.avg_us = 1000.0 * total / n;
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        body(0);  // warm (code objects, TLB)
+        HIP_CHECK(hipEventRecord(e0, st));
+        for (int i = 0; i < n; ++i) body(i);
+        HIP_CHECK(hipEventRecord(e1, st));
+        HIP_CHECK(hipEventSynchronize(e1));
+        kp.avg_us = 1000.0 * ms_between(e0, e1) / n;
         kp.launches = n;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
     };
     std::vector<int> moe_layers;
     for (int l = 0; l < L.layers; ++l)
         if (layers_[l].moe) moe_layers.push_back(l);
     if (!moe_layers.empty()) {
         const int E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
-        std::vector<int> eoff(E + 1);
-        HIP_CHECK(hipMemcpy(eoff.data(), wsi("s_eoff", E + 1), (E + 1) * 4, hipMemcpyDeviceToHost));
-        for (int e = 0; e < E; ++e) prof.experts_touched += eoff[e + 1] > eoff[e] ? 1 : 0;
+        std::vector<int> ids(TK);
+        HIP_CHECK(hipMemcpy(ids.data(), wsi("s_ids", TK), TK * 4, hipMemcpyDeviceToHost));
+        std::vector<char> seen(E, 0);
+        for (int v : ids)
+            if (v >= 0 && v < E && !seen[v]) { seen[v] = 1; ++prof.experts_touched; }
         const float* Xc = wsf("s_x", (size_t)B * H);
         // replay on a scratch copy of the residual stream so the engine state is untouched
         float* Xs = wsf("p_x", (size_t)B * H);
         HIP_CHECK(hipMemcpyAsync(Xs, Xc, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
-        auto args = [&](int l) {
-            DecLayer& d = layers_[l];
-            MoeDec2Args m;
-            m.T = B; m.K = H; m.Hout = H; m.x = Xs; m.norm_w = B <= 2 ? d.post_norm.w : nullptr; m.eps = L.rms_eps;
-            m.out = Xs; m.topk = K; m.E = E; m.I = I; m.slots = std::min(E, TK);
-            m.eoff = wsi("s_eoff", E + 1); m.arow = wsi("s_arow", TK); m.apos = wsi("s_apos", TK);
-            m.ids = wsi("s_ids", TK); m.active = wsi("s_active", E); m.n_active = wsi("s_nact", 1);
-            m.aw = wsf("s_aw", TK); m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
-            m.h = wsf("s_ehh", (size_t)TK * I);
-            if (d.has_shared) { m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is); }
-            return m;
-        };
+        auto args = [&](int l) { return moe_decode_args(l, B, Xs, B <= 2 ? layers_[l].post_norm.w : nullptr, Xs); };
         const int n = iters * (int)moe_layers.size();
         // rotating over the layers (~55 MB each) defeats the 256 MB Infinity Cache
         timed(prof.moe_gateup, n, [&](int i) { launch_moe_gateup2(args(moe_layers[i % moe_layers.size()]), st); });

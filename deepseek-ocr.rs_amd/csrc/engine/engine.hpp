@@ -163,6 +163,7 @@ class Engine {
     float* vision_pass(const float* imgs, int n, int S, const std::string& out);
     void prefill(int B, const std::vector<int>& rows_per_page, const float* x0, int Lmax);
     void decode_step(int B, int Lmax);
+    MoeDec2Args moe_decode_args(int l, int B, const float* x, const float* norm, float* out);
     void decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen);
     void layer_forward_prefill(int l, int T, int B, const int* row_page, const int* row_pos, const long* q_off,
                                const long* kv_off, const long* o_off, const int* seq_len, int max_len, int Lmax);

@@ -64,6 +64,91 @@ __device__ __forceinline__ void stage_rows(const float* x, long ldx, const int* 
     __syncthreads();
 }
 
+// Two-phase staging for the hot kernels.  vmcnt is in-order on CDNA: a load issued after
+// the weight stream can only be consumed once every weight load has landed.  So the
+// activation rows (and the norm weight) are loaded into registers FIRST (xload), the weight
+// stream is issued next, and xstage then normalises / writes LDS waiting only for the
+// activation loads.  XR float4 per thread per row covers K <= XR * 4 * blockDim.
+template <int MT, int XR>
+struct XRegs {
+    float4 v[MT][XR];
+    float4 w[XR];
+};
+
+template <int MT, int XR>
+__device__ __forceinline__ void xload(XRegs<MT, XR>& r, const float* x, long ldx, const int* rows, int M, int K,
+                                      const float* nw) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    // unconditional loads from clamped addresses (a predicated load becomes an exec-masked
+    // branch plus a vmcnt(0) drain in hipcc's output); lanes past K / M are ignored by xstage
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int mm = min(m, M - 1);
+        const float* xr = x + (long)(rows ? rows[mm] : mm) * ldx;
+#pragma unroll
+        for (int i = 0; i < XR; ++i) {
+            const int k = min((tid + i * nt) * 4, K - 4);
+            r.v[m][i] = *reinterpret_cast<const float4*>(xr + k);
+        }
+    }
+    const float* nwp = nw ? nw : x;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+        const int k = min((tid + i * nt) * 4, K - 4);
+        r.w[i] = *reinterpret_cast<const float4*>(nwp + k);
+    }
+}
+
+template <int MT, int XR>
+__device__ __forceinline__ void xstage(const XRegs<MT, XR>& r, int M, int K, bool norm, float eps, float* smem) {
+    float* red = smem;
+    float* xs = smem + XS_RED;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nt = blockDim.x, nwv = nt >> 6;
+    if (norm) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            if (m < M) {
+                float q = 0.f;
+#pragma unroll
+                for (int i = 0; i < XR; ++i) {
+                    const float4 v = r.v[m][i];
+                    if ((tid + i * nt) * 4 < K) q += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+                }
+                q = wave_sum(q);
+                if (lane == 0) red[m * nwv + wave] = q;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        if (m < M) {
+            float den = 1.f;
+            if (norm) {
+                float q = 0.f;
+                for (int w = 0; w < nwv; ++w) q += red[m * nwv + w];
+                den = sqrtf(q / (float)K + eps);
+            }
+#pragma unroll
+            for (int i = 0; i < XR; ++i) {
+                const int k = (tid + i * nt) * 4;
+                if (k < K) {
+                    float4 v = r.v[m][i];
+                    if (norm) {
+                        const float4 w = r.w[i];
+                        v.x = (v.x / den) * w.x;
+                        v.y = (v.y / den) * w.y;
+                        v.z = (v.z / den) * w.z;
+                        v.w = (v.w / den) * w.w;
+                    }
+                    *reinterpret_cast<float4*>(xs + m * K + k) = v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
 // 8 consecutive f32 (LDS or global) into registers
 __device__ __forceinline__ void ld_x8(const float* xs, float* o) {
     const float4 a = *reinterpret_cast<const float4*>(xs);
@@ -87,6 +172,10 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
     const bool active = n0 < a.N;
     const WT* W = reinterpret_cast<const WT*>(a.W);
     const int chunks = a.K >> 3;
+    constexpr int XR = 2;
+    const bool fast = a.K <= XR * 4 * 256;
+    XRegs<MT, XR> xr;
+    if (fast) xload<MT, XR>(xr, a.x, a.ldx, nullptr, a.M, a.K, a.norm_w);
     uint4 wq[U][RB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -94,10 +183,11 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const int n = min(n0 + r, a.N - 1);
-            wq[u][r] = (active && c < chunks) ? ldg_nt16(W + (long)n * a.ldw + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+            wq[u][r] = ldg_nt16(W + (long)n * a.ldw + (min(c, chunks - 1) << 3));
         }
     }
-    stage_rows(a.x, a.ldx, nullptr, a.M, a.K, a.norm_w, a.eps, smem);
+    if (fast) xstage<MT, XR>(xr, a.M, a.K, a.norm_w != nullptr, a.eps, smem);
+    else stage_rows(a.x, a.ldx, nullptr, a.M, a.K, a.norm_w, a.eps, smem);
     if (!active) return;
     const float* xs = smem + XS_RED;
     float acc[RB][MT];
@@ -134,7 +224,7 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
                 const int n = min(n0 + r, a.N - 1);
-                wq[u][r] = c < chunks ? ldg_nt16(W + (long)n * a.ldw + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                wq[u][r] = ldg_nt16(W + (long)n * a.ldw + (min(c, chunks - 1) << 3));
             }
         }
     }
@@ -153,6 +243,93 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
         }
 }
 
+// Large-N variant (lm_head: 129280 rows): a fixed grid of waves walks the row groups with a
+// two-deep register pipeline (the loads of group i+1 are in flight while group i is
+// reduced), so the per-block x staging / norm prologue is paid once per ~8 row groups.
+template <typename WT, int U, int RB>
+__device__ __forceinline__ void gemv_issue(uint4 (&q)[U][RB], const WT* W, int n0, int N, long ldw, int chunks,
+                                           int lane, bool ok) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int n = min(n0 + r, N - 1);
+            q[u][r] = ldg_nt16(W + (long)n * ldw + (min(c, chunks - 1) << 3));
+            (void)ok;
+        }
+    }
+}
+
+template <typename WT, int MT, int U, int RB>
+__device__ __forceinline__ void gemv_finish(const uint4 (&q)[U][RB], const float* xs, const DecGemvArgs& a, int n0,
+                                            int chunks, int lane) {
+    float acc[RB][MT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        if (c < chunks) {
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                float w8[8];
+                unpack8<WT>(q[u][r], w8);
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    if (m < a.M) {
+                        float xv[8];
+                        ld_x8(xs + m * a.K + (c << 3), xv);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc[r][m] = fmaf(xv[j], w8[j], acc[r][m]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            float v = wave_sum(acc[r][m]);
+            const int n = n0 + r;
+            if (lane == 0 && m < a.M && n < a.N) {
+                v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
+                float* yp = a.y + (long)m * a.ldy + n;
+                if (a.accumulate) v = *yp + v;
+                *yp = v;
+            }
+        }
+}
+
+template <typename WT, int MT, int RB>
+__global__ __launch_bounds__(256) void dec_gemv_stream_kernel(DecGemvArgs a) {
+    extern __shared__ float smem[];
+    constexpr int U = 3;  // K <= 1536: one batch per row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    const int ngroups = (a.N + RB - 1) / RB;
+    const int stride = gridDim.x * 4;
+    int g = blockIdx.x * 4 + wave;
+    uint4 qa[U][RB], qb[U][RB];
+    XRegs<MT, 2> xr;  // K <= 1536 here
+    xload<MT, 2>(xr, a.x, a.ldx, nullptr, a.M, a.K, a.norm_w);
+    gemv_issue<WT, U, RB>(qa, W, g * RB, a.N, a.ldw, chunks, lane, g < ngroups);
+    xstage<MT, 2>(xr, a.M, a.K, a.norm_w != nullptr, a.eps, smem);
+    const float* xs = smem + XS_RED;
+    for (; g < ngroups; g += 2 * stride) {
+        const int g2 = g + stride, g3 = g2 + stride;
+        gemv_issue<WT, U, RB>(qb, W, g2 * RB, a.N, a.ldw, chunks, lane, g2 < ngroups);
+        gemv_finish<WT, MT, U, RB>(qa, xs, a, g * RB, chunks, lane);
+        if (g2 >= ngroups) break;
+        gemv_issue<WT, U, RB>(qa, W, g3 * RB, a.N, a.ldw, chunks, lane, g3 < ngroups);
+        gemv_finish<WT, MT, U, RB>(qb, xs, a, g2 * RB, chunks, lane);
+    }
+}
+
 template <typename WT, int MT>
 static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     const size_t lds = stage_bytes(a.M, a.K);
@@ -160,6 +337,20 @@ static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     if (a.N <= 16384) {
         constexpr int RB = 1;
         hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
+    } else if (a.K <= 64 * 3 * 8 && MT <= 2) {
+        constexpr int RB = 4;
+        // exactly one resident wave of blocks (no tail of late-starting blocks)
+        static int resident = 0;
+        if (!resident) {
+            int per_cu = 0, dev = 0, cus = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_gemv_stream_kernel<WT, MT, RB>, 256, lds);
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            resident = std::max(1, per_cu) * std::max(1, cus);
+        }
+        const int groups = (a.N + RB - 1) / RB;
+        const int blocks = std::min((groups + 3) / 4, resident);
+        hipLaunchKernelGGL((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
     } else {
         constexpr int RB = MT <= 2 ? 4 : 2;
         hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
@@ -197,19 +388,6 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
 // with one agent-scope release / acquire (cdna_hip_programming.md §5 split-K recipe).
 constexpr int DA2_CH = 64;
 
-__device__ __forceinline__ float rope_elem(const float* base, int d, int hd, int rd, int mla, const float* cs,
-                                           const float* sn) {
-    if (d >= rd) return base[d];
-    const int half = rd / 2;
-    auto xr = [&](int i) -> float {
-        if (!mla) return base[i];
-        return i < half ? base[2 * i] : base[2 * (i - half) + 1];
-    };
-    const float x = xr(d);
-    const float rot = d < half ? -xr(d + half) : xr(d - half);
-    return x * cs[d] + rot * sn[d];
-}
-
 template <int HD>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     constexpr int DPL = HD / 4;                                  // dims per lane when scoring (4 lanes / key)
@@ -231,40 +409,57 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     const int kvh = h / (a.heads / a.kv_heads);
     float* Kc = a.kc + (long)b * a.page_stride + (long)kvh * a.head_stride;
     float* Vc = a.vc + (long)b * a.page_stride + (long)kvh * a.head_stride;
-    // 1. cache loads for this thread's keys (the slot at pos is replaced by the new k / v below)
+    const bool own = pos >= k0 && pos < k0 + DA2_CH;
+    // 1. RoPE inputs first (vmcnt is in-order: these must not queue behind the K/V stream)
+    const float* row = a.qkv + (long)b * a.ld;
+    const float* krow = row + a.heads * HD + kvh * HD;
+    const float* vrow = row + (a.heads + a.kv_heads) * HD + kvh * HD;
+    float qx = 0.f, qr = 0.f, kx = 0.f, kr = 0.f, vx = 0.f, cs = 1.f, sn = 0.f, sg = 0.f;
+    if (tid < HD) {
+        int ix = tid, ir = tid;
+        if (tid < a.rope_dim) {
+            const int half = a.rope_dim / 2;
+            auto map = [&](int i) { return !a.use_mla ? i : (i < half ? 2 * i : 2 * (i - half) + 1); };
+            ix = map(tid);
+            ir = tid < half ? map(tid + half) : map(tid - half);
+            sg = tid < half ? -1.f : 1.f;
+            cs = a.cos[(long)pos * a.rope_dim + tid];
+            sn = a.sin[(long)pos * a.rope_dim + tid];
+        }
+        qx = row[h * HD + ix];
+        qr = row[h * HD + ir];
+        if (own) {
+            kx = krow[ix];
+            kr = krow[ir];
+            vx = vrow[tid];
+        }
+    }
+    // 2. cache loads for this thread's keys (the slot at pos is replaced by the new k / v below)
     const int key = wave * 16 + (lane >> 2), sub = lane & 3;
+    // unconditional loads (keys clamped into [k0, k0 + kn)); invalid keys are masked at use
     float4 kreg[DPL / 4];
     {
-        const bool ok = key < kn && k0 + key != pos;
-        const float4* kp = reinterpret_cast<const float4*>(Kc + (long)(k0 + key) * HD + sub * DPL);
+        const float4* kp = reinterpret_cast<const float4*>(Kc + (long)(k0 + min(key, kn - 1)) * HD + sub * DPL);
 #pragma unroll
-        for (int i = 0; i < DPL / 4; ++i) kreg[i] = ok ? kp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < DPL / 4; ++i) kreg[i] = kp[i];
     }
     const int dg = tid % DG, kg = tid / DG;
     float4 vreg[KPG];
 #pragma unroll
     for (int j = 0; j < KPG; ++j) {
-        const int kk = k0 + kg * KPG + j;
-        vreg[j] = (kg * KPG + j < kn && kk != pos) ? *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4)
-                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int kk = k0 + min(kg * KPG + j, kn - 1);
+        vreg[j] = *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4);
     }
-    // 2. rotated q (and the new k, v in the owning chunk)
-    const float* row = a.qkv + (long)b * a.ld;
-    const float* cs = a.cos + (long)pos * a.rope_dim;
-    const float* sn = a.sin + (long)pos * a.rope_dim;
-    const bool own = pos >= k0 && pos < k0 + DA2_CH;
+    // 3. rotated q (and the new k, v in the owning chunk): x*cos + sign*partner*sin
     if (tid < HD) {
-        qs[tid] = rope_elem(row + h * HD, tid, HD, a.rope_dim, a.use_mla, cs, sn);
+        qs[tid] = qx * cs + (sg * qr) * sn;
         if (own) {
-            const float* kr = row + a.heads * HD + kvh * HD;
-            const float* vr = row + (a.heads + a.kv_heads) * HD + kvh * HD;
-            const float kv = rope_elem(kr, tid, HD, a.rope_dim, a.use_mla, cs, sn);
-            const float vv = vr[tid];
+            const float kv = kx * cs + (sg * kr) * sn;
             knew[tid] = kv;
-            vnew[tid] = vv;
+            vnew[tid] = vx;
             if (h == kvh * (a.heads / a.kv_heads)) {  // one writer per kv head
                 Kc[(long)pos * HD + tid] = kv;
-                Vc[(long)pos * HD + tid] = vv;
+                Vc[(long)pos * HD + tid] = vx;
             }
         }
     }
@@ -286,8 +481,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
                 }
             }
         }
-        acc += __shfl_xor(acc, 1, 64);
-        acc += __shfl_xor(acc, 2, 64);
+        acc = quad_sum(acc);
         const float sc = key < kn ? acc * a.scale : -INFINITY;
         if (sub == 0) p_s[key] = sc;
         const float mw = wave_max(sc);
@@ -304,10 +498,11 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     __syncthreads();
     // 4. P.V over this thread's KPG keys
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (own) {
 #pragma unroll
-        for (int j = 0; j < KPG; ++j)
-            if (k0 + kg * KPG + j == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
+    for (int j = 0; j < KPG; ++j) {
+        const int key2 = kg * KPG + j;
+        if (key2 >= kn) vreg[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // never 0 * (stale cache bits)
+        else if (k0 + key2 == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
     }
 #pragma unroll
     for (int j = 0; j < KPG; ++j) {
@@ -319,28 +514,34 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     }
     o_s[tid] = o;
     __syncthreads();
+    // partial record of chunk c: [m, l, -, -, o[HD]] (16-byte aligned), stored WRITE-THROUGH (sc1)
+    // so the hand-off needs no L2-writeback release fence (cdna_hip_programming.md Guideline 16 R1)
+    constexpr int PR = HD + 4;
     const int chunks = (a.max_len + DA2_CH - 1) / DA2_CH;
-    float* part0 = a.part + ((long)b * a.heads + h) * chunks * (HD + 2);
-    float* part = part0 + (long)c * (HD + 2);
+    float* part0 = a.part + ((long)b * a.heads + h) * chunks * PR;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part0, (short)0, chunks * PR * 4, 0x00020000);
     if (tid < DG) {
         float4 t = o_s[tid];
         for (int g = 1; g < KG; ++g) {
             const float4 u = o_s[g * DG + tid];
             t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
         }
-        *reinterpret_cast<float4*>(part + 2 + tid * 4) = t;
+        u32x4 bits;
+        __builtin_memcpy(&bits, &t, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (c * PR + 4 + tid * 4) * 4, 0, 16);
     }
     if (tid == 0) {
-        part[0] = m;
-        part[1] = red[4];
+        const float ml[4] = {m, red[4], 0.f, 0.f};
+        u32x4 bits;
+        __builtin_memcpy(&bits, ml, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
     }
-    // 5. arrival ticket; the last chunk block of (b, h) merges every partial
+    // 5. arrival ticket (every storing wave drains, then one relaxed agent add); the last
+    //    chunk block of (b, h) acquires once and merges every partial
     const int nc = (len + DA2_CH - 1) / DA2_CH;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int* cnt = a.counters + (long)b * a.heads + h;
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == nc - 1;
@@ -360,8 +561,8 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     float* accp = ms + 1024;
     float* lp = ms + 1280;
     for (int cc = tid; cc < nc; cc += 256) {
-        ms[cc] = part0[cc * (HD + 2)];
-        ls[cc] = part0[cc * (HD + 2) + 1];
+        ms[cc] = part0[cc * PR];
+        ls[cc] = part0[cc * PR + 1];
     }
     __syncthreads();
     float mm = -INFINITY;
@@ -373,7 +574,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     for (int cc = grp; cc < nc; cc += KS) {
         const float w = expf(ms[cc] - mm);
         l += ls[cc] * w;
-        acc += part0[cc * (HD + 2) + 2 + dim] * w;
+        acc += part0[cc * PR + 4 + dim] * w;
     }
     accp[grp * HD + dim] = acc;
     lp[grp * HD + dim] = l;
@@ -387,7 +588,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
 }
 
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
-    return (size_t)B * heads * ((max_len + DA2_CH - 1) / DA2_CH) * (hd + 2) * sizeof(float);
+    return (size_t)B * heads * ((max_len + DA2_CH - 1) / DA2_CH) * (hd + 4) * sizeof(float);
 }
 
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
@@ -450,12 +651,7 @@ __device__ __forceinline__ void route_token(const MoeRouteArgs& a, const float* 
             const int e = lane + 64 * j;
             if (e < E && (sc[j] > bv || (sc[j] == bv && e < bi))) { bv = sc[j]; bi = e; }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ov = __shfl_xor(bv, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-        }
+        wave_argmax(bv, bi);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if (lane + 64 * j == bi) sc[j] = -INFINITY;
@@ -526,110 +722,58 @@ __global__ __launch_bounds__(256) void moe_route_kernel(MoeRouteArgs a) {
     group_assignments(a, L);
 }
 
-// One block of 1024 threads: [RMSNorm] + router logits + top-k + grouping (T <= 8 tokens).
-// Router weights (E x K, 164 KB at E = 64) are streamed by 16 waves, R expert rows per
-// wave per batch, the first batch issued before the norm prologue.
-template <typename WT, int U, int R>
-__device__ __forceinline__ void load_rows(uint4 (&q)[U][R], const WT* W, int e0, int E, int K, int base, int lane) {
-    const int chunks = K >> 3;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int c = base + u * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int e = min(e0 + r, E - 1);
-            q[u][r] = (e0 < E && c < chunks) ? ldg_nt16(W + (long)e * K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
-        }
-    }
-}
-
-constexpr int RT_FUSED_MAXT = 8;
-
-template <typename WT, int MT>
-__global__ __launch_bounds__(1024) void moe_router_kernel(MoeRouteArgs a) {
-    extern __shared__ float smem[];
-    __shared__ RouteLds L;
-    __shared__ float lg_s[RT_FUSED_MAXT * 256];
-    constexpr int R = 2, U = 3;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int E = a.E, K = a.Kdim, T = a.T;
-    const WT* W = reinterpret_cast<const WT*>(a.router);
-    const int chunks = K >> 3;
-    for (int e = tid; e <= E; e += 1024) { L.cnt[e] = 0; L.cur[e] = 0; }
-    uint4 q[U][R];
-    int e0 = wave * R;
-    load_rows<WT, U, R>(q, W, e0, E, K, 0, lane);
-    stage_rows(a.x, K, nullptr, T, K, a.norm_w, a.eps, smem);
-    const float* xs = smem + XS_RED;
-    for (; e0 < E; e0 += 16 * R) {
-        float acc[R][MT];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int t = 0; t < MT; ++t) acc[r][t] = 0.f;
-        for (int base = 0;;) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c = base + u * 64 + lane;
-                if (c >= chunks) continue;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    float w8[8];
-                    unpack8<WT>(q[u][r], w8);
-#pragma unroll
-                    for (int t = 0; t < MT; ++t) {
-                        if (t < T) {
-                            float xv[8];
-                            ld_x8(xs + t * K + (c << 3), xv);
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) acc[r][t] = fmaf(xv[j], w8[j], acc[r][t]);
-                        }
-                    }
-                }
-            }
-            base += 64 * U;
-            if (base >= chunks) break;
-            load_rows<WT, U, R>(q, W, e0, E, K, base, lane);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                const float v = wave_sum(acc[r][t]);
-                const int e = e0 + r;
-                if (lane == 0 && t < T && e < E) lg_s[t * E + e] = v + (a.bias ? a.bias[e] : 0.f);
-            }
-        if (e0 + 16 * R < E) load_rows<WT, U, R>(q, W, e0 + 16 * R, E, K, 0, lane);
-    }
-    __syncthreads();
-    for (int t = wave; t < T; t += 16) route_token(a, lg_s + t * E, t, L);
-    __syncthreads();
-    group_assignments(a, L);
-}
-
-bool moe_router_fused_ok(int T, int E, int K) {
-    return T <= RT_FUSED_MAXT && E <= 256 && stage_bytes(T, K) <= 48 * 1024;
-}
-
 void launch_moe_route(const MoeRouteArgs& a, hipStream_t s) {
     if (a.T > RT_MAXT || a.E > 256 || a.topk > 8) throw std::runtime_error("EINVAL: routing supports T <= 64, E <= 256, top_k <= 8");
-    if (a.router) {
-        if (!moe_router_fused_ok(a.T, a.E, a.Kdim)) throw std::runtime_error("EINTERNAL: fused router out of range");
-        const size_t lds = stage_bytes(a.T, a.Kdim);
-        const dim3 g(1), bl(1024);
-        if (a.wdtype == WDT_BF16) {
-            if (a.T == 1) hipLaunchKernelGGL((moe_router_kernel<bf16_t, 1>), g, bl, lds, s, a);
-            else if (a.T == 2) hipLaunchKernelGGL((moe_router_kernel<bf16_t, 2>), g, bl, lds, s, a);
-            else if (a.T <= 4) hipLaunchKernelGGL((moe_router_kernel<bf16_t, 4>), g, bl, lds, s, a);
-            else hipLaunchKernelGGL((moe_router_kernel<bf16_t, 8>), g, bl, lds, s, a);
-        } else {
-            if (a.T == 1) hipLaunchKernelGGL((moe_router_kernel<f16_t, 1>), g, bl, lds, s, a);
-            else if (a.T == 2) hipLaunchKernelGGL((moe_router_kernel<f16_t, 2>), g, bl, lds, s, a);
-            else if (a.T <= 4) hipLaunchKernelGGL((moe_router_kernel<f16_t, 4>), g, bl, lds, s, a);
-            else hipLaunchKernelGGL((moe_router_kernel<f16_t, 8>), g, bl, lds, s, a);
+    hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(256), 0, s, a);
+}
+
+// One wave: greedy top-k of E router logits (softmax or sigmoid scores, stable: ties -> lower
+// expert id, block.rs:1271-1301); returns the `want`-th pick (e, its score) and the sum of the
+// top-k scores (for norm_topk_prob).  Results are wave-uniform.
+__device__ __forceinline__ void topk_select(const float* lg, int E, int K, int softmax_scoring, int want, int& e_out,
+                                            float& v_out, float& wsum) {
+    const int lane = threadIdx.x & 63;
+    float sc[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = lane + 64 * j;
+        sc[j] = e < E ? lg[e] : -INFINITY;
+        mx = fmaxf(mx, sc[j]);
+    }
+    if (softmax_scoring) {
+        mx = wave_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = lane + 64 * j;
+            sc[j] = e < E ? expf(sc[j] - mx) : 0.f;
+            sum += sc[j];
         }
+        sum = wave_sum(sum);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[j] = (lane + 64 * j) < E ? sc[j] / sum : -INFINITY;
     } else {
-        hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(256), 0, s, a);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[j] = (lane + 64 * j) < E ? 1.0f / (1.0f + expf(-sc[j])) : -INFINITY;
+    }
+    wsum = 0.f;
+    e_out = 0;
+    v_out = 0.f;
+    for (int k = 0; k < K; ++k) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = lane + 64 * j;
+            if (e < E && (sc[j] > bv || (sc[j] == bv && e < bi))) { bv = sc[j]; bi = e; }
+        }
+        wave_argmax(bv, bi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (lane + 64 * j == bi) sc[j] = -INFINITY;
+        wsum += bv;
+        if (k == want) { e_out = bi; v_out = bv; }
     }
 }
 
@@ -645,12 +789,52 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
     const int bid = blockIdx.x;
+    __shared__ int sel_e;
+    __shared__ float sel_w;
     const WT* Wg;
     const WT* Wu;
     int rows_I, u, p0, cnt;
     float* hout;
     const int* rowmap;
-    if (bid < a.slots * units_r) {
+    const float* xb = a.x;    // rows come from xb[rowmap[p]] (grouped) or xb[t0 + m]
+    float slot_w = 1.f;       // slot mode: routing weight of this (token, k) slot
+    constexpr int XR = 2;
+    const bool fast = a.K <= XR * 4 * 256;
+    XRegs<MT, XR> xr;
+    bool xpre = false;        // slot mode loads its activation row before routing itself
+    if (bid < a.slots * units_r && a.slot_mode) {
+        // slot mode (T <= 8): block (s = t*topk + k, unit) picks its own expert from the router
+        // logits (the same greedy top-k as moe_route), no grouping pass
+        const int sl = bid / units_r, t = sl / a.topk, k = sl % a.topk;
+        u = bid % units_r;
+        if (fast) {
+            xload<MT, XR>(xr, a.x + (long)t * a.K, a.K, nullptr, 1, a.K, a.norm_w);
+            xpre = true;
+        }
+        if (wave == 0) {
+            int e;
+            float v, wsum;
+            topk_select(a.logits + (long)t * a.E, a.E, a.topk, a.softmax_scoring, k, e, v, wsum);
+            if (a.topk > 1 && a.norm_topk) v = v / (wsum + 1e-20f);
+            if (a.scaling != 1.0f) v = v * a.scaling;
+            if (lane == 0) {
+                sel_e = e;
+                sel_w = v;
+                if (u == 0) { a.ids_out[sl] = e; a.w_out[sl] = v; }
+            }
+        }
+        __syncthreads();
+        const int e = sel_e;
+        slot_w = sel_w;
+        rows_I = a.I;
+        Wg = reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
+        Wu = Wg + (long)a.I * a.K;
+        p0 = sl;
+        cnt = 1;
+        hout = a.h;
+        rowmap = nullptr;
+        xb = a.x + (long)t * a.K;
+    } else if (bid < a.slots * units_r) {
         const int s = bid / units_r;
         if (s >= *a.n_active) return;
         const int e = a.active[s];
@@ -679,6 +863,11 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
     const float* xs = smem + XS_RED;
     for (int t0 = 0; t0 < cnt; t0 += MT) {
         const int tn = min(MT, cnt - t0);
+        if (fast && !xpre) {
+            if (rowmap) xload<MT, XR>(xr, xb, a.K, rowmap + p0 + t0, tn, a.K, a.norm_w);
+            else xload<MT, XR>(xr, xb + (long)t0 * a.K, a.K, nullptr, tn, a.K, a.norm_w);
+        }
+        xpre = false;
         uint4 qg[U][RB], qu[U][RB];
 #pragma unroll
         for (int uu = 0; uu < U; ++uu) {
@@ -686,14 +875,15 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
                 const int i = min(i0 + r, rows_I - 1);
-                const bool ok = active && c < chunks;
-                qg[uu][r] = ok ? ldg_nt16(Wg + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
-                qu[uu][r] = ok ? ldg_nt16(Wu + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                const int cc = min(c, chunks - 1);
+                qg[uu][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
+                qu[uu][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
             }
         }
         if (t0 > 0) __syncthreads();  // previous group's LDS rows fully consumed
-        if (rowmap) stage_rows(a.x, a.K, rowmap + p0 + t0, tn, a.K, a.norm_w, a.eps, smem);
-        else stage_rows(a.x + (long)t0 * a.K, a.K, nullptr, tn, a.K, a.norm_w, a.eps, smem);
+        if (fast) xstage<MT, XR>(xr, tn, a.K, a.norm_w != nullptr, a.eps, smem);
+        else if (rowmap) stage_rows(xb, a.K, rowmap + p0 + t0, tn, a.K, a.norm_w, a.eps, smem);
+        else stage_rows(xb + (long)t0 * a.K, a.K, nullptr, tn, a.K, a.norm_w, a.eps, smem);
         if (!active) continue;
         float ag[RB][MT], au[RB][MT];
 #pragma unroll
@@ -705,21 +895,22 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
             for (int uu = 0; uu < U; ++uu) {
                 const int c = base + uu * 64 + lane;
                 if (c >= chunks) continue;
-                float wg[RB][8], wu[RB][8];
 #pragma unroll
-                for (int r = 0; r < RB; ++r) { unpack8<WT>(qg[uu][r], wg[r]); unpack8<WT>(qu[uu][r], wu[r]); }
+                for (int r = 0; r < RB; ++r) {
+                    float wg[8], wu[8];
+                    unpack8<WT>(qg[uu][r], wg);
+                    unpack8<WT>(qu[uu][r], wu);
 #pragma unroll
-                for (int m = 0; m < MT; ++m) {
-                    if (m < tn) {
-                        float xv[8];
-                        ld_x8(xs + m * a.K + (c << 3), xv);
-#pragma unroll
-                        for (int r = 0; r < RB; ++r)
+                    for (int m = 0; m < MT; ++m) {
+                        if (m < tn) {
+                            float xv[8];
+                            ld_x8(xs + m * a.K + (c << 3), xv);
 #pragma unroll
                             for (int j = 0; j < 8; ++j) {
-                                ag[r][m] = fmaf(xv[j], wg[r][j], ag[r][m]);
-                                au[r][m] = fmaf(xv[j], wu[r][j], au[r][m]);
+                                ag[r][m] = fmaf(xv[j], wg[j], ag[r][m]);
+                                au[r][m] = fmaf(xv[j], wu[j], au[r][m]);
                             }
+                        }
                     }
                 }
             }
@@ -731,8 +922,9 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {
                     const int i = min(i0 + r, rows_I - 1);
-                    qg[uu][r] = c < chunks ? ldg_nt16(Wg + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
-                    qu[uu][r] = c < chunks ? ldg_nt16(Wu + (long)i * a.K + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                    const int cc = min(c, chunks - 1);
+                    qg[uu][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
+                    qu[uu][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
                 }
             }
         }
@@ -746,50 +938,196 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
                 if (lane == 0 && m < tn && i < rows_I) {
                     float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
                     if (rowmap) hv = hv * a.aw[p0 + t0 + m];
+                    else if (hout == a.h) hv = hv * slot_w;
                     hout[(long)(p0 + t0 + m) * rows_I + i] = hv;
                 }
             }
     }
 }
 
-// ------------------------------------------------------------------ MoE down + combine + residual
-// A wave owns output row j of every token: v = sum_k h~[apos(t,k)] . Wd_{e_k}[j]
-// (h~ already carries w_k) + hs[t] . Wsd[j];  X[t][j] += v.  All routed and shared
-// weight loads of a token are issued before the first FMA.
-template <typename WT>
-__global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
+// Slot-mode gate/up (T <= 8, the decode configurations): straight-line code so that the
+// in-order vmcnt accounting stays exact (activation loads -> [routing] -> weight stream ->
+// stage -> FMA).  Blocks [0, T*topk*units_r) are (token, pick) slots that route themselves;
+// the rest are the shared experts over all T tokens (MT >= T).
+template <typename WT, int MT>
+__global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
+    extern __shared__ float smem[];
+    __shared__ int sel_e;
+    __shared__ float sel_w;
+    constexpr int RB = 2, U = 3, XR = 2;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
+    const int bid = blockIdx.x;
+    const bool routed = bid < a.slots * units_r;
+    if (!routed && !a.sWgu) return;
+    const int sl = routed ? bid / units_r : 0;
+    const int t = sl / max(1, a.topk), k = sl % max(1, a.topk);
+    const int u = routed ? bid % units_r : bid - a.slots * units_r;
+    const int M = routed ? 1 : a.T;
+    XRegs<MT, XR> xr;
+    xload<MT, XR>(xr, a.x + (routed ? (long)t * a.K : 0L), a.K, nullptr, M, a.K, a.norm_w);
+    if (routed && (a.dbg & 1)) {
+        if (threadIdx.x == 0) { sel_e = sl % a.E; sel_w = 1.f; }
+        __syncthreads();
+    } else if (routed) {
+        if (wave == 0) {
+            int e;
+            float v, wsum;
+            topk_select(a.logits + (long)t * a.E, a.E, a.topk, a.softmax_scoring, k, e, v, wsum);
+            if (a.topk > 1 && a.norm_topk) v = v / (wsum + 1e-20f);
+            if (a.scaling != 1.0f) v = v * a.scaling;
+            if (lane == 0) {
+                sel_e = e;
+                sel_w = v;
+                if (u == 0) { a.ids_out[sl] = e; a.w_out[sl] = v; }
+            }
+        }
+        __syncthreads();
+    }
+    const int rows_I = routed ? a.I : a.Is;
+    const WT* Wg = routed ? reinterpret_cast<const WT*>(a.Wgu) + (long)sel_e * 2 * a.I * a.K
+                          : reinterpret_cast<const WT*>(a.sWgu);
+    const WT* Wu = Wg + (long)rows_I * a.K;
+    const int i0 = (u * 4 + wave) * RB;
+    const bool active = i0 < rows_I;
+    const int chunks = a.K >> 3;
+    uint4 qg[U][RB], qu[U][RB];
+#pragma unroll
+    for (int uu = 0; uu < U; ++uu) {
+        const int c = uu * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int i = min(i0 + r, rows_I - 1);
+            const int cc = min(c, chunks - 1);
+            if (a.dbg & 2) {
+                qg[uu][r] = make_uint4(cc, i, 0u, 0u);
+                qu[uu][r] = make_uint4(i, cc, 0u, 0u);
+            } else {
+                qg[uu][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
+                qu[uu][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
+            }
+        }
+    }
+    xstage<MT, XR>(xr, M, a.K, a.norm_w != nullptr && !(a.dbg & 4), a.eps, smem);
+    if (!active) return;
+    const float* xs = smem + XS_RED;
+    float ag[RB][MT], au[RB][MT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) { ag[r][m] = 0.f; au[r][m] = 0.f; }
+#pragma unroll
+    for (int uu = 0; uu < U; ++uu) {
+        const int c = uu * 64 + lane;
+        if (c >= chunks || (a.dbg & 8)) continue;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            float wg[8], wu[8];
+            unpack8<WT>(qg[uu][r], wg);
+            unpack8<WT>(qu[uu][r], wu);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                if (m < M) {
+                    float xv[8];
+                    ld_x8(xs + m * a.K + (c << 3), xv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        ag[r][m] = fmaf(xv[j], wg[j], ag[r][m]);
+                        au[r][m] = fmaf(xv[j], wu[j], au[r][m]);
+                    }
+                }
+            }
+        }
+    }
+    const float scale = routed ? sel_w : 1.f;
+    float* hout = routed ? a.h + (long)sl * a.I : a.hs;
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const float gs = wave_sum(ag[r][m]);
+            const float us = wave_sum(au[r][m]);
+            const int i = i0 + r;
+            if (lane == 0 && m < M && i < rows_I) {
+                float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
+                if (routed) hv = hv * scale;
+                hout[(long)m * rows_I + i] = hv;
+            }
+        }
+}
+
+// ------------------------------------------------------------------ MoE down + combine + residual
+// A wave owns output row j of every token: v = sum_k h~[row(t,k)] . Wd_{e_k}[j]
+// (h~ already carries w_k) + hs[t] . Wsd[j];  X[t][j] += v.  Per token the block first
+// loads the activations it needs ([topk x I] routed rows + [Is] shared row) into registers,
+// then issues every weight load, then stages the activations through LDS (STAGE: when
+// they fit in 64 KB), so that no activation load queues behind the weight stream.
+constexpr int DN_HREG = 8;  // float4 activation registers per thread (topk*I + Is <= 8192)
+
+template <typename WT, bool STAGE>
+__global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
+    extern __shared__ float hsm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = blockIdx.x * 4 + wave;
-    if (j >= a.Hout) return;
+    const bool active = j < a.Hout;
+    if (!STAGE && !active) return;
     const int K = a.topk;
     const int ch_r = K > 0 ? (a.I >> 3) : 0, ch_s = a.sWd ? (a.Is >> 3) : 0;
-    const WT* Ws = reinterpret_cast<const WT*>(a.sWd) + (long)j * a.Is;
+    const int jj0 = min(j, a.Hout - 1);
+    const WT* Ws = reinterpret_cast<const WT*>(a.sWd) + (long)jj0 * a.Is;
+    const int nr4 = K * (a.I >> 2), ns4 = ch_s ? (a.Is >> 2) : 0;  // float4 counts (routed, shared)
     for (int t = 0; t < a.T; ++t) {
+        float4 hreg[DN_HREG];
+        if (STAGE) {
+#pragma unroll
+            for (int r = 0; r < DN_HREG; ++r) {
+                const int f = tid + r * 256;
+                const float* src = nullptr;
+                if (f < nr4) {
+                    const int k = f / (a.I >> 2), off = f - k * (a.I >> 2);
+                    const int row = a.apos ? a.apos[t * K + k] : t * K + k;
+                    src = a.h + (long)row * a.I + off * 4;
+                } else if (f < nr4 + ns4) {
+                    src = a.hs + (long)t * a.Is + (f - nr4) * 4;
+                }
+                hreg[r] = src ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
         float acc = 0.f;
-        const float* hs = a.hs + (long)t * a.Is;
         for (int br = 0, bs = 0; br < ch_r || bs < ch_s; br += 128, bs += 256) {
             uint4 qr[8][2], qs[4];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (k < K) {
                     const int e = a.ids[t * K + k];
-                    const WT* Wd = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + j) * a.I;
+                    const WT* Wd = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + jj0) * a.I;
 #pragma unroll
                     for (int uu = 0; uu < 2; ++uu) {
                         const int c = br + uu * 64 + lane;
-                        qr[k][uu] = c < ch_r ? ldg_nt16(Wd + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                        qr[k][uu] = ldg_nt16(Wd + (min(c, ch_r - 1) << 3));
                     }
                 }
             }
 #pragma unroll
             for (int uu = 0; uu < 4; ++uu) {
                 const int c = bs + uu * 64 + lane;
-                qs[uu] = c < ch_s ? ldg_nt16(Ws + (c << 3)) : make_uint4(0u, 0u, 0u, 0u);
+                qs[uu] = ch_s ? ldg_nt16(Ws + (min(c, ch_s - 1) << 3)) : make_uint4(0u, 0u, 0u, 0u);
             }
+            if (STAGE && br == 0) {
+                if (t > 0) __syncthreads();  // previous token's rows consumed
+#pragma unroll
+                for (int r = 0; r < DN_HREG; ++r) {
+                    const int f = tid + r * 256;
+                    if (f < nr4 + ns4) *reinterpret_cast<float4*>(hsm + f * 4) = hreg[r];
+                }
+                __syncthreads();
+            }
+            if (!active) continue;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (k < K) {
-                    const float* hp = a.h + (long)a.apos[t * K + k] * a.I;
+                    const float* hp = STAGE ? hsm + (long)k * a.I
+                                            : a.h + (long)(a.apos ? a.apos[t * K + k] : t * K + k) * a.I;
 #pragma unroll
                     for (int uu = 0; uu < 2; ++uu) {
                         const int c = br + uu * 64 + lane;
@@ -798,11 +1136,12 @@ __global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
                             ld_x8(hp + (c << 3), hv);
                             unpack8<WT>(qr[k][uu], w8);
 #pragma unroll
-                            for (int jj = 0; jj < 8; ++jj) acc = fmaf(hv[jj], w8[jj], acc);
+                            for (int q = 0; q < 8; ++q) acc = fmaf(hv[q], w8[q], acc);
                         }
                     }
                 }
             }
+            const float* hs = STAGE ? hsm + (long)K * a.I : a.hs + (long)t * a.Is;
 #pragma unroll
             for (int uu = 0; uu < 4; ++uu) {
                 const int c = bs + uu * 64 + lane;
@@ -811,12 +1150,89 @@ __global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
                     ld_x8(hs + (c << 3), hv);
                     unpack8<WT>(qs[uu], w8);
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) acc = fmaf(hv[jj], w8[jj], acc);
+                    for (int q = 0; q < 8; ++q) acc = fmaf(hv[q], w8[q], acc);
                 }
             }
         }
+        if (active) {
+            const float v = wave_sum(acc);
+            if (lane == 0) {
+                float* xp = a.out + (long)t * a.Hout + j;
+                *xp = *xp + v;
+            }
+        }
+    }
+}
+
+// Slot-mode down (T <= 8, topk = KT at compile time, I <= 1024, Is <= 2048): per token,
+// activations -> registers, every routed + shared weight load, then LDS staging and FMAs;
+// straight-line so each consumer waits only for the loads it needs.
+template <typename WT, int KT>
+__global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
+    extern __shared__ float hsm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int j = blockIdx.x * 4 + wave;
+    const bool active = j < a.Hout;
+    const int jj = min(j, a.Hout - 1);
+    const int ch_r = a.I >> 3, ch_s = a.sWd ? (a.Is >> 3) : 0;
+    const int nr4 = KT * (a.I >> 2), ns4 = a.sWd ? (a.Is >> 2) : 0, n4 = nr4 + ns4;
+    const WT* Ws = a.sWd ? reinterpret_cast<const WT*>(a.sWd) + (long)jj * a.Is
+                         : reinterpret_cast<const WT*>(a.Wd) + (long)jj * a.I;
+    const int cs_max = a.sWd ? ch_s - 1 : ch_r - 1;
+    for (int t = 0; t < a.T; ++t) {
+        // slot rows t*KT .. t*KT+KT-1 of h are contiguous: [KT*I routed | Is shared] as one vector
+        const float* hr = a.h + (long)t * KT * a.I;
+        const float* hsh = a.sWd ? a.hs + (long)t * a.Is : hr;
+        f32x4 hreg[DN_HREG];  // native vector type: a float4 struct array stays in scratch here
+#pragma unroll
+        for (int r = 0; r < DN_HREG; ++r) {
+            const int f = min(tid + r * 256, n4 - 1);
+            const float* src = f < nr4 ? hr + f * 4 : hsh + (f - nr4) * 4;
+            hreg[r] = *reinterpret_cast<const f32x4*>(src);
+        }
+        uint4 qr[KT][2], qs[4];
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            const int e = a.ids[t * KT + k];
+            const WT* Wd = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + jj) * a.I;
+#pragma unroll
+            for (int uu = 0; uu < 2; ++uu) qr[k][uu] = ldg_nt16(Wd + (min(uu * 64 + lane, ch_r - 1) << 3));
+        }
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) qs[uu] = ldg_nt16(Ws + (min(uu * 64 + lane, cs_max) << 3));
+        __syncthreads();  // previous token's rows consumed (unconditional: keeps hreg in VGPRs)
+#pragma unroll
+        for (int r = 0; r < DN_HREG; ++r)  // LDS holds 256*DN_HREG float4: no bounds branch
+            *reinterpret_cast<f32x4*>(hsm + (tid + r * 256) * 4) = hreg[r];
+        __syncthreads();
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+#pragma unroll
+            for (int uu = 0; uu < 2; ++uu) {
+                const int c = uu * 64 + lane;
+                if (c < ch_r) {
+                    float hv[8], w8[8];
+                    ld_x8(hsm + k * a.I + (c << 3), hv);
+                    unpack8<WT>(qr[k][uu], w8);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) acc = fmaf(hv[q], w8[q], acc);
+                }
+            }
+        }
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) {
+            const int c = uu * 64 + lane;
+            if (c < ch_s) {
+                float hv[8], w8[8];
+                ld_x8(hsm + nr4 * 4 + (c << 3), hv);
+                unpack8<WT>(qs[uu], w8);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) acc = fmaf(hv[q], w8[q], acc);
+            }
+        }
         const float v = wave_sum(acc);
-        if (lane == 0) {
+        if (active && lane == 0) {
             float* xp = a.out + (long)t * a.Hout + j;
             *xp = *xp + v;
         }
@@ -828,6 +1244,20 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
     const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
     dim3 grid(a.slots * units_r + units_s);
+    if (a.slot_mode && a.K <= 64 * 3 * 8 && a.T <= 8) {
+        const int mt = a.T == 1 ? 1 : (a.T <= 2 ? 2 : (a.T <= 4 ? 4 : 8));
+        const size_t lds = stage_bytes(mt, a.K);
+#define DSOCR_SLOT(WTY, MTV) hipLaunchKernelGGL((moe_gateup_slot_kernel<WTY, MTV>), grid, dim3(256), lds, s, a)
+        if (a.wdtype == WDT_BF16) {
+            if (mt == 1) DSOCR_SLOT(bf16_t, 1); else if (mt == 2) DSOCR_SLOT(bf16_t, 2);
+            else if (mt == 4) DSOCR_SLOT(bf16_t, 4); else DSOCR_SLOT(bf16_t, 8);
+        } else {
+            if (mt == 1) DSOCR_SLOT(f16_t, 1); else if (mt == 2) DSOCR_SLOT(f16_t, 2);
+            else if (mt == 4) DSOCR_SLOT(f16_t, 4); else DSOCR_SLOT(f16_t, 8);
+        }
+#undef DSOCR_SLOT
+        return;
+    }
     const int mt = a.T == 1 ? 1 : (a.T <= 4 ? 4 : 8);
     const size_t lds = stage_bytes(mt, a.K);
     if (lds > STAGE_LDS_MAX) throw std::runtime_error("EINVAL: moe_gateup2 hidden size too large for LDS staging");
@@ -844,8 +1274,26 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
     if (a.topk > 8) throw std::runtime_error("EINVAL: moe_down2 supports top_k <= 8");
     dim3 grid((a.Hout + 3) / 4);
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down2_kernel<bf16_t>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((moe_down2_kernel<f16_t>), grid, dim3(256), 0, s, a);
+    const long n4 = (long)a.topk * (a.I / 4) + (a.sWd ? a.Is / 4 : 0);
+    if (a.slot_mode && !a.apos && (a.topk == 6 || a.topk == 3) && a.I <= 1024 && (!a.sWd || a.Is <= 2048) &&
+        n4 <= 256L * DN_HREG) {
+        const size_t lds = (size_t)256 * DN_HREG * 16;
+#define DSOCR_DSLOT(WTY, KTV) hipLaunchKernelGGL((moe_down_slot_kernel<WTY, KTV>), grid, dim3(256), lds, s, a)
+        if (a.wdtype == WDT_BF16) { if (a.topk == 6) DSOCR_DSLOT(bf16_t, 6); else DSOCR_DSLOT(bf16_t, 3); }
+        else { if (a.topk == 6) DSOCR_DSLOT(f16_t, 6); else DSOCR_DSLOT(f16_t, 3); }
+#undef DSOCR_DSLOT
+        return;
+    }
+    const long f4 = (long)a.topk * (a.I / 4) + (a.sWd ? a.Is / 4 : 0);
+    const bool stage = f4 <= 256L * DN_HREG && f4 * 16 <= (long)STAGE_LDS_MAX;
+    const size_t lds = stage ? (size_t)f4 * 16 : 0;
+    if (a.wdtype == WDT_BF16) {
+        if (stage) hipLaunchKernelGGL((moe_down2_kernel<bf16_t, true>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((moe_down2_kernel<bf16_t, false>), grid, dim3(256), 0, s, a);
+    } else {
+        if (stage) hipLaunchKernelGGL((moe_down2_kernel<f16_t, true>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((moe_down2_kernel<f16_t, false>), grid, dim3(256), 0, s, a);
+    }
 }
 
 // ------------------------------------------------------------------ sampling (fused)
@@ -861,12 +1309,7 @@ __device__ __forceinline__ bool sp_better(float v, int i, float bv, int bi) { re
 // (value, index) argmax over the block (first index on ties); result in sv[0] / si[0]
 __device__ __forceinline__ void block_argmax(float bv, int bi, float* sv, int* si) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (sp_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
+    wave_argmax(bv, bi);
     if (lane == 0) { sv[wave] = bv; si[wave] = bi; }
     __syncthreads();
     if (threadIdx.x == 0) {

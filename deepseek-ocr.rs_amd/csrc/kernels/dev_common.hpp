@@ -53,14 +53,62 @@ __device__ __forceinline__ void unpack8(const uint4 q, float* o) {
     o[6] = wbits_to_f32<WT>(q.w); o[7] = wbits_to_f32<WT>(q.w >> 16);
 }
 
+// Wave64 reductions on DPP row operations (a few cycles each) instead of __shfl_xor, which
+// lowers to ds_bpermute (an LDS-crossbar round trip, ~120 cycles) — a 6-step butterfly of
+// those dominated the small decode kernels.  Pattern: quad xor 1, quad xor 2, row half
+// mirror, row mirror (every lane of a 16-lane row now holds the row total), then
+// row_bcast15 / row_bcast31 fold the rows into lane 63, which is broadcast.  Requires all
+// 64 lanes active (every call site is in wave-uniform control flow).
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dpp_f(float old, float src) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, ROWMASK, 0xf, false));
+}
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ int dpp_i(int old, int src) {
+    return __builtin_amdgcn_update_dpp(old, src, CTRL, ROWMASK, 0xf, false);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1, DPP_QUAD_XOR2 = 0x4E, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_MIRROR = 0x140,
+              DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_f<DPP_QUAD_XOR1>(0.f, v);
+    v += dpp_f<DPP_QUAD_XOR2>(0.f, v);
+    v += dpp_f<DPP_ROW_HALF_MIRROR>(0.f, v);
+    v += dpp_f<DPP_ROW_MIRROR>(0.f, v);
+    v += dpp_f<DPP_ROW_BCAST15, 0xA>(0.f, v);
+    v += dpp_f<DPP_ROW_BCAST31, 0xC>(0.f, v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    v = fmaxf(v, dpp_f<DPP_QUAD_XOR1>(-INFINITY, v));
+    v = fmaxf(v, dpp_f<DPP_QUAD_XOR2>(-INFINITY, v));
+    v = fmaxf(v, dpp_f<DPP_ROW_HALF_MIRROR>(-INFINITY, v));
+    v = fmaxf(v, dpp_f<DPP_ROW_MIRROR>(-INFINITY, v));
+    v = fmaxf(v, dpp_f<DPP_ROW_BCAST15, 0xA>(-INFINITY, v));
+    v = fmaxf(v, dpp_f<DPP_ROW_BCAST31, 0xC>(-INFINITY, v));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// (value, index) argmax over the wave, ties -> lower index; result broadcast to all lanes
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ void argmax_step(float& bv, int& bi) {
+    const float ov = dpp_f<CTRL, ROWMASK>(-INFINITY, bv);
+    const int oi = dpp_i<CTRL, ROWMASK>(0x7fffffff, bi);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+__device__ __forceinline__ void wave_argmax(float& bv, int& bi) {
+    argmax_step<DPP_QUAD_XOR1>(bv, bi);
+    argmax_step<DPP_QUAD_XOR2>(bv, bi);
+    argmax_step<DPP_ROW_HALF_MIRROR>(bv, bi);
+    argmax_step<DPP_ROW_MIRROR>(bv, bi);
+    argmax_step<DPP_ROW_BCAST15, 0xA>(bv, bi);
+    argmax_step<DPP_ROW_BCAST31, 0xC>(bv, bi);
+    bv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv), 63));
+    bi = __builtin_amdgcn_readlane(bi, 63);
+}
+// sum over the 4 lanes of a quad (lanes 4q .. 4q+3), result in every lane of the quad
+__device__ __forceinline__ float quad_sum(float v) {
+    v += dpp_f<DPP_QUAD_XOR1>(0.f, v);
+    v += dpp_f<DPP_QUAD_XOR2>(0.f, v);
     return v;
 }
 

@@ -139,12 +139,9 @@ struct DecAttn2Args {
 };
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
-// Router top-k + grouping in one block (T <= 64, E <= 256, top_k <= 8).  With `router` set
-// the block also computes the logits of rmsnorm(x) (T <= 8, see moe_router_fused_ok).
+// Router top-k + grouping by expert in one block (T <= 64, E <= 256, top_k <= 8).
 struct MoeRouteArgs {
     const float* logits = nullptr;
-    const float* x = nullptr; const float* norm_w = nullptr; float eps = 0.f;
-    const void* router = nullptr; const float* bias = nullptr; int Kdim = 0; int wdtype = WDT_F16;
     int T = 0, E = 0, topk = 0, softmax_scoring = 1, norm_topk = 0;
     float scaling = 1.f;
     int* ids = nullptr; float* w = nullptr;
@@ -153,7 +150,6 @@ struct MoeRouteArgs {
     int* active = nullptr; int* n_active = nullptr;
 };
 void launch_moe_route(const MoeRouteArgs& a, hipStream_t s);
-bool moe_router_fused_ok(int T, int E, int K);
 // Routed experts + shared experts (gate/up: one launch; down + weighted combine + residual: one launch).
 struct MoeDec2Args {
     int T = 0, topk = 0, E = 0, K = 0, I = 0, Is = 0, Hout = 0, slots = 0;
@@ -167,6 +163,14 @@ struct MoeDec2Args {
     int wdtype = WDT_F16;
     float* h = nullptr; float* hs = nullptr;
     float* out = nullptr;           // [T][Hout], += combined
+    // slot mode (T <= 8): gate/up blocks route themselves from the router logits; h row of
+    // (token t, pick k) = t*topk + k; ids_out / w_out receive the picks (apos must be null)
+    int slot_mode = 0;
+    const float* logits = nullptr;
+    int softmax_scoring = 1, norm_topk = 0;
+    float scaling = 1.f;
+    int* ids_out = nullptr; float* w_out = nullptr;
+    int dbg = 0;  // experiment knobs (DSOCR_DBG_GU): 1 skip routing, 2 skip weight stream
 };
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);

@@ -16,6 +16,8 @@ for step in "$@"; do
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
     bench_full) run 1100 python bench.py > gpurun_out/bench_full.log 2>&1 ;;
     prof) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
+    mb) run 120 ./tools/mb_stream > gpurun_out/mb_stream.log 2>&1 ;;
+    mbprof) run 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mbprof -o mb --output-format csv -- ./tools/mb_stream > gpurun_out/mbprof.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
