@@ -387,7 +387,6 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
         dsocr::DecGemvArgs ra;
         ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
         ra.y = log; ra.ldy = E; ra.norm_w = norm_w; ra.eps = eps;
-        dsocr::launch_dec_gemv(ra, nullptr);
         // same dispatch as Engine::moe_decode_args: slot mode for T <= 8, grouped by expert above
         dsocr::MoeDec2Args m;
         m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H;
@@ -399,10 +398,21 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
         if (sWgu && sWd && Is > 0) {
             m.Is = Is; m.sWgu = sWgu; m.sWd = sWd; m.hs = (float*)alloc(sizeof(float) * (size_t)T * Is);
         }
-        if (T <= 8) {
+        const char* epi = getenv("DSOCR_ROUTER_EPI");
+        if (T <= 8 && epi && atoi(epi) && dsocr::dec_router_ok(T, E, H, topk)) {
+            int* cnt = (int*)alloc(sizeof(int) * 16);
+            check_hip(hipMemset(cnt, 0, sizeof(int) * 16), "hipMemset");
+            dsocr::DecRouteEpi re;
+            re.topk = topk; re.softmax_scoring = 1; re.norm_topk = norm_topk; re.scaling = scaling;
+            re.ids = ids; re.w = wts; re.counter = cnt;
+            dsocr::launch_dec_router(ra, re, nullptr);
+            m.slot_mode = 1; m.slots = TK; m.logits = nullptr; m.aw = wts;
+        } else if (T <= 8) {  // engine default: gate/up blocks route themselves
+            dsocr::launch_dec_gemv(ra, nullptr);
             m.slot_mode = 1; m.slots = TK; m.logits = log; m.softmax_scoring = 1; m.norm_topk = norm_topk;
             m.scaling = scaling; m.ids_out = ids; m.w_out = wts;
         } else {
+            dsocr::launch_dec_gemv(ra, nullptr);
             dsocr::MoeRouteArgs r;
             r.logits = log; r.T = T; r.E = E; r.topk = topk; r.softmax_scoring = 1; r.norm_topk = norm_topk;
             r.scaling = scaling; r.ids = ids; r.w = wts;

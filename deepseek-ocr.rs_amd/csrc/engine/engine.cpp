@@ -781,7 +781,13 @@ MoeDec2Args Engine::moe_decode_args(int l, int B, const float* x, const float* n
         if (d.s_gu.wdt != d.e_wdt) throw std::runtime_error("EINTERNAL: shared/routed expert dtype mismatch");
         m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is);
     }
-    if (B <= 8) {
+    static const bool router_epi = getenv("DSOCR_ROUTER_EPI") && atoi(getenv("DSOCR_ROUTER_EPI"));
+    if (B <= 8 && router_epi && dec_router_ok(B, E, H, K)) {
+        // slot mode routed by dec_router's last-block epilogue (measured +1.6 us / layer on
+        // MI355X vs self-routing: the write-through + ticket hand-off costs more than it saves)
+        m.slot_mode = 1; m.slots = TK; m.logits = nullptr; m.aw = wsf("s_wts", TK);
+    } else if (B <= 8) {
+        // slot mode: every gate/up block routes itself from the router logits in s_log
         m.slot_mode = 1; m.slots = TK; m.logits = wsf("s_log", (size_t)B * E);
         m.softmax_scoring = L.scoring == "softmax"; m.norm_topk = L.norm_topk; m.scaling = L.routed_scaling;
         m.ids_out = wsi("s_ids", TK); m.w_out = wsf("s_wts", TK);
@@ -853,8 +859,16 @@ void Engine::decode_step(int B, int Lmax) {
         DecGemvArgs gr;
         gr.M = B; gr.N = E; gr.K = H; gr.x = mx; gr.ldx = H; gr.W = d.router.W; gr.ldw = H; gr.wdtype = d.router.wdt;
         gr.bias = d.router.b; gr.y = LOG; gr.ldy = E; gr.norm_w = mnorm; gr.eps = L.rms_eps;
-        launch_dec_gemv(gr, st);
         m = moe_decode_args(l, B, mx, mnorm, X);
+        if (m.slot_mode && !m.logits) {
+            DecRouteEpi re;
+            re.topk = K; re.softmax_scoring = L.scoring == "softmax"; re.norm_topk = L.norm_topk;
+            re.scaling = L.routed_scaling; re.ids = const_cast<int*>(m.ids); re.w = const_cast<float*>(m.aw);
+            re.counter = wsi("s_route_cnt", 16);
+            launch_dec_router(gr, re, st);
+        } else {
+            launch_dec_gemv(gr, st);
+        }
         if (!m.slot_mode) {  // B > 8: one block sorts the assignments by expert
             MoeRouteArgs ra;
             ra.logits = LOG; ra.T = B; ra.E = E; ra.topk = K; ra.softmax_scoring = L.scoring == "softmax";
@@ -1052,6 +1066,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     vc_ = wsf("kv_v", kv_need / 4);
     // arrival tickets of the decode-attention combine: zero here, every launch leaves them zero
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
+    HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
     const int QKVN = layers_[0].qkv.N;
     r0 = 0;
     for (int b = 0; b < B; ++b) {

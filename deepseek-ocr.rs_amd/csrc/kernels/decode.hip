@@ -379,6 +379,156 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
     }
 }
 
+// ------------------------------------------------------------------ router + top-k
+// MoE router logits (E x K GEMV, norm fused) whose LAST-arriving block routes every token:
+// softmax (or sigmoid) + greedy top-k (block.rs:1254-1301) -> ids[t*topk+k], w[t*topk+k].
+// Logits are stored write-through (sc1 atomics) so the hand-off needs only the arrival
+// ticket and one agent acquire in the last block (cdna_hip_programming.md Guideline 16 R1).
+__device__ __forceinline__ void topk_write(const float* lg, int E, int K, int softmax_scoring, int norm_topk,
+                                           float scaling, int* ids, float* w) {
+    const int lane = threadIdx.x & 63;
+    float sc[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = min(lane + 64 * j, E - 1);
+        sc[j] = lg[e];
+        if (lane + 64 * j >= E) sc[j] = -INFINITY;
+        mx = fmaxf(mx, sc[j]);
+    }
+    if (softmax_scoring) {
+        mx = wave_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sc[j] = (lane + 64 * j) < E ? expf(sc[j] - mx) : 0.f;
+            sum += sc[j];
+        }
+        sum = wave_sum(sum);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[j] = (lane + 64 * j) < E ? sc[j] / sum : -INFINITY;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sc[j] = (lane + 64 * j) < E ? 1.0f / (1.0f + expf(-sc[j])) : -INFINITY;
+    }
+    float picked[8];
+    int pid[8];
+    float wsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        picked[k] = 0.f;
+        pid[k] = 0;
+        if (k < K) {
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = lane + 64 * j;
+                if (e < E && (sc[j] > bv || (sc[j] == bv && e < bi))) { bv = sc[j]; bi = e; }
+            }
+            wave_argmax(bv, bi);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (lane + 64 * j == bi) sc[j] = -INFINITY;
+            picked[k] = bv;
+            pid[k] = bi;
+            wsum += bv;
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k < K) {
+                float v = picked[k];
+                if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
+                if (scaling != 1.0f) v = v * scaling;
+                ids[k] = pid[k];
+                w[k] = v;
+            }
+        }
+    }
+}
+
+template <typename WT, int MT>
+__global__ __launch_bounds__(256) void dec_router_kernel(DecGemvArgs a, DecRouteEpi r) {
+    extern __shared__ float smem[];
+    __shared__ int last_s;
+    constexpr int U = 3, XR = 2;  // K <= 1536
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n = blockIdx.x * 4 + wave;
+    const bool active = n < a.N;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    XRegs<MT, XR> xr;
+    xload<MT, XR>(xr, a.x, a.ldx, nullptr, a.M, a.K, a.norm_w);
+    uint4 wq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) wq[u] = ldg_nt16(W + (long)min(n, a.N - 1) * a.ldw + (min(u * 64 + lane, chunks - 1) << 3));
+    xstage<MT, XR>(xr, a.M, a.K, a.norm_w != nullptr, a.eps, smem);
+    const float* xs = smem + XS_RED;
+    float acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        if (c < chunks) {
+            float w8[8];
+            unpack8<WT>(wq[u], w8);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                if (m < a.M) {
+                    float xv[8];
+                    ld_x8(xs + m * a.K + (c << 3), xv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[m] = fmaf(xv[j], w8[j], acc[m]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const float v = wave_sum(acc[m]) + (a.bias ? a.bias[min(n, a.N - 1)] : 0.f);
+        if (lane == 0 && active && m < a.M)
+            __hip_atomic_store(a.y + (long)m * a.ldy + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(r.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (int)gridDim.x - 1;
+        if (last) {
+            __hip_atomic_store(r.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    for (int t = wave; t < a.M; t += 4)
+        topk_write(a.y + (long)t * a.ldy, a.N, r.topk, r.softmax_scoring, r.norm_topk, r.scaling, r.ids + t * r.topk,
+                   r.w + t * r.topk);
+}
+
+bool dec_router_ok(int T, int E, int K, int topk) { return T <= 8 && E <= 256 && K <= 64 * 3 * 8 && topk <= 8; }
+
+void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s) {
+    if (!dec_router_ok(a.M, a.N, a.K, r.topk) || !r.counter) throw std::runtime_error("EINVAL: dec_router out of range");
+    const int mt = a.M == 1 ? 1 : (a.M <= 2 ? 2 : (a.M <= 4 ? 4 : 8));
+    const size_t lds = stage_bytes(mt, a.K);
+    dim3 grid((a.N + 3) / 4);
+#define DSOCR_RT(WTY, MTV) hipLaunchKernelGGL((dec_router_kernel<WTY, MTV>), grid, dim3(256), lds, s, a, r)
+    if (a.wdtype == WDT_BF16) {
+        if (mt == 1) DSOCR_RT(bf16_t, 1); else if (mt == 2) DSOCR_RT(bf16_t, 2);
+        else if (mt == 4) DSOCR_RT(bf16_t, 4); else DSOCR_RT(bf16_t, 8);
+    } else {
+        if (mt == 1) DSOCR_RT(f16_t, 1); else if (mt == 2) DSOCR_RT(f16_t, 2);
+        else if (mt == 4) DSOCR_RT(f16_t, 4); else DSOCR_RT(f16_t, 8);
+    }
+#undef DSOCR_RT
+}
+
 // ------------------------------------------------------------------ decode attention
 // grid (chunks of 64 keys, heads, B).  The token being decoded sits at pos = kv_pos[b]:
 // q and k are rotated here (rotate_half RoPE, block.rs:1403-1471), the block owning
@@ -966,7 +1116,13 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
     const int M = routed ? 1 : a.T;
     XRegs<MT, XR> xr;
     xload<MT, XR>(xr, a.x + (routed ? (long)t * a.K : 0L), a.K, nullptr, M, a.K, a.norm_w);
-    if (routed && (a.dbg & 1)) {
+    int e_pre = 0;
+    float w_pre = 1.f;
+    const bool pre = routed && !a.logits;  // routed by dec_router: ids / aw already in memory
+    if (pre) {
+        e_pre = a.ids[sl];
+        w_pre = a.aw[sl];
+    } else if (routed && (a.dbg & 1)) {
         if (threadIdx.x == 0) { sel_e = sl % a.E; sel_w = 1.f; }
         __syncthreads();
     } else if (routed) {
@@ -985,7 +1141,8 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
         __syncthreads();
     }
     const int rows_I = routed ? a.I : a.Is;
-    const WT* Wg = routed ? reinterpret_cast<const WT*>(a.Wgu) + (long)sel_e * 2 * a.I * a.K
+    const int e_sel = pre ? e_pre : sel_e;
+    const WT* Wg = routed ? reinterpret_cast<const WT*>(a.Wgu) + (long)e_sel * 2 * a.I * a.K
                           : reinterpret_cast<const WT*>(a.sWgu);
     const WT* Wu = Wg + (long)rows_I * a.K;
     const int i0 = (u * 4 + wave) * RB;
@@ -1039,7 +1196,7 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
             }
         }
     }
-    const float scale = routed ? sel_w : 1.f;
+    const float scale = routed ? (pre ? w_pre : sel_w) : 1.f;
     float* hout = routed ? a.h + (long)sl * a.I : a.hs;
 #pragma unroll
     for (int r = 0; r < RB; ++r)

@@ -13,6 +13,9 @@
 // Optional row gather for A (a_rows), row scatter for C (c_rows, -1 = drop),
 // and grouping (blockIdx.z = group, rows [goff[g], goff[g+1]) of the gathered
 // list, weight slab g) for the MoE prefill grouped GEMM.
+#include <cstdint>
+#include <cstdlib>
+
 #include "dev_common.hpp"
 #include "kernels.hpp"
 
@@ -150,11 +153,193 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-bf16 GEMM (same contract, same result to f32 rounding): every f32 activation is
+// split exactly into three bf16 terms a = hi + mid + lo (RNE at each step; the residuals
+// are exact in f32 by Sterbenz), weights are bf16 (vision: one exact plane) or f16 (decoder:
+// hi + lo bf16 planes, exact since f16 has an 11-bit significand).  A.W^T is then the sum
+// of 3 (bf16 W) or 5 (f16 W; the lo x lo term is below f32 rounding) products on
+// v_mfma_f32_32x32x16_bf16 — bf16 x bf16 products are exact in the f32 accumulator — at
+// 16x the per-instruction rate of the f32-input MFMA (MI355X_MICROARCH.md constants).
+// Tile 128x128x32, 4 waves as 2x2 of 64x64 (2x2 MFMA 32x32 tiles each); LDS holds the
+// bf16 planes row-major with k contiguous (row stride 80 B: conflict-free fragment reads).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr int XB_M = 128, XB_N = 128, XB_K = 32, XB_KP = 40;
+
+__device__ __forceinline__ void split3(float a, __bf16& hi, __bf16& mid, __bf16& lo) {
+    hi = (__bf16)a;
+    const float r1 = a - (float)hi;
+    mid = (__bf16)r1;
+    const float r2 = r1 - (float)mid;
+    lo = (__bf16)r2;
+}
+
+template <typename WT>
+__global__ __launch_bounds__(256) void gemm_x3_kernel(GemmArgs g) {
+    constexpr int WP = sizeof(WT) == 2 && __is_same(WT, bf16_t) ? 1 : 2;
+    __shared__ __attribute__((aligned(16))) __bf16 As[3][XB_M][XB_KP];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[WP][XB_N][XB_KP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    int m_begin = 0, m_count = g.M;
+    const WT* W = reinterpret_cast<const WT*>(g.W);
+    const float* bias = g.bias;
+    if (g.group_off) {
+        const int grp = blockIdx.z;
+        m_begin = g.group_off[grp];
+        m_count = g.group_off[grp + 1] - m_begin;
+        W += (size_t)grp * g.w_group_stride;
+        if (bias) bias += (size_t)grp * g.bias_group_stride;
+    }
+    const int m0 = blockIdx.y * XB_M;
+    if (m0 >= m_count) return;
+    const int n0 = blockIdx.x * XB_N;
+    // staging coordinates: thread -> (row tid>>1, 16 consecutive k at (tid&1)*16)
+    const int s_r = tid >> 1, s_k = (tid & 1) * 16;
+    const bool a_ok = m0 + s_r < m_count;
+    const int arr = m_begin + (a_ok ? m0 + s_r : 0);
+    const float* a_ptr = g.A + (long)(g.a_rows ? g.a_rows[arr] : arr) * g.lda + s_k;
+    const bool b_ok = n0 + s_r < g.N;
+    const WT* w_ptr = W + (long)(b_ok ? n0 + s_r : 0) * g.ldw + s_k;
+    float4 ra[4];
+    uint4 rb[2];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const float4*>(a_ptr + k0 + 4 * i);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) rb[i] = *reinterpret_cast<const uint4*>(w_ptr + k0 + 8 * i);
+    };
+    auto lstore = [&]() {
+        __bf16 h[16], m[16], l[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float v[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) split3(a_ok ? v[j] : 0.f, h[4 * i + j], m[4 * i + j], l[4 * i + j]);
+        }
+        bf16x8_t* ah = reinterpret_cast<bf16x8_t*>(&As[0][s_r][s_k]);
+        bf16x8_t* am = reinterpret_cast<bf16x8_t*>(&As[1][s_r][s_k]);
+        bf16x8_t* al = reinterpret_cast<bf16x8_t*>(&As[2][s_r][s_k]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            bf16x8_t vh, vm, vl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { vh[j] = h[8 * q + j]; vm[j] = m[8 * q + j]; vl[j] = l[8 * q + j]; }
+            ah[q] = vh;
+            am[q] = vm;
+            al[q] = vl;
+        }
+        if constexpr (WP == 1) {
+            bf16x8_t* bp = reinterpret_cast<bf16x8_t*>(&Bs[0][s_r][s_k]);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint4 u = b_ok ? rb[q] : make_uint4(0u, 0u, 0u, 0u);
+                bf16x8_t v;
+                __builtin_memcpy(&v, &u, 16);
+                bp[q] = v;
+            }
+        } else {
+            bf16x8_t* bh = reinterpret_cast<bf16x8_t*>(&Bs[0][s_r][s_k]);
+            bf16x8_t* bl = reinterpret_cast<bf16x8_t*>(&Bs[1][s_r][s_k]);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                float w8[8];
+                unpack8<WT>(rb[q], w8);
+                bf16x8_t vh, vl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float w = b_ok ? w8[j] : 0.f;
+                    const __bf16 wh = (__bf16)w;
+                    vh[j] = wh;
+                    vl[j] = (__bf16)(w - (float)wh);
+                }
+                bh[q] = vh;
+                bl[q] = vl;
+            }
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int half = lane >> 5, l32 = lane & 31;
+    const int ksteps = g.K / XB_K;
+    gload(0);
+    for (int kt = 0; kt < ksteps; ++kt) {
+        lstore();
+        __syncthreads();
+        if (kt + 1 < ksteps) gload((kt + 1) * XB_K);
+#pragma unroll
+        for (int ks = 0; ks < XB_K / 16; ++ks) {
+            const int kb = ks * 16 + 8 * half;
+            bf16x8_t af[2][3], bfr[2][WP];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    af[mi][p] = *reinterpret_cast<const bf16x8_t*>(&As[p][wm * 64 + mi * 32 + l32][kb]);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int q = 0; q < WP; ++q)
+                    bfr[ni][q] = *reinterpret_cast<const bf16x8_t*>(&Bs[q][wn * 64 + ni * 32 + l32][kb]);
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    // small terms first, the dominant hi x hi product last
+                    if constexpr (WP == 2) {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][1], bfr[ni][1], acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][0], bfr[ni][1], acc[mi][ni], 0, 0, 0);
+                    }
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][2], bfr[ni][0], acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][1], bfr[ni][0], acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][0], bfr[ni][0], acc[mi][ni], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+            const int col = n0 + wn * 64 + ni * 32 + l32;
+            if (col >= g.N) continue;
+            const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (row >= m_count) continue;
+                const long orow = g.c_rows ? (long)g.c_rows[m_begin + row] : (long)(m_begin + row);
+                if (orow < 0) continue;
+                float v = apply_act(acc[mi][ni][r] + bv, g.act);
+                float* cp = g.C + orow * (long)g.ldc + col;
+                if (g.accumulate) v += *cp;
+                *cp = v;
+            }
+        }
+    }
+}
+
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
     dim3 block(256);
     int mtiles = (g.group_off ? g.max_group_rows : g.M);
     dim3 grid((g.N + GB_N - 1) / GB_N, (mtiles + GB_M - 1) / GB_M, g.group_off ? g.groups : 1);
     if (grid.y == 0 || grid.x == 0) return;
+    // split-bf16 MFMA path when the tiles are whole along K and the rows 16-byte aligned;
+    // DSOCR_GEMM_F32=1 forces the f32-input MFMA kernel (A/B comparisons)
+    static const bool force_f32 = getenv("DSOCR_GEMM_F32") && atoi(getenv("DSOCR_GEMM_F32"));
+    const bool x3 = !force_f32 && g.K % XB_K == 0 && g.lda % 4 == 0 && g.ldw % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.W) & 15) == 0;
+    if (x3) {
+        dim3 gx((g.N + XB_N - 1) / XB_N, (mtiles + XB_M - 1) / XB_M, g.group_off ? g.groups : 1);
+        if (g.wdtype == WDT_BF16) hipLaunchKernelGGL(gemm_x3_kernel<bf16_t>, gx, block, 0, s, g);
+        else hipLaunchKernelGGL(gemm_x3_kernel<f16_t>, gx, block, 0, s, g);
+        return;
+    }
     if (g.wdtype == WDT_BF16)
         hipLaunchKernelGGL(gemm_f32_kernel<bf16_t>, grid, block, 0, s, g);
     else

@@ -125,6 +125,15 @@ struct DecGemvArgs {
     float eps = 0.f;
 };
 void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s);
+// Router GEMV whose last-arriving block writes the greedy top-k of every token (T <= 8).
+struct DecRouteEpi {
+    int topk = 0, softmax_scoring = 1, norm_topk = 0;
+    float scaling = 1.f;
+    int* ids = nullptr; float* w = nullptr;   // [T][topk]
+    int* counter = nullptr;                   // zero between launches
+};
+void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s);
+bool dec_router_ok(int T, int E, int K, int topk);
 // RoPE on q / new k + KV-cache append + flash-decoding over 64-key chunks + combine.
 struct DecAttn2Args {
     const float* qkv = nullptr; long ld = 0;           // [B][(heads + 2 kv_heads) * hd]
@@ -163,8 +172,9 @@ struct MoeDec2Args {
     int wdtype = WDT_F16;
     float* h = nullptr; float* hs = nullptr;
     float* out = nullptr;           // [T][Hout], += combined
-    // slot mode (T <= 8): gate/up blocks route themselves from the router logits; h row of
-    // (token t, pick k) = t*topk + k; ids_out / w_out receive the picks (apos must be null)
+    // slot mode (T <= 8): h row of (token t, pick k) = t*topk + k (apos must be null).  With
+    // `logits` set the gate/up blocks route themselves (ids_out / w_out receive the picks);
+    // with logits == null the picks come from dec_router in ids / aw.
     int slot_mode = 0;
     const float* logits = nullptr;
     int softmax_scoring = 1, norm_topk = 0;

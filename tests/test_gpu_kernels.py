@@ -194,10 +194,14 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len):
             assert np.max(np.abs(got[b, h * hd:(h + 1) * hd] - ref)) < 2e-5, (b, h)
 
 
-@pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(3, 256, 16, 6, 64, 2, False), (1, 256, 16, 6, 64, 2, True),
-                                                  (2, 1280, 64, 6, 896, 2, True), (9, 128, 8, 3, 32, 1, False)])
-def test_moe_decode_layer(gpu, T, H, E, topk, I, ns, norm):
-    """Decode MoE (north-star kernel chain) vs the oracle's run_moe (block.rs:1215-1395)."""
+@pytest.mark.parametrize("T,H,E,topk,I,ns,norm,epi", [(3, 256, 16, 6, 64, 2, False, 0), (1, 256, 16, 6, 64, 2, True, 0),
+                                                      (2, 1280, 64, 6, 896, 2, True, 0), (9, 128, 8, 3, 32, 1, False, 0),
+                                                      (1, 1280, 64, 6, 896, 2, True, 1), (4, 256, 16, 6, 64, 2, False, 1)])
+def test_moe_decode_layer(gpu, monkeypatch, T, H, E, topk, I, ns, norm, epi):
+    """Decode MoE (north-star kernel chain) vs the oracle's run_moe (block.rs:1215-1395).
+    T <= 8: slot mode (gate/up blocks route themselves; epi=1: the router kernel's epilogue routes);
+    T > 8: one block groups the assignments by expert."""
+    monkeypatch.setenv("DSOCR_ROUTER_EPI", str(epi))
     from oracle.decoder import Decoder
     rng = np.random.default_rng(5 + T)
     Is = I * ns
