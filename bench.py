@@ -33,6 +33,53 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def blas_threads():
+    """Threads the oracle's BLAS actually runs with (numpy's OpenBLAS pool)."""
+    try:
+        from threadpoolctl import threadpool_info
+        n = [p["num_threads"] for p in threadpool_info() if p.get("user_api") == "blas"]
+        if n:
+            return int(max(n))
+    except Exception:
+        pass
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def page_indices(step, world, rank, ppg):
+    """Pages of one bench step on one rank: rank r of W takes pages [(step*W + r)*ppg, +ppg) —
+    disjoint across ranks and steps (data parallel, no collective on the data path)."""
+    base = (step * world + rank) * ppg
+    return list(range(base, base + ppg))
+
+
+def reduce_over_ranks(dist, elapsed, tok_s):
+    """Job time = max over ranks (the slowest rank ends the step); decode tok/s = sum."""
+    if dist is None:
+        return elapsed, tok_s
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    r = torch.tensor([tok_s], dtype=torch.float64)
+    dist.all_reduce(r, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(r.item())
+
+
+def pmc_traffic(kernel_prefix):
+    """Per-launch HBM bytes of a kernel from the committed rocprofv3 PMC summary
+    (latest profiles/rNN_pmc_traffic.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 (gfx950
+    reports half of wide streaming reads) + WRITE_SIZE, each from its own --pmc pass)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    try:
+        d = json.load(open(paths[-1]))
+    except Exception:
+        return None
+    for name, v in d.get("kernels", {}).items():
+        if name.startswith(kernel_prefix):
+            return v.get("hbm_bytes_per_launch")
+    return None
+
+
 def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
     """The repo's CPU oracle (numpy restatement of the reference path) on rank 0's host
     cores: bounded sample = 1 page vision + prefill + `decode_steps` decode forwards,
@@ -65,7 +112,7 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
     t3 = time.time()
     per_step = (t3 - t2) / decode_steps
     page_s = (t1 - t0) + (t2 - t1) + per_step * (max_new - 1)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = blas_threads()
     return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads, "kind": "port",
             "decode_tok_s": 1.0 / per_step,
             "sample": f"1 synthetic 1024x1024 page: vision {t1 - t0:.2f}s + prefill {t2 - t1:.2f}s "
@@ -114,8 +161,7 @@ def main():
 
     def make_batch(step):
         imgs, reqs = [], []
-        for i in range(ppg):
-            idx = (step * world + rank) * ppg + i
+        for idx in page_indices(step, world, rank, ppg):
             img = synthetic_page(idx)
             page = Page(img, vs)
             ids, mask = build_prompt_tokens(tok, BENCH_PROMPT, [page.n_image_tokens])
@@ -144,16 +190,7 @@ def main():
              for k in ("vision_compute_ms", "decode_prefill_ms", "decode_iterative_ms")}
     tokens_rank = args.steps * ppg * args.max_new_tokens
     tok_s_rank = tokens_rank / iterative_s if iterative_s > 0 else 0.0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        ts = torch.tensor([tok_s_rank], dtype=torch.float64)
-        dist.all_reduce(ts, op=dist.ReduceOp.SUM)
-        tok_s = float(ts.item())
-    else:
-        tok_s = tok_s_rank
+    elapsed, tok_s = reduce_over_ranks(dist, elapsed, tok_s_rank)
     pages_total = args.steps * ppg * world
     value = pages_total / elapsed
 
@@ -163,8 +200,9 @@ def main():
         gu = prof["moe_gateup"]
         achieved = gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "moe_gateup2_kernel (decode MoE gate/up: routed top-6 + shared experts, one layer)",
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_traffic("moe_gateup_slot_kernel"),
+                    "kernel": "moe_gateup_slot_kernel (decode MoE gate/up: self-routed top-6 + shared experts, one layer)",
                     "avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
                     "experts_touched": prof["experts_touched"],
                     "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
