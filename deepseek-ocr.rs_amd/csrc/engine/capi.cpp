@@ -142,6 +142,13 @@ dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t w, uint32_t h, cons
 
 void dsocr_page_free(dsocr_page_pixels* p) { delete p; }
 
+dsocr_status dsocr_page_to_device(dsocr_engine* e, dsocr_page_pixels* p) {
+    return guarded([&] {
+        if (!e || !p) throw std::runtime_error("EINVAL: NULL argument");
+        e->impl->upload_page(p->px);
+    });
+}
+
 dsocr_status dsocr_page_info(const dsocr_page_pixels* p, uint32_t* cw, uint32_t* ch, uint32_t* nt, size_t* ntok) {
     return guarded([&] {
         if (!p) throw std::runtime_error("EINVAL: NULL page");
@@ -338,7 +345,7 @@ dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale,
         }
         dsocr::launch_attention(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
-        if (rb) hipFree(rb);
+        if (rb) (void)hipFree(rb);
         check_hip(e, "attention");
     });
 }
@@ -362,8 +369,8 @@ dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, in
         a.o_ld = (long)heads * hd; a.counters = cnt;
         dsocr::launch_dec_attn(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
-        hipFree(part);
-        hipFree(cnt);
+        (void)hipFree(part);
+        (void)hipFree(cnt);
         check_hip(e, "decode attention");
     });
 }
@@ -453,7 +460,7 @@ dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, 
         a.out_tok = out_tok; a.done = done;
         dsocr::launch_dec_sample(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
-        hipFree(ridx); hipFree(rval); hipFree(done);
+        (void)hipFree(ridx); (void)hipFree(rval); (void)hipFree(done);
         check_hip(e, "sample");
     });
 }

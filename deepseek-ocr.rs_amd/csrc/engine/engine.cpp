@@ -178,8 +178,44 @@ Engine::Engine(const std::string& config_path, const std::string& weights_path, 
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
+PagePixels::~PagePixels() {
+    if (global_dev) (void)hipFree(global_dev);
+    if (tiles_dev) (void)hipFree(tiles_dev);
+}
+
+void* Engine::pinned(const std::string& name, size_t bytes) {
+    auto it = pinned_.find(name);
+    if (it != pinned_.end() && it->second.second >= bytes) return it->second.first;
+    if (it != pinned_.end()) {
+        HIP_CHECK(hipStreamSynchronize(stream_));  // an in-flight copy may still read the old buffer
+        (void)hipHostFree(it->second.first);
+    }
+    void* h = nullptr;
+    const size_t cap = bytes + bytes / 8 + 256;
+    if (hipHostMalloc(&h, cap) != hipSuccess) throw std::runtime_error("ENOMEM: pinned staging " + name);
+    pinned_[name] = {h, cap};
+    return h;
+}
+
+// Stage a page's preprocessed pixels in HBM once (outside any timed region): generate() then
+// gathers them device-to-device.
+void Engine::upload_page(PagePixels& pg) {
+    if (pg.global_dev && pg.dev_ordinal == device_) return;
+    if (pg.global_dev) { (void)hipFree(pg.global_dev); pg.global_dev = nullptr; }
+    if (pg.tiles_dev) { (void)hipFree(pg.tiles_dev); pg.tiles_dev = nullptr; }
+    HIP_CHECK(hipMalloc(&pg.global_dev, pg.global_chw.size() * 4));
+    HIP_CHECK(hipMemcpy(pg.global_dev, pg.global_chw.data(), pg.global_chw.size() * 4, hipMemcpyHostToDevice));
+    if (!pg.tiles_chw.empty()) {
+        HIP_CHECK(hipMalloc(&pg.tiles_dev, pg.tiles_chw.size() * 4));
+        HIP_CHECK(hipMemcpy(pg.tiles_dev, pg.tiles_chw.data(), pg.tiles_chw.size() * 4, hipMemcpyHostToDevice));
+    }
+    pg.dev_ordinal = device_;
+}
+
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& kv : pinned_) (void)hipHostFree(kv.second.first);
+    for (auto& kv : winmaps_) { (void)hipFree(kv.second.first); (void)hipFree(kv.second.second); }
     for (auto& kv : ws_) (void)hipFree(kv.second.first);
     for (void* p : allocations_) (void)hipFree(p);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -517,17 +553,26 @@ float* Engine::vision_pass(const float* imgs, int n, int Spx, const std::string&
     const int W = S.window;
     const int gp = g + (W - g % W) % W, nw = gp / W;
     const long wrows = (long)n * nw * nw * W * W;
-    std::vector<int> tok2win(rows), win2tok(wrows, -1);
-    for (int b = 0; b < n; ++b)
-        for (int y = 0; y < g; ++y)
-            for (int xx = 0; xx < g; ++xx) {
-                long t = ((long)b * g + y) * g + xx;
-                long w = (((long)b * nw + y / W) * nw + xx / W) * W * W + (y % W) * W + (xx % W);
-                tok2win[t] = (int)w;
-                win2tok[w] = (int)t;
-            }
-    int* d_tok2win = upload("v_tok2win", tok2win);
-    int* d_win2tok = upload("v_win2tok", win2tok);
+    auto wm = winmaps_.find({n, g});
+    if (wm == winmaps_.end()) {  // built once per (images, grid): tok -> window slot and back
+        std::vector<int> tok2win(rows), win2tok(wrows, -1);
+        for (int b = 0; b < n; ++b)
+            for (int y = 0; y < g; ++y)
+                for (int xx = 0; xx < g; ++xx) {
+                    long t = ((long)b * g + y) * g + xx;
+                    long w = (((long)b * nw + y / W) * nw + xx / W) * W * W + (y % W) * W + (xx % W);
+                    tok2win[t] = (int)w;
+                    win2tok[w] = (int)t;
+                }
+        int *a = nullptr, *b2 = nullptr;
+        HIP_CHECK(hipMalloc(&a, tok2win.size() * 4));
+        HIP_CHECK(hipMalloc(&b2, win2tok.size() * 4));
+        HIP_CHECK(hipMemcpy(a, tok2win.data(), tok2win.size() * 4, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(b2, win2tok.data(), win2tok.size() * 4, hipMemcpyHostToDevice));
+        wm = winmaps_.emplace(std::make_pair(n, g), std::make_pair(a, b2)).first;
+    }
+    int* d_tok2win = wm->second.first;
+    int* d_win2tok = wm->second.second;
     const long maxrows = std::max(rows, wrows);
     float* xn = wsf("v_xn", (size_t)maxrows * C);
     float* qkv = wsf("v_qkv", (size_t)maxrows * 3 * C);
@@ -943,11 +988,35 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     std::vector<const float*> gpost(B, nullptr), lpost(B, nullptr);
     std::vector<float*> pass_outputs;
     int pass_id = 0;
+    // pixels of one size group as one contiguous device batch: device-to-device gathers of
+    // HBM-resident pages (dsocr_page_to_device), else one staged host upload
+    auto gather = [&](const std::vector<int>& pages, bool tiles, size_t n_floats) -> float* {
+        const std::string name = "g_img" + std::to_string(pass_id);
+        bool resident = true;
+        for (int b : pages) resident &= (tiles ? reqs[b].page->tiles_dev : reqs[b].page->global_dev) != nullptr &&
+                                         reqs[b].page->dev_ordinal == device_;
+        if (!resident) {
+            std::vector<float> imgs;
+            imgs.reserve(n_floats);
+            for (int b : pages) {
+                const auto& v = tiles ? reqs[b].page->tiles_chw : reqs[b].page->global_chw;
+                imgs.insert(imgs.end(), v.begin(), v.end());
+            }
+            return upload(name, imgs);
+        }
+        float* d = wsf(name, n_floats);
+        size_t off = 0;
+        for (int b : pages) {
+            const size_t nf = tiles ? reqs[b].page->tiles_chw.size() : reqs[b].page->global_chw.size();
+            HIP_CHECK(hipMemcpyAsync(d + off, tiles ? reqs[b].page->tiles_dev : reqs[b].page->global_dev, nf * 4,
+                                     hipMemcpyDeviceToDevice, st));
+            off += nf;
+        }
+        return d;
+    };
     for (auto& kv : gsz) {
         const int S = kv.first;
-        std::vector<float> imgs;
-        for (int b : kv.second) imgs.insert(imgs.end(), reqs[b].page->global_chw.begin(), reqs[b].page->global_chw.end());
-        float* dimg = upload("g_img" + std::to_string(pass_id), imgs);
+        float* dimg = gather(kv.second, false, kv.second.size() * 3 * (size_t)S * S);
         std::string name = "vis_out" + std::to_string(pass_id++);
         float* post = vision_pass(dimg, (int)kv.second.size(), S, name);
         const int Sq = (S / 64) * (S / 64);
@@ -955,13 +1024,9 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     for (auto& kv : tsz) {
         const int S = kv.first;
-        std::vector<float> imgs;
         int n = 0;
-        for (int b : kv.second) {
-            imgs.insert(imgs.end(), reqs[b].page->tiles_chw.begin(), reqs[b].page->tiles_chw.end());
-            n += reqs[b].page->n_tiles;
-        }
-        float* dimg = upload("g_img" + std::to_string(pass_id), imgs);
+        for (int b : kv.second) n += reqs[b].page->n_tiles;
+        float* dimg = gather(kv.second, true, (size_t)n * 3 * S * S);
         std::string name = "vis_out" + std::to_string(pass_id++);
         float* post = vision_pass(dimg, n, S, name);
         const int Sq = (S / 64) * (S / 64);

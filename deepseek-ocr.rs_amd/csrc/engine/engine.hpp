@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -87,6 +88,12 @@ struct PagePixels {
     std::vector<float> tiles_chw;   // [n][3][T][T]
     int n_tiles = 0;
     size_t n_image_tokens = 0;
+    // optional device-resident copies (dsocr_page_to_device): generate() then reads the pixels
+    // from HBM (device-to-device gather) instead of uploading the host arrays
+    float* global_dev = nullptr;
+    float* tiles_dev = nullptr;
+    int dev_ordinal = -1;
+    ~PagePixels();
 };
 
 struct Timings {
@@ -134,6 +141,7 @@ class Engine {
     };
     DecodeProfile profile_decode(int iters);
     hipStream_t stream() const { return stream_; }
+    void upload_page(PagePixels& pg);
 
   private:
     // ---- loading
@@ -145,14 +153,19 @@ class Engine {
     long* wsl(const std::string& name, size_t n) { return (long*)ws(name, n * sizeof(long)); }
     template <typename T>
     T* upload(const std::string& name, const std::vector<T>& v) {
-        // synchronous: host vectors are often temporaries (pageable memory)
-        T* p = (T*)ws(name, v.size() * sizeof(T) + 16);
+        // host vectors are often temporaries: stage them in a per-name pinned buffer and copy
+        // asynchronously (each name is uploaded at most once per generate(), which ends with a
+        // stream synchronisation, so a staging buffer is never rewritten while in flight)
+        const size_t bytes = v.size() * sizeof(T);
+        T* p = (T*)ws(name, bytes + 16);
         if (!v.empty()) {
-            HIP_CHECK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream_));
-            HIP_CHECK(hipStreamSynchronize(stream_));
+            void* h = pinned(name, bytes);
+            std::memcpy(h, v.data(), bytes);
+            HIP_CHECK(hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, stream_));
         }
         return p;
     }
+    void* pinned(const std::string& name, size_t bytes);
     // ---- compute pieces
     void linear(const float* x, int M, int ldx, const Lin& l, float* y, int ldy, int act = 0, int accumulate = 0,
                 const int* c_rows = nullptr);
@@ -199,6 +212,8 @@ class Engine {
     long page_stride_ = 0, head_stride_ = 0;
     Timings timings_;
     int last_B_ = 0;
+    std::map<std::string, std::pair<void*, size_t>> pinned_;
+    std::map<std::pair<int, int>, std::pair<int*, int*>> winmaps_;  // (n, grid) -> tok2win, win2tok
     int last_Lmax_ = 0;
 
     void* dev_alloc(size_t bytes);

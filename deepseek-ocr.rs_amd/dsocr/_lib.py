@@ -68,7 +68,7 @@ STREAM_CB = C.CFUNCTYPE(None, C.c_size_t, C.POINTER(C.c_int64), C.c_void_p)
 # every symbol include/dsocr.h declares (tests check the library exports all of them)
 EXPORTS = [
     "dsocr_engine_load", "dsocr_engine_free", "dsocr_last_error", "dsocr_engine_info", "dsocr_prepare_page",
-    "dsocr_page_free", "dsocr_page_info", "dsocr_page_pixels_view", "dsocr_image_embeddings", "dsocr_generate",
+    "dsocr_page_free", "dsocr_page_to_device", "dsocr_page_info", "dsocr_page_pixels_view", "dsocr_image_embeddings", "dsocr_generate",
     "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
@@ -94,6 +94,7 @@ def lib():
     L.dsocr_prepare_page.argtypes = [vp, u32, u32, C.POINTER(VisionSettingsC), C.POINTER(vp)]
     L.dsocr_page_free.argtypes = [vp]
     L.dsocr_page_free.restype = None
+    L.dsocr_page_to_device.argtypes = [vp, vp]
     L.dsocr_page_info.argtypes = [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(sz)]
     L.dsocr_page_pixels_view.argtypes = [vp, C.POINTER(vp), C.POINTER(u32), C.POINTER(vp), C.POINTER(u32)]
     L.dsocr_image_embeddings.argtypes = [vp, C.POINTER(vp), sz, vp, sz, C.POINTER(sz)]

@@ -118,6 +118,11 @@ class Page:
         self.n_tiles = nt.value
         self.n_image_tokens = ntok.value
 
+    def to_device(self, engine) -> "Page":
+        """Stage the pixels in the engine's HBM (dsocr_page_to_device); returns self."""
+        check(lib().dsocr_page_to_device(engine._h, self._h))
+        return self
+
     def pixels(self):
         g, gs, t, ts = C.c_void_p(), C.c_uint32(), C.c_void_p(), C.c_uint32()
         check(lib().dsocr_page_pixels_view(self._h, C.byref(g), C.byref(gs), C.byref(t), C.byref(ts)))

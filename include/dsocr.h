@@ -119,6 +119,11 @@ dsocr_status dsocr_engine_info(const dsocr_engine* e, size_t* hidden, size_t* vo
 dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t width, uint32_t height,
                                 const dsocr_vision_settings* vs, dsocr_page_pixels** out);
 void dsocr_page_free(dsocr_page_pixels* p);
+/* Stage the page's preprocessed pixels in the engine's device memory (HBM) once, e.g. ahead of
+ * a timed or latency-critical generate; later calls gather them device-to-device.  The device
+ * copy is owned by the page (freed by dsocr_page_free).  Reference counterpart: none (the
+ * reference re-uploads every tensor per call, model/mod.rs:2332-2347). */
+dsocr_status dsocr_page_to_device(dsocr_engine* e, dsocr_page_pixels* p);
 /* crop grid (w,h), tile count, and the number of <image> slots build_image_placeholders emits */
 dsocr_status dsocr_page_info(const dsocr_page_pixels* p, uint32_t* crop_w, uint32_t* crop_h, uint32_t* n_tiles,
                              size_t* n_image_tokens);

@@ -205,3 +205,17 @@ def test_full_page_vision_parity(full_engine):
     assert got.shape == ref.shape == (693, 1280)
     err = np.max(np.abs(got - ref))
     assert err < 1e-3 * max(1.0, np.max(np.abs(ref))), err
+
+
+def test_tiny_device_resident_page_equals_host(tiny_engine):
+    """dsocr_page_to_device: HBM-resident pixels (device-to-device gather) give the same ids."""
+    tok = SyntheticTokenizer(512)
+    p = DecodeParameters(max_new_tokens=16)
+    reqs_h, reqs_d = [], []
+    for i, hw in enumerate([(300, 420), (220, 180)]):
+        img = _img(300 + i, *hw)
+        ph, pd = Page(img, TINY_VS), Page(img, TINY_VS).to_device(tiny_engine)
+        ids, mask = _prompt(tok, ph)
+        reqs_h.append((ids, mask, ph, None))
+        reqs_d.append((ids, mask, pd, None))
+    assert tiny_engine.generate_batch(reqs_d, p) == tiny_engine.generate_batch(reqs_h, p)
