@@ -248,6 +248,10 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
         out->experts_touched = p.experts_touched;
         out->tokens = p.tokens;
         out->kv_len = p.kv_len;
+        out->qkv = cp(p.qkv);
+        out->o_proj = cp(p.o_proj);
+        out->router = cp(p.router);
+        out->layers_step = cp(p.layers_step);
     });
 }
 

@@ -858,6 +858,13 @@ void Engine::decode_step(int B, int Lmax) {
     float* CTX = wsf("s_ctx", (size_t)B * H);
     float* part = wsf("s_part", dec_attn_workspace(B, L.heads, hd, Lmax) / 4 + 16);
     if (L.heads % L.kv_heads) throw std::runtime_error("EINVAL: num_attention_heads must be a multiple of num_key_value_heads");
+    // in-launch hand-off counters of the fused kernels: one block of SYNC_INTS per layer, zeroed
+    // by one memset node at the head of every step (a multiple of 16 bytes from the allocation start)
+    // (experiment, off by default: measured slower on MI355X at B = 1)
+    static const bool fused_moe = getenv("DSOCR_FUSED_MOE") && atoi(getenv("DSOCR_FUSED_MOE")) != 0;
+    int* sync = wsi("s_sync", (size_t)L.layers * SYNC_INTS);
+    int* err = wsi("s_err", 4);
+    if (fused_moe) HIP_CHECK(hipMemsetAsync(sync, 0, sizeof(int) * L.layers * SYNC_INTS, st));
     for (int l = 0; l < L.layers; ++l) {
         DecLayer& d = layers_[l];
         const int QKVN = d.qkv.N;
@@ -922,6 +929,12 @@ void Engine::decode_step(int B, int Lmax) {
             ra.arow = const_cast<int*>(m.arow); ra.apos = const_cast<int*>(m.apos); ra.aw = const_cast<float*>(m.aw);
             ra.active = const_cast<int*>(m.active); ra.n_active = const_cast<int*>(m.n_active);
             launch_moe_route(ra, st);
+        }
+        m.sync = sync + (size_t)l * SYNC_INTS;
+        m.err = err;
+        if (fused_moe && moe_fused_ok(m)) {
+            launch_moe_fused(m, st);
+            continue;
         }
         launch_moe_gateup2(m, st);
         launch_moe_down2(m, st);
@@ -1132,6 +1145,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // arrival tickets of the decode-attention combine: zero here, every launch leaves them zero
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
+    HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
     const int QKVN = layers_[0].qkv.N;
     r0 = 0;
     for (int b = 0; b < B; ++b) {
@@ -1277,6 +1291,11 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipEventRecord(ev[5], st));
     HIP_CHECK(hipStreamSynchronize(st));
     HIP_CHECK(hipHostFree(pin_done));
+    {
+        int e = 0;
+        HIP_CHECK(hipMemcpy(&e, wsi("s_err", 4), sizeof(int), hipMemcpyDeviceToHost));
+        if (e) throw std::runtime_error("EINTERNAL: decode hand-off timed out inside a fused kernel");
+    }
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
 
@@ -1314,19 +1333,32 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     HIP_CHECK(hipMemcpy(d_pos, pm1.data(), B * 4, hipMemcpyHostToDevice));
     prof.tokens = B;
     prof.kv_len = pm1[0] + 1;
-    // n back-to-back launches between two events on the engine stream: per-launch time =
-    // span / n (a single event-bracketed launch carries ~10 us of event overhead on MI355X)
+    // n back-to-back launches captured in one hipGraph, replayed between two events on the
+    // engine stream: per-launch time = span / n = device time + the dependent-kernel boundary
+    // (eager launches go host-bound below ~3.5 us per kernel, MI355X_MICROARCH.md
+    // graph-replay-floor, so they cannot time the short decode kernels)
     auto timed = [&](KernelProfile& kp, int n, const std::function<void(int)>& body) {
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
-        body(0);  // warm (code objects, TLB)
-        HIP_CHECK(hipEventRecord(e0, st));
+        body(0);  // warm (code objects, TLB) and every workspace allocated before capture
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t gexec = nullptr;
+        capturing_ = true;
+        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
         for (int i = 0; i < n; ++i) body(i);
+        HIP_CHECK(hipStreamEndCapture(st, &graph));
+        capturing_ = false;
+        HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphLaunch(gexec, st));  // warm replay
+        HIP_CHECK(hipEventRecord(e0, st));
+        HIP_CHECK(hipGraphLaunch(gexec, st));
         HIP_CHECK(hipEventRecord(e1, st));
         HIP_CHECK(hipEventSynchronize(e1));
         kp.avg_us = 1000.0 * ms_between(e0, e1) / n;
         kp.launches = n;
+        (void)hipGraphExecDestroy(gexec);
+        (void)hipGraphDestroy(graph);
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     };
@@ -1349,6 +1381,22 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         // rotating over the layers (~55 MB each) defeats the 256 MB Infinity Cache
         timed(prof.moe_gateup, n, [&](int i) { launch_moe_gateup2(args(moe_layers[i % moe_layers.size()]), st); });
         timed(prof.moe_down, n, [&](int i) { launch_moe_down2(args(moe_layers[i % moe_layers.size()]), st); });
+        if (const char* path = getenv("DSOCR_STAMPS_OUT")) {
+            // dev: per-block phase clocks of one gate/up launch (moe_gateup_slot_kernel)
+            const size_t nstamp = 4096 * 8;
+            auto* d_st = (unsigned long long*)ws("p_stamps", nstamp * 8);
+            HIP_CHECK(hipMemsetAsync(d_st, 0, nstamp * 8, st));
+            MoeDec2Args m = args(moe_layers[0]);
+            m.stamps = d_st;
+            launch_moe_gateup2(m, st);
+            std::vector<unsigned long long> h(nstamp);
+            HIP_CHECK(hipMemcpyAsync(h.data(), d_st, nstamp * 8, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            if (FILE* f = fopen(path, "wb")) {
+                fwrite(h.data(), 8, nstamp, f);
+                fclose(f);
+            }
+        }
         const DecLayer& d0 = layers_[moe_layers[0]];
         const double Is = d0.has_shared ? d0.s_d.K : 0;
         const double touched = (double)prof.experts_touched;
@@ -1394,6 +1442,97 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         });
         prof.lm_head.bytes = (double)L.vocab * H * 2.0 + (double)B * (L.vocab + H) * 4.0;
         prof.lm_head.flops = 2.0 * B * (double)L.vocab * H;
+    }
+    {
+        // attention-side GEMVs of every layer, replayed on scratch outputs
+        const int QKVN = layers_[0].qkv.N;
+        const float* SX = wsf("s_x", (size_t)B * H);
+        float* Y = wsf("p_qkv", (size_t)B * QKVN);
+        float* XO = wsf("p_xo", (size_t)B * H);
+        float* LG = wsf("p_rlog", (size_t)B * std::max(1, L.n_routed));
+        const int n = iters * L.layers;
+        const bool fuse_norm = B <= 2;
+        timed(prof.qkv, n, [&](int i) {
+            const DecLayer& d = layers_[i % L.layers];
+            DecGemvArgs g;
+            g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
+            g.y = Y; g.ldy = QKVN; g.x = SX; g.ldx = H;
+            if (fuse_norm) { g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
+            launch_dec_gemv(g, st);
+        });
+        prof.qkv.bytes = (double)QKVN * H * 2.0 + (double)B * (H + QKVN) * 4.0;
+        prof.qkv.flops = 2.0 * B * (double)QKVN * H;
+        timed(prof.o_proj, n, [&](int i) {
+            const DecLayer& d = layers_[i % L.layers];
+            DecGemvArgs go;
+            go.M = B; go.N = H; go.K = L.heads * hd; go.x = SX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
+            go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = XO; go.ldy = H; go.accumulate = 0;
+            launch_dec_gemv(go, st);
+        });
+        prof.o_proj.bytes = (double)H * L.heads * hd * 2.0 + (double)B * 2 * H * 4.0;
+        prof.o_proj.flops = 2.0 * B * (double)H * L.heads * hd;
+        std::vector<int> moe_l;
+        for (int l = 0; l < L.layers; ++l)
+            if (layers_[l].moe) moe_l.push_back(l);
+        if (!moe_l.empty()) {
+            timed(prof.router, iters * (int)moe_l.size(), [&](int i) {
+                const int l = moe_l[i % moe_l.size()];
+                const DecLayer& d = layers_[l];
+                DecGemvArgs gr;
+                gr.M = B; gr.N = L.n_routed; gr.K = H; gr.x = SX; gr.ldx = H; gr.W = d.router.W; gr.ldw = H;
+                gr.wdtype = d.router.wdt; gr.bias = d.router.b; gr.y = LG; gr.ldy = L.n_routed;
+                if (fuse_norm) { gr.norm_w = d.post_norm.w; gr.eps = L.rms_eps; }
+                const MoeDec2Args m = moe_decode_args(l, B, SX, fuse_norm ? d.post_norm.w : nullptr, XO);
+                if (m.slot_mode && !m.logits) {  // the router kernel also routes (as in decode_step)
+                    DecRouteEpi re;
+                    re.topk = L.topk; re.softmax_scoring = L.scoring == "softmax"; re.norm_topk = L.norm_topk;
+                    re.scaling = L.routed_scaling; re.ids = wsi("p_ids", (size_t)B * L.topk);
+                    re.w = wsf("p_w", (size_t)B * L.topk); re.counter = wsi("s_route_cnt", 16);
+                    launch_dec_router(gr, re, st);
+                } else {
+                    launch_dec_gemv(gr, st);
+                }
+            });
+            prof.router.bytes = (double)L.n_routed * H * 2.0 + (double)B * (H + L.n_routed) * 4.0;
+            prof.router.flops = 2.0 * B * (double)L.n_routed * H;
+        }
+    }
+    {
+        // every decoder layer of one step as one hipGraph (what the decode loop replays, minus
+        // lm_head and selection); the residual stream is restored at the head of each replay and
+        // the KV slot written is the next free position (past every generated token)
+        float* X = wsf("s_x", (size_t)B * H);
+        float* X0 = wsf("p_x0", (size_t)B * H);
+        HIP_CHECK(hipMemcpyAsync(X0, X, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
+        decode_step(B, Lmax);  // every workspace exists before capture
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t gexec = nullptr;
+        capturing_ = true;
+        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
+        decode_step(B, Lmax);
+        HIP_CHECK(hipStreamEndCapture(st, &graph));
+        capturing_ = false;
+        HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+        {
+            const int n = std::max(8, iters * 4);
+            hipEvent_t e0, e1;
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            HIP_CHECK(hipGraphLaunch(gexec, st));
+            HIP_CHECK(hipEventRecord(e0, st));
+            for (int i = 0; i < n; ++i) HIP_CHECK(hipGraphLaunch(gexec, st));
+            HIP_CHECK(hipEventRecord(e1, st));
+            HIP_CHECK(hipEventSynchronize(e1));
+            prof.layers_step.avg_us = 1000.0 * ms_between(e0, e1) / n;
+            prof.layers_step.launches = n;
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+        }
+        HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        (void)hipGraphExecDestroy(gexec);
+        (void)hipGraphDestroy(graph);
     }
     return prof;
 }

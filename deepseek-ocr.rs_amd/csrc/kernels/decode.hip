@@ -149,6 +149,25 @@ __device__ __forceinline__ void xstage(const XRegs<MT, XR>& r, int M, int K, boo
     __syncthreads();
 }
 
+// In-launch hand-off counters: SYNC_SHARDS arrival counters per hand-off, one per 128-byte line
+// (arrivals spread over shards so no single word serialises every producer's atomic).
+// One lane polls every shard with relaxed agent-scope (sc1) loads, s_sleep between polls; a
+// bounded spin that gives up sets *err (checked by the host after the step) instead of hanging.
+__device__ __noinline__ void wait_arrivals(const int* sync, int target, int* err) {
+    for (unsigned it = 0;; ++it) {
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < SYNC_SHARDS; ++i)
+            n += __hip_atomic_load(sync + i * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n >= target) return;
+        if (it > (1u << 21) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // 8 consecutive f32 (LDS or global) into registers
 __device__ __forceinline__ void ld_x8(const float* xs, float* o) {
     const float4 a = *reinterpret_cast<const float4*>(xs);
@@ -334,7 +353,14 @@ template <typename WT, int MT>
 static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     const size_t lds = stage_bytes(a.M, a.K);
     // small N: one row per wave so the whole matrix is in flight at once; large N: RB rows per wave
-    if (a.N <= 16384) {
+    // (DSOCR_GEMV_STREAM=G: small N on the streaming kernel with at most G blocks, experiment)
+    static const int stream_blocks = getenv("DSOCR_GEMV_STREAM") ? atoi(getenv("DSOCR_GEMV_STREAM")) : 0;
+    if (stream_blocks > 0 && a.N <= 16384 && a.K <= 64 * 3 * 8 && MT <= 2) {
+        constexpr int RB = 2;
+        const int groups = (a.N + RB - 1) / RB;
+        const int blocks = std::max(1, std::min((groups + 3) / 4, stream_blocks));
+        hipLaunchKernelGGL((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
+    } else if (a.N <= 16384) {
         constexpr int RB = 1;
         hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
     } else if (a.K <= 64 * 3 * 8 && MT <= 2) {
@@ -385,14 +411,15 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
 // Logits are stored write-through (sc1 atomics) so the hand-off needs only the arrival
 // ticket and one agent acquire in the last block (cdna_hip_programming.md Guideline 16 R1).
 __device__ __forceinline__ void topk_write(const float* lg, int E, int K, int softmax_scoring, int norm_topk,
-                                           float scaling, int* ids, float* w) {
+                                           float scaling, int* ids, float* w, bool sc1 = false) {
     const int lane = threadIdx.x & 63;
     float sc[4];
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int e = min(lane + 64 * j, E - 1);
-        sc[j] = lg[e];
+        // sc1: logits handed over inside the launch (stored sc1 by other blocks)
+        sc[j] = sc1 ? __hip_atomic_load(lg + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : lg[e];
         if (lane + 64 * j >= E) sc[j] = -INFINITY;
         mx = fmaxf(mx, sc[j]);
     }
@@ -497,18 +524,17 @@ __global__ __launch_bounds__(256) void dec_router_kernel(DecGemvArgs a, DecRoute
     if (threadIdx.x == 0) {
         const int old = __hip_atomic_fetch_add(r.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == (int)gridDim.x - 1;
-        if (last) {
-            __hip_atomic_store(r.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (last) __hip_atomic_store(r.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_s = last;
     }
     __syncthreads();
     if (!last_s) return;
+    // every logit was stored sc1 and is read back with sc1 loads: no acquire fence needed
+    // (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int t = wave; t < a.M; t += 4)
         topk_write(a.y + (long)t * a.ldy, a.N, r.topk, r.softmax_scoring, r.norm_topk, r.scaling, r.ids + t * r.topk,
-                   r.w + t * r.topk);
+                   r.w + t * r.topk, true);
 }
 
 bool dec_router_ok(int T, int E, int K, int topk) { return T <= 8 && E <= 256 && K <= 64 * 3 * 8 && topk <= 8; }
@@ -536,31 +562,64 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 // Each block issues its K and V cache loads first, then builds q; the block that
 // arrives last for a (page, head) merges the chunk partials (flash-decoding combine)
 // with one agent-scope release / acquire (cdna_hip_programming.md §5 split-K recipe).
-constexpr int DA2_CH = 64;
+// CH keys per block (64 or 32: env DSOCR_ATT_CH); LPK = 256 / CH lanes score one key.
+constexpr int DA2_CH_MIN = 32;
 
-template <int HD>
+// sum over aligned groups of N lanes (N = 4 or 8), result in every lane of the group
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {
+    v += dpp_f<DPP_QUAD_XOR1>(0.f, v);
+    v += dpp_f<DPP_QUAD_XOR2>(0.f, v);
+    if (N == 8) v += dpp_f<DPP_ROW_HALF_MIRROR>(0.f, v);
+    return v;
+}
+
+template <int HD, int CH, bool EARLY>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
-    constexpr int DPL = HD / 4;                                  // dims per lane when scoring (4 lanes / key)
-    constexpr int DG = HD / 4, KG = 256 / DG, KPG = DA2_CH / KG;  // PV: float4 dim groups x key groups
+    constexpr int LPK = 256 / CH;                                // lanes per key when scoring
+    constexpr int DPL = HD / LPK;                                // dims per lane when scoring
+    constexpr int DG = HD / 4, KG = 256 / DG, KPG = CH / KG;     // PV: float4 dim groups x key groups
+    static_assert(LPK == 4 || LPK == 8, "CH must be 64 or 32");
+    static_assert(KPG >= 1 && DPL % 4 == 0, "unsupported head_dim / chunk");
     __shared__ float qs[HD];
     __shared__ float knew[HD];
     __shared__ float vnew[HD];
-    __shared__ float p_s[DA2_CH];
+    __shared__ float p_s[CH];
     __shared__ float red[8];
     __shared__ int last_s;
     __shared__ float4 o_s[384];  // P.V partials; reused by the combine (m, l per chunk + per-group sums)
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int pos = a.kv_pos[b];
-    const int len = pos + 1;
-    const int k0 = c * DA2_CH;
-    if (k0 >= len) return;
-    const int kn = min(DA2_CH, len - k0);
+    const int k0 = c * CH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvh = h / (a.heads / a.kv_heads);
     float* Kc = a.kc + (long)b * a.page_stride + (long)kvh * a.head_stride;
     float* Vc = a.vc + (long)b * a.page_stride + (long)kvh * a.head_stride;
-    const bool own = pos >= k0 && pos < k0 + DA2_CH;
-    // 1. RoPE inputs first (vmcnt is in-order: these must not queue behind the K/V stream)
+    // 1. the chunk's K / V cache loads go out first and depend on nothing computed this step
+    //    (keys clamped to the cache capacity, not to the position: keys past pos are masked
+    //    at use), so the HBM stream overlaps the position / RoPE-table round trips below
+    const int key = tid / LPK, sub = tid % LPK;
+    const int kcap = a.max_len - 1;
+    const int dg = tid % DG, kg = tid / DG;
+    float4 kreg[DPL / 4];
+    float4 vreg[KPG];
+    auto issue_kv = [&](int klim) {
+        const float4* kp = reinterpret_cast<const float4*>(Kc + (long)min(k0 + key, klim) * HD + sub * DPL);
+#pragma unroll
+        for (int i = 0; i < DPL / 4; ++i) kreg[i] = kp[i];
+#pragma unroll
+        for (int j = 0; j < KPG; ++j) {
+            const int kk = min(k0 + kg * KPG + j, klim);
+            vreg[j] = *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4);
+        }
+    };
+    if (EARLY) issue_kv(kcap);
+    const int pos = a.kv_pos[b];
+    const int len = pos + 1;
+    if (k0 >= len) return;
+    const int kn = min(CH, len - k0);
+    if (!EARLY) issue_kv(k0 + kn - 1);
+    const bool own = pos >= k0 && pos < k0 + CH;
+    // 2. RoPE inputs
     const float* row = a.qkv + (long)b * a.ld;
     const float* krow = row + a.heads * HD + kvh * HD;
     const float* vrow = row + (a.heads + a.kv_heads) * HD + kvh * HD;
@@ -584,22 +643,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
             vx = vrow[tid];
         }
     }
-    // 2. cache loads for this thread's keys (the slot at pos is replaced by the new k / v below)
-    const int key = wave * 16 + (lane >> 2), sub = lane & 3;
-    // unconditional loads (keys clamped into [k0, k0 + kn)); invalid keys are masked at use
-    float4 kreg[DPL / 4];
-    {
-        const float4* kp = reinterpret_cast<const float4*>(Kc + (long)(k0 + min(key, kn - 1)) * HD + sub * DPL);
-#pragma unroll
-        for (int i = 0; i < DPL / 4; ++i) kreg[i] = kp[i];
-    }
-    const int dg = tid % DG, kg = tid / DG;
-    float4 vreg[KPG];
-#pragma unroll
-    for (int j = 0; j < KPG; ++j) {
-        const int kk = k0 + min(kg * KPG + j, kn - 1);
-        vreg[j] = *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4);
-    }
     // 3. rotated q (and the new k, v in the owning chunk): x*cos + sign*partner*sin
     if (tid < HD) {
         qs[tid] = qx * cs + (sg * qr) * sn;
@@ -614,7 +657,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
         }
     }
     __syncthreads();
-    // 3. scores: wave w owns keys w*16 .. w*16+15
+    // 4. scores: LPK lanes per key, wave w owns keys w*CH/4 .. (w+1)*CH/4 - 1
     {
         float acc = 0.f;
         if (key < kn) {
@@ -631,7 +674,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
                 }
             }
         }
-        acc = quad_sum(acc);
+        acc = group_sum<LPK>(acc);
         const float sc = key < kn ? acc * a.scale : -INFINITY;
         if (sub == 0) p_s[key] = sc;
         const float mw = wave_max(sc);
@@ -639,14 +682,14 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     }
     __syncthreads();
     const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (tid < DA2_CH) {
-        const float p = tid < kn ? expf(p_s[tid] - m) : 0.f;
-        p_s[tid] = p;
+    if (wave == 0) {  // whole wave active for the DPP reduction
+        const float p = (tid < CH && tid < kn) ? expf(p_s[tid] - m) : 0.f;
+        if (tid < CH) p_s[tid] = p;
         const float l = wave_sum(p);
         if (tid == 0) red[4] = l;
     }
     __syncthreads();
-    // 4. P.V over this thread's KPG keys
+    // 5. P.V over this thread's KPG keys
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int j = 0; j < KPG; ++j) {
@@ -667,7 +710,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     // partial record of chunk c: [m, l, -, -, o[HD]] (16-byte aligned), stored WRITE-THROUGH (sc1)
     // so the hand-off needs no L2-writeback release fence (cdna_hip_programming.md Guideline 16 R1)
     constexpr int PR = HD + 4;
-    const int chunks = (a.max_len + DA2_CH - 1) / DA2_CH;
+    const int chunks = (a.max_len + CH - 1) / CH;
     float* part0 = a.part + ((long)b * a.heads + h) * chunks * PR;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part0, (short)0, chunks * PR * 4, 0x00020000);
     if (tid < DG) {
@@ -686,33 +729,34 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
         __builtin_memcpy(&bits, ml, 16);
         __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
     }
-    // 5. arrival ticket (every storing wave drains, then one relaxed agent add); the last
-    //    chunk block of (b, h) acquires once and merges every partial
-    const int nc = (len + DA2_CH - 1) / DA2_CH;
+    // 6. arrival ticket (every storing wave drains, then one relaxed agent add); the last
+    //    chunk block of (b, h) merges every partial.  Every partial byte was stored sc1 and
+    //    every load of it below is an sc1 buffer load, so no acquire fence is needed
+    //    (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row).
+    const int nc = (len + CH - 1) / CH;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         int* cnt = a.counters + (long)b * a.heads + h;
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == nc - 1;
-        if (last) {
-            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_s = last;
     }
     __syncthreads();
     if (!last_s) return;
-    // every partial of (b, h) is loaded in parallel: chunk maxima / sums into LDS, then each
-    // of the 256/HD thread groups folds a strided subset of the chunks for its dim
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    auto ld1 = [&](int idx) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, idx * 4, 0, 16)); };
+    // chunk maxima / sums into LDS, then each of the 256/HD thread groups folds a strided
+    // subset of the chunks for its dim (unconditional loads: a predicated load becomes an
+    // exec-masked branch with a vmcnt(0) drain)
     float* ms = reinterpret_cast<float*>(o_s);
     float* ls = ms + 512;
     float* accp = ms + 1024;
     float* lp = ms + 1280;
     for (int cc = tid; cc < nc; cc += 256) {
-        ms[cc] = part0[cc * PR];
-        ls[cc] = part0[cc * PR + 1];
+        ms[cc] = ld1(cc * PR);
+        ls[cc] = ld1(cc * PR + 1);
     }
     __syncthreads();
     float mm = -INFINITY;
@@ -724,7 +768,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     for (int cc = grp; cc < nc; cc += KS) {
         const float w = expf(ms[cc] - mm);
         l += ls[cc] * w;
-        acc += part0[cc * PR + 4 + dim] * w;
+        acc += ld1(cc * PR + 4 + dim) * w;
     }
     accp[grp * HD + dim] = acc;
     lp[grp * HD + dim] = l;
@@ -737,18 +781,35 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     }
 }
 
+static int dec_attn_ch() {
+    const char* e = getenv("DSOCR_ATT_CH");
+    return (e && atoi(e) == 32) ? 32 : 64;
+}
+
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
-    return (size_t)B * heads * ((max_len + DA2_CH - 1) / DA2_CH) * (hd + 4) * sizeof(float);
+    return (size_t)B * heads * ((max_len + DA2_CH_MIN - 1) / DA2_CH_MIN) * (hd + 4) * sizeof(float);
 }
 
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     if (!a.counters) throw std::runtime_error("EINTERNAL: dec_attn needs a zeroed counter array");
-    if (a.max_len > 512 * DA2_CH) throw std::runtime_error("EINVAL: decode context longer than 32768 tokens");
-    const int chunks = (a.max_len + DA2_CH - 1) / DA2_CH;
+    const int ch = dec_attn_ch();
+    if (a.max_len > 512 * ch) throw std::runtime_error("EINVAL: decode context too long for the attention combine");
+    if (a.hd != 128 && a.hd != 64 && a.hd != 32) throw std::runtime_error("EINVAL: decode attention supports head_dim 32 / 64 / 128");
+    const int chunks = (a.max_len + ch - 1) / ch;
     dim3 g1(chunks, a.heads, a.B);
-    if (a.hd == 128) hipLaunchKernelGGL(dec_attn_kernel<128>, g1, dim3(256), 0, s, a);
-    else if (a.hd == 64) hipLaunchKernelGGL(dec_attn_kernel<64>, g1, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(dec_attn_kernel<32>, g1, dim3(256), 0, s, a);
+    const char* ee = getenv("DSOCR_ATT_EARLY");
+    const bool early = ee && atoi(ee) != 0;
+#define DSOCR_DA(HDV, CHV)                                                                         \
+    do {                                                                                            \
+        if (early) hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, true>), g1, dim3(256), 0, s, a);  \
+        else hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, false>), g1, dim3(256), 0, s, a);       \
+    } while (0)
+    if (ch == 64) {
+        if (a.hd == 128) DSOCR_DA(128, 64); else if (a.hd == 64) DSOCR_DA(64, 64); else DSOCR_DA(32, 64);
+    } else {
+        if (a.hd == 128) DSOCR_DA(128, 32); else if (a.hd == 64) DSOCR_DA(64, 32); else DSOCR_DA(32, 32);
+    }
+#undef DSOCR_DA
 }
 
 // ------------------------------------------------------------------ MoE routing (one block)
@@ -1099,29 +1160,38 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
 // in-order vmcnt accounting stays exact (activation loads -> [routing] -> weight stream ->
 // stage -> FMA).  Blocks [0, T*topk*units_r) are (token, pick) slots that route themselves;
 // the rest are the shared experts over all T tokens (MT >= T).
-template <typename WT, int MT>
-__global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
-    extern __shared__ float smem[];
+// FUSED: the block is a producer inside moe_fused_slot_kernel: every store of h (and of the
+// picks) is write-through (sc1) so the down blocks of the same launch can read it (Guideline 16 R1).
+template <typename WT, int MT, bool FUSED>
+__device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int bid, float* smem) {
     __shared__ int sel_e;
     __shared__ float sel_w;
     constexpr int RB = 2, U = 3, XR = 2;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
-    const int bid = blockIdx.x;
+    // dev stamps: [0] wall clock (100 MHz) at entry, [1..7] shader clock at phase points
+#define GU_STAMP(i)                                                                          \
+    if (a.stamps && threadIdx.x == 0) {                                                      \
+        if ((i) == 0) a.stamps[(long)bid * 8] = __builtin_amdgcn_s_memrealtime();            \
+        a.stamps[(long)bid * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();                    \
+    }
+    GU_STAMP(0);
     const bool routed = bid < a.slots * units_r;
     if (!routed && !a.sWgu) return;
     const int sl = routed ? bid / units_r : 0;
     const int t = sl / max(1, a.topk), k = sl % max(1, a.topk);
     const int u = routed ? bid % units_r : bid - a.slots * units_r;
     const int M = routed ? 1 : a.T;
-    XRegs<MT, XR> xr;
-    xload<MT, XR>(xr, a.x + (routed ? (long)t * a.K : 0L), a.K, nullptr, M, a.K, a.norm_w);
     int e_pre = 0;
     float w_pre = 1.f;
     const bool pre = routed && !a.logits;  // routed by dec_router: ids / aw already in memory
-    if (pre) {
+    if (pre) {  // first in the vmcnt queue: the weight stream waits only for this load
         e_pre = a.ids[sl];
         w_pre = a.aw[sl];
+    }
+    XRegs<MT, XR> xr;
+    xload<MT, XR>(xr, a.x + (routed ? (long)t * a.K : 0L), a.K, nullptr, M, a.K, a.norm_w);
+    if (pre) {
     } else if (routed && (a.dbg & 1)) {
         if (threadIdx.x == 0) { sel_e = sl % a.E; sel_w = 1.f; }
         __syncthreads();
@@ -1135,11 +1205,20 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
             if (lane == 0) {
                 sel_e = e;
                 sel_w = v;
-                if (u == 0) { a.ids_out[sl] = e; a.w_out[sl] = v; }
+                if (u == 0) {
+                    if (FUSED) {
+                        __hip_atomic_store(a.ids_out + sl, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(a.w_out + sl, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        a.ids_out[sl] = e;
+                        a.w_out[sl] = v;
+                    }
+                }
             }
         }
         __syncthreads();
     }
+    GU_STAMP(1);
     const int rows_I = routed ? a.I : a.Is;
     const int e_sel = pre ? e_pre : sel_e;
     const WT* Wg = routed ? reinterpret_cast<const WT*>(a.Wgu) + (long)e_sel * 2 * a.I * a.K
@@ -1165,7 +1244,9 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
             }
         }
     }
+    GU_STAMP(2);
     xstage<MT, XR>(xr, M, a.K, a.norm_w != nullptr && !(a.dbg & 4), a.eps, smem);
+    GU_STAMP(3);
     if (!active) return;
     const float* xs = smem + XS_RED;
     float ag[RB][MT], au[RB][MT];
@@ -1196,6 +1277,7 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
             }
         }
     }
+    GU_STAMP(4);
     const float scale = routed ? (pre ? w_pre : sel_w) : 1.f;
     float* hout = routed ? a.h + (long)sl * a.I : a.hs;
 #pragma unroll
@@ -1208,9 +1290,18 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
             if (lane == 0 && m < M && i < rows_I) {
                 float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
                 if (routed) hv = hv * scale;
-                hout[(long)m * rows_I + i] = hv;
+                if (FUSED) __hip_atomic_store(hout + (long)m * rows_I + i, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else hout[(long)m * rows_I + i] = hv;
             }
         }
+    GU_STAMP(5);
+#undef GU_STAMP
+}
+
+template <typename WT, int MT>
+__global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
+    extern __shared__ float smem[];
+    gateup_slot_body<WT, MT, false>(a, blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------------ MoE down + combine + residual
@@ -1324,11 +1415,15 @@ __global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
 // Slot-mode down (T <= 8, topk = KT at compile time, I <= 1024, Is <= 2048): per token,
 // activations -> registers, every routed + shared weight load, then LDS staging and FMAs;
 // straight-line so each consumer waits only for the loads it needs.
-template <typename WT, int KT>
-__global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
-    extern __shared__ float hsm[];
+// FUSED: the block is a consumer inside moe_fused_slot_kernel: it routes itself (the same
+// greedy top-k as the gate/up blocks) so its weight loads go out before h exists, then waits
+// for every gate/up block's arrival and reads h with sc1 loads only (no acquire needed:
+// MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire).
+template <typename WT, int KT, bool FUSED>
+__device__ __forceinline__ void down_slot_body(const MoeDec2Args& a, const int bid, float* hsm) {
+    __shared__ int ids_s[8 * KT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int j = blockIdx.x * 4 + wave;
+    const int j = bid * 4 + wave;
     const bool active = j < a.Hout;
     const int jj = min(j, a.Hout - 1);
     const int ch_r = a.I >> 3, ch_s = a.sWd ? (a.Is >> 3) : 0;
@@ -1336,27 +1431,54 @@ __global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
     const WT* Ws = a.sWd ? reinterpret_cast<const WT*>(a.sWd) + (long)jj * a.Is
                          : reinterpret_cast<const WT*>(a.Wd) + (long)jj * a.I;
     const int cs_max = a.sWd ? ch_s - 1 : ch_r - 1;
+    if (FUSED) {
+        // picks of every token (wave t routes token t), then every weight load, then the wait
+        __shared__ float w_s[8 * KT];
+        if (wave < a.T)
+            topk_write(a.logits + (long)wave * a.E, a.E, KT, a.softmax_scoring, a.norm_topk, a.scaling,
+                       ids_s + wave * KT, w_s + wave * KT);
+        __syncthreads();
+    }
+    // h of the fused launch is read with sc1 buffer loads (bypass the non-coherent L1)
+    const auto hr_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.h, (short)0, a.T * KT * a.I * 4, 0x00020000);
+    const auto hs_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.sWd ? a.hs : a.h, (short)0,
+                                                           a.sWd ? a.T * a.Is * 4 : a.T * KT * a.I * 4, 0x00020000);
     for (int t = 0; t < a.T; ++t) {
         // slot rows t*KT .. t*KT+KT-1 of h are contiguous: [KT*I routed | Is shared] as one vector
         const float* hr = a.h + (long)t * KT * a.I;
         const float* hsh = a.sWd ? a.hs + (long)t * a.Is : hr;
         f32x4 hreg[DN_HREG];  // native vector type: a float4 struct array stays in scratch here
+        if (!FUSED) {
 #pragma unroll
-        for (int r = 0; r < DN_HREG; ++r) {
-            const int f = min(tid + r * 256, n4 - 1);
-            const float* src = f < nr4 ? hr + f * 4 : hsh + (f - nr4) * 4;
-            hreg[r] = *reinterpret_cast<const f32x4*>(src);
+            for (int r = 0; r < DN_HREG; ++r) {
+                const int f = min(tid + r * 256, n4 - 1);
+                const float* src = f < nr4 ? hr + f * 4 : hsh + (f - nr4) * 4;
+                hreg[r] = *reinterpret_cast<const f32x4*>(src);
+            }
         }
         uint4 qr[KT][2], qs[4];
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-            const int e = a.ids[t * KT + k];
+            const int e = FUSED ? ids_s[t * KT + k] : a.ids[t * KT + k];
             const WT* Wd = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + jj) * a.I;
 #pragma unroll
             for (int uu = 0; uu < 2; ++uu) qr[k][uu] = ldg_nt16(Wd + (min(uu * 64 + lane, ch_r - 1) << 3));
         }
 #pragma unroll
         for (int uu = 0; uu < 4; ++uu) qs[uu] = ldg_nt16(Ws + (min(uu * 64 + lane, cs_max) << 3));
+        if (FUSED) {
+            if (t == 0) {  // every gate/up block of this launch has stored its h rows
+                if (tid == 0) wait_arrivals(a.sync, a.sync_target, a.err);
+                __syncthreads();
+            }
+#pragma unroll
+            for (int r = 0; r < DN_HREG; ++r) {
+                const int f = min(tid + r * 256, n4 - 1);
+                const u32x4 bits = f < nr4 ? __builtin_amdgcn_raw_buffer_load_b128(hr_rsrc, (t * nr4 + f) * 16, 0, 16)
+                                           : __builtin_amdgcn_raw_buffer_load_b128(hs_rsrc, (t * ns4 + f - nr4) * 16, 0, 16);
+                __builtin_memcpy(&hreg[r], &bits, 16);
+            }
+        }
         __syncthreads();  // previous token's rows consumed (unconditional: keeps hreg in VGPRs)
 #pragma unroll
         for (int r = 0; r < DN_HREG; ++r)  // LDS holds 256*DN_HREG float4: no bounds branch
@@ -1394,6 +1516,59 @@ __global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
             *xp = *xp + v;
         }
     }
+}
+
+template <typename WT, int KT>
+__global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
+    extern __shared__ float hsm[];
+    down_slot_body<WT, KT, false>(a, blockIdx.x, hsm);
+}
+
+// One launch for the whole decode MoE of a layer (slot mode): blocks [0, NG) are the gate/up
+// blocks (producers of h), blocks [NG, NG + ND) the down blocks.  Producers have the lower
+// block ids, so a resident down block only ever waits for blocks dispatched before it.
+template <typename WT, int MT, int KT>
+__global__ __launch_bounds__(256) void moe_fused_slot_kernel(MoeDec2Args a, int NG) {
+    extern __shared__ float smem[];
+    const int bid = blockIdx.x;
+    if (bid < NG) {
+        gateup_slot_body<WT, MT, true>(a, bid, smem);
+        // R1 publish: every storing wave drains its sc1 stores, then ONE lane counts the block
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(a.sync + (bid % SYNC_SHARDS) * SYNC_STRIDE, 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        down_slot_body<WT, KT, true>(a, bid - NG, smem);
+    }
+}
+
+bool moe_fused_ok(const MoeDec2Args& a) {
+    const long n4 = (long)a.topk * (a.I / 4) + (a.sWd ? a.Is / 4 : 0);
+    return a.slot_mode && a.logits && a.T <= 2 && a.K <= 64 * 3 * 8 && (a.topk == 6 || a.topk == 3) &&
+           a.I <= 1024 && (!a.sWd || a.Is <= 2048) && n4 <= 256L * DN_HREG && a.sync && a.err;
+}
+
+void launch_moe_fused(const MoeDec2Args& a, hipStream_t s) {
+    if (!moe_fused_ok(a)) throw std::runtime_error("EINVAL: fused decode MoE outside its slot-mode range");
+    constexpr int RB = 2;
+    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
+    const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
+    const int NG = a.slots * units_r + units_s;
+    const int ND = (a.Hout + 3) / 4;
+    MoeDec2Args b = a;
+    b.sync_target = NG;
+    const size_t lds = std::max(stage_bytes(a.T == 1 ? 1 : 2, a.K), (size_t)256 * DN_HREG * 16);
+#define DSOCR_FU(WTY, MTV, KTV) hipLaunchKernelGGL((moe_fused_slot_kernel<WTY, MTV, KTV>), dim3(NG + ND), dim3(256), lds, s, b, NG)
+    if (a.wdtype == WDT_BF16) {
+        if (a.T == 1) { if (a.topk == 6) DSOCR_FU(bf16_t, 1, 6); else DSOCR_FU(bf16_t, 1, 3); }
+        else { if (a.topk == 6) DSOCR_FU(bf16_t, 2, 6); else DSOCR_FU(bf16_t, 2, 3); }
+    } else {
+        if (a.T == 1) { if (a.topk == 6) DSOCR_FU(f16_t, 1, 6); else DSOCR_FU(f16_t, 1, 3); }
+        else { if (a.topk == 6) DSOCR_FU(f16_t, 2, 6); else DSOCR_FU(f16_t, 2, 3); }
+    }
+#undef DSOCR_FU
 }
 
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {

@@ -181,7 +181,15 @@ struct MoeDec2Args {
     float scaling = 1.f;
     int* ids_out = nullptr; float* w_out = nullptr;
     int dbg = 0;  // experiment knobs (DSOCR_DBG_GU): 1 skip routing, 2 skip weight stream
+    unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
+    // fused launch (moe_fused_slot_kernel): arrival counters (SYNC_SHARDS lines, zeroed before
+    // the launch), arrivals to wait for (set by the launcher), give-up flag
+    int* sync = nullptr; int sync_target = 0; int* err = nullptr;
 };
+constexpr int SYNC_SHARDS = 8, SYNC_STRIDE = 32;  // counters per hand-off, ints between counters
+constexpr int SYNC_INTS = SYNC_SHARDS * SYNC_STRIDE;  // ints of one hand-off's counter block
+bool moe_fused_ok(const MoeDec2Args& a);
+void launch_moe_fused(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
 // Greedy selection (ngram ban evaluated in-kernel) + step bookkeeping + KV advance.

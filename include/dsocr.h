@@ -162,6 +162,10 @@ typedef struct dsocr_decode_profile {
     int experts_touched;              /* routed experts active in the replayed step (per layer, summed / layers) */
     int tokens;                       /* pages in the batch */
     int kv_len;                       /* keys attended by page 0 */
+    dsocr_kernel_profile qkv;         /* dec_gemv: RMSNorm + fused q/k/v projection, one layer */
+    dsocr_kernel_profile o_proj;      /* dec_gemv: o_proj + residual, one layer */
+    dsocr_kernel_profile router;      /* MoE router logits (+ top-k when routed by the router kernel) */
+    dsocr_kernel_profile layers_step; /* every decoder layer of one decode step, replayed as one hipGraph */
 } dsocr_decode_profile;
 dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out);
 

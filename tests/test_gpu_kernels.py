@@ -155,10 +155,13 @@ def test_attention_sam_relpos(gpu, g, rel_len):
 
 @pytest.mark.parametrize("B,heads,kvh,hd,max_len", [(1, 10, 10, 128, 1218), (3, 4, 4, 32, 300),
                                                    (5, 12, 4, 64, 700), (2, 10, 10, 128, 257), (1, 10, 10, 128, 64)])
-def test_decode_attention(gpu, B, heads, kvh, hd, max_len):
+@pytest.mark.parametrize("chunk", ["64", "32"])
+def test_decode_attention(gpu, B, heads, kvh, hd, max_len, chunk, monkeypatch):
     """Fused decode attention (block.rs:608-789 at seq_len 1): RoPE on q / new k (block.rs:1403-1471),
-    K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the f32 cache."""
+    K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the f32 cache (64- and
+    32-key chunks per block)."""
     from types import SimpleNamespace
+    monkeypatch.setenv("DSOCR_ATT_CH", chunk)
     from oracle.decoder import apply_rope, rope_tables
     rng = np.random.default_rng(B * hd + max_len)
     qkvw = (heads + 2 * kvh) * hd
