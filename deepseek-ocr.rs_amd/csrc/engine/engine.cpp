@@ -871,12 +871,6 @@ void Engine::decode_step(int B, int Lmax) {
         float* QKV = wsf("s_qkv", (size_t)B * QKVN);
         const long layer_kv = (long)B * page_stride_;
         // attention: [norm] qkv -> rope + append + flash-decoding -> o_proj + residual
-        DecGemvArgs g;
-        g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
-        g.y = QKV; g.ldy = QKVN;
-        if (fuse_norm) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
-        else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
-        launch_dec_gemv(g, st);
         DecAttn2Args da;
         da.qkv = QKV; da.ld = QKVN; da.kv_pos = kv_pos; da.B = B; da.heads = L.heads; da.kv_heads = L.kv_heads;
         da.hd = hd; da.rope_dim = L.rope_dim; da.use_mla = L.use_mla; da.max_len = Lmax;
@@ -885,7 +879,25 @@ void Engine::decode_step(int B, int Lmax) {
         da.page_stride = page_stride_; da.head_stride = head_stride_;
         da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
         da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
-        launch_dec_attn(da, st);
+        // q/k/v projection: fused into the attention launch (each head's chunk blocks compute
+        // that head's rows, dec_qkv_attn) when in range, else its own GEMV launch
+        // (off by default: measured +7 us / layer on MI355X at B = 1 — 160 blocks carry both the
+        // projection and the KV stream; DSOCR_FUSED_QKV=1 enables it)
+        static const bool fused_qkv = getenv("DSOCR_FUSED_QKV") && atoi(getenv("DSOCR_FUSED_QKV")) != 0;
+        da.x = X; da.ldx = H; da.norm_w = d.in_norm.w; da.eps = L.rms_eps; da.K = H;
+        da.Wqkv = d.qkv.W; da.wdtype = d.qkv.wdt; da.qkv_bias = d.qkv.b;
+        da.qkv_cnt = wsi("s_qkv_cnt", (size_t)B * L.heads); da.err = err;
+        if (fused_qkv && fuse_norm && dec_qkv_attn_ok(da)) {
+            launch_dec_qkv_attn(da, st);
+        } else {
+            DecGemvArgs g;
+            g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
+            g.y = QKV; g.ldy = QKVN;
+            if (fuse_norm) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
+            else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
+            launch_dec_gemv(g, st);
+            launch_dec_attn(da, st);
+        }
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
         go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
@@ -912,6 +924,10 @@ void Engine::decode_step(int B, int Lmax) {
         gr.M = B; gr.N = E; gr.K = H; gr.x = mx; gr.ldx = H; gr.W = d.router.W; gr.ldw = H; gr.wdtype = d.router.wdt;
         gr.bias = d.router.b; gr.y = LOG; gr.ldy = E; gr.norm_w = mnorm; gr.eps = L.rms_eps;
         m = moe_decode_args(l, B, mx, mnorm, X);
+        static const bool gu_mix = !(getenv("DSOCR_GU_MIX") && atoi(getenv("DSOCR_GU_MIX")) == 0);
+        const bool mix = gu_mix && fuse_norm && moe_gateup_mix_ok(m);
+        float* XNR = wsf("s_xn_router", (size_t)B * H);
+        if (mix) gr.xn_out = XNR;  // the router hands its normalised row to the gate/up waves
         if (m.slot_mode && !m.logits) {
             DecRouteEpi re;
             re.topk = K; re.softmax_scoring = L.scoring == "softmax"; re.norm_topk = L.norm_topk;
@@ -936,7 +952,8 @@ void Engine::decode_step(int B, int Lmax) {
             launch_moe_fused(m, st);
             continue;
         }
-        launch_moe_gateup2(m, st);
+        if (mix) launch_moe_gateup_mix(m, XNR, st);
+        else launch_moe_gateup2(m, st);
         launch_moe_down2(m, st);
     }
 }
@@ -1146,6 +1163,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
+    HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     const int QKVN = layers_[0].qkv.N;
     r0 = 0;
     for (int b = 0; b < B; ++b) {
@@ -1379,7 +1397,13 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         auto args = [&](int l) { return moe_decode_args(l, B, Xs, B <= 2 ? layers_[l].post_norm.w : nullptr, Xs); };
         const int n = iters * (int)moe_layers.size();
         // rotating over the layers (~55 MB each) defeats the 256 MB Infinity Cache
-        timed(prof.moe_gateup, n, [&](int i) { launch_moe_gateup2(args(moe_layers[i % moe_layers.size()]), st); });
+        static const bool gu_mix = !(getenv("DSOCR_GU_MIX") && atoi(getenv("DSOCR_GU_MIX")) == 0);
+        float* XNR = wsf("s_xn_router", (size_t)B * H);
+        timed(prof.moe_gateup, n, [&](int i) {
+            const MoeDec2Args m = args(moe_layers[i % moe_layers.size()]);
+            if (gu_mix && B <= 2 && moe_gateup_mix_ok(m)) launch_moe_gateup_mix(m, XNR, st);
+            else launch_moe_gateup2(m, st);
+        });
         timed(prof.moe_down, n, [&](int i) { launch_moe_down2(args(moe_layers[i % moe_layers.size()]), st); });
         if (const char* path = getenv("DSOCR_STAMPS_OUT")) {
             // dev: per-block phase clocks of one gate/up launch (moe_gateup_slot_kernel)

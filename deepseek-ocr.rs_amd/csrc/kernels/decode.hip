@@ -207,8 +207,11 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
     }
     if (fast) xstage<MT, XR>(xr, a.M, a.K, a.norm_w != nullptr, a.eps, smem);
     else stage_rows(a.x, a.ldx, nullptr, a.M, a.K, a.norm_w, a.eps, smem);
-    if (!active) return;
     const float* xs = smem + XS_RED;
+    if (a.xn_out && blockIdx.x == 0)  // hand the normalised rows to the next kernel
+        for (int i = threadIdx.x * 4; i < a.M * a.K; i += blockDim.x * 4)
+            *reinterpret_cast<float4*>(a.xn_out + i) = *reinterpret_cast<const float4*>(xs + i);
+    if (!active) return;
     float acc[RB][MT];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -574,8 +577,93 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
-template <int HD, int CH, bool EARLY>
-__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
+// q / k / v rows of head h for page b, computed by chunk block c of the nc active blocks:
+// flattened rows f in [c*R, (c+1)*R) of the head's 3*HD rows (q, then k, then v), R = ceil(3HD/nc),
+// wave w owning f = c*R + w + 4j.  x = rmsnorm(x_b) staged once (xload / xstage, the dec_gemv
+// arithmetic), every row a wave dot product in dec_gemv's order (chunk u-major, then j),
+// stored write-through; then the per-head arrival counter and the wait for all nc blocks.
+template <int HD>
+__device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, int h, int c, int nc, float* smem) {
+    constexpr int U = 3, XR = 2, RBM = 8;  // K <= 1536; up to 8 rows per wave per batch
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int R = (3 * HD + nc - 1) / nc;
+    const int f0 = c * R, f1 = min(3 * HD, f0 + R);
+    const int chunks = a.K >> 3;
+    auto row_of = [&](int f) {
+        const int seg = f / HD, i = f % HD;
+        return seg == 0 ? h * HD + i : (seg == 1 ? a.heads * HD + h * HD + i : (2 * a.heads) * HD + h * HD + i);
+    };
+    XRegs<1, XR> xr;
+    xload<1, XR>(xr, a.x + (long)b * a.ldx, a.ldx, nullptr, 1, a.K, a.norm_w);
+    bool staged = false;
+    float* yrow = const_cast<float*>(a.qkv) + (long)b * a.ld;
+    const int nbat = (R + 4 * RBM - 1) / (4 * RBM);  // uniform over the block's waves
+    for (int bt = 0; bt < nbat; ++bt) {
+        // batch: rows fb, fb + 4, ..., fb + 4 * (RBM - 1) of this wave (clamped loads past f1)
+        const int fb = f0 + wave + bt * 4 * RBM;
+        uint4 wq[RBM][U];
+        const bool any = fb < f1;
+#pragma unroll
+        for (int r = 0; r < RBM; ++r) {
+            const int f = min(fb + 4 * r, f1 - 1);
+            const uint16_t* W = reinterpret_cast<const uint16_t*>(a.Wqkv) + (long)row_of(f) * a.K;
+#pragma unroll
+            for (int u = 0; u < U; ++u) wq[r][u] = ldg_nt16(W + (min(u * 64 + lane, chunks - 1) << 3));
+        }
+        if (!staged) {
+            xstage<1, XR>(xr, 1, a.K, a.norm_w != nullptr, a.eps, smem);
+            staged = true;
+        }
+        const float* xs = smem + XS_RED;
+        if (any) {
+#pragma unroll
+            for (int r = 0; r < RBM; ++r) {
+                float acc = 0.f;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int cc = u * 64 + lane;
+                    if (cc < chunks) {
+                        float w8[8], xv[8];
+                        if (a.wdtype == WDT_BF16) unpack8<bf16_t>(wq[r][u], w8);
+                        else unpack8<f16_t>(wq[r][u], w8);
+                        ld_x8(xs + (cc << 3), xv);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], w8[j], acc);
+                    }
+                }
+                float v = wave_sum(acc);
+                const int f = fb + 4 * r;
+                if (lane == 0 && f < f1) {
+                    const int n = row_of(f);
+                    v = v + (a.qkv_bias ? a.qkv_bias[n] : 0.f);
+                    __hip_atomic_store(yrow + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    }
+    // R1 publish: every storing wave drains its sc1 stores, one lane counts the block, then
+    // one lane waits for all nc blocks of the head
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int* cnt = a.qkv_cnt + (long)b * a.heads + h;
+        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned it = 0;; ++it) {
+            if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nc) break;
+            if (it > (1u << 21)) { __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
+}
+
+// FUSED (dec_qkv_attn): the blocks of one (page, head) first compute that head's q / k / v
+// rows of the fused projection themselves (RMSNorm + GEMV, the same per-row arithmetic as
+// dec_gemv), hand them over through a per-head arrival counter (write-through stores, sc1
+// loads), then run the attention chunk exactly as the unfused kernel.
+template <int HD, int CH, bool EARLY, bool FUSED>
+__device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
     constexpr int DG = HD / 4, KG = 256 / DG, KPG = CH / KG;     // PV: float4 dim groups x key groups
@@ -619,10 +707,15 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     const int kn = min(CH, len - k0);
     if (!EARLY) issue_kv(k0 + kn - 1);
     const bool own = pos >= k0 && pos < k0 + CH;
-    // 2. RoPE inputs
+    const int nc = (len + CH - 1) / CH;
     const float* row = a.qkv + (long)b * a.ld;
+    if (FUSED) qkv_rows_for_head<HD>(a, b, h, c, nc, smem);
+    // 2. RoPE inputs
     const float* krow = row + a.heads * HD + kvh * HD;
     const float* vrow = row + (a.heads + a.kv_heads) * HD + kvh * HD;
+    auto ldv = [&](const float* p) {
+        return FUSED ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+    };
     float qx = 0.f, qr = 0.f, kx = 0.f, kr = 0.f, vx = 0.f, cs = 1.f, sn = 0.f, sg = 0.f;
     if (tid < HD) {
         int ix = tid, ir = tid;
@@ -635,12 +728,12 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
             cs = a.cos[(long)pos * a.rope_dim + tid];
             sn = a.sin[(long)pos * a.rope_dim + tid];
         }
-        qx = row[h * HD + ix];
-        qr = row[h * HD + ir];
+        qx = ldv(row + h * HD + ix);
+        qr = ldv(row + h * HD + ir);
         if (own) {
-            kx = krow[ix];
-            kr = krow[ir];
-            vx = vrow[tid];
+            kx = ldv(krow + ix);
+            kr = ldv(krow + ir);
+            vx = ldv(vrow + tid);
         }
     }
     // 3. rotated q (and the new k, v in the owning chunk): x*cos + sign*partner*sin
@@ -733,14 +826,17 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     //    chunk block of (b, h) merges every partial.  Every partial byte was stored sc1 and
     //    every load of it below is an sc1 buffer load, so no acquire fence is needed
     //    (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row).
-    const int nc = (len + CH - 1) / CH;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         int* cnt = a.counters + (long)b * a.heads + h;
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == nc - 1;
-        if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) {
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // every block of (b, h) has passed its q/k/v wait before adding its ticket
+            if (FUSED) __hip_atomic_store(a.qkv_cnt + (long)b * a.heads + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         last_s = last;
     }
     __syncthreads();
@@ -779,6 +875,31 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
         for (int g = 0; g < KS; ++g) { at += accp[g * HD + tid]; lt += lp[g * HD + tid]; }
         a.o[(long)b * a.o_ld + (long)h * HD + tid] = at / lt;
     }
+}
+
+template <int HD, int CH, bool EARLY>
+__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
+    attn_body<HD, CH, EARLY, false>(a, nullptr);
+}
+
+template <int HD, int CH>
+__global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecAttn2Args a) {
+    extern __shared__ float smem[];
+    attn_body<HD, CH, false, true>(a, smem);
+}
+
+bool dec_qkv_attn_ok(const DecAttn2Args& a) {
+    return a.heads == a.kv_heads && a.hd == 128 && a.x && a.Wqkv && a.qkv_cnt && a.err && a.K % 8 == 0 &&
+           a.K <= 64 * 3 * 8 && a.max_len <= 512 * 64;
+}
+
+void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s) {
+    if (!dec_qkv_attn_ok(a) || !a.counters) throw std::runtime_error("EINVAL: fused q/k/v + attention outside its range");
+    const int chunks = (a.max_len + 63) / 64;
+    dim3 g1(chunks, a.heads, a.B);
+    const size_t lds = stage_bytes(1, a.K);
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
 }
 
 static int dec_attn_ch() {
@@ -1542,6 +1663,157 @@ __global__ __launch_bounds__(256) void moe_fused_slot_kernel(MoeDec2Args a, int 
     } else {
         down_slot_body<WT, KT, true>(a, bid - NG, smem);
     }
+}
+
+// ------------------------------------------------------------------ decode gate/up, T = 1 (mix)
+// Rank form of the greedy top-k (block.rs:1254-1301: softmax, stable descending sort, ties ->
+// lower expert id): lane e holds score s_e; rank_e = #{j : s_j > s_e or (s_j == s_e and j < e)};
+// pick k is the lane whose rank is k.  Identical picks to topk_select, no serial argmax rounds.
+// lds: 64 floats private to the calling wave.  Returns (expert, weight) of pick `want`.
+__device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int softmax_scoring, int norm_topk,
+                                               float scaling, int want, float* lds, int& e_out, float& w_out) {
+    const int lane = threadIdx.x & 63;
+    float sc;
+    if (softmax_scoring) {
+        const float v = lane < E ? logit : -INFINITY;
+        const float mx = wave_max(v);
+        const float ex = lane < E ? expf(v - mx) : 0.f;
+        const float sum = wave_sum(ex);
+        sc = lane < E ? ex / sum : -INFINITY;
+    } else {
+        sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
+    }
+    lds[lane] = sc;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    int rank = 0;
+#pragma unroll
+    for (int j4 = 0; j4 < 16; ++j4) {
+        const float4 o = reinterpret_cast<const float4*>(lds)[j4];
+        const float oj[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = j4 * 4 + q;
+            rank += (oj[q] > sc || (oj[q] == sc && j < lane)) ? 1 : 0;
+        }
+    }
+    if (lane >= E) rank = 1 << 20;
+    // sum of the top-k scores in pick order (topk_select adds them in rank order)
+    float wsum = 0.f;
+    if (K > 1 && norm_topk) {
+        for (int k = 0; k < K; ++k) {
+            const unsigned long long bm = __ballot(rank == k);
+            const int e = __builtin_ctzll(bm);
+            wsum += __shfl(sc, e);
+        }
+    }
+    const unsigned long long bm = __ballot(rank == want);
+    const int e = __builtin_ctzll(bm);
+    float v = __shfl(sc, e);
+    if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
+    if (scaling != 1.0f) v = v * scaling;
+    e_out = e;
+    w_out = v;
+}
+
+template <typename WT>
+__global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn) {
+    __shared__ __attribute__((aligned(16))) float rank_lds[4][64];
+    constexpr int RB = 2, U = 3;  // K <= 1536
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    const int wpr = (a.I + RB - 1) / RB;                 // routed waves per pick
+    const int n_sh = a.sWgu ? (a.Is + RB - 1) / RB : 0;  // shared waves
+    const int n_rt = a.topk * wpr;
+    const bool shared = wave == 0;
+    const int widx = shared ? b : 3 * b + wave - 1;
+    if (shared ? widx >= n_sh : widx >= n_rt) return;   // whole wave: no block barrier below
+    const int chunks = a.K >> 3;
+    const int sl = shared ? 0 : widx / wpr;
+    const int i0 = (shared ? widx : widx % wpr) * RB;
+    int e = 0;
+    float wk = 1.f;
+    uint4 qg[U][RB], qu[U][RB];
+    float xr[U][8];
+    auto issue = [&](const WT* Wg, const WT* Wu, int rows) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int cc = min(u * 64 + lane, chunks - 1);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const int i = min(i0 + r, rows - 1);
+                qg[u][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
+                qu[u][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
+            }
+        }
+    };
+    auto load_x = [&]() {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int cc = min(u * 64 + lane, chunks - 1);
+            ld_x8(xn + (cc << 3), xr[u]);
+        }
+    };
+    if (shared) {
+        // the shared expert needs nothing from this step: its weight stream goes out first
+        const WT* Wg = reinterpret_cast<const WT*>(a.sWgu);
+        issue(Wg, Wg + (long)a.Is * a.K, a.Is);
+        load_x();
+    } else {
+        const float lg = a.logits[min(lane, a.E - 1)];
+        load_x();
+        topk_rank_pick(lg, a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, sl, rank_lds[wave], e, wk);
+        const WT* Wg = reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
+        issue(Wg, Wg + (long)a.I * a.K, a.I);
+        if (i0 == 0 && lane == 0) { a.ids_out[sl] = e; a.w_out[sl] = wk; }
+    }
+    const int rows = shared ? a.Is : a.I;
+    float ag[RB], au[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) { ag[r] = 0.f; au[r] = 0.f; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int cc = u * 64 + lane;
+        if (cc >= chunks) continue;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            float wg[8], wu[8];
+            unpack8<WT>(qg[u][r], wg);
+            unpack8<WT>(qu[u][r], wu);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ag[r] = fmaf(xr[u][j], wg[j], ag[r]);
+                au[r] = fmaf(xr[u][j], wu[j], au[r]);
+            }
+        }
+    }
+    float* hout = shared ? a.hs : a.h + (long)sl * a.I;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const float gs = wave_sum(ag[r]);
+        const float us = wave_sum(au[r]);
+        const int i = i0 + r;
+        if (lane == 0 && i < rows) {
+            float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
+            if (!shared) hv = hv * wk;
+            hout[i] = hv;
+        }
+    }
+}
+
+bool moe_gateup_mix_ok(const MoeDec2Args& a) {
+    return a.slot_mode && a.logits && a.T == 1 && a.E <= 64 && a.topk <= 8 && a.K % 8 == 0 && a.K <= 64 * 3 * 8 &&
+           a.ids_out && a.w_out;
+}
+
+void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s) {
+    if (!moe_gateup_mix_ok(a) || !xn) throw std::runtime_error("EINVAL: moe_gateup_mix outside its range");
+    constexpr int RB = 2;
+    const int n_sh = a.sWgu ? (a.Is + RB - 1) / RB : 0;
+    const int n_rt = a.topk * ((a.I + RB - 1) / RB);
+    dim3 grid(std::max(n_sh, (n_rt + 2) / 3));
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL(moe_gateup_mix_kernel<bf16_t>, grid, dim3(256), 0, s, a, xn);
+    else hipLaunchKernelGGL(moe_gateup_mix_kernel<f16_t>, grid, dim3(256), 0, s, a, xn);
 }
 
 bool moe_fused_ok(const MoeDec2Args& a) {

@@ -123,6 +123,7 @@ struct DecGemvArgs {
     int accumulate = 0;
     const float* norm_w = nullptr;
     float eps = 0.f;
+    float* xn_out = nullptr;  // optional: block 0 writes the staged (normalised) rows [M][K] here
 };
 void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s);
 // Router GEMV whose last-arriving block writes the greedy top-k of every token (T <= 8).
@@ -145,8 +146,16 @@ struct DecAttn2Args {
     float* part = nullptr;
     int* counters = nullptr;                            // [B][heads] arrival tickets, zero between launches
     float* o = nullptr; long o_ld = 0;
+    // fused q/k/v projection (dec_qkv_attn): residual rows x [B][ldx], RMSNorm weight, fused
+    // [(heads + 2 kv_heads) hd][K] weight, per-(page, head) arrival counters (zero between
+    // launches; the combine resets them), give-up flag; qkv above is then the OUTPUT buffer
+    const float* x = nullptr; long ldx = 0; const float* norm_w = nullptr; float eps = 0.f; int K = 0;
+    const void* Wqkv = nullptr; int wdtype = WDT_F16; const float* qkv_bias = nullptr;
+    int* qkv_cnt = nullptr; int* err = nullptr;
 };
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
+bool dec_qkv_attn_ok(const DecAttn2Args& a);
+void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
 // Router top-k + grouping by expert in one block (T <= 64, E <= 256, top_k <= 8).
 struct MoeRouteArgs {
@@ -189,6 +198,12 @@ struct MoeDec2Args {
 constexpr int SYNC_SHARDS = 8, SYNC_STRIDE = 32;  // counters per hand-off, ints between counters
 constexpr int SYNC_INTS = SYNC_SHARDS * SYNC_STRIDE;  // ints of one hand-off's counter block
 bool moe_fused_ok(const MoeDec2Args& a);
+// Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams
+// shared-expert rows from its first instruction, 3 of 4 route themselves (rank-based top-k of
+// the router logits) and stream their routed expert's rows; activations = the normalised row
+// the router kernel wrote (xn).
+bool moe_gateup_mix_ok(const MoeDec2Args& a);
+void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s);
 void launch_moe_fused(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
