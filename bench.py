@@ -27,6 +27,7 @@ for _p in (ROOT, PKG):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+GATEUP_KERNEL = "moe_gateup_mix_kernel"  # the decode MoE grouped GEMM at B = 1 (decode.hip)
 
 
 def log(*a):
@@ -129,7 +130,7 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-decode-steps", type=int, default=2)
-    ap.add_argument("--roofline-iters", type=int, default=3)
+    ap.add_argument("--roofline-iters", type=int, default=20)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -201,8 +202,8 @@ def main():
         achieved = gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic("moe_gateup_slot_kernel"),
-                    "kernel": "moe_gateup_slot_kernel (decode MoE gate/up: self-routed top-6 + shared experts, one layer)",
+                    "traffic": pmc_traffic(GATEUP_KERNEL),
+                    "kernel": GATEUP_KERNEL + " (decode MoE gate/up: shared-expert waves + self-routed top-6 waves, one layer)",
                     "avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
                     "experts_touched": prof["experts_touched"],
                     "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],

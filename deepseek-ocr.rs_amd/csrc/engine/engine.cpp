@@ -887,8 +887,31 @@ void Engine::decode_step(int B, int Lmax) {
         da.x = X; da.ldx = H; da.norm_w = d.in_norm.w; da.eps = L.rms_eps; da.K = H;
         da.Wqkv = d.qkv.W; da.wdtype = d.qkv.wdt; da.qkv_bias = d.qkv.b;
         da.qkv_cnt = wsi("s_qkv_cnt", (size_t)B * L.heads); da.err = err;
+        static const bool qkv_rope = !(getenv("DSOCR_QKV_ROPE") && atoi(getenv("DSOCR_QKV_ROPE")) == 0);
+        // attention combine fused into the o_proj launch (B = 1; experiment, off: every o_proj
+        // block re-reads every partial, measured +4 us / layer on MI355X)
+        static const bool oc_env = getenv("DSOCR_OPROJ_COMB") && atoi(getenv("DSOCR_OPROJ_COMB")) != 0;
+        DecGemvArgs go;
+        go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
+        go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
+        DecCombArgs cb;
+        cb.part = part; cb.kv_pos = kv_pos; cb.heads = L.heads; cb.hd = hd; cb.cm = (Lmax + 63) / 64; cb.ch = 64;
+        const bool oproj_comb = oc_env && B == 1 && qkv_rope && !L.use_mla && L.rope_dim == hd && fuse_norm &&
+                                dec_oproj_comb_ok(go, cb) && !(getenv("DSOCR_ATT_CH") && atoi(getenv("DSOCR_ATT_CH")) == 32);
+        DecRopeEpi re;
+        re.kv_pos = kv_pos; re.cos = rope_cos_; re.sin = rope_sin_; re.hd = hd;
+        re.rot_rows = (L.heads + L.kv_heads) * hd;
         if (fused_qkv && fuse_norm && dec_qkv_attn_ok(da)) {
             launch_dec_qkv_attn(da, st);
+        } else if (qkv_rope && B == 1 && !L.use_mla && L.rope_dim == hd && fuse_norm) {
+            // RoPE in the projection epilogue: the attention reads q / k already rotated
+            DecGemvArgs g;
+            g.M = 1; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
+            g.y = QKV; g.ldy = QKVN; g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps;
+            launch_dec_qkv_rope(g, re, st);
+            da.prerot = 1;
+            da.split = oproj_comb ? 1 : 0;
+            launch_dec_attn(da, st);
         } else {
             DecGemvArgs g;
             g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
@@ -898,10 +921,8 @@ void Engine::decode_step(int B, int Lmax) {
             launch_dec_gemv(g, st);
             launch_dec_attn(da, st);
         }
-        DecGemvArgs go;
-        go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
-        go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
-        launch_dec_gemv(go, st);
+        if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
+        else launch_dec_gemv(go, st);
         // MLP / MoE
         const float* mx = X;
         const float* mnorm = d.post_norm.w;
@@ -954,7 +975,9 @@ void Engine::decode_step(int B, int Lmax) {
         }
         if (mix) launch_moe_gateup_mix(m, XNR, st);
         else launch_moe_gateup2(m, st);
-        launch_moe_down2(m, st);
+        static const bool dn_mix = !(getenv("DSOCR_DN_MIX") && atoi(getenv("DSOCR_DN_MIX")) == 0);
+        if (dn_mix && moe_down_mix_ok(m)) launch_moe_down_mix(m, st);
+        else launch_moe_down2(m, st);
     }
 }
 
@@ -1404,7 +1427,12 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             if (gu_mix && B <= 2 && moe_gateup_mix_ok(m)) launch_moe_gateup_mix(m, XNR, st);
             else launch_moe_gateup2(m, st);
         });
-        timed(prof.moe_down, n, [&](int i) { launch_moe_down2(args(moe_layers[i % moe_layers.size()]), st); });
+        timed(prof.moe_down, n, [&](int i) {
+            const MoeDec2Args m = args(moe_layers[i % moe_layers.size()]);
+            static const bool dn_mix = !(getenv("DSOCR_DN_MIX") && atoi(getenv("DSOCR_DN_MIX")) == 0);
+            if (dn_mix && moe_down_mix_ok(m)) launch_moe_down_mix(m, st);
+            else launch_moe_down2(m, st);
+        });
         if (const char* path = getenv("DSOCR_STAMPS_OUT")) {
             // dev: per-block phase clocks of one gate/up launch (moe_gateup_slot_kernel)
             const size_t nstamp = 4096 * 8;
@@ -1447,6 +1475,28 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
             launch_dec_attn(da, st);
         });
+        if (const char* path = getenv("DSOCR_ATT_STAMPS_OUT")) {
+            const size_t nstamp = 4096 * 8;
+            auto* d_st = (unsigned long long*)ws("p_stamps", nstamp * 8);
+            HIP_CHECK(hipMemsetAsync(d_st, 0, nstamp * 8, st));
+            DecAttn2Args da;
+            da.qkv = wsf("s_qkv", (size_t)B * QKVN); da.ld = QKVN; da.kv_pos = d_pos; da.B = B; da.heads = L.heads;
+            da.kv_heads = L.kv_heads; da.hd = hd; da.rope_dim = L.rope_dim; da.use_mla = L.use_mla; da.max_len = Lmax;
+            da.cos = rope_cos_; da.sin = rope_sin_;
+            da.kc = kc_; da.vc = vc_;
+            da.page_stride = page_stride_; da.head_stride = head_stride_;
+            da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
+            da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
+            da.stamps = d_st;
+            launch_dec_attn(da, st);
+            std::vector<unsigned long long> h(nstamp);
+            HIP_CHECK(hipMemcpyAsync(h.data(), d_st, nstamp * 8, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            if (FILE* f = fopen(path, "wb")) {
+                fwrite(h.data(), 8, nstamp, f);
+                fclose(f);
+            }
+        }
         // K and V of every attended key (f32 cache) + q/k/v row + context out
         prof.attention.bytes = (double)keys * L.kv_heads * hd * 4.0 * 2.0 + (double)B * (QKVN + H) * 4.0;
         prof.attention.flops = 4.0 * keys * L.heads * hd;

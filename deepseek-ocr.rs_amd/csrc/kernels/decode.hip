@@ -408,6 +408,205 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
     }
 }
 
+// ------------------------------------------------------------------ q/k/v projection + RoPE
+// dec_gemv for the fused q/k/v rows with the rotation (rotate_half RoPE, block.rs:1403-1471) in
+// the epilogue: a wave owns the row pair (d, d + HD/2) of one head segment, so both halves of
+// the rotation meet in one lane; q and k segments are rotated at the decode position, v rows pass
+// through.  The per-row arithmetic is dec_gemv's (chunk u-major, then j), the rotation is the
+// attention kernel's formula x*cos + sign*partner*sin.  One token (M = 1).
+template <typename WT>
+__global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRopeEpi r) {
+    extern __shared__ float smem[];
+    constexpr int U = 3, XR = 2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int half = r.hd / 2;
+    const int p = blockIdx.x * 4 + wave;                 // pair index
+    const int npairs = a.N / 2;
+    const bool active = p < npairs;
+    const int pp = min(p, npairs - 1);
+    const int n0 = (pp / half) * r.hd + pp % half, n1 = n0 + half;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    XRegs<1, XR> xr;
+    xload<1, XR>(xr, a.x, a.ldx, nullptr, 1, a.K, a.norm_w);
+    const int pos = r.kv_pos[0];
+    uint4 w0[U], w1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int cc = min(u * 64 + lane, chunks - 1);
+        w0[u] = ldg_nt16(W + (long)n0 * a.ldw + (cc << 3));
+        w1[u] = ldg_nt16(W + (long)n1 * a.ldw + (cc << 3));
+    }
+    const int d = n0 % r.hd;
+    const bool rot = n0 < r.rot_rows;
+    const float c0 = rot ? r.cos[(long)pos * r.hd + d] : 1.f, s0 = rot ? r.sin[(long)pos * r.hd + d] : 0.f;
+    const float c1 = rot ? r.cos[(long)pos * r.hd + d + half] : 1.f, s1 = rot ? r.sin[(long)pos * r.hd + d + half] : 0.f;
+    xstage<1, XR>(xr, 1, a.K, a.norm_w != nullptr, a.eps, smem);
+    if (!active) return;
+    const float* xs = smem + XS_RED;
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int cc = u * 64 + lane;
+        if (cc < chunks) {
+            float f0[8], f1[8], xv[8];
+            unpack8<WT>(w0[u], f0);
+            unpack8<WT>(w1[u], f1);
+            ld_x8(xs + (cc << 3), xv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                acc0 = fmaf(xv[j], f0[j], acc0);
+                acc1 = fmaf(xv[j], f1[j], acc1);
+            }
+        }
+    }
+    float y0 = wave_sum(acc0), y1 = wave_sum(acc1);
+    if (lane == 0) {
+        y0 = y0 + (a.bias ? a.bias[n0] : 0.f);
+        y1 = y1 + (a.bias ? a.bias[n1] : 0.f);
+        if (rot) {
+            const float o0 = y0 * c0 + (-1.f * y1) * s0;
+            const float o1 = y1 * c1 + (1.f * y0) * s1;
+            y0 = o0;
+            y1 = o1;
+        }
+        a.y[n0] = y0;
+        a.y[n1] = y1;
+    }
+}
+
+bool dec_qkv_rope_ok(const DecGemvArgs& a, const DecRopeEpi& r) {
+    return a.M == 1 && r.hd % 2 == 0 && a.N % r.hd == 0 && a.K % 8 == 0 && a.K <= 64 * 3 * 8 && r.kv_pos && r.cos &&
+           r.sin;
+}
+
+void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t s) {
+    if (!dec_qkv_rope_ok(a, r)) throw std::runtime_error("EINVAL: dec_qkv_rope outside its range");
+    const size_t lds = stage_bytes(1, a.K);
+    dim3 grid((a.N / 2 + 3) / 4);
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL(dec_qkv_rope_kernel<bf16_t>, grid, dim3(256), lds, s, a, r);
+    else hipLaunchKernelGGL(dec_qkv_rope_kernel<f16_t>, grid, dim3(256), lds, s, a, r);
+}
+
+// ------------------------------------------------------------------ attention combine + o_proj
+// One token: the flash-decoding combine of every head (the split-mode records of dec_attn) runs
+// in each block's prologue — the same arithmetic as the in-kernel combine (per head: global max,
+// even / odd chunk partial sums in chunk order, (a0 + a1) / (l0 + l1)) — while the block's o_proj
+// weight rows stream; then y[j] (+)= W_o[j] . ctx (dec_gemv's per-row order).  Records: per head
+// [m[CM] | l[CM] | o[HD][CM]].  Writes ctx to ctx_out (block 0) for the tests / fallbacks.
+template <typename WT, int RW, int NCM, int EPT>
+__global__ __launch_bounds__(256) void dec_oproj_comb_kernel(DecGemvArgs a, DecCombArgs cb) {
+    constexpr int U = 3;  // K <= 1536; NCM >= chunks per head (even), EPT * 256 >= heads * hd
+    __shared__ __attribute__((aligned(16))) float xs[1536];
+    __shared__ float wts[16][NCM];  // expf(m - max) per (head, chunk)
+    __shared__ float lsum[16][NCM];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const int n0 = (blockIdx.x * 4 + wave) * RW;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    // 1. this wave's weight rows first (independent of everything in this step)
+    uint4 wq[RW][U];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int n = min(n0 + r, a.N - 1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) wq[r][u] = ldg_nt16(W + (long)n * a.ldw + (min(u * 64 + lane, chunks - 1) << 3));
+    }
+    const int pos = cb.kv_pos[0];
+    const int nc = (pos + cb.ch) / cb.ch;  // chunks holding keys 0..pos
+    const int CM = cb.cm, HD = cb.hd, heads = cb.heads;
+    // 2. every o partial this thread folds: elements e = tid + 256 i, chunks 0..NCM-1 (clamped
+    //    to the capacity; chunks >= nc get weight 0 by a select)
+    float ov[EPT][NCM];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int e = min(tid + 256 * i, heads * HD - 1);
+        const float* src = cb.part + (long)(e / HD) * (2 + HD) * CM + 2 * CM + e % HD;
+#pragma unroll
+        for (int q = 0; q < NCM; ++q) ov[i][q] = src[(long)min(q, CM - 1) * HD];
+    }
+    // 3. chunk maxima / sums -> per-head weights in LDS
+    for (int t = tid; t < heads * NCM; t += 256) {
+        const int hh = t / NCM, q = t % NCM;
+        const float* Q = cb.part + (long)hh * (2 + HD) * CM;
+        wts[hh][q] = Q[min(q, CM - 1)];
+        lsum[hh][q] = Q[CM + min(q, CM - 1)];
+    }
+    __syncthreads();
+    if (tid < heads) {
+        float mm = -INFINITY;
+        for (int q = 0; q < nc; ++q) mm = fmaxf(mm, wts[tid][q]);
+        for (int q = 0; q < NCM; ++q) wts[tid][q] = q < nc ? expf(wts[tid][q] - mm) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+        const int e = tid + 256 * i;
+        if (e < heads * HD) {
+            const int hh = e / HD;
+            float a0 = 0.f, a1 = 0.f, l0 = 0.f, l1 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NCM; q += 2) {
+                const float w0 = wts[hh][q], w1 = wts[hh][q + 1];
+                if (q < nc) { l0 += lsum[hh][q] * w0; a0 += ov[i][q] * w0; }
+                if (q + 1 < nc) { l1 += lsum[hh][q + 1] * w1; a1 += ov[i][q + 1] * w1; }
+            }
+            float at = 0.f, lt = 0.f;
+            at += a0; at += a1;
+            lt += l0; lt += l1;
+            xs[e] = at / lt;
+        }
+    }
+    __syncthreads();
+    if (cb.ctx_out && blockIdx.x == 0)
+        for (int e = tid; e < heads * HD; e += 256) cb.ctx_out[e] = xs[e];
+    // 4. the rows
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int cc = u * 64 + lane;
+            if (cc < chunks) {
+                float w8[8], xv[8];
+                unpack8<WT>(wq[r][u], w8);
+                ld_x8(xs + (cc << 3), xv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], w8[j], acc);
+            }
+        }
+        float v = wave_sum(acc);
+        const int n = n0 + r;
+        if (lane == 0 && n < a.N) {
+            v = v + (a.bias ? a.bias[n] : 0.f);
+            float* yp = a.y + n;
+            if (a.accumulate) v = *yp + v;
+            *yp = v;
+        }
+    }
+}
+
+bool dec_oproj_comb_ok(const DecGemvArgs& a, const DecCombArgs& cb) {
+    return a.M == 1 && a.K == cb.heads * cb.hd && a.K <= 1536 && a.K % 8 == 0 && cb.heads <= 16 && cb.cm <= 24 &&
+           cb.part && cb.kv_pos && cb.ch > 0;
+}
+
+void launch_dec_oproj_comb(const DecGemvArgs& a, const DecCombArgs& cb, hipStream_t s) {
+    if (!dec_oproj_comb_ok(a, cb)) throw std::runtime_error("EINVAL: dec_oproj_comb outside its range");
+    static const int rw = getenv("DSOCR_OC_RW") ? atoi(getenv("DSOCR_OC_RW")) : 1;
+#define DSOCR_OC(WTY, R, NC, E) \
+    hipLaunchKernelGGL((dec_oproj_comb_kernel<WTY, R, NC, E>), dim3((a.N + 4 * R - 1) / (4 * R)), dim3(256), 0, s, a, cb)
+#define DSOCR_OC2(WTY, NC, E) do { if (rw == 2) DSOCR_OC(WTY, 2, NC, E); else DSOCR_OC(WTY, 1, NC, E); } while (0)
+#define DSOCR_OC3(WTY) do { \
+        if (cb.cm <= 20 && a.K <= 1280) DSOCR_OC2(WTY, 20, 5); else if (cb.cm <= 20) DSOCR_OC2(WTY, 20, 6); \
+        else if (a.K <= 1280) DSOCR_OC2(WTY, 24, 5); else DSOCR_OC2(WTY, 24, 6); } while (0)
+    if (a.wdtype == WDT_BF16) DSOCR_OC3(bf16_t);
+    else DSOCR_OC3(f16_t);
+#undef DSOCR_OC3
+#undef DSOCR_OC2
+#undef DSOCR_OC
+}
+
 // ------------------------------------------------------------------ router + top-k
 // MoE router logits (E x K GEMV, norm fused) whose LAST-arriving block routes every token:
 // softmax (or sigmoid) + greedy top-k (block.rs:1254-1301) -> ids[t*topk+k], w[t*topk+k].
@@ -662,7 +861,9 @@ __device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, 
 // rows of the fused projection themselves (RMSNorm + GEMV, the same per-row arithmetic as
 // dec_gemv), hand them over through a per-head arrival counter (write-through stores, sc1
 // loads), then run the attention chunk exactly as the unfused kernel.
-template <int HD, int CH, bool EARLY, bool FUSED>
+// PREROT: the q / k rows arrive already rotated (dec_qkv_rope applied RoPE in its epilogue), so
+// q, k_new and v_new are loaded before the position and no RoPE table is read here.
+template <int HD, int CH, bool PREROT, bool FUSED>
 __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
@@ -677,6 +878,13 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     __shared__ int last_s;
     __shared__ float4 o_s[384];  // P.V partials; reused by the combine (m, l per chunk + per-group sums)
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const long sbid = ((long)b * gridDim.y + h) * gridDim.x + c;
+#define AT_STAMP(i)                                                                          \
+    if (a.stamps && threadIdx.x == 0) {                                                      \
+        if ((i) == 0) a.stamps[sbid * 8] = __builtin_amdgcn_s_memrealtime();                 \
+        a.stamps[sbid * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();                         \
+    }
+    AT_STAMP(0);
     const int k0 = c * CH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvh = h / (a.heads / a.kv_heads);
@@ -700,15 +908,22 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
             vreg[j] = *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4);
         }
     };
-    if (EARLY) issue_kv(kcap);
+    const float* row = a.qkv + (long)b * a.ld;
+    float q_pre = 0.f, k_pre = 0.f, v_pre = 0.f;
+    if (PREROT) {  // unconditional (every thread loads a valid element): one round trip with pos
+        const int td = tid & (HD - 1);
+        q_pre = row[h * HD + td];
+        k_pre = row[a.heads * HD + kvh * HD + td];
+        v_pre = row[(a.heads + a.kv_heads) * HD + kvh * HD + td];
+    }
     const int pos = a.kv_pos[b];
     const int len = pos + 1;
     if (k0 >= len) return;
     const int kn = min(CH, len - k0);
-    if (!EARLY) issue_kv(k0 + kn - 1);
+    issue_kv(k0 + kn - 1);
+    (void)kcap;
     const bool own = pos >= k0 && pos < k0 + CH;
     const int nc = (len + CH - 1) / CH;
-    const float* row = a.qkv + (long)b * a.ld;
     if (FUSED) qkv_rows_for_head<HD>(a, b, h, c, nc, smem);
     // 2. RoPE inputs
     const float* krow = row + a.heads * HD + kvh * HD;
@@ -717,7 +932,19 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         return FUSED ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
     };
     float qx = 0.f, qr = 0.f, kx = 0.f, kr = 0.f, vx = 0.f, cs = 1.f, sn = 0.f, sg = 0.f;
-    if (tid < HD) {
+    if (PREROT) {
+        if (tid < HD) {
+            qs[tid] = q_pre;
+            if (own) {
+                knew[tid] = k_pre;
+                vnew[tid] = v_pre;
+                if (h == kvh * (a.heads / a.kv_heads)) {  // one writer per kv head
+                    Kc[(long)pos * HD + tid] = k_pre;
+                    Vc[(long)pos * HD + tid] = v_pre;
+                }
+            }
+        }
+    } else if (tid < HD) {
         int ix = tid, ir = tid;
         if (tid < a.rope_dim) {
             const int half = a.rope_dim / 2;
@@ -737,7 +964,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         }
     }
     // 3. rotated q (and the new k, v in the owning chunk): x*cos + sign*partner*sin
-    if (tid < HD) {
+    if (!PREROT && tid < HD) {
         qs[tid] = qx * cs + (sg * qr) * sn;
         if (own) {
             const float kv = kx * cs + (sg * kr) * sn;
@@ -750,6 +977,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         }
     }
     __syncthreads();
+    AT_STAMP(1);
     // 4. scores: LPK lanes per key, wave w owns keys w*CH/4 .. (w+1)*CH/4 - 1
     {
         float acc = 0.f;
@@ -782,6 +1010,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         if (tid == 0) red[4] = l;
     }
     __syncthreads();
+    AT_STAMP(2);
     // 5. P.V over this thread's KPG keys
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -800,6 +1029,25 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     }
     o_s[tid] = o;
     __syncthreads();
+    if (a.split) {
+        // split mode: no in-kernel combine; per (page, head) [m[CM] | l[CM] | o[CM][HD]] for the o_proj
+        // kernel's combine prologue (next launch: plain stores; o rows coalesce along d)
+        const int CM = (a.max_len + CH - 1) / CH;
+        float* Q = a.part + ((long)b * a.heads + h) * (2 + HD) * CM;
+        if (tid < DG) {
+            float4 t = o_s[tid];
+            for (int g = 1; g < KG; ++g) {
+                const float4 u = o_s[g * DG + tid];
+                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+            }
+            *reinterpret_cast<float4*>(Q + 2 * CM + (long)c * HD + tid * 4) = t;
+        }
+        if (tid == 0) {
+            Q[c] = m;
+            Q[CM + c] = red[4];
+        }
+        return;
+    }
     // partial record of chunk c: [m, l, -, -, o[HD]] (16-byte aligned), stored WRITE-THROUGH (sc1)
     // so the hand-off needs no L2-writeback release fence (cdna_hip_programming.md Guideline 16 R1)
     constexpr int PR = HD + 4;
@@ -840,6 +1088,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         last_s = last;
     }
     __syncthreads();
+    AT_STAMP(3);
     if (!last_s) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
     auto ld1 = [&](int idx) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, idx * 4, 0, 16)); };
@@ -850,21 +1099,45 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     float* ls = ms + 512;
     float* accp = ms + 1024;
     float* lp = ms + 1280;
-    for (int cc = tid; cc < nc; cc += 256) {
-        ms[cc] = ld1(cc * PR);
-        ls[cc] = ld1(cc * PR + 1);
-    }
-    __syncthreads();
-    float mm = -INFINITY;
-    for (int cc = 0; cc < nc; ++cc) mm = fmaxf(mm, ms[cc]);
     constexpr int KS = 256 / HD;
     const int dim = tid % HD, grp = tid / HD;
     float l = 0.f, acc = 0.f;
+    constexpr int NJ = 12;  // o partials per thread held in registers (nc <= KS * NJ)
+    if (nc <= KS * NJ && nc <= 256) {
+        // ONE round trip: (m, l) of chunk tid and this thread's o partials (clamped indices,
+        // weight 0 past nc by a select) are all in flight together
+        float ov[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) ov[j] = ld1(min(grp + KS * j, nc - 1) * PR + 4 + dim);
+        const int tc = min(tid, nc - 1);
+        const float mt = ld1(tc * PR), lt0 = ld1(tc * PR + 1);
+        if (tid < nc) { ms[tid] = mt; ls[tid] = lt0; }
+        __syncthreads();
+        float mm = -INFINITY;
+        for (int cc = 0; cc < nc; ++cc) mm = fmaxf(mm, ms[cc]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int cc = grp + KS * j;
+            if (cc < nc) {
+                const float w = expf(ms[cc] - mm);
+                l += ls[cc] * w;
+                acc += ov[j] * w;
+            }
+        }
+    } else {
+        for (int cc = tid; cc < nc; cc += 256) {
+            ms[cc] = ld1(cc * PR);
+            ls[cc] = ld1(cc * PR + 1);
+        }
+        __syncthreads();
+        float mm = -INFINITY;
+        for (int cc = 0; cc < nc; ++cc) mm = fmaxf(mm, ms[cc]);
 #pragma unroll 4
-    for (int cc = grp; cc < nc; cc += KS) {
-        const float w = expf(ms[cc] - mm);
-        l += ls[cc] * w;
-        acc += ld1(cc * PR + 4 + dim) * w;
+        for (int cc = grp; cc < nc; cc += KS) {
+            const float w = expf(ms[cc] - mm);
+            l += ls[cc] * w;
+            acc += ld1(cc * PR + 4 + dim) * w;
+        }
     }
     accp[grp * HD + dim] = acc;
     lp[grp * HD + dim] = l;
@@ -875,11 +1148,13 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         for (int g = 0; g < KS; ++g) { at += accp[g * HD + tid]; lt += lp[g * HD + tid]; }
         a.o[(long)b * a.o_ld + (long)h * HD + tid] = at / lt;
     }
+    AT_STAMP(4);
+#undef AT_STAMP
 }
 
-template <int HD, int CH, bool EARLY>
+template <int HD, int CH, bool PREROT>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
-    attn_body<HD, CH, EARLY, false>(a, nullptr);
+    attn_body<HD, CH, PREROT, false>(a, nullptr);
 }
 
 template <int HD, int CH>
@@ -918,12 +1193,11 @@ void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     if (a.hd != 128 && a.hd != 64 && a.hd != 32) throw std::runtime_error("EINVAL: decode attention supports head_dim 32 / 64 / 128");
     const int chunks = (a.max_len + ch - 1) / ch;
     dim3 g1(chunks, a.heads, a.B);
-    const char* ee = getenv("DSOCR_ATT_EARLY");
-    const bool early = ee && atoi(ee) != 0;
-#define DSOCR_DA(HDV, CHV)                                                                         \
-    do {                                                                                            \
-        if (early) hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, true>), g1, dim3(256), 0, s, a);  \
-        else hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, false>), g1, dim3(256), 0, s, a);       \
+    const bool prerot = a.prerot != 0;
+#define DSOCR_DA(HDV, CHV)                                                                          \
+    do {                                                                                             \
+        if (prerot) hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, true>), g1, dim3(256), 0, s, a);  \
+        else hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, false>), g1, dim3(256), 0, s, a);        \
     } while (0)
     if (ch == 64) {
         if (a.hd == 128) DSOCR_DA(128, 64); else if (a.hd == 64) DSOCR_DA(64, 64); else DSOCR_DA(32, 64);
@@ -1799,6 +2073,96 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
             hout[i] = hv;
         }
     }
+}
+
+// Decode down + combine + residual for one token (T = 1), split-K over the block's 4 waves:
+// the K axis [topk routed h rows (I each, slot order, w_k already folded) | shared h (Is)] is
+// cut in 4 contiguous chunk ranges, wave w owns one for the block's RPB output rows, its h
+// values come straight from L2 into registers (no block barrier before the FMAs); the 4 wave
+// partials meet once in LDS and x[j] += (p0 + p1) + (p2 + p3).
+template <typename WT, int RPB>
+__global__ __launch_bounds__(256) void moe_down_mix_kernel(MoeDec2Args a) {
+    __shared__ float part[4][RPB];
+    constexpr int U = 4;  // chunks per lane: (topk * I + Is) / 8 / 4 waves <= 256
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int j0 = blockIdx.x * RPB;
+    const int cpi = a.I >> 3, cps = a.sWd ? (a.Is >> 3) : 0;
+    const int nr = a.topk * cpi, nch = nr + cps;
+    const int per = (nch + 3) / 4;
+    const int c0 = wave * per, c1 = min(nch, c0 + per);
+    // 1. h of this wave's chunks (independent of the picks)
+    f32x4 hv[U][2];
+    int seg[U], off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int g = min(c0 + u * 64 + lane, nch - 1);
+        const bool rt = g < nr;
+        seg[u] = rt ? g / cpi : -1;
+        off[u] = (rt ? g % cpi : g - nr) << 3;
+        const float* src = rt ? a.h + (long)seg[u] * a.I + off[u] : a.hs + off[u];
+        hv[u][0] = *reinterpret_cast<const f32x4*>(src);
+        hv[u][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+    // 2. the picked experts' down rows (+ shared) for RPB output rows
+    uint4 q[RPB][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = a.ids[max(seg[u], 0)];  // (shared chunks ignore it)
+#pragma unroll
+        for (int r = 0; r < RPB; ++r) {
+            const int j = min(j0 + r, a.Hout - 1);
+            const WT* W = seg[u] >= 0 ? reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + j) * a.I + off[u]
+                                      : reinterpret_cast<const WT*>(a.sWd) + (long)j * a.Is + off[u];
+            q[r][u] = ldg_nt16(W);
+        }
+    }
+    float acc[RPB];
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (c0 + u * 64 + lane < c1) {
+            const float hx[8] = {hv[u][0][0], hv[u][0][1], hv[u][0][2], hv[u][0][3],
+                                 hv[u][1][0], hv[u][1][1], hv[u][1][2], hv[u][1][3]};
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) {
+                float w8[8];
+                unpack8<WT>(q[r][u], w8);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[r] = fmaf(hx[k], w8[k], acc[r]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+        const float v = wave_sum(acc[r]);
+        if (lane == 0) part[wave][r] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < RPB && j0 + threadIdx.x < a.Hout) {
+        const int r = threadIdx.x;
+        const float v = (part[0][r] + part[1][r]) + (part[2][r] + part[3][r]);
+        float* xp = a.out + j0 + r;
+        *xp = *xp + v;
+    }
+}
+
+bool moe_down_mix_ok(const MoeDec2Args& a) {
+    const int nch = a.topk * (a.I >> 3) + (a.sWd ? (a.Is >> 3) : 0);
+    return a.slot_mode && a.T == 1 && !a.apos && a.I % 8 == 0 && (!a.sWd || a.Is % 8 == 0) && (nch + 3) / 4 <= 256 &&
+           a.ids;
+}
+
+void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s) {
+    if (!moe_down_mix_ok(a)) throw std::runtime_error("EINVAL: moe_down_mix outside its range");
+    static const int rpb = getenv("DSOCR_DN_RPB") ? atoi(getenv("DSOCR_DN_RPB")) : 2;  // 2: measured best
+#define DSOCR_DM(WTY, R) hipLaunchKernelGGL((moe_down_mix_kernel<WTY, R>), dim3((a.Hout + R - 1) / R), dim3(256), 0, s, a)
+    if (a.wdtype == WDT_BF16) {
+        if (rpb == 4) DSOCR_DM(bf16_t, 4); else if (rpb == 1) DSOCR_DM(bf16_t, 1); else DSOCR_DM(bf16_t, 2);
+    } else {
+        if (rpb == 4) DSOCR_DM(f16_t, 4); else if (rpb == 1) DSOCR_DM(f16_t, 1); else DSOCR_DM(f16_t, 2);
+    }
+#undef DSOCR_DM
 }
 
 bool moe_gateup_mix_ok(const MoeDec2Args& a) {

@@ -152,8 +152,29 @@ struct DecAttn2Args {
     const float* x = nullptr; long ldx = 0; const float* norm_w = nullptr; float eps = 0.f; int K = 0;
     const void* Wqkv = nullptr; int wdtype = WDT_F16; const float* qkv_bias = nullptr;
     int* qkv_cnt = nullptr; int* err = nullptr;
+    unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
+    int prerot = 0;                        // q / k rows already rotated (dec_qkv_rope)
+    int split = 0;                         // no in-kernel combine: dim-major records for dec_oproj_comb
 };
+// Attention combine (split-mode records of dec_attn, one token) fused into the o_proj GEMV.
+struct DecCombArgs {
+    const float* part = nullptr;   // [heads][(2 + hd) * cm] records
+    const int* kv_pos = nullptr;
+    int heads = 0, hd = 0, cm = 0, ch = 64;  // cm = chunk capacity per head, ch = keys per chunk
+    float* ctx_out = nullptr;      // optional: the combined context row (block 0 writes it)
+};
+bool dec_oproj_comb_ok(const DecGemvArgs& a, const DecCombArgs& cb);
+void launch_dec_oproj_comb(const DecGemvArgs& a, const DecCombArgs& cb, hipStream_t s);
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
+// q/k/v projection of one token with RoPE applied in the epilogue (rows < rot_rows rotated at
+// position kv_pos[0]; table layout [pos][hd], rope on the full head dim, rotate_half pairing).
+struct DecRopeEpi {
+    const int* kv_pos = nullptr;
+    const float* cos = nullptr; const float* sin = nullptr;
+    int hd = 0, rot_rows = 0;
+};
+bool dec_qkv_rope_ok(const DecGemvArgs& a, const DecRopeEpi& r);
+void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t s);
 bool dec_qkv_attn_ok(const DecAttn2Args& a);
 void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
@@ -204,6 +225,9 @@ bool moe_fused_ok(const MoeDec2Args& a);
 // the router kernel wrote (xn).
 bool moe_gateup_mix_ok(const MoeDec2Args& a);
 void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s);
+// Decode down + combine + residual for one token: split-K over each block's waves.
+bool moe_down_mix_ok(const MoeDec2Args& a);
+void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_fused(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
