@@ -400,6 +400,20 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
                                                : upf(std::vector<float>(cfg_.proj_out, 0.f));
     separator_ = vecf("model.view_seperator", cfg_.proj_out);
 
+    // the split-plane GEMM's tripled weights [W | W | W] (bf16 vision linears; ~1.2 GB of HBM)
+    auto triple = [&](Lin& l) {
+        if (l.wdt != WDT_BF16 || l.K % 64) return;
+        l.W3 = dev_alloc((size_t)l.N * 3 * l.K * 2);
+        for (int p = 0; p < 3; ++p)
+            HIP_CHECK(hipMemcpy2D((char*)l.W3 + (size_t)p * l.K * 2, (size_t)3 * l.K * 2, l.W, (size_t)l.K * 2,
+                                  (size_t)l.K * 2, l.N, hipMemcpyDeviceToDevice));
+    };
+    triple(sam_.patch);
+    for (auto& blk : sam_.blocks) { triple(blk.qkv); triple(blk.proj); triple(blk.fc1); triple(blk.fc2); }
+    triple(sam_.neck0); triple(sam_.neck2); triple(sam_.net2); triple(sam_.net3);
+    for (auto& cl : clip_.layers) { triple(cl.qkv); triple(cl.out); triple(cl.fc1); triple(cl.fc2); }
+    triple(proj_);
+
     // ---------------- language model (transformer/weights.rs:444-606)
     const LangConfig& L = cfg_.lang;
     {
@@ -454,8 +468,19 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
                 d.s_d = lin(lp + "mlp.shared_experts.down_proj", H, Is, true);
             }
         }
+        // prefill GEMM forms of the decoder linears (the decode path keeps reading W)
+        for (Lin* l : {&d.qkv, &d.o, &d.gu, &d.down, &d.router, &d.s_gu, &d.s_d}) {
+            if (!l->W || l->K % 64) continue;
+            if (l->wdt == WDT_F16) {
+                l->W5 = dev_alloc((size_t)l->N * 5 * l->K * 2);
+                launch_make_w5(l->W, l->N, l->K, l->W5, nullptr);
+            } else {
+                triple(*l);
+            }
+        }
         layers_.push_back(d);
     }
+    HIP_CHECK(hipDeviceSynchronize());
     final_norm_ = vecf("model.norm.weight", H);  // f32 copy (model/mod.rs:1008-1014)
     lm_head_ = lin("lm_head", L.vocab, H, false);
 }
@@ -468,6 +493,26 @@ void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int 
         a.M = M; a.N = l.N; a.K = l.K; a.x = x; a.ldx = ldx; a.W = l.W; a.ldw = l.K; a.wdtype = l.wdt;
         a.bias = l.b; a.y = y; a.ldy = ldy; a.act = act; a.accumulate = accumulate;
         launch_dec_gemv(a, stream_);
+    } else if (l.W5 && ldx % 4 == 0 && !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
+        // f16 weights: [lo | mid | mid | hi | hi] planes against W5, one bf16 NT GEMM over K5 = 5K
+        void* planes = ws("g_planes", (size_t)M * 5 * l.K * 2);
+        launch_split5_rows(x, ldx, M, l.K, planes, 5L * l.K, stream_);
+        GemmBf16Args g;
+        g.M = M; g.N = l.N; g.K = 5 * l.K; g.A = planes; g.lda = 5L * l.K; g.W = l.W5; g.ldw = 5L * l.K;
+        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
+        g.splits = gemm_bf16_splits(M, l.N, 5 * l.K);
+        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
+        launch_gemm_bf16(g, stream_);
+    } else if (l.W3 && ldx % 4 == 0 && !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
+        // f32 rows -> [lo | mid | hi] bf16 planes, then one bf16 NT GEMM over K3 = 3K
+        void* planes = ws("g_planes", (size_t)M * 3 * l.K * 2);
+        launch_split3_rows(x, ldx, nullptr, M, l.K, planes, 3L * l.K, stream_);
+        GemmBf16Args g;
+        g.M = M; g.N = l.N; g.K = 3 * l.K; g.A = planes; g.lda = 3L * l.K; g.W = l.W3; g.ldw = 3L * l.K;
+        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
+        g.splits = gemm_bf16_splits(M, l.N, 3 * l.K);
+        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
+        launch_gemm_bf16(g, stream_);
     } else {
         GemmArgs g;
         g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.wdtype = l.wdt;

@@ -26,6 +26,8 @@ namespace dsocr {
 
 struct Lin {
     void* W = nullptr;
+    void* W3 = nullptr;  // vision (bf16) linears: [W | W | W] along K for the split-plane GEMM
+    void* W5 = nullptr;  // decoder (f16) prefill linears: [w_hi | w_lo | w_hi | w_lo | w_hi] bf16
     int wdt = WDT_BF16;
     int N = 0, K = 0;
     float* b = nullptr;

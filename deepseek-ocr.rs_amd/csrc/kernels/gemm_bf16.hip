@@ -1,0 +1,290 @@
+// bf16 x bf16 -> f32 GEMM on the gfx950 matrix cores for the f32-exact split formulation of the
+// vision linears (sam.rs:656-701 linear_forward, clip.rs:418-447 apply_linear, model/mod.rs:392-444
+// projector): every f32 activation row is split exactly into three bf16 planes
+// a = lo + mid + hi (split3_rows_kernel; RNE at each step, residuals exact by Sterbenz) laid out
+// [lo | mid | hi] along K, and the bf16 weight is tripled [W | W | W] at load, so
+//     A . W^T = A3 . W3^T   with K3 = 3 K,
+// a plain NT GEMM whose bf16 x bf16 products are exact in the f32 accumulator (the small planes
+// accumulate first).  Same result as f32 matmul up to summation order.
+//
+// Kernel: 128 x 128 x 64 tiles, 256 threads = 4 waves as 2 x 2 of 64 x 64 (2 x 2 MFMA 32x32x16),
+// two LDS stages filled by 16-byte global_load_lds (lane-linear LDS image, XOR-swizzled 16-byte
+// chunks via the SOURCE address so the fragment ds_read_b128s are conflict-free), counted vmcnt +
+// raw s_barrier (cdna_hip_programming.md §5, "Pipelining across barriers"), XCD-aware tile order.
+#include <cstdint>
+#include <stdexcept>
+
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+typedef __bf16 bf16x8_v __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int TB_M = 128, TB_N = 128, TB_K = 64;
+constexpr int TB_STAGE = (TB_M + TB_N) * TB_K;  // bf16 elements per stage
+
+// 128 rows x 64 bf16 (128-byte rows): wave w, instruction i fills rows (4w + i) * 8 .. + 7; lane L
+// writes LDS row R + L / 8, slot L % 8, which holds global chunk (L % 8) ^ (row & 7).
+__device__ __forceinline__ void stage_tile(const uint16_t* g, long ld, int r0, int rmax, int k0, uint16_t* lds,
+                                           int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int R = (wave * 4 + i) * 8;
+        const int r = R + (lane >> 3);
+        const int j = (lane & 7) ^ (r & 7);
+        const long row = min(r0 + r, rmax);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + row * ld + k0 + j * 8),
+                                         (lds_void*)(lds + R * TB_K), 16, 0, 0);
+    }
+}
+
+// fragment of rows r .. r + 31 (lane & 31), k chunk kc + (lane >> 5), from a swizzled tile
+__device__ __forceinline__ bf16x8_v frag(const uint16_t* lds, int r, int kc) {
+    const int c = kc ^ (r & 7);
+    return *reinterpret_cast<const bf16x8_v*>(lds + r * TB_K + c * 8);
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
+    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * TB_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware tile order (bijective; blocks b and b + 8 share an XCD): consecutive tiles of one
+    // XCD walk the N tiles of one M row band, so the A band stays in that XCD's L2
+    const int ntn = (g.N + TB_N - 1) / TB_N;
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    // split-K: wgid = tile * splits + split (a tile's K slices on one XCD, adjacent in time)
+    const int split = wgid % g.splits, tile = wgid / g.splits;
+    const int bm = tile / ntn, bn = tile % ntn;
+    const int m0 = bm * TB_M, n0 = bn * TB_N;
+    const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A);
+    const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nk_all = g.K / TB_K;
+    const int kbeg = (int)((long)nk_all * split / g.splits), kend = (int)((long)nk_all * (split + 1) / g.splits);
+    const int nk = kend - kbeg;
+    auto issue = [&](int kt) {
+        uint16_t* st = smem + (kt & 1) * TB_STAGE;
+        stage_tile(A, g.lda, m0, g.M - 1, (kbeg + kt) * TB_K, st, wave, lane);
+        stage_tile(W, g.ldw, n0, g.N - 1, (kbeg + kt) * TB_K, st + TB_M * TB_K, wave, lane);
+    };
+    if (nk > 0) issue(0);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) {
+            issue(kt + 1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage kt landed (8 DMAs of kt+1 in flight)
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const uint16_t* As = smem + (kt & 1) * TB_STAGE;
+        const uint16_t* Bs = As + TB_M * TB_K;
+#pragma unroll
+        for (int ks = 0; ks < TB_K / 16; ++ks) {
+            const int kc = ks * 2 + (lane >> 5);
+            bf16x8_v af[2], bfv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = frag(As, wm * 64 + i * 32 + (lane & 31), kc);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bfv[j] = frag(Bs, wn * 64 + j * 32 + (lane & 31), kc);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is done with this stage before it is refilled
+        asm volatile("" ::: "memory");
+    }
+    // epilogue: D layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    const int half = lane >> 5, l32 = lane & 31;
+    if (g.splits > 1) {  // raw partial sums of this K slice: [split][M][N], reduced in split order
+        float* P = g.part + (long)split * g.M * g.N;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    if (row < g.M && col < g.N) P[(long)row * g.N + col] = acc[i][j][r];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + l32;
+            if (col >= g.N) continue;
+            const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (row >= g.M) continue;
+                const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;
+                if (orow < 0) continue;
+                float v = apply_act(acc[i][j][r] + bv, g.act);
+                float* cp = g.C + orow * (long)g.ldc + col;
+                if (g.accumulate) v += *cp;
+                *cp = v;
+            }
+        }
+    }
+}
+
+// split-K reduction: C = act(sum_s P[s] + bias) (+ C), rows scattered through c_rows
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmBf16Args g) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)g.M * g.N) return;
+    const int row = (int)(i / g.N), col = (int)(i % g.N);
+    float v = 0.f;
+    for (int sp = 0; sp < g.splits; ++sp) v += g.part[(long)sp * g.M * g.N + i];
+    const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;
+    if (orow < 0) return;
+    v = apply_act(v + (g.bias ? g.bias[col] : 0.f), g.act);
+    float* cp = g.C + orow * g.ldc + col;
+    if (g.accumulate) v += *cp;
+    *cp = v;
+}
+
+int gemm_bf16_splits(int M, int N, int K) {
+    const int tiles = ((M + TB_M - 1) / TB_M) * ((N + TB_N - 1) / TB_N);
+    const int nk = K / TB_K;
+    int sp = 1;
+    // fill the chip (>= 256 blocks) while every slice keeps >= 8 K steps of 64
+    while (tiles * sp < 256 && nk / (sp * 2) >= 8) sp *= 2;
+    return sp;
+}
+
+void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
+    GemmBf16Args g = g0;
+    if (g.M <= 0 || g.N <= 0) return;
+    if (g.K % TB_K || g.lda % 8 || g.ldw % 8 || (reinterpret_cast<uintptr_t>(g.A) & 15) ||
+        (reinterpret_cast<uintptr_t>(g.W) & 15))
+        throw std::runtime_error("EINVAL: gemm_bf16 needs K % 64 == 0 and 16-byte aligned rows");
+    if (g.splits < 1 || !g.part) g.splits = 1;
+    const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);
+    hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    if (g.splits > 1) {
+        const long n = (long)g.M * g.N;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// f32 rows -> [lo | mid | hi] bf16 planes (row r of the output = input row rows ? rows[r] : r).
+// a = hi + mid + lo exactly: hi = RNE(a), mid = RNE(a - hi), lo = RNE(a - hi - mid) (the two
+// residuals are exact in f32).  One thread per 4 consecutive elements.
+__global__ __launch_bounds__(256) void split3_rows_kernel(const float* __restrict__ x, long ldx, const int* rows, int M,
+                                                          int K, uint16_t* __restrict__ out, long ldo) {
+    const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+    const int per = K >> 2;
+    if (i4 >= (long)M * per) return;
+    const int r = (int)(i4 / per), k = (int)(i4 % per) * 4;
+    const long src = rows ? (long)rows[r] : (long)r;
+    const float4 v = *reinterpret_cast<const float4*>(x + src * ldx + k);
+    const float a[4] = {v.x, v.y, v.z, v.w};
+    __bf16 h[4], m[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h[j] = (__bf16)a[j];
+        const float r1 = a[j] - (float)h[j];
+        m[j] = (__bf16)r1;
+        l[j] = (__bf16)(r1 - (float)m[j]);
+    }
+    uint16_t* o = out + (long)r * ldo + k;
+    uint2 ul, um, uh;
+    __builtin_memcpy(&ul, l, 8);
+    __builtin_memcpy(&um, m, 8);
+    __builtin_memcpy(&uh, h, 8);
+    *reinterpret_cast<uint2*>(o) = ul;
+    *reinterpret_cast<uint2*>(o + K) = um;
+    *reinterpret_cast<uint2*>(o + 2 * K) = uh;
+}
+
+// f32 rows -> [lo | mid | mid | hi | hi] bf16 planes: the activation side of the f16-weight form,
+// paired with W5 = [w_hi | w_lo | w_hi | w_lo | w_hi] (make_w5) so that A5 . W5^T holds the five
+// products lo.hi, mid.lo, mid.hi, hi.lo, hi.hi (lo.lo is below f32 rounding), as gemm_x3 does.
+__global__ __launch_bounds__(256) void split5_rows_kernel(const float* __restrict__ x, long ldx, int M, int K,
+                                                          uint16_t* __restrict__ out, long ldo) {
+    const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+    const int per = K >> 2;
+    if (i4 >= (long)M * per) return;
+    const int r = (int)(i4 / per), k = (int)(i4 % per) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(x + (long)r * ldx + k);
+    const float a[4] = {v.x, v.y, v.z, v.w};
+    __bf16 h[4], m[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h[j] = (__bf16)a[j];
+        const float r1 = a[j] - (float)h[j];
+        m[j] = (__bf16)r1;
+        l[j] = (__bf16)(r1 - (float)m[j]);
+    }
+    uint16_t* o = out + (long)r * ldo + k;
+    uint2 ul, um, uh;
+    __builtin_memcpy(&ul, l, 8);
+    __builtin_memcpy(&um, m, 8);
+    __builtin_memcpy(&uh, h, 8);
+    *reinterpret_cast<uint2*>(o) = ul;
+    *reinterpret_cast<uint2*>(o + K) = um;
+    *reinterpret_cast<uint2*>(o + 2 * K) = um;
+    *reinterpret_cast<uint2*>(o + 3 * K) = uh;
+    *reinterpret_cast<uint2*>(o + 4 * K) = uh;
+}
+
+void launch_split5_rows(const float* x, long ldx, int M, int K, void* out, long ldo, hipStream_t s) {
+    if (M <= 0) return;
+    if (K % 4 || ldx % 4 || ldo < 5L * K) throw std::runtime_error("EINVAL: split5_rows needs K % 4 == 0");
+    const long n4 = (long)M * (K / 4);
+    hipLaunchKernelGGL(split5_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, ldx, M, K,
+                       reinterpret_cast<uint16_t*>(out), ldo);
+}
+
+// f16 weight rows -> [w_hi | w_lo | w_hi | w_lo | w_hi] bf16 (w = w_hi + w_lo exactly: f16 has 11
+// significant bits)
+__global__ __launch_bounds__(256) void make_w5_kernel(const uint16_t* __restrict__ w, int N, int K,
+                                                      uint16_t* __restrict__ out) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)N * K) return;
+    const int r = (int)(i / K), k = (int)(i % K);
+    _Float16 hv;
+    __builtin_memcpy(&hv, &w[i], 2);
+    const float f = (float)hv;
+    const __bf16 hi = (__bf16)f;
+    const __bf16 lo = (__bf16)(f - (float)hi);
+    uint16_t uh, ul;
+    __builtin_memcpy(&uh, &hi, 2);
+    __builtin_memcpy(&ul, &lo, 2);
+    uint16_t* o = out + (long)r * 5 * K + k;
+    o[0] = uh; o[K] = ul; o[2 * K] = uh; o[3 * K] = ul; o[4 * K] = uh;
+}
+
+void launch_make_w5(const void* w, int N, int K, void* out, hipStream_t s) {
+    const long n = (long)N * K;
+    hipLaunchKernelGGL(make_w5_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint16_t*>(w), N, K, reinterpret_cast<uint16_t*>(out));
+}
+
+void launch_split3_rows(const float* x, long ldx, const int* rows, int M, int K, void* out, long ldo, hipStream_t s) {
+    if (M <= 0) return;
+    if (K % 4 || ldx % 4 || ldo < 3L * K) throw std::runtime_error("EINVAL: split3_rows needs K % 4 == 0");
+    const long n4 = (long)M * (K / 4);
+    hipLaunchKernelGGL(split3_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, ldx, rows, M, K,
+                       reinterpret_cast<uint16_t*>(out), ldo);
+}
+
+}  // namespace dsocr

@@ -10,6 +10,26 @@ enum WDType : int { WDT_BF16 = 0, WDT_F16 = 1 };
 enum Act : int { ACT_NONE = 0, ACT_GELU_ERF = 1, ACT_QUICK_GELU = 2, ACT_SILU = 3 };
 
 // ------------------------------------------------------------------ GEMM (gemm.hip)
+// bf16 NT GEMM C[M][N] (+)= act(A[M][K] . W[N][K]^T + bias) with f32 accumulate (gemm_bf16.hip):
+// the split-plane form of the f32 vision linears (A = [lo|mid|hi] planes, W = [W|W|W]).
+struct GemmBf16Args {
+    int M = 0, N = 0, K = 0;          // K % 64 == 0
+    const void* A = nullptr; long lda = 0;
+    const void* W = nullptr; long ldw = 0;
+    const float* bias = nullptr;
+    float* C = nullptr; long ldc = 0;
+    const int* c_rows = nullptr;      // optional row scatter for C (-1 drops the row)
+    int act = 0, accumulate = 0;
+    int splits = 1; float* part = nullptr;  // split-K: [splits][M][N] f32 partials (reduced in order)
+};
+void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
+int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)
+// f16-weight form: A5 = [lo | mid | mid | hi | hi] planes, W5 = [w_hi | w_lo | w_hi | w_lo | w_hi]
+void launch_split5_rows(const float* x, long ldx, int M, int K, void* out, long ldo, hipStream_t s);
+void launch_make_w5(const void* w, int N, int K, void* out, hipStream_t s);
+// f32 rows (optionally gathered) -> bf16 planes [lo | mid | hi] of K each (row stride ldo >= 3K)
+void launch_split3_rows(const float* x, long ldx, const int* rows, int M, int K, void* out, long ldo, hipStream_t s);
+
 struct GemmArgs {
     int M = 0, N = 0, K = 0;
     const float* A = nullptr;
