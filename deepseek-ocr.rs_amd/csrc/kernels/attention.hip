@@ -12,6 +12,8 @@
 // 2. sam_relbias: per-query rel-pos dot products q.Rh / q.Rw.
 // 3. rope_kv: rotate_half RoPE (block.rs:1403-1471) + KV-cache append (prefill rows;
 //    the decode step fuses both into dec_attn_kernel, decode.hip).
+#include <cstdlib>
+
 #include "dev_common.hpp"
 #include "kernels.hpp"
 
@@ -141,12 +143,166 @@ __global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
     }
 }
 
+// attention_fwd2: the same flash attention with the P.V product computed TRANSPOSED
+// (O^T = V^T . P^T: the accumulator's column is the lane's own query, so the online-softmax
+// rescale needs no cross-lane shuffles), the dot-product dims split as d = i + half * HD/2 so
+// every K fragment is a 16-byte LDS read, V staged transposed in LDS (16-byte reads of 4 keys),
+// K/V tile t+1 prefetched into registers while tile t is consumed (one barrier per tile), and the
+// rel-pos bias column indices of a tile computed once per tile in LDS (no per-score division).
+template <int HD>
+__global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
+    constexpr int KP = HD + 4, VP = AT_KT + 4;
+    constexpr int F4 = AT_KT * HD / 4 / 256;  // float4 per thread per operand per tile
+    __shared__ __attribute__((aligned(16))) float Ks[2][AT_KT][KP];
+    __shared__ __attribute__((aligned(16))) float Vt[2][HD][VP];
+    __shared__ int rbh[2][AT_KT], rbw[2][AT_KT];
+    const int s = blockIdx.z, h = blockIdx.y;
+    const int len = a.seq_len ? a.seq_len[s] : a.L;
+    const int qb0 = blockIdx.x * (4 * AT_Q);
+    if (qb0 >= len) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = lane >> 5, l32 = lane & 31;
+    const int kvh = h / (a.heads / a.kv_heads);
+    const long qoff = a.q.seq_off ? a.q.seq_off[s] : (long)s * a.L * a.q.row_stride;
+    const long koff = a.k.seq_off ? a.k.seq_off[s] : (long)s * a.L * a.k.row_stride;
+    const long voff = a.v.seq_off ? a.v.seq_off[s] : (long)s * a.L * a.v.row_stride;
+    const long ooff = a.o_seq_off ? a.o_seq_off[s] : (long)s * a.L * a.o_row_stride;
+    const float* Q = a.q.ptr + qoff + (long)h * a.q.head_stride;
+    const float* K = a.k.ptr + koff + (long)kvh * a.k.head_stride;
+    const float* V = a.v.ptr + voff + (long)kvh * a.v.head_stride;
+    const int q_lane = qb0 + wave * AT_Q + l32;
+    const bool q_valid = q_lane < len;
+    float qreg[HD / 2];
+    {
+        const float* qr = Q + (long)(q_valid ? q_lane : 0) * a.q.row_stride + half * (HD / 2);
+#pragma unroll
+        for (int i = 0; i < HD / 2; i += 4) {
+            const float4 v4 = *reinterpret_cast<const float4*>(qr + i);
+            qreg[i] = v4.x; qreg[i + 1] = v4.y; qreg[i + 2] = v4.z; qreg[i + 3] = v4.w;
+        }
+    }
+    const float* rb = nullptr;
+    if (a.relbias) rb = a.relbias + (((long)s * a.heads + h) * a.L + (q_valid ? q_lane : 0)) * (a.rel_h + a.rel_w);
+    int kend = len;
+    if (a.causal) kend = min(len, qb0 + 4 * AT_Q);
+    // staging: thread covers float4 f = tid + 256 j of the tile: key f / (HD/4), cols (f % (HD/4)) * 4
+    // (macros, not lambdas: a captured register array is demoted to scratch)
+    float4 rk[F4], rv[F4];
+#define AT2_GLOAD(K0)                                                                          \
+    _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
+        const int f = tid + 256 * j;                                                           \
+        const int key = min((K0) + f / (HD / 4), len - 1);                                     \
+        const int c4 = (f % (HD / 4)) * 4;                                                     \
+        rk[j] = *reinterpret_cast<const float4*>(K + (long)key * a.k.row_stride + c4);         \
+        rv[j] = *reinterpret_cast<const float4*>(V + (long)key * a.v.row_stride + c4);         \
+    }
+#define AT2_LSTORE(BUF, K0)                                                                    \
+    _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
+        const int f = tid + 256 * j;                                                           \
+        const int kr = f / (HD / 4), c4 = (f % (HD / 4)) * 4;                                  \
+        *reinterpret_cast<float4*>(&Ks[BUF][kr][c4]) = rk[j];                                  \
+        Vt[BUF][c4 + 0][kr] = rv[j].x;                                                         \
+        Vt[BUF][c4 + 1][kr] = rv[j].y;                                                         \
+        Vt[BUF][c4 + 2][kr] = rv[j].z;                                                         \
+        Vt[BUF][c4 + 3][kr] = rv[j].w;                                                         \
+    }                                                                                          \
+    if (rb && tid < AT_KT) {                                                                   \
+        const int key = (K0) + tid;                                                            \
+        rbh[BUF][tid] = key / a.rel_w;                                                         \
+        rbw[BUF][tid] = a.rel_h + key % a.rel_w;                                               \
+    }
+    f32x16 o[HD / 32];
+#pragma unroll
+    for (int t = 0; t < HD / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    AT2_GLOAD(0);
+    AT2_LSTORE(0, 0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < kend; k0 += AT_KT, buf ^= 1) {
+        AT2_GLOAD(k0 + AT_KT);  // unconditional (clamped keys): a guarded prefetch demotes rk/rv to scratch
+        // S^T = K . Q^T: lane (half, l32) feeds dims i + half*HD/2
+        f32x16 sc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+#pragma unroll
+        for (int i = 0; i < HD / 2; i += 4) {
+            const float4 k4 = *reinterpret_cast<const float4*>(&Ks[buf][l32][half * (HD / 2) + i]);
+            sc = __builtin_amdgcn_mfma_f32_32x32x2f32(k4.x, qreg[i], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x2f32(k4.y, qreg[i + 1], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x2f32(k4.z, qreg[i + 2], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x2f32(k4.w, qreg[i + 3], sc, 0, 0, 0);
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int kl = (r & 3) + 8 * (r >> 2) + 4 * half;
+            const int key = k0 + kl;
+            float v = sc[r] * a.scale;
+            if (rb) v += rb[rbh[buf][kl]] + rb[rbw[buf][kl]];
+            if (key >= len || (a.causal && key > q_lane)) v = -INFINITY;
+            sc[r] = v;
+            tmax = fmaxf(tmax, v);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = (m_new == -INFINITY) ? 0.f : expf(sc[r] - m_new);
+            sc[r] = p;
+            psum += p;
+        }
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+#pragma unroll
+        for (int t = 0; t < HD / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+        // O^T += V^T . P^T, keys in the accumulator's permuted order kappa(st, half)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int kb = 8 * g4 + 4 * half;
+#pragma unroll
+            for (int t = 0; t < HD / 32; ++t) {
+                const float4 v4 = *reinterpret_cast<const float4*>(&Vt[buf][t * 32 + l32][kb]);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, sc[4 * g4 + 0], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, sc[4 * g4 + 1], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, sc[4 * g4 + 2], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, sc[4 * g4 + 3], o[t], 0, 0, 0);
+            }
+        }
+        AT2_LSTORE(buf ^ 1, k0 + AT_KT);
+        __syncthreads();
+    }
+    // O^T accumulator: row = d (within t), column = this lane's query
+    if (q_valid) {
+        float* op = a.o + ooff + (long)q_lane * a.o_row_stride + (long)h * a.o_head_stride;
+#pragma unroll
+        for (int t = 0; t < HD / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) op[t * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = o[t][r] / l_run;
+    }
+#undef AT2_GLOAD
+#undef AT2_LSTORE
+}
+
 void launch_attention(const AttnArgs& a, hipStream_t s) {
     int maxlen = a.L;
     dim3 grid((maxlen + 4 * AT_Q - 1) / (4 * AT_Q), a.heads, a.n_seq);
     if (grid.x == 0 || a.n_seq == 0) return;
     AttnArgs b = a;
     if (b.kv_heads == 0) b.kv_heads = b.heads;
+    static const bool v1 = getenv("DSOCR_ATTN_V1") && atoi(getenv("DSOCR_ATTN_V1")) != 0;
+    if (!v1 && (a.hd == 64 || a.hd == 128)) {
+        if (a.hd == 64) hipLaunchKernelGGL(attention_fwd2_kernel<64>, grid, dim3(256), 0, s, b);
+        else hipLaunchKernelGGL(attention_fwd2_kernel<128>, grid, dim3(256), 0, s, b);
+        return;
+    }
     if (a.hd == 64) hipLaunchKernelGGL(attention_fwd_kernel<64>, grid, dim3(256), 0, s, b);
     else if (a.hd == 128) hipLaunchKernelGGL(attention_fwd_kernel<128>, grid, dim3(256), 0, s, b);
     else if (a.hd == 32) hipLaunchKernelGGL(attention_fwd_kernel<32>, grid, dim3(256), 0, s, b);
