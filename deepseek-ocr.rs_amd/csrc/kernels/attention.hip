@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
 // every K fragment is a 16-byte LDS read, V staged transposed in LDS (16-byte reads of 4 keys),
 // K/V tile t+1 prefetched into registers while tile t is consumed (one barrier per tile), and the
 // rel-pos bias column indices of a tile computed once per tile in LDS (no per-score division).
-template <int HD>
+template <int HD, bool REL>
 __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
     constexpr int KP = HD + 4, VP = AT_KT + 4;
     constexpr int F4 = AT_KT * HD / 4 / 256;  // float4 per thread per operand per tile
@@ -181,8 +181,19 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
             qreg[i] = v4.x; qreg[i + 1] = v4.y; qreg[i + 2] = v4.z; qreg[i + 3] = v4.w;
         }
     }
+    // REL: the block's 128 query rows of the rel-pos table staged once into LDS (row pitch R + 1:
+    // the lanes of a wave read 32 different rows at one column without bank conflicts)
+    extern __shared__ float rbs[];
+    const int R = a.rel_h + a.rel_w, RP = R + 1;
     const float* rb = nullptr;
-    if (a.relbias) rb = a.relbias + (((long)s * a.heads + h) * a.L + (q_valid ? q_lane : 0)) * (a.rel_h + a.rel_w);
+    if (REL) {
+        const float* tab = a.relbias + (((long)s * a.heads + h) * a.L) * R;
+        for (int i = tid; i < 4 * AT_Q * R; i += 256) {
+            const int ql = i / R, j = i % R;
+            rbs[ql * RP + j] = tab[(long)min(qb0 + ql, len - 1) * R + j];
+        }
+        rb = rbs + (wave * AT_Q + l32) * RP;
+    }
     int kend = len;
     if (a.causal) kend = min(len, qb0 + 4 * AT_Q);
     // staging: thread covers float4 f = tid + 256 j of the tile: key f / (HD/4), cols (f % (HD/4)) * 4
@@ -206,7 +217,7 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
         Vt[BUF][c4 + 2][kr] = rv[j].z;                                                         \
         Vt[BUF][c4 + 3][kr] = rv[j].w;                                                         \
     }                                                                                          \
-    if (rb && tid < AT_KT) {                                                                   \
+    if (REL && tid < AT_KT) {                                                                  \
         const int key = (K0) + tid;                                                            \
         rbh[BUF][tid] = key / a.rel_w;                                                         \
         rbw[BUF][tid] = a.rel_h + key % a.rel_w;                                               \
@@ -235,13 +246,23 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
             sc = __builtin_amdgcn_mfma_f32_32x32x2f32(k4.z, qreg[i + 2], sc, 0, 0, 0);
             sc = __builtin_amdgcn_mfma_f32_32x32x2f32(k4.w, qreg[i + 3], sc, 0, 0, 0);
         }
+        // rel-pos bias: every table load of the tile issued together (REL is a template flag:
+        // a runtime `if (rb)` per score became 16 exec-masked branches with a vmcnt(0) each)
+        float bias[16];
+        if (REL) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int kl = (r & 3) + 8 * (r >> 2) + 4 * half;
+                bias[r] = rb[rbh[buf][kl]] + rb[rbw[buf][kl]];
+            }
+        }
         float tmax = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int kl = (r & 3) + 8 * (r >> 2) + 4 * half;
             const int key = k0 + kl;
             float v = sc[r] * a.scale;
-            if (rb) v += rb[rbh[buf][kl]] + rb[rbw[buf][kl]];
+            if (REL) v += bias[r];
             if (key >= len || (a.causal && key > q_lane)) v = -INFINITY;
             sc[r] = v;
             tmax = fmaxf(tmax, v);
@@ -299,8 +320,23 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     if (b.kv_heads == 0) b.kv_heads = b.heads;
     static const bool v1 = getenv("DSOCR_ATTN_V1") && atoi(getenv("DSOCR_ATTN_V1")) != 0;
     if (!v1 && (a.hd == 64 || a.hd == 128)) {
-        if (a.hd == 64) hipLaunchKernelGGL(attention_fwd2_kernel<64>, grid, dim3(256), 0, s, b);
-        else hipLaunchKernelGGL(attention_fwd2_kernel<128>, grid, dim3(256), 0, s, b);
+        const bool rel = b.relbias != nullptr;
+        const size_t lds = rel ? (size_t)4 * AT_Q * (b.rel_h + b.rel_w + 1) * 4 : 0;
+        static bool attr = false;
+        if (!attr) {  // dynamic LDS beyond 64 KB (the global SAM table: 128 rows x 129 floats)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_fwd2_kernel<64, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_fwd2_kernel<128, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+            attr = true;
+        }
+        if (a.hd == 64) {
+            if (rel) hipLaunchKernelGGL((attention_fwd2_kernel<64, true>), grid, dim3(256), lds, s, b);
+            else hipLaunchKernelGGL((attention_fwd2_kernel<64, false>), grid, dim3(256), 0, s, b);
+        } else {
+            if (rel) hipLaunchKernelGGL((attention_fwd2_kernel<128, true>), grid, dim3(256), lds, s, b);
+            else hipLaunchKernelGGL((attention_fwd2_kernel<128, false>), grid, dim3(256), 0, s, b);
+        }
         return;
     }
     if (a.hd == 64) hipLaunchKernelGGL(attention_fwd_kernel<64>, grid, dim3(256), 0, s, b);
@@ -344,10 +380,60 @@ __global__ __launch_bounds__(256) void sam_relbias_kernel(const float* q, long q
     }
 }
 
+// Thread per query (one head per block row): the query row lives in registers, the two rel-pos
+// tables of the head dim in LDS (row pitch hd + 1: lanes reading different rows of one column do
+// not collide on a bank), the R outputs of the query written contiguously.  Same dot-product order
+// as sam_relbias_kernel (d ascending, one fmaf chain).
+template <int HD>
+__global__ __launch_bounds__(256) void sam_relbias2_kernel(const float* q, long q_rs, int n_seq, int gh, int gw,
+                                                           int heads, const float* Rh, const float* Rw, float* out) {
+    extern __shared__ float tabs[];
+    constexpr int P = HD + 1;
+    const int nh = 2 * gh - 1, nw = 2 * gw - 1;
+    float* th = tabs;
+    float* tw = tabs + nh * P;
+    for (int i = threadIdx.x; i < nh * HD; i += 256) th[(i / HD) * P + i % HD] = Rh[i];
+    for (int i = threadIdx.x; i < nw * HD; i += 256) tw[(i / HD) * P + i % HD] = Rw[i];
+    __syncthreads();
+    const int L = gh * gw, R = gh + gw;
+    const int sh = blockIdx.y, h = sh % heads, s = sh / heads;
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    if (qi >= L) return;
+    float qr[HD];
+    const float* qp = q + ((long)s * L + qi) * q_rs + (long)h * HD;
+#pragma unroll
+    for (int d = 0; d < HD; d += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(qp + d);
+        qr[d] = v.x; qr[d + 1] = v.y; qr[d + 2] = v.z; qr[d + 3] = v.w;
+    }
+    const int qh = qi / gw, qw = qi % gw;
+    float* o = out + (((long)s * heads + h) * L + qi) * R;
+    for (int j = 0; j < R; ++j) {
+        const float* rr = j < gh ? th + (qh - j + gh - 1) * P : tw + (qw - (j - gh) + gw - 1) * P;
+        float acc = 0.f;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) acc = fmaf(qr[d], rr[d], acc);
+        o[j] = acc;
+    }
+}
+
 void launch_sam_relbias(const float* q, long q_row_stride, int n_seq, int gh, int gw, int heads, int hd,
                         const float* Rh, const float* Rw, float* out, hipStream_t s) {
     long total = (long)n_seq * heads * gh * gw * (gh + gw);
     if (total == 0) return;
+    const size_t lds = (size_t)((2 * gh - 1) + (2 * gw - 1)) * (hd + 1) * 4;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sam_relbias2_kernel<64>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr = true;
+    }
+    if (hd == 64 && lds <= 96 * 1024 && !(getenv("DSOCR_RELBIAS_V1") && atoi(getenv("DSOCR_RELBIAS_V1")))) {
+        dim3 grid((gh * gw + 255) / 256, n_seq * heads);
+        hipLaunchKernelGGL(sam_relbias2_kernel<64>, grid, dim3(256), lds, s, q, q_row_stride, n_seq, gh, gw, heads, Rh,
+                           Rw, out);
+        return;
+    }
     long blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(sam_relbias_kernel, dim3((unsigned)blocks), dim3(256), 0, s, q, q_row_stride, n_seq, gh, gw,
