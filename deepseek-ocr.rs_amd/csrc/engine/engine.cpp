@@ -1428,6 +1428,18 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
         body(0);  // warm (code objects, TLB) and every workspace allocated before capture
+        if (getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0) {
+            // eager (profiler runs: rocprofv3 kernel tracing of graph capture is unreliable here)
+            HIP_CHECK(hipEventRecord(e0, st));
+            for (int i = 0; i < n; ++i) body(i);
+            HIP_CHECK(hipEventRecord(e1, st));
+            HIP_CHECK(hipEventSynchronize(e1));
+            kp.avg_us = 1000.0 * ms_between(e0, e1) / n;
+            kp.launches = n;
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            return;
+        }
         hipGraph_t graph = nullptr;
         hipGraphExec_t gexec = nullptr;
         capturing_ = true;
@@ -1616,7 +1628,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             prof.router.flops = 2.0 * B * (double)L.n_routed * H;
         }
     }
-    {
+    if (!(getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0)) {
         // every decoder layer of one step as one hipGraph (what the decode loop replays, minus
         // lm_head and selection); the residual stream is restored at the head of each replay and
         // the KV slot written is the next free position (past every generated token)
