@@ -483,6 +483,14 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
     HIP_CHECK(hipDeviceSynchronize());
     final_norm_ = vecf("model.norm.weight", H);  // f32 copy (model/mod.rs:1008-1014)
     lm_head_ = lin("lm_head", L.vocab, H, false);
+    if (lm_head_.wdt == WDT_BF16 && H % 16 == 0 && H <= 1536) {
+        // int8 screening copy of the lm_head (per-row scale + rigorous error bound), lmhead.hip
+        lmq_ = dev_alloc((size_t)L.vocab * H);
+        lmq_scale_ = (float*)dev_alloc((size_t)L.vocab * 4);
+        lmq_bound_ = (float*)dev_alloc((size_t)L.vocab * 4);
+        launch_lmhead_quantize(lm_head_.W, L.vocab, H, lmq_, lmq_scale_, lmq_bound_, nullptr);
+        HIP_CHECK(hipDeviceSynchronize());
+    }
 }
 
 // ============================================================================ compute helpers
@@ -1026,12 +1034,55 @@ void Engine::decode_step(int B, int Lmax) {
     }
 }
 
+// workspaces of the screened head (allocated before a graph capture)
+void Engine::reserve_head_ws(int B) {
+    if (!lmq_ || B > 2) return;
+    const LangConfig& L = cfg_.lang;
+    int nblk = 0;
+    long slot = 0;
+    lmhead_q8_grid(L.vocab, L.hidden, B, &nblk, &slot);
+    wsi("s_blkcnt", (size_t)B * nblk);
+    wsf("s_blkt", (size_t)B * nblk);
+    wsi("s_cand", (size_t)B * nblk * slot);
+    wsf("s_candhi", (size_t)B * nblk * slot);
+    wsf("s_lmxn", (size_t)B * L.hidden);
+}
+
+// screened selection applies (lmhead.hip): int8 copy present, B <= 2, no repetition penalty
+// (DSOCR_SCREEN=0 forces the exact lm_head; read per generate call)
+bool Engine::screen_applies(int B, float rep_penalty) const {
+    if (getenv("DSOCR_SCREEN") && atoi(getenv("DSOCR_SCREEN")) == 0) return false;
+    const bool pen = rep_penalty > 0.f && fabsf(rep_penalty - 1.0f) > 1.1920929e-07f;
+    return lmq_ && B <= 2 && !pen;
+}
+
 // final norm + lm_head + greedy selection + step bookkeeping for the B decode rows in s_x
 void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
     const LangConfig& L = cfg_.lang;
     hipStream_t st = stream_;
     const int H = L.hidden;
     float* SX = wsf("s_x", (size_t)B * H);
+    if (sa.ban_out) {
+        // screened selection: int8 lm_head intervals + running threshold, exact rescoring of the
+        // few kept rows — the exact path's token from half the lm_head bytes
+        reserve_head_ws(B);
+        LmHeadQ8Args q;
+        q.x = SX; q.ldx = H; q.norm_w = final_norm_; q.eps = L.rms_eps;
+        q.q = lmq_; q.scale = lmq_scale_; q.bound = lmq_bound_; q.B = B; q.N = L.vocab; q.K = H;
+        q.ban = sa.ban_out; q.ban_ld = sa.ban_ld;
+        lmhead_q8_grid(L.vocab, H, B, &q.nblk, &q.slot);
+        q.blk_cnt = wsi("s_blkcnt", (size_t)B * q.nblk); q.blk_t = wsf("s_blkt", (size_t)B * q.nblk);
+        q.cand = wsi("s_cand", (size_t)B * q.nblk * q.slot); q.cand_hi = wsf("s_candhi", (size_t)B * q.nblk * q.slot);
+        q.xn_out = wsf("s_lmxn", (size_t)B * H);
+        if (getenv("DSOCR_LQ_MODE")) q.mode = atoi(getenv("DSOCR_LQ_MODE"));  // diagnostics only
+        launch_lmhead_q8(q, st);
+        DecSampleArgs ss = sa;
+        ss.blk_cnt = q.blk_cnt; ss.blk_t = q.blk_t; ss.cand = q.cand; ss.cand_hi = q.cand_hi; ss.nblk = q.nblk; ss.slot = q.slot;
+        ss.w_exact = lm_head_.W; ss.xn = q.xn_out; ss.K = H;
+        if (getenv("DSOCR_SCREEN_STATS")) ss.stats = reinterpret_cast<unsigned long long*>(wsi("s_scrstats", 32));
+        launch_dec_sample(ss, st);
+        return;
+    }
     DecGemvArgs g;
     g.M = B; g.N = L.vocab; g.K = H; g.W = lm_head_.W; g.ldw = H; g.wdtype = lm_head_.wdt; g.bias = lm_head_.b;
     g.y = const_cast<float*>(sa.logits); g.ldy = L.vocab;
@@ -1307,6 +1358,13 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     sa.out_tok = d_tok; sa.out_ids = d_out; sa.out_len = d_outlen; sa.out_cap = (long)p.max_new; sa.done = d_done;
     sa.eos = p.ignore_eos ? -1 : (int)p.eos;
     sa.table = embed_; sa.table_dt = embed_dt_; sa.H = H; sa.x_next = SX; sa.kv_pos = d_kvpos; sa.kv_len = d_kvlen;
+    if (screen_applies(B, p.rep_penalty)) {
+        // the screened head reads the n-gram ban list each selection kernel leaves for the next step
+        sa.ban_ld = ctx_cap + 1;
+        sa.ban_out = wsi("s_ban", (size_t)B * sa.ban_ld);
+        reserve_head_ws(B);
+        if (getenv("DSOCR_SCREEN_STATS")) HIP_CHECK(hipMemsetAsync(wsi("s_scrstats", 32), 0, 128, st));
+    }
     // the fused selection kernel advances the KV position; after the prefill the first
     // decode position must be P, so start one behind
     launch_rep_penalty(pen, st);
@@ -1381,6 +1439,14 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         int e = 0;
         HIP_CHECK(hipMemcpy(&e, wsi("s_err", 4), sizeof(int), hipMemcpyDeviceToHost));
         if (e) throw std::runtime_error("EINTERNAL: decode hand-off timed out inside a fused kernel");
+    }
+    if (sa.ban_out && getenv("DSOCR_SCREEN_STATS")) {
+        unsigned long long h[16] = {0};
+        HIP_CHECK(hipMemcpy(h, wsi("s_scrstats", 32), sizeof(h), hipMemcpyDeviceToHost));
+        const double st = h[0] ? (double)h[0] : 1.0;
+        fprintf(stderr, "[screen] steps %llu kept/step %.1f survivors/step %.2f phase_us", h[0], h[1] / st, h[2] / st);
+        for (int k = 0; k < 7; ++k) fprintf(stderr, " %.2f", h[4 + k] / st / 100.0);  // wall clock: 100 MHz
+        fprintf(stderr, "\n");
     }
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);

@@ -180,6 +180,8 @@ class Engine {
     void decode_step(int B, int Lmax);
     MoeDec2Args moe_decode_args(int l, int B, const float* x, const float* norm, float* out);
     void decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen);
+    void reserve_head_ws(int B);
+    bool screen_applies(int B, float rep_penalty) const;
     void layer_forward_prefill(int l, int T, int B, const int* row_page, const int* row_pos, const long* q_off,
                                const long* kv_off, const long* o_off, const int* seq_len, int max_len, int Lmax);
 
@@ -201,6 +203,9 @@ class Engine {
     std::vector<DecLayer> layers_;
     float* final_norm_ = nullptr;
     Lin lm_head_;
+    void* lmq_ = nullptr;            // int8 [vocab][hidden] screening copy of lm_head
+    float* lmq_scale_ = nullptr;     // per-row scale
+    float* lmq_bound_ = nullptr;     // per-row error-bound factor (times ||x||)
     float* rope_cos_ = nullptr;
     float* rope_sin_ = nullptr;
     int rope_cap_ = 0;

@@ -414,10 +414,77 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
 // the rotation meet in one lane; q and k segments are rotated at the decode position, v rows pass
 // through.  The per-row arithmetic is dec_gemv's (chunk u-major, then j), the rotation is the
 // attention kernel's formula x*cos + sign*partner*sin.  One token (M = 1).
-template <typename WT>
+// WAVENORM: every wave normalises the row itself (its lanes hold exactly the 24 elements their
+// dot-product chunks use, the sum of squares is one wave reduction): no LDS and no block barrier.
+template <typename WT, bool WAVENORM>
 __global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRopeEpi r) {
     extern __shared__ float smem[];
     constexpr int U = 3, XR = 2;
+    if (WAVENORM) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int half = r.hd / 2;
+        const int p = blockIdx.x * 4 + wave;
+        const int npairs = a.N / 2;
+        if (p >= npairs) return;  // whole wave: nothing below synchronises the block
+        const int n0 = (p / half) * r.hd + p % half, n1 = n0 + half;
+        const WT* W = reinterpret_cast<const WT*>(a.W);
+        const int chunks = a.K >> 3;
+        float xv[U][8], nw[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int cc = min(u * 64 + lane, chunks - 1);
+            ld_x8(a.x + (cc << 3), xv[u]);
+            ld_x8(a.norm_w + (cc << 3), nw[u]);
+        }
+        const int pos = r.kv_pos[0];
+        uint4 w0[U], w1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int cc = min(u * 64 + lane, chunks - 1);
+            w0[u] = ldg_nt16(W + (long)n0 * a.ldw + (cc << 3));
+            w1[u] = ldg_nt16(W + (long)n1 * a.ldw + (cc << 3));
+        }
+        const int d = n0 % r.hd;
+        const bool rot = n0 < r.rot_rows;
+        const float c0 = rot ? r.cos[(long)pos * r.hd + d] : 1.f, s0 = rot ? r.sin[(long)pos * r.hd + d] : 0.f;
+        const float c1 = rot ? r.cos[(long)pos * r.hd + d + half] : 1.f, s1 = rot ? r.sin[(long)pos * r.hd + d + half] : 0.f;
+        float q = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u * 64 + lane < chunks)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) q += xv[u][j] * xv[u][j];
+        const float den = sqrtf(wave_sum(q) / (float)a.K + a.eps);
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u * 64 + lane < chunks) {
+                float f0[8], f1[8];
+                unpack8<WT>(w0[u], f0);
+                unpack8<WT>(w1[u], f1);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float xn = (xv[u][j] / den) * nw[u][j];
+                    acc0 = fmaf(xn, f0[j], acc0);
+                    acc1 = fmaf(xn, f1[j], acc1);
+                }
+            }
+        }
+        float y0 = wave_sum(acc0), y1 = wave_sum(acc1);
+        if (lane == 0) {
+            y0 = y0 + (a.bias ? a.bias[n0] : 0.f);
+            y1 = y1 + (a.bias ? a.bias[n1] : 0.f);
+            if (rot) {
+                const float o0 = y0 * c0 + (-1.f * y1) * s0;
+                const float o1 = y1 * c1 + (1.f * y0) * s1;
+                y0 = o0;
+                y1 = o1;
+            }
+            a.y[n0] = y0;
+            a.y[n1] = y1;
+        }
+        return;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int half = r.hd / 2;
     const int p = blockIdx.x * 4 + wave;                 // pair index
@@ -484,8 +551,15 @@ void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t 
     if (!dec_qkv_rope_ok(a, r)) throw std::runtime_error("EINVAL: dec_qkv_rope outside its range");
     const size_t lds = stage_bytes(1, a.K);
     dim3 grid((a.N / 2 + 3) / 4);
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL(dec_qkv_rope_kernel<bf16_t>, grid, dim3(256), lds, s, a, r);
-    else hipLaunchKernelGGL(dec_qkv_rope_kernel<f16_t>, grid, dim3(256), lds, s, a, r);
+    // (off by default: every wave re-reading x and the norm weight from L2 measured +0.75 us/layer)
+    static const bool wn = getenv("DSOCR_WAVENORM") && atoi(getenv("DSOCR_WAVENORM")) != 0;
+    if (wn && a.norm_w) {
+        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((dec_qkv_rope_kernel<bf16_t, true>), grid, dim3(256), 0, s, a, r);
+        else hipLaunchKernelGGL((dec_qkv_rope_kernel<f16_t, true>), grid, dim3(256), 0, s, a, r);
+        return;
+    }
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((dec_qkv_rope_kernel<bf16_t, false>), grid, dim3(256), lds, s, a, r);
+    else hipLaunchKernelGGL((dec_qkv_rope_kernel<f16_t, false>), grid, dim3(256), lds, s, a, r);
 }
 
 // ------------------------------------------------------------------ attention combine + o_proj
@@ -2342,14 +2416,264 @@ __global__ __launch_bounds__(SP_BLOCK) void dec_argmax_partial_kernel(DecSampleA
     }
 }
 
-__global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArgs a) {
+// exact logit of row v: the dec_gemv_stream arithmetic (lane chunks u*64 + lane, 8 fmaf each in
+// order, DPP wave sum) on the staged row xs (one wave)
+__device__ __forceinline__ float exact_row_logit(const uint16_t* W, int v, int K, const float* xs) {
+    const int lane = threadIdx.x & 63, chunks = K >> 3;
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int c = u * 64 + lane;
+        const uint4 q = ldg_nt16(W + (long)v * K + (min(c, chunks - 1) << 3));
+        if (c < chunks) {
+            float w8[8], xv[8];
+            unpack8<bf16_t>(q, w8);
+            ld_x8(xs + (c << 3), xv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], w8[j], acc);
+        }
+    }
+    return wave_sum(acc);
+}
+
+// (value, index) argmax over the block's waves: each wave's result to its LDS slot (sv / si must
+// not be in use), one barrier, every thread reduces the slots itself; result in (bv, bi)
+__device__ __forceinline__ void waves_argmax(float& bv, int& bi, float* sv, int* si) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane == 0) { sv[wave] = bv; si[wave] = bi; }
+    __syncthreads();
+    bv = sv[0];
+    bi = si[0];
+    for (int w = 1; w < nw; ++w)
+        if (sp_better(sv[w], si[w], bv, bi)) { bv = sv[w]; bi = si[w]; }
+}
+
+// Screened final selection (one block per page): T = the best lower bound over the unbanned rows
+// (max of the lm_head blocks'); every kept row whose upper bound reaches T is rescored exactly
+// and the first-index argmax taken — the exact path's token (sampling.rs:104-118).  If nothing
+// survives (every unbanned logit non-finite) the reference's fallback runs: the argmax over every
+// token, unbanned.  The kernel is a chain of dependent memory round trips, so everything that
+// does not depend on the token is loaded up front: the step bookkeeping words, and the next
+// step's n-gram ban as PREFIX matches (positions whose first g-2 tokens equal the known part of
+// the next suffix) that only need the new token compared once it is known.
+constexpr int SP_LIST = 1024;  // LDS survivor list (more: rescored straight from the block slots)
+constexpr int SP_PM = 256;     // LDS prefix matches (more: the ban is rescanned after the update)
+
+__device__ __forceinline__ void screened_rescore(const DecSampleArgs& a, const uint16_t* W, const float* xs,
+                                                 const int* list, int n, float T, const int* bc, long sb,
+                                                 float& bv, int& bi) {
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (n <= SP_LIST) {
+        for (int c = wave; c < n; c += nw) {
+            const int v = list[c];
+            const float x = exact_row_logit(W, v, a.K, xs);
+            if ((x > -INFINITY) && (x < INFINITY) && sp_better(x, v, bv, bi)) { bv = x; bi = v; }
+        }
+        return;
+    }
+    for (int j = wave; j < a.nblk; j += nw) {
+        const int c = bc[j];
+        for (int i = 0; i < c; ++i) {
+            if (!(a.cand_hi[sb + (long)i * a.nblk + j] >= T)) continue;
+            const int v = a.cand[sb + (long)i * a.nblk + j];
+            const float x = exact_row_logit(W, v, a.K, xs);
+            if ((x > -INFINITY) && (x < INFINITY) && sp_better(x, v, bv, bi)) { bv = x; bi = v; }
+        }
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float dyn[];  // [K] staged row | survivor list
+    __shared__ float sv[NT / 64], sv2[NT / 64];
+    __shared__ int si2[NT / 64];
+    __shared__ int nlist, nban_s, pm_n;
+    __shared__ int pm_c1[SP_PM], pm_c2[SP_PM];
+    float* xs = dyn;
+    int* list = reinterpret_cast<int*>(dyn + a.K);
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint16_t* W = reinterpret_cast<const uint16_t*>(a.w_exact);
+    const int* bc = a.blk_cnt + (long)b * a.nblk;
+    const float* bt = a.blk_t + (long)b * a.nblk;
+    const long sb = (long)b * a.nblk * a.slot;
+    const int* cx = a.ctx + (long)b * a.ctx_cap;
+    const unsigned long long t0 = a.stats ? wall_clock64() : 0;
+#define SP_STAMP(k) if (a.stats && tid == 0) a.stats[4 + (k)] += wall_clock64() - t0;
+    // ---- token-independent loads
+    const int n = a.ctx_len[b], g = a.ngram;
+    int done0 = 0, olen0 = 0, kvp0 = 0, kvl0 = 0;
+    if (tid == 0) {
+        if (a.out_ids) { done0 = a.done[b]; olen0 = a.out_len[b]; }
+        if (a.kv_pos) { kvp0 = a.kv_pos[b]; kvl0 = a.kv_len[b]; }
+        nlist = 0;
+        pm_n = 0;
+        nban_s = 0;
+    }
+    // per-block threshold and count (thread j < nblk), the first token of the two prefix-match
+    // positions this thread checks, and the staged row: all in flight before the first barrier
+    const bool ban = a.ban_out && g > 1 && n + 1 >= g - 1;
+    const int last_i = n + 1 - g;  // next step's positions: 0 .. n+1-g
+    const int jc = min(tid, a.nblk - 1);
+    float T = bt[jc];
+    const int c0 = bc[jc];
+    if (tid >= a.nblk) T = -INFINITY;
+    for (int j = tid + NT; j < a.nblk; j += NT) T = fmaxf(T, bt[j]);
+    const int lc = max(last_i, 0);
+    const int pa = cx[min(tid, lc)], pb = cx[min(tid + NT, lc)], s0 = cx[max(n + 2 - g, 0)];
+    for (int k = tid * 4; k < a.K; k += NT * 4)
+        *reinterpret_cast<float4*>(xs + k) = *reinterpret_cast<const float4*>(a.xn + (long)b * a.K + k);
+    T = wave_max(T);
+    if (lane == 0) sv[wave] = T;
+    __syncthreads();
+    T = sv[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) T = fmaxf(T, sv[w]);
+    SP_STAMP(0)
+    // ---- kept rows whose upper bound reaches T: a block's first E entries in one round trip
+    if (tid < a.nblk) {
+        constexpr int E = 16;
+        float h[E];
+        int v[E];
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            const long e = sb + (long)min(i, (int)a.slot - 1) * a.nblk + tid;
+            h[i] = a.cand_hi[e];
+            v[i] = a.cand[e];
+        }
+        if (a.stats) atomicAdd(&nban_s, c0);  // (diagnostics: kept rows, reset below)
+#pragma unroll
+        for (int i = 0; i < E; ++i)
+            if (i < c0 && h[i] >= T) {
+                const int p = atomicAdd(&nlist, 1);
+                if (p < SP_LIST) list[p] = v[i];
+            }
+        for (int i = E; i < c0; ++i) {
+            const float hh = a.cand_hi[sb + (long)i * a.nblk + tid];
+            const int vv = a.cand[sb + (long)i * a.nblk + tid];
+            if (hh >= T) {
+                const int p = atomicAdd(&nlist, 1);
+                if (p < SP_LIST) list[p] = vv;
+            }
+        }
+    }
+    for (int j = tid + NT; j < a.nblk; j += NT) {  // more blocks than threads
+        const int c = bc[j];
+        for (int i = 0; i < c; ++i) {
+            const float hh = a.cand_hi[sb + (long)i * a.nblk + j];
+            const int vv = a.cand[sb + (long)i * a.nblk + j];
+            if (hh >= T) {
+                const int p = atomicAdd(&nlist, 1);
+                if (p < SP_LIST) list[p] = vv;
+            }
+        }
+    }
+    SP_STAMP(6)
+    // ---- next step's n-gram ban, prefix part: ctx'[i..i+g-3] == ctx[n+2-g..n-1] (first token
+    // compared from the preloaded values; the rest only for the rare positions that pass)
+    if (ban)
+        for (int i = tid, r = 0; i <= last_i; i += NT, ++r) {
+            const int first = r == 0 ? pa : (r == 1 ? pb : cx[i]);
+            bool match = g < 3 || first == s0;
+            for (int jj = 1; match && jj < g - 2; ++jj)
+                if (cx[i + jj] != cx[n + 2 - g + jj]) match = false;
+            if (match) {
+                const int p = atomicAdd(&pm_n, 1);
+                if (p < SP_PM) {
+                    pm_c1[p] = cx[i + g - 2];                          // index <= n-1
+                    pm_c2[p] = i + g - 1 < n ? cx[i + g - 1] : -1;     // -1: the new token
+                }
+            }
+        }
+    __syncthreads();
+    SP_STAMP(1)
+    const int nl = nlist;
+    if (a.stats) {
+        if (tid == 0) { a.stats[0] += 1; a.stats[1] += (unsigned long long)nban_s; a.stats[2] += (unsigned long long)nl; }
+        __syncthreads();
+        if (tid == 0) nban_s = 0;
+    }
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    screened_rescore(a, W, xs, list, nl, T, bc, sb, bv, bi);
+    SP_STAMP(2)
+    waves_argmax(bv, bi, sv2, si2);
+    SP_STAMP(3)
+    if (bi == 0x7fffffff) {
+        // fallback (sampling.rs:34-96): argmax of every token ignoring the ban
+        bv = -INFINITY;
+        bi = 0x7fffffff;
+        for (int v = wave; v < a.V; v += NT / 64) {
+            const float x = exact_row_logit(W, v, a.K, xs);
+            if ((x > -INFINITY) && (x < INFINITY) && sp_better(x, v, bv, bi)) { bv = x; bi = v; }
+        }
+        __syncthreads();
+        waves_argmax(bv, bi, sv2, si2);
+    }
+    const int t = bi == 0x7fffffff ? 0 : bi;
+    if (tid == 0) {
+        a.out_tok[b] = t;
+        if (a.out_ids && !done0) {
+            if (a.eos >= 0 && t == a.eos) {
+                a.done[b] = 1;
+            } else {
+                if (olen0 < a.out_cap) { a.out_ids[(long)b * a.out_cap + olen0] = t; a.out_len[b] = olen0 + 1; }
+                if (olen0 + 1 >= a.out_cap) a.done[b] = 1;
+                if (n < a.ctx_cap) { a.ctx[(long)b * a.ctx_cap + n] = t; a.ctx_len[b] = n + 1; }
+            }
+        }
+        if (a.kv_pos) {
+            a.kv_pos[b] = kvp0 + 1;
+            a.kv_len[b] = kvl0 + 1;
+        }
+    }
+    if (a.table) {
+        const uint16_t* tab = reinterpret_cast<const uint16_t*>(a.table);
+        for (int c = tid; c < a.H; c += NT) {
+            const uint32_t bits = tab[(long)t * a.H + c];
+            a.x_next[(long)b * a.H + c] = a.table_dt == WDT_BF16 ? bf16_bits_to_f32(bits) : f16_bits_to_f32(bits);
+        }
+    }
+    SP_STAMP(4)
+    if (!a.ban_out) return;
+    // (a page that did not take the token is done: its later selections are never read)
+    int* out = a.ban_out + (long)b * a.ban_ld;
+    if (pm_n <= SP_PM) {
+        for (int p = tid; p < pm_n; p += NT)
+            if (pm_c1[p] == t) {
+                const int q = atomicAdd(&nban_s, 1);
+                if (q + 1 < a.ban_ld) out[1 + q] = pm_c2[p] < 0 ? t : pm_c2[p];
+            }
+    } else {
+        // too many prefix matches (tiny n-gram sizes): full scan of the updated context
+        __syncthreads();
+        const int n1 = n + 1;
+        for (int i = tid; i <= n1 - g; i += NT) {
+            bool match = true;
+            for (int jj = 0; jj < g - 1; ++jj) {
+                const int x0 = i + jj < n ? cx[i + jj] : t, x1 = n1 - g + 1 + jj < n ? cx[n1 - g + 1 + jj] : t;
+                if (x0 != x1) { match = false; break; }
+            }
+            if (match) {
+                const int q = atomicAdd(&nban_s, 1);
+                if (q + 1 < a.ban_ld) out[1 + q] = i + g - 1 < n ? cx[i + g - 1] : t;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) out[0] = min(nban_s, (int)a.ban_ld - 1);
+    SP_STAMP(5)
+#undef SP_STAMP
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void dec_sample_final_kernel(DecSampleArgs a) {
     __shared__ float sv[SP_BLOCK];
     __shared__ int si[SP_BLOCK];
-    __shared__ int tok_s;
+    __shared__ int tok_s, nban_s;
     const int b = blockIdx.x;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int j = threadIdx.x; j < a.red_blocks; j += SP_BLOCK) {
+    for (int j = threadIdx.x; j < a.red_blocks; j += NT) {
         float v = a.red_val[(long)b * a.red_blocks + j];
         int i = a.red_idx[(long)b * a.red_blocks + j];
         if (i != 0x7fffffff && sp_better(v, i, bv, bi)) { bv = v; bi = i; }
@@ -2361,7 +2685,7 @@ __global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArg
         const float* lg = a.logits + (long)b * a.ld;
         bv = -INFINITY;
         bi = 0x7fffffff;
-        for (int v = threadIdx.x; v < a.V; v += SP_BLOCK) {
+        for (int v = threadIdx.x; v < a.V; v += NT) {
             float x = lg[v];
             if (!(x > -INFINITY) || !(x < INFINITY)) continue;
             if (sp_better(x, v, bv, bi)) { bv = x; bi = v; }
@@ -2369,7 +2693,7 @@ __global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArg
         sv[threadIdx.x] = bv;
         si[threadIdx.x] = bi;
         __syncthreads();
-        for (int o = SP_BLOCK / 2; o > 0; o >>= 1) {
+        for (int o = NT / 2; o > 0; o >>= 1) {
             if (threadIdx.x < o && sp_better(sv[threadIdx.x + o], si[threadIdx.x + o], sv[threadIdx.x], si[threadIdx.x])) {
                 sv[threadIdx.x] = sv[threadIdx.x + o];
                 si[threadIdx.x] = si[threadIdx.x + o];
@@ -2380,6 +2704,7 @@ __global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArg
     if (threadIdx.x == 0) {
         const int t = si[0] == 0x7fffffff ? 0 : si[0];
         tok_s = t;
+        nban_s = 0;
         a.out_tok[b] = t;
         if (a.out_ids && !a.done[b]) {
             if (a.eos >= 0 && t == a.eos) {
@@ -2398,10 +2723,28 @@ __global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArg
         }
     }
     __syncthreads();
+    if (a.ban_out) {
+        // the next step's banned tokens (sampling.rs:141-158 on the updated context)
+        const int n = a.ctx_len[b], g = a.ngram;
+        const int* cx = a.ctx + (long)b * a.ctx_cap;
+        int* out = a.ban_out + (long)b * a.ban_ld;
+        if (g > 1 && n >= g - 1)
+            for (int i = threadIdx.x; i <= n - g; i += NT) {
+                bool match = true;
+                for (int jj = 0; jj < g - 1; ++jj)
+                    if (cx[i + jj] != cx[n - g + 1 + jj]) { match = false; break; }
+                if (match) {
+                    const int p = atomicAdd(&nban_s, 1);
+                    if (p + 1 < a.ban_ld) out[1 + p] = cx[i + g - 1];
+                }
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) out[0] = min(nban_s, (int)a.ban_ld - 1);
+    }
     if (!a.table) return;
     const int t = tok_s;
     const uint16_t* tab = reinterpret_cast<const uint16_t*>(a.table);
-    for (int c = threadIdx.x; c < a.H; c += SP_BLOCK) {
+    for (int c = threadIdx.x; c < a.H; c += NT) {
         const uint32_t bits = tab[(long)t * a.H + c];
         a.x_next[(long)b * a.H + c] = a.table_dt == WDT_BF16 ? bf16_bits_to_f32(bits) : f16_bits_to_f32(bits);
     }
@@ -2410,12 +2753,17 @@ __global__ __launch_bounds__(SP_BLOCK) void dec_sample_final_kernel(DecSampleArg
 void launch_dec_sample(const DecSampleArgs& a0, hipStream_t s) {
     DecSampleArgs a = a0;
     a.red_blocks = (int)dec_sample_blocks(a.V);
-    if (a.ctx_cap <= 16384)
-        hipLaunchKernelGGL(dec_argmax_partial_kernel<true>, dim3(a.red_blocks, a.B), dim3(SP_BLOCK),
-                           sizeof(int) * a.ctx_cap, s, a);
-    else
-        hipLaunchKernelGGL(dec_argmax_partial_kernel<false>, dim3(a.red_blocks, a.B), dim3(SP_BLOCK), 0, s, a);
-    hipLaunchKernelGGL(dec_sample_final_kernel, dim3(a.B), dim3(SP_BLOCK), 0, s, a);
+    const bool screen = a.blk_cnt && a.blk_t && a.cand && a.cand_hi && a.w_exact && a.xn && a.nblk > 0;
+    if (a.ban_out && a.ban_ld < a.ctx_cap + 1) throw std::runtime_error("EINVAL: ban list shorter than the context");
+    if (screen) {
+        if (a.K % 8 || a.K > 1536) throw std::runtime_error("EINVAL: screened selection needs K % 8 == 0, K <= 1536");
+        const size_t lds = sizeof(float) * a.K + sizeof(int) * SP_LIST;
+        hipLaunchKernelGGL((dec_screen_final_kernel<1024>), dim3(a.B), dim3(1024), lds, s, a);
+        return;
+    }
+    if (a.ctx_cap <= 16384) hipLaunchKernelGGL((dec_argmax_partial_kernel<true>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), sizeof(int) * a.ctx_cap, s, a);
+    else hipLaunchKernelGGL((dec_argmax_partial_kernel<false>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), 0, s, a);
+    hipLaunchKernelGGL((dec_sample_final_kernel<SP_BLOCK>), dim3(a.B), dim3(SP_BLOCK), 0, s, a);
 }
 
 }  // namespace dsocr

@@ -123,4 +123,15 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     }
 }
 
+// order-preserving float <-> unsigned key (atomicMax over floats); key 0 sorts below every
+// float and decodes to -inf
+__device__ __forceinline__ unsigned fkey(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_dec(unsigned k) {
+    if (k == 0u) return -INFINITY;
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 }  // namespace dsocr

@@ -261,8 +261,37 @@ struct DecSampleArgs {
     int* done = nullptr; int eos = -1;
     const void* table = nullptr; int table_dt = 0; int H = 0; float* x_next = nullptr;
     int* kv_pos = nullptr; int* kv_len = nullptr;
+    // n-gram ban list for the NEXT step ([count | tokens], ban_ld ints per page), written by the
+    // final kernel after the context update when set (read by the screened lm_head)
+    int* ban_out = nullptr; long ban_ld = 0;
+    // screened selection (lmhead.hip): the candidate rows the int8 lm_head kept, the running
+    // threshold key, exact rescoring from the bf16 rows and the normalised row xn
+    // per lm_head block: kept-row count, best lower bound, and up to `slot` (row, hi) entries stored
+    // entry-major ([page][entry][block]: the final kernel reads one entry of every block per load)
+    const int* blk_cnt = nullptr; const float* blk_t = nullptr; const int* cand = nullptr; const float* cand_hi = nullptr;
+    int nblk = 0; long slot = 0;
+    const void* w_exact = nullptr; const float* xn = nullptr; int K = 0;
+    unsigned long long* stats = nullptr;  // [steps, kept rows, survivors] accumulated (diagnostics)
 };
 void launch_dec_sample(const DecSampleArgs& a, hipStream_t s);
 size_t dec_sample_blocks(int V);
+// Screened lm_head (lmhead.hip): int8 rows + per-row scale / error bound give every row an
+// interval [lo, hi] that provably contains the exact kernel's logit; each block keeps the best
+// lower bound of its unbanned rows and the rows whose hi reached its running threshold (its own
+// slot: no cross-block atomics); block 0 writes the normalised row.
+struct LmHeadQ8Args {
+    const float* x = nullptr; long ldx = 0; const float* norm_w = nullptr; float eps = 0.f;
+    const void* q = nullptr; const float* scale = nullptr; const float* bound = nullptr;
+    int B = 0, N = 0, K = 0;
+    const int* ban = nullptr; long ban_ld = 0;
+    int* blk_cnt = nullptr; float* blk_t = nullptr; int* cand = nullptr; float* cand_hi = nullptr;
+    int nblk = 0; long slot = 0;  // from lmhead_q8_grid
+    float* xn_out = nullptr;  // [B][K]
+    int mode = 0;             // diagnostics: 1 = stream only (no selection state; results invalid)
+};
+void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s);
+// grid of the screened lm_head for B pages: blocks per page and the per-block slot length
+void lmhead_q8_grid(int N, int K, int B, int* nblk, long* slot);
+void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s);
 
 }  // namespace dsocr

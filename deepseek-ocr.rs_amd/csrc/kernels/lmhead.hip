@@ -1,0 +1,368 @@
+// Screened greedy selection for the decode step (B <= 2 pages): the full-precision lm_head
+// (129280 x 1280 bf16, 331 MB, transformer/model.rs:243-270) is replaced on the critical path by
+// an int8 copy (per-row scale, 165 MB) that gives every row an approximate logit A_v and a
+// RIGOROUS bound eps_v with |L_v - A_v| <= eps_v, where L_v is the logit the exact kernel
+// (dec_gemv_stream over the bf16 rows) would produce bit for bit.  Selection then keeps every
+// row whose interval [A - eps, A + eps] can still reach the best lower bound T, rescores exactly
+// those candidates with the exact kernel's arithmetic, and takes the first-index argmax
+// (sampling.rs:104-118) over them: the same token as the exact path, from half the bytes.
+//
+// Bound (per row v, K = hidden, x = the RMS-normalised row, u = 2^-24):
+//   L_v - A_v = [fl(x.W) - x.W] + [x.(W - s Q)] + [s x.Q - fl(s fl(x.Q))]
+//   |.| <= ||x|| (E_v + g (||W_v|| + s_v ||Q_v||)) + |A_v| 2u          (g = 2 K u, generous)
+// with E_v = ||W_v - s_v Q_v||, all row constants computed in f64 at load and rounded up.
+#include <cstdint>
+#include <stdexcept>
+
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+// ---------------------------------------------------------------- load time: quantise one row per block
+__global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __restrict__ w, int K, int8_t* q,
+                                                              float* scale, float* bound) {
+    __shared__ double red[256];
+    const int v = blockIdx.x;
+    const uint16_t* row = w + (long)v * K;
+    float mx = 0.f;
+    for (int k = threadIdx.x; k < K; k += 256) mx = fmaxf(mx, fabsf(bf16_bits_to_f32(row[k])));
+    red[threadIdx.x] = mx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    const float s = red[0] > 0.0 ? (float)(red[0] / 127.0) : 1.f;
+    __syncthreads();
+    double e2 = 0.0, w2 = 0.0, q2 = 0.0;
+    for (int k = threadIdx.x; k < K; k += 256) {
+        const float x = bf16_bits_to_f32(row[k]);
+        float qf = rintf(x / s);
+        qf = fminf(127.f, fmaxf(-127.f, qf));
+        q[(long)v * K + k] = (int8_t)qf;
+        const double e = (double)x - (double)s * (double)qf;
+        e2 += e * e;
+        w2 += (double)x * x;
+        q2 += (double)qf * qf;
+    }
+    double* sums = red;
+    for (int part = 0; part < 3; ++part) {
+        __syncthreads();
+        sums[threadIdx.x] = part == 0 ? e2 : (part == 1 ? w2 : q2);
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (threadIdx.x < o) sums[threadIdx.x] += sums[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (part == 0) e2 = sums[0];
+        else if (part == 1) w2 = sums[0];
+        else q2 = sums[0];
+    }
+    if (threadIdx.x == 0) {
+        const double g = 2.0 * K * 5.9604644775390625e-8;  // 2 K u
+        const double b = (sqrt(e2) + g * (sqrt(w2) + (double)s * sqrt(q2))) * (1.0 + 1e-6) + 1e-30;
+        scale[v] = s;
+        bound[v] = __double2float_ru(b);
+    }
+}
+
+void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s) {
+    hipLaunchKernelGGL(lmhead_quantize_kernel, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
+                       reinterpret_cast<int8_t*>(q), scale, bound);
+}
+
+// ---------------------------------------------------------------- per step: screened lm_head
+// x staged once per block exactly as dec_gemv_stream stages it (RMSNorm fused); block 0 also
+// writes the staged row (the exact rescoring reads it).  A wave walks groups of RB rows with a
+// two-deep register pipeline of 16-byte int8 loads (K / 16 chunks per row); per row it forms the
+// interval [lo, hi] (row r's in lane r: one pass, one ballot) and keeps the row when hi reaches
+// the wave's running threshold Tw (the best lo of the unbanned rows seen by this wave or,
+// refreshed once per group, by its block: an LDS atomicMax key).  Kept rows go to an LDS list;
+// at the end the block writes its list, count and best lo to its own slot, and the final kernel
+// reduces the blocks (no cross-block atomics: a device-wide threshold / counter was 2-10x
+// slower, every wave hitting one address).
+constexpr int LQ_RB = 8;   // rows per group
+constexpr int LQ_XS = 128;
+constexpr int LQ_LIST = 1024;  // rows one block may keep (the grid keeps rows per block <= this)
+// Load layout of one group (K/16 16-byte chunks per row): load r (r < RB) is row r's chunks
+// 0..63, one per lane; the rows' remaining chunks (TSEG = 16 or 32 of them at most) are packed
+// TSEG lanes per row into RB*TSEG/64 shared tail loads — every lane's bytes are useful.
+template <int TSEG>
+struct LqGroup {
+    static constexpr int NTL = TSEG ? LQ_RB * TSEG / 64 : 0;
+    uint4 m[LQ_RB];
+    uint4 t[NTL > 0 ? NTL : 1];
+    float sc, bd;  // lane r: row r's scale / bound
+};
+
+template <int TSEG>
+__device__ __forceinline__ void lq_issue(LqGroup<TSEG>& q, const LmHeadQ8Args& a, const int8_t* W, int n0, int lane) {
+    const int chunks = a.K >> 4, N = a.N, K = a.K;
+    const int nr = min(n0 + (lane & (LQ_RB - 1)), N - 1);
+    q.sc = a.scale[nr];
+    q.bd = a.bound[nr];
+#pragma unroll
+    for (int r = 0; r < LQ_RB; ++r) {
+        const int n = min(n0 + r, N - 1);
+        q.m[r] = ldg_nt16(W + (long)n * K + (min(lane, chunks - 1) << 4));
+    }
+    if (TSEG) {
+        constexpr int RPT = TSEG ? 64 / TSEG : 1;
+#pragma unroll
+        for (int t = 0; t < LqGroup<TSEG>::NTL; ++t) {
+            const int n = min(n0 + t * RPT + lane / TSEG, N - 1);
+            q.t[t] = ldg_nt16(W + (long)n * K + (min(64 + lane % TSEG, chunks - 1) << 4));
+        }
+    }
+}
+
+__device__ __forceinline__ float i8f(uint32_t w, int byte) {
+    // signed byte: shift it to the top, arithmetic shift back (one sdwa sext convert).
+    // (__builtin_amdgcn_sbfe on this compiler folds into an UNSIGNED sdwa convert: wrong.)
+    return (float)((int32_t)(w << (24 - 8 * byte)) >> 24);
+}
+
+// the page's banned rows: staged in LDS (a global read here would drain the prefetch: vmcnt is
+// in order); longer lists are read from global memory
+constexpr int LQ_BANS = 256;
+__device__ __forceinline__ float lq_dot16(const float* xv, uint4 q, float acc) {
+    const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = fmaf(xv[4 * i + j], i8f(wd[i], j), acc);
+    return acc;
+}
+
+__device__ __forceinline__ void ld_x16(const float* p, float* xv) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 t = *reinterpret_cast<const float4*>(p + 4 * i);
+        xv[4 * i] = t.x; xv[4 * i + 1] = t.y; xv[4 * i + 2] = t.z; xv[4 * i + 3] = t.w;
+    }
+}
+
+__device__ __forceinline__ bool lq_banned(int n, int nban, const int* ban_s, const int* ban_g) {
+    if (nban <= LQ_BANS) {
+        for (int j = 0; j < nban; ++j)
+            if (ban_s[j] == n) return true;
+        return false;
+    }
+    for (int j = 0; j < nban; ++j)
+        if (ban_g[j] == n) return true;
+    return false;
+}
+
+template <int TSEG>
+__global__ __launch_bounds__(256) void lmhead_q8_kernel(LmHeadQ8Args a) {
+    __shared__ __attribute__((aligned(16))) float xs[LQ_XS + 1536];
+    __shared__ float nrm_s;
+    __shared__ unsigned tkey_s;
+    __shared__ int ban_s[LQ_BANS];
+    __shared__ int lst_n;
+    __shared__ int lst_idx[LQ_LIST];
+    __shared__ float lst_hi[LQ_LIST];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int K = a.K, chunks = K >> 4;
+    const int b = blockIdx.y;
+    const float* xrow = a.x + (long)b * a.ldx;
+    const int8_t* W = reinterpret_cast<const int8_t*>(a.q);
+    const int ngroups = (a.N + LQ_RB - 1) / LQ_RB;
+    const int stride = gridDim.x * 4;
+    LqGroup<TSEG> qa;
+    int g = blockIdx.x * 4 + wave;
+    // loads in order of use: x / norm weight, the ban list, then the first row group (its
+    // latency overlaps the norm prologue)
+    float4 v[2], w[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int k = min((tid + i * 256) * 4, K - 4);
+        v[i] = *reinterpret_cast<const float4*>(xrow + k);
+        w[i] = *reinterpret_cast<const float4*>(a.norm_w + k);
+    }
+    int nban = 0, bent = 0;
+    const int* ban_g = nullptr;
+    if (a.ban) {
+        ban_g = a.ban + (long)b * a.ban_ld + 1;
+        nban = a.ban[(long)b * a.ban_ld];
+        bent = ban_g[min(tid, (int)a.ban_ld - 2)];
+    }
+    lq_issue<TSEG>(qa, a, W, min(g, ngroups - 1) * LQ_RB, lane);
+    // stage x = rmsnorm(x) (the dec_gemv staging arithmetic: 256 threads, float4 each, XR = 2)
+    {
+        float qs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            if ((tid + i * 256) * 4 < K) qs += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+        qs = wave_sum(qs);
+        if (lane == 0) xs[wave] = qs;
+        if (tid == 0) { tkey_s = 0u; lst_n = 0; }
+        if (tid < LQ_BANS) ban_s[tid] = bent;
+        __syncthreads();
+        float q = 0.f;
+        for (int ww = 0; ww < 4; ++ww) q += xs[ww];
+        const float den = sqrtf(q / (float)K + a.eps);
+        __syncthreads();
+        float n2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int k = (tid + i * 256) * 4;
+            if (k < K) {
+                float4 o;
+                o.x = (v[i].x / den) * w[i].x;
+                o.y = (v[i].y / den) * w[i].y;
+                o.z = (v[i].z / den) * w[i].z;
+                o.w = (v[i].w / den) * w[i].w;
+                *reinterpret_cast<float4*>(xs + LQ_XS + k) = o;
+                n2 += (o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w);
+                if (blockIdx.x == 0 && a.xn_out) *reinterpret_cast<float4*>(a.xn_out + (long)b * K + k) = o;
+            }
+        }
+        n2 = wave_sum(n2);
+        if (lane == 0) xs[4 + wave] = n2;
+        __syncthreads();
+        if (tid == 0) {
+            // ||x||, rounded up (the partial-sum rounding is < 1e-4 relative at K <= 1536)
+            nrm_s = sqrtf((xs[4] + xs[5] + xs[6] + xs[7]) * (1.f + 1e-4f)) * (1.f + 1e-6f);
+        }
+        __syncthreads();
+    }
+    const float nrm = nrm_s;
+    const float* x = xs + LQ_XS;
+    float Tw = -INFINITY;
+    for (; g < ngroups; g += stride) {
+        LqGroup<TSEG> qn;
+        const int g2 = g + stride;
+        lq_issue<TSEG>(qn, a, W, min(g2, ngroups - 1) * LQ_RB, lane);  // clamped: no predicated loads
+        float acc[LQ_RB];
+        {
+            // every lane computes (clamped chunks past K hold valid bytes), masked after
+            float xv[16];
+            ld_x16(x + (min(lane, chunks - 1) << 4), xv);
+            const bool ok = lane < chunks;
+#pragma unroll
+            for (int r = 0; r < LQ_RB; ++r) {
+                const float d = lq_dot16(xv, qa.m[r], 0.f);
+                acc[r] = ok ? d : 0.f;
+            }
+            if (TSEG) {
+                constexpr int RPT = TSEG ? 64 / TSEG : 1;
+                const int tc = 64 + lane % TSEG;
+                ld_x16(x + (min(tc, chunks - 1) << 4), xv);
+                const bool tok = tc < chunks;
+                const int seg = lane / TSEG;
+#pragma unroll
+                for (int t = 0; t < LqGroup<TSEG>::NTL; ++t) {
+                    float tv = lq_dot16(xv, qa.t[t], 0.f);
+                    tv = tok ? tv : 0.f;
+#pragma unroll
+                    for (int rr = 0; rr < RPT; ++rr) acc[t * RPT + rr] += seg == rr ? tv : 0.f;
+                }
+            }
+        }
+        // row r's dot product to lane r (which holds its scale / bound): the intervals of the
+        // group in one pass, one ballot; only rows that can matter take the serial path
+        float my = 0.f;
+#pragma unroll
+        for (int r = 0; r < LQ_RB; ++r) {
+            const float sd = wave_sum(acc[r]);
+            my = (lane & (LQ_RB - 1)) == r ? sd : my;
+        }
+        const float A = qa.sc * my;
+        // |L - A| <= nrm * bound + |A| 2u; the extra factors cover the rounding of e and of A -/+ e
+        const float e = (nrm * qa.bd) * (1.f + 4.8e-7f) + fabsf(A) * 3.6e-7f;
+        const float lo = A - e, hi = A + e;
+        const int nrow = g * LQ_RB + lane;
+        const bool trig = lane < LQ_RB && nrow < a.N && (lo > Tw || hi >= Tw);
+        unsigned long long m = __ballot(trig);
+        if (a.mode == 1) m = 0;  // diagnostics: stream only
+        while (m) {
+            const int r = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const float lo_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lo), r));
+            const float hi_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi), r));
+            const int n = g * LQ_RB + r;
+            if (!(lo_r > Tw) && !(hi_r >= Tw)) continue;
+            if (lq_banned(n, nban, ban_s, ban_g)) continue;
+            if (lo_r > Tw) {
+                Tw = lo_r;
+                if (lane == 0) atomicMax(&tkey_s, fkey(lo_r));
+            }
+            if (lane == 0) {
+                const int p = atomicAdd(&lst_n, 1);
+                lst_idx[p] = n;
+                lst_hi[p] = hi_r;
+            }
+        }
+        Tw = fmaxf(Tw, __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fkey_dec(tkey_s)))));
+        qa = qn;
+    }
+    __syncthreads();
+    // the block's list against its final threshold (most rows kept early fall out here)
+    const int cnt = lst_n;
+    const float Tb = fkey_dec(tkey_s);
+    // entry p of this block at [b][p][block] (the final kernel reads a row of blocks per load)
+    const long sb = (long)b * a.nblk * a.slot + blockIdx.x;
+    __syncthreads();
+    if (tid == 0) lst_n = 0;
+    __syncthreads();
+    for (int i = tid; i < cnt; i += 256) {
+        const float h = lst_hi[i];
+        if (h >= Tb) {
+            const int p = atomicAdd(&lst_n, 1);
+            a.cand[sb + (long)p * a.nblk] = lst_idx[i];
+            a.cand_hi[sb + (long)p * a.nblk] = h;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.blk_cnt[(long)b * a.nblk + blockIdx.x] = lst_n;
+        a.blk_t[(long)b * a.nblk + blockIdx.x] = Tb;
+    }
+}
+
+static int lq_tseg(int K) {
+    const int chunks = K >> 4;
+    return chunks <= 64 ? 0 : (chunks <= 80 ? 16 : 32);
+}
+
+void lmhead_q8_grid(int N, int K, int B, int* nblk, long* slot) {
+    static int resident[3] = {0, 0, 0};
+    const int ti = lq_tseg(K) / 16;
+    if (!resident[ti]) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (ti == 0) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lmhead_q8_kernel<0>, 256, 0);
+        else if (ti == 1) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lmhead_q8_kernel<16>, 256, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lmhead_q8_kernel<32>, 256, 0);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        resident[ti] = std::max(1, per_cu) * std::max(1, cus);
+    }
+    const int groups = (N + LQ_RB - 1) / LQ_RB;
+    int blocks = std::min((groups + 3) / 4, std::max(1, resident[ti] / std::max(1, B)));
+    // rows one block walks (its kept list is bounded by them) must fit the LDS list
+    constexpr int max_per_wave = LQ_LIST / (4 * LQ_RB);
+    blocks = std::max(blocks, (groups + 4 * max_per_wave - 1) / (4 * max_per_wave));
+    const int per_wave = (groups + 4 * blocks - 1) / (4 * blocks);
+    *nblk = blocks;
+    *slot = (long)per_wave * 4 * LQ_RB;
+}
+
+void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s) {
+    if (a.K % 16 || a.K > 1536 || a.K < 16) throw std::runtime_error("EINVAL: lmhead_q8 needs K % 16 == 0, K <= 1536");
+    int nblk = 0;
+    long slot = 0;
+    lmhead_q8_grid(a.N, a.K, a.B, &nblk, &slot);
+    if (!a.blk_cnt || !a.blk_t || !a.cand || !a.cand_hi || a.nblk != nblk || a.slot != slot)
+        throw std::runtime_error("EINVAL: lmhead_q8 block lists missing or not sized by lmhead_q8_grid");
+    if (a.ban && a.ban_ld < 2) throw std::runtime_error("EINVAL: lmhead_q8 ban list stride < 2");
+    const int tseg = lq_tseg(a.K);
+    const dim3 grid(nblk, a.B);
+    if (tseg == 0) hipLaunchKernelGGL(lmhead_q8_kernel<0>, grid, dim3(256), 0, s, a);
+    else if (tseg == 16) hipLaunchKernelGGL(lmhead_q8_kernel<16>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(lmhead_q8_kernel<32>, grid, dim3(256), 0, s, a);
+}
+
+}  // namespace dsocr

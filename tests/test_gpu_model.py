@@ -219,3 +219,17 @@ def test_tiny_device_resident_page_equals_host(tiny_engine):
         reqs_h.append((ids, mask, ph, None))
         reqs_d.append((ids, mask, pd, None))
     assert tiny_engine.generate_batch(reqs_d, p) == tiny_engine.generate_batch(reqs_h, p)
+
+
+def test_full_screened_selection_equals_exact(full_engine, monkeypatch):
+    """Screened greedy selection (int8 lm_head intervals + exact rescoring, lmhead.hip) picks the
+    same tokens as the exact bf16 lm_head path on a full-size page with the 20-gram ban on."""
+    tok = SyntheticTokenizer(129280)
+    page = Page(synthetic_page(5), VisionSettings())
+    ids, mask = build_prompt_tokens(tok, "<image>\n<|grounding|>Convert the document to markdown.", [page.n_image_tokens])
+    p = DecodeParameters(max_new_tokens=48)
+    monkeypatch.setenv("DSOCR_SCREEN", "1")
+    screened = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
+    monkeypatch.setenv("DSOCR_SCREEN", "0")
+    exact = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
+    assert screened == exact, (screened, exact)
