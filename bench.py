@@ -208,7 +208,8 @@ def main():
                     "experts_touched": prof["experts_touched"],
                     "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
                                    "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
-                               for k in ("moe_down", "attention", "lm_head")},
+                               for k in ("moe_down", "attention", "lm_head", "lm_head_screened")
+                               if prof.get(k, {}).get("avg_us", 0) > 0},
                     "kv_len": prof["kv_len"]}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

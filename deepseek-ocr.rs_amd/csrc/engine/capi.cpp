@@ -252,6 +252,7 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
         out->o_proj = cp(p.o_proj);
         out->router = cp(p.router);
         out->layers_step = cp(p.layers_step);
+        out->lm_head_screened = cp(p.lm_head_screened);
     });
 }
 

@@ -1639,6 +1639,29 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         });
         prof.lm_head.bytes = (double)L.vocab * H * 2.0 + (double)B * (L.vocab + H) * 4.0;
         prof.lm_head.flops = 2.0 * B * (double)L.vocab * H;
+        if (lmq_ && B <= 2) {
+            // screened head: int8 lm_head + selection (no bookkeeping, no ban: side-effect free)
+            reserve_head_ws(B);
+            LmHeadQ8Args q;
+            q.x = SX; q.ldx = H; q.norm_w = final_norm_; q.eps = L.rms_eps;
+            q.q = lmq_; q.scale = lmq_scale_; q.bound = lmq_bound_; q.B = B; q.N = L.vocab; q.K = H;
+            lmhead_q8_grid(L.vocab, H, B, &q.nblk, &q.slot);
+            q.blk_cnt = wsi("s_blkcnt", (size_t)B * q.nblk); q.blk_t = wsf("s_blkt", (size_t)B * q.nblk);
+            q.cand = wsi("s_cand", (size_t)B * q.nblk * q.slot); q.cand_hi = wsf("s_candhi", (size_t)B * q.nblk * q.slot);
+            q.xn_out = wsf("s_lmxn", (size_t)B * H);
+            DecSampleArgs ss;
+            ss.B = B; ss.V = L.vocab; ss.ld = L.vocab; ss.ctx = wsi("p_sctx", 64); ss.ctx_cap = 64;
+            ss.ctx_len = wsi("p_ctxlen", B); ss.ngram = 0; ss.out_tok = wsi("p_tok", B);
+            ss.blk_cnt = q.blk_cnt; ss.blk_t = q.blk_t; ss.cand = q.cand; ss.cand_hi = q.cand_hi; ss.nblk = q.nblk;
+            ss.slot = q.slot; ss.w_exact = lm_head_.W; ss.xn = q.xn_out; ss.K = H;
+            HIP_CHECK(hipMemsetAsync(ss.ctx_len, 0, B * 4, st));
+            timed(prof.lm_head_screened, iters, [&](int) {
+                launch_lmhead_q8(q, st);
+                launch_dec_sample(ss, st);
+            });
+            prof.lm_head_screened.bytes = (double)L.vocab * H + (double)L.vocab * 8.0 + (double)B * H * 4.0;
+            prof.lm_head_screened.flops = 2.0 * B * (double)L.vocab * H;
+        }
     }
     {
         // attention-side GEMVs of every layer, replayed on scratch outputs

@@ -138,7 +138,7 @@ class Engine {
         int launches = 0;
     };
     struct DecodeProfile {
-        KernelProfile moe_gateup, moe_down, attention, lm_head, qkv, o_proj, router, layers_step;
+        KernelProfile moe_gateup, moe_down, attention, lm_head, qkv, o_proj, router, layers_step, lm_head_screened;
         int experts_touched = 0, tokens = 0, kv_len = 0;
     };
     DecodeProfile profile_decode(int iters);

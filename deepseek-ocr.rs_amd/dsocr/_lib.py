@@ -62,7 +62,7 @@ class DecodeProfileC(C.Structure):
     _fields_ = [("moe_gateup", KernelProfileC), ("moe_down", KernelProfileC), ("attention", KernelProfileC),
                 ("lm_head", KernelProfileC), ("experts_touched", C.c_int), ("tokens", C.c_int), ("kv_len", C.c_int),
                 ("qkv", KernelProfileC), ("o_proj", KernelProfileC), ("router", KernelProfileC),
-                ("layers_step", KernelProfileC)]
+                ("layers_step", KernelProfileC), ("lm_head_screened", KernelProfileC)]
 
 
 STREAM_CB = C.CFUNCTYPE(None, C.c_size_t, C.POINTER(C.c_int64), C.c_void_p)

@@ -256,7 +256,8 @@ class DeepseekOcrEngine:
         p = DecodeProfileC()
         check(lib().dsocr_profile_decode(self._h, iters, C.byref(p)))
         out = {}
-        for k in ("moe_gateup", "moe_down", "attention", "lm_head", "qkv", "o_proj", "router", "layers_step"):
+        for k in ("moe_gateup", "moe_down", "attention", "lm_head", "qkv", "o_proj", "router", "layers_step",
+                  "lm_head_screened"):
             kp = getattr(p, k)
             out[k] = {"avg_us": kp.avg_us, "bytes": kp.bytes, "flops": kp.flops, "launches": kp.launches}
         out.update(experts_touched=p.experts_touched, tokens=p.tokens, kv_len=p.kv_len)

@@ -166,6 +166,7 @@ typedef struct dsocr_decode_profile {
     dsocr_kernel_profile o_proj;      /* dec_gemv: o_proj + residual, one layer */
     dsocr_kernel_profile router;      /* MoE router logits (+ top-k when routed by the router kernel) */
     dsocr_kernel_profile layers_step; /* every decoder layer of one decode step, replayed as one hipGraph */
+    dsocr_kernel_profile lm_head_screened; /* int8 screened lm_head + exact rescoring selection (B <= 2, no penalty) */
 } dsocr_decode_profile;
 dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out);
 
