@@ -84,12 +84,12 @@ dsocr_status dsocr_engine_load(const dsocr_load_args* args, dsocr_engine** out) 
     return guarded([&] {
         if (!args || !out) throw std::runtime_error("EINVAL: NULL argument");
         if (!args->config_path) throw std::runtime_error("EINVAL: config_path is required");
-        if (args->snapshot_path) throw std::runtime_error("EINVAL: .dsq snapshots are not supported yet");
         if (args->dtype < DSOCR_F32 || args->dtype > DSOCR_BF16) throw std::runtime_error("EINVAL: bad dtype");
         auto* e = new dsocr_engine;
         try {
             e->impl.reset(new dsocr::Engine(args->config_path, args->weights_path ? args->weights_path : "",
-                                            args->device_ordinal, (int)args->dtype, args->synthetic_seed));
+                                            args->device_ordinal, (int)args->dtype, args->synthetic_seed,
+                                            args->snapshot_path ? args->snapshot_path : ""));
         } catch (...) {
             delete e;
             throw;
@@ -320,6 +320,18 @@ dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* 
         if (cols % 4) throw std::runtime_error("EINVAL: cols must be a multiple of 4");
         dsocr::launch_layernorm(x, cols, y, cols, nullptr, rows, cols, w, b, eps, nullptr);
         check_hip(hipDeviceSynchronize(), "layernorm");
+    });
+}
+dsocr_status dsocr_k_dsq_dequant(int qtype, const void* src, size_t src_bytes, size_t out_dim, size_t in_dim,
+                                 void* out_f16) {
+    return guarded([&] {
+        const size_t need = dsocr::dsq_payload_bytes(qtype, (long)out_dim, (long)in_dim);
+        if (need == 0) throw std::runtime_error("EINVAL: unsupported snapshot tensor dtype code " + std::to_string(qtype));
+        if (src_bytes != need)
+            throw std::runtime_error("EINVAL: payload is " + std::to_string(src_bytes) + " bytes, expected " + std::to_string(need));
+        dsocr::launch_dsq_dequant(qtype, src, (long)out_dim, (long)in_dim, out_f16, nullptr);
+        check_hip(hipGetLastError(), "dsq_dequant launch");
+        check_hip(hipDeviceSynchronize(), "dsq_dequant");
     });
 }
 dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w, float eps, float* y) {

@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "../common/host_util.hpp"
+#include "dsq.hpp"
 #include "host_ops.hpp"
 
 namespace dsocr {
@@ -28,8 +29,23 @@ struct Source {
     uint64_t seed = 0;
     bool synth = false;
     int mode = 1;  // dsocr_dtype: 0 f32, 1 f16, 2 bf16
+    // .dsq snapshot (crates/dsq-runtime): its records replace the checkpoint's linears, decoded to
+    // fp16 on the GPU (dequant); a snapshot linear's bias comes from its record only, as
+    // SnapshotLinear::{Quantized, Float} carries it (dsq-runtime/src/lib.rs:336-366)
+    const DsqFile* snap = nullptr;
+    std::function<void(const DsqRecord&, uint16_t*)> dequant;
 
-    bool has(const std::string& n) const { return synth ? synth_has(n) : st->has(n); }
+    const DsqRecord* snap_weight_of_bias(const std::string& n) const {
+        if (!snap || n.size() < 5 || n.compare(n.size() - 5, 5, ".bias") != 0) return nullptr;
+        return snap->find(n.substr(0, n.size() - 5) + ".weight");
+    }
+    bool has(const std::string& n) const {
+        if (snap) {
+            if (snap->find(n)) return true;
+            if (const DsqRecord* r = snap_weight_of_bias(n)) return r->has_bias;
+        }
+        return synth ? synth_has(n) : st->has(n);
+    }
 
     static bool is_language(const std::string& n) {
         return n.rfind("model.layers.", 0) == 0 || n.rfind("model.embed_tokens.", 0) == 0;
@@ -38,6 +54,13 @@ struct Source {
 
     // exact f32 values (with the f16 rounding rule applied)
     std::vector<float> f32(const std::string& n, size_t numel) const {
+        if (const DsqRecord* r = snap_weight_of_bias(n)) {
+            std::vector<float> b = snap->bias(*r);
+            if (b.size() != numel)
+                throw std::runtime_error("EINVAL: snapshot bias for `" + r->name + "` has " + std::to_string(b.size()) +
+                                         " values, expected " + std::to_string(numel));
+            return b;
+        }
         std::vector<float> out(numel);
         if (synth) {
             std::vector<uint16_t> b(numel);
@@ -67,9 +90,19 @@ struct Source {
 
     // 16-bit storage: f16 for language tensors in f16 mode (bf16 -> f16 RNE, the
     // reference's VarBuilder F16 load), otherwise the checkpoint's own 16-bit type.
-    HostMat h16(const std::string& n, size_t numel) const {
+    // out_dim / in_dim (when known) are checked against a snapshot record (dsq-runtime/src/lib.rs:326-334)
+    HostMat h16(const std::string& n, size_t numel, long out_dim = -1, long in_dim = -1) const {
         HostMat m;
         m.data.resize(numel);
+        if (const DsqRecord* r = snap ? snap->find(n) : nullptr) {
+            if ((size_t)r->out_dim * r->in_dim != numel || (out_dim >= 0 && (long)r->out_dim != out_dim) ||
+                (in_dim >= 0 && (long)r->in_dim != in_dim))
+                throw std::runtime_error("EINVAL: snapshot tensor `" + n + "` dims mismatch (" + std::to_string(r->out_dim) +
+                                         "x" + std::to_string(r->in_dim) + " for " + std::to_string(numel) + " values)");
+            dequant(*r, m.data.data());
+            m.dt = WDT_F16;
+            return m;
+        }
         const bool to_f16 = round16(n);
         if (synth) {
             synth_bf16(n, seed, numel, m.data.data());
@@ -153,7 +186,8 @@ void* Engine::ws(const std::string& name, size_t bytes) {
     return p;
 }
 
-Engine::Engine(const std::string& config_path, const std::string& weights_path, int device, int dtype, uint64_t seed)
+Engine::Engine(const std::string& config_path, const std::string& weights_path, int device, int dtype, uint64_t seed,
+               const std::string& snapshot_path)
     : device_(device), dtype_(dtype) {
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
@@ -172,7 +206,9 @@ Engine::Engine(const std::string& config_path, const std::string& weights_path, 
     if (L.hidden_act != "silu" && L.hidden_act != "swish") throw std::runtime_error("EINVAL: activation `" + L.hidden_act + "` not implemented on this engine");
     if (L.n_routed > 256) throw std::runtime_error("EINVAL: at most 256 routed experts supported");
     if (L.topk > 8) throw std::runtime_error("EINVAL: at most 8 experts per token supported");
-    load_weights(weights_path, seed);
+    if (!snapshot_path.empty() && dtype != 1)
+        throw std::runtime_error("EINVAL: .dsq snapshots load as fp16 (dequant-on-load): use dtype f16");
+    load_weights(weights_path, seed, snapshot_path);
     ensure_rope(4096);
     ensure_small(64);
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -255,7 +291,7 @@ void Engine::ensure_rope(int len) {
 }
 
 // ============================================================================ loading
-void Engine::load_weights(const std::string& path, uint64_t seed) {
+void Engine::load_weights(const std::string& path, uint64_t seed, const std::string& snapshot_path) {
     Source src;
     src.mode = dtype_;
     if (path.empty()) {
@@ -263,6 +299,25 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
         src.seed = seed;
     } else {
         src.st.reset(new SafeTensors(path));
+    }
+    std::unique_ptr<DsqFile> snap;
+    if (!snapshot_path.empty()) {
+        snap.reset(new DsqFile(snapshot_path));
+        src.snap = snap.get();
+        src.dequant = [&](const DsqRecord& r, uint16_t* host_out) {
+            const size_t need = dsq_payload_bytes(r.q_dtype, r.out_dim, r.in_dim);
+            if (r.q_len != need)
+                throw std::runtime_error("EINVAL: snapshot tensor `" + r.name + "` payload is " + std::to_string(r.q_len) +
+                                         " bytes, expected " + std::to_string(need));
+            const size_t n = (size_t)r.out_dim * r.in_dim;
+            void* d_src = ws("load_dsq_src", need);
+            void* d_dst = ws("load_dsq_dst", n * 2);
+            HIP_CHECK(hipMemcpyAsync(d_src, snap->payload(r), need, hipMemcpyHostToDevice, stream_));
+            launch_dsq_dequant(r.q_dtype, d_src, r.out_dim, r.in_dim, d_dst, stream_);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(host_out, d_dst, n * 2, hipMemcpyDeviceToHost, stream_));
+            HIP_CHECK(hipStreamSynchronize(stream_));
+        };
     }
     auto up16 = [&](const HostMat& m) -> void* {
         void* p = dev_alloc(m.data.size() * 2);
@@ -278,7 +333,7 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
     auto optvec = [&](const std::string& n, size_t numel) -> float* { return src.has(n) ? vecf(n, numel) : nullptr; };
     auto lin = [&](const std::string& pre, int N, int K, bool allow_bias) -> Lin {
         Lin l;
-        HostMat m = src.h16(pre + ".weight", (size_t)N * K);
+        HostMat m = src.h16(pre + ".weight", (size_t)N * K, N, K);
         l.W = up16(m);
         l.wdt = m.dt;
         l.N = N;
@@ -294,7 +349,7 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
         bool any_bias = false;
         int N = 0;
         for (size_t i = 0; i < pres.size(); ++i) {
-            HostMat m = src.h16(pres[i] + ".weight", (size_t)Ns[i] * K);
+            HostMat m = src.h16(pres[i] + ".weight", (size_t)Ns[i] * K, Ns[i], K);
             if (i == 0) all.dt = m.dt;
             else if (m.dt != all.dt) throw std::runtime_error("EINVAL: mixed dtypes in fused linear " + pres[i]);
             all.data.insert(all.data.end(), m.data.begin(), m.data.end());
@@ -448,9 +503,9 @@ void Engine::load_weights(const std::string& path, uint64_t seed) {
             dn.data.resize((size_t)E * H * I);
             for (int e = 0; e < E; ++e) {
                 const std::string ep = lp + "mlp.experts." + std::to_string(e) + ".";
-                HostMat g = src.h16(ep + "gate_proj.weight", (size_t)I * H);
-                HostMat u = src.h16(ep + "up_proj.weight", (size_t)I * H);
-                HostMat w = src.h16(ep + "down_proj.weight", (size_t)H * I);
+                HostMat g = src.h16(ep + "gate_proj.weight", (size_t)I * H, I, H);
+                HostMat u = src.h16(ep + "up_proj.weight", (size_t)I * H, I, H);
+                HostMat w = src.h16(ep + "down_proj.weight", (size_t)H * I, H, I);
                 if (src.has(ep + "gate_proj.bias") || src.has(ep + "down_proj.bias"))
                     throw std::runtime_error("EINVAL: biased experts not supported");
                 std::copy(g.data.begin(), g.data.end(), gu.data.begin() + (size_t)e * 2 * I * H);

@@ -121,7 +121,8 @@ typedef void (*TokenCb)(size_t, const int64_t*, void*);
 
 class Engine {
   public:
-    Engine(const std::string& config_path, const std::string& weights_path, int device, int dtype, uint64_t seed);
+    Engine(const std::string& config_path, const std::string& weights_path, int device, int dtype, uint64_t seed,
+           const std::string& snapshot_path = "");
     ~Engine();
 
     const ModelConfig& cfg() const { return cfg_; }
@@ -147,7 +148,7 @@ class Engine {
 
   private:
     // ---- loading
-    void load_weights(const std::string& path, uint64_t seed);
+    void load_weights(const std::string& path, uint64_t seed, const std::string& snapshot_path);
     // ---- workspace
     void* ws(const std::string& name, size_t bytes);
     float* wsf(const std::string& name, size_t n) { return (float*)ws(name, n * sizeof(float)); }

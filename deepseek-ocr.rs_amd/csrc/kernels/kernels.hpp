@@ -294,4 +294,10 @@ void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s);
 void lmhead_q8_grid(int N, int K, int B, int* nblk, long* slot);
 void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s);
 
+// DSQ snapshot tensors (dsq.hip): dtype codes of crates/dsq/src/lib.rs:60-110; decode a record's
+// payload ([out][in], row-major blocks) into fp16 on the device
+constexpr int DSQ_F32 = 0, DSQ_F16 = 1, DSQ_Q8_0 = 8, DSQ_Q4K = 12, DSQ_Q6K = 14, DSQ_BF16 = 16;
+size_t dsq_payload_bytes(int qtype, long out_dim, long in_dim);
+void launch_dsq_dequant(int qtype, const void* src, long out_dim, long in_dim, void* out_f16, hipStream_t s);
+
 }  // namespace dsocr

@@ -74,7 +74,7 @@ EXPORTS = [
     "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
-    "dsocr_k_sample_greedy",
+    "dsocr_k_sample_greedy", "dsocr_k_dsq_dequant",
 ]
 
 _lib = None
@@ -116,6 +116,7 @@ def lib():
     L.dsocr_k_gemv.argtypes = [i32, i32, i32, vp, vp, f32, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_layernorm.argtypes = [i32, i32, vp, vp, vp, f32, vp]
     L.dsocr_k_rmsnorm.argtypes = [i32, i32, vp, vp, f32, vp]
+    L.dsocr_k_dsq_dequant.argtypes = [i32, vp, sz, sz, sz, vp]
     L.dsocr_k_attention.argtypes = [i32, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp, vp, i32, i32]
     L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]

@@ -46,7 +46,9 @@ typedef struct dsocr_page_pixels dsocr_page_pixels;
 typedef struct {
     const char* config_path;
     const char* weights_path;
-    const char* snapshot_path; /* .dsq snapshot: not supported yet -> DSOCR_EINVAL */
+    const char* snapshot_path; /* optional .dsq snapshot (crates/dsq): its Q4_K / Q6_K / Q8_0 / float linears
+                                  replace the checkpoint's, decoded to fp16 on the GPU at load (dtype must be
+                                  DSOCR_F16); NULL = none */
     int device_ordinal;
     dsocr_dtype dtype;
     uint64_t synthetic_seed;
@@ -193,6 +195,11 @@ dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm
                           int wdtype, const float* bias, float* y, int act, int accumulate);
 dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* w, const float* b, float eps,
                                float* y);
+/* DSQ record payload (device bytes, crates/dsq/src/lib.rs:60-110 dtype codes 0/1/8/12/14/16) ->
+ * fp16 [out_dim][in_dim] on the device; replaces dsq-runtime's qtensor_from_ggml + QMatMul for the
+ * dequant-on-load path (crates/dsq-runtime/src/lib.rs:336-366). */
+dsocr_status dsocr_k_dsq_dequant(int qtype, const void* src, size_t src_bytes, size_t out_dim, size_t in_dim,
+                                 void* out_f16);
 dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w, float eps, float* y);
 /* softmax(scale * q.k^T [+ SAM decomposed rel-pos] [causal]) . v over n_seq uniform sequences of L
  * rows; q,k,v,o are [n_seq*L][heads*hd]; relh/relw (optional) are the resized [2g-1][hd] tables of

@@ -91,9 +91,14 @@ def is_language_tensor(name: str) -> bool:
 class Weights:
     """name -> f32 numpy array, applying the dtype rule above."""
 
-    def __init__(self, path: str | None = None, seed: int | None = None, dtype: str = "f16", shapes=None):
+    def __init__(self, path: str | None = None, seed: int | None = None, dtype: str = "f16", shapes=None,
+                 snapshot=None):
         assert (path is None) != (seed is None), "exactly one of path / seed"
         self.path, self.seed, self.dtype = path, seed, dtype
+        # oracle.dsq.Snapshot: its records replace the base tensors, dequantised and stored fp16
+        # (BASELINE config 5, dequant-on-load); a snapshot linear's bias comes from its record only
+        # (crates/dsq-runtime/src/lib.rs:336-366)
+        self.snapshot = snapshot
         self._cache = {}
         self._st = None
         if path is not None:
@@ -117,7 +122,19 @@ class Weights:
             raise ValueError(f"shape mismatch for {name}: {arr.shape} vs {shape}")
         return arr
 
+    def _snap_bias_owner(self, name):
+        if self.snapshot is None or not name.endswith(".bias"):
+            return None
+        w = name[:-5] + ".weight"
+        return w if self.snapshot.has(w) else None
+
     def has(self, name) -> bool:
+        if self.snapshot is not None:
+            if self.snapshot.has(name):
+                return True
+            owner = self._snap_bias_owner(name)
+            if owner is not None:
+                return self.snapshot.bias_for(owner) is not None
         if self.seed is not None:
             return synthetic_has(name)
         if self._st is None:
@@ -129,6 +146,20 @@ class Weights:
             return self._cache[name]
         if shape is None:
             shape = self.shapes[name] if self.shapes is not None else None
+        if self.snapshot is not None and self.snapshot.has(name):
+            a = round_f16(self.snapshot.weight(name))
+            if shape is not None and a.size != int(np.prod(shape)):
+                raise ValueError(f"snapshot tensor {name} dims mismatch")
+            a = np.ascontiguousarray(a.reshape(shape) if shape is not None else a, dtype=np.float32)
+            self._cache[name] = a
+            return a
+        owner = self._snap_bias_owner(name)
+        if owner is not None:
+            b = self.snapshot.bias_for(owner)
+            if b is None:
+                raise KeyError(name)
+            self._cache[name] = np.ascontiguousarray(b, dtype=np.float32)
+            return self._cache[name]
         a = self._raw_f32(name, tuple(shape) if shape is not None else None)
         if self.dtype == "f16" and is_language_tensor(name):
             a = round_f16(a)
