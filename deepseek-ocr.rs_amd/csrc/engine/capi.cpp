@@ -140,6 +140,36 @@ dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t w, uint32_t h, cons
     });
 }
 
+dsocr_status dsocr_prepare_page_device(dsocr_engine* e, const uint8_t* rgb, uint32_t w, uint32_t h,
+                                       const dsocr_vision_settings* vs, dsocr_page_pixels** out) {
+    return guarded([&] {
+        if (!e || !rgb || !vs || !out) throw std::runtime_error("EINVAL: NULL argument");
+        auto* p = new dsocr_page_pixels;
+        p->px.base = (int)vs->base_size;
+        p->px.tile = (int)vs->image_size;
+        p->px.crop = vs->crop_mode != 0;
+        try {
+            e->impl->prepare_page_device(rgb, (int)w, (int)h, p->px);
+        } catch (...) {
+            delete p;
+            throw;
+        }
+        *out = p;
+    });
+}
+
+dsocr_status dsocr_page_read_device(const dsocr_page_pixels* p, float* global_out, float* tiles_out) {
+    return guarded([&] {
+        if (!p) throw std::runtime_error("EINVAL: NULL page");
+        if (!p->px.global_dev) throw std::runtime_error("EINVAL: page has no device pixels");
+        const size_t G = (size_t)p->px.gsize, T = (size_t)p->px.tile;
+        check_hip(hipSetDevice(p->px.dev_ordinal), "hipSetDevice");
+        if (global_out) check_hip(hipMemcpy(global_out, p->px.global_dev, 3 * G * G * 4, hipMemcpyDeviceToHost), "d2h");
+        if (tiles_out && p->px.tiles_dev)
+            check_hip(hipMemcpy(tiles_out, p->px.tiles_dev, (size_t)p->px.n_tiles * 3 * T * T * 4, hipMemcpyDeviceToHost), "d2h");
+    });
+}
+
 void dsocr_page_free(dsocr_page_pixels* p) { delete p; }
 
 dsocr_status dsocr_page_to_device(dsocr_engine* e, dsocr_page_pixels* p) {
@@ -163,9 +193,9 @@ dsocr_status dsocr_page_pixels_view(const dsocr_page_pixels* p, const float** g,
                                     uint32_t* ts) {
     return guarded([&] {
         if (!p) throw std::runtime_error("EINVAL: NULL page");
-        if (g) *g = p->px.global_chw.data();
+        if (g) *g = p->px.global_chw.empty() ? nullptr : p->px.global_chw.data();
         if (gs) *gs = p->px.gsize;
-        if (t) *t = p->px.n_tiles ? p->px.tiles_chw.data() : nullptr;
+        if (t) *t = p->px.tiles_chw.empty() ? nullptr : p->px.tiles_chw.data();
         if (ts) *ts = p->px.tile;
     });
 }

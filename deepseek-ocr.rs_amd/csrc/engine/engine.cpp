@@ -237,6 +237,7 @@ void* Engine::pinned(const std::string& name, size_t bytes) {
 // gathers them device-to-device.
 void Engine::upload_page(PagePixels& pg) {
     if (pg.global_dev && pg.dev_ordinal == device_) return;
+    if (pg.global_chw.empty()) throw std::runtime_error("EINVAL: page pixels live on another device");
     if (pg.global_dev) { (void)hipFree(pg.global_dev); pg.global_dev = nullptr; }
     if (pg.tiles_dev) { (void)hipFree(pg.tiles_dev); pg.tiles_dev = nullptr; }
     HIP_CHECK(hipMalloc(&pg.global_dev, pg.global_chw.size() * 4));
@@ -246,6 +247,72 @@ void Engine::upload_page(PagePixels& pg) {
         HIP_CHECK(hipMemcpy(pg.tiles_dev, pg.tiles_chw.data(), pg.tiles_chw.size() * 4, hipMemcpyHostToDevice));
     }
     pg.dev_ordinal = device_;
+}
+
+// a1-a3 on the GPU (preprocess.hip): the page's RGB8 bytes go up once; the tap tables and the
+// geometry come from the host functions the host path uses; the f32 CHW tensors are produced in
+// HBM (px.global_dev / px.tiles_dev), bit-identical to dsocr_prepare_page's arrays
+void Engine::prepare_page_device(const uint8_t* rgb, int w, int h, PagePixels& px) {
+    hipStream_t st = stream_;
+    const int G = px.crop ? px.base : px.tile;  // model/mod.rs:1714
+    px.gsize = G;
+    if (px.global_dev) { (void)hipFree(px.global_dev); px.global_dev = nullptr; }
+    if (px.tiles_dev) { (void)hipFree(px.tiles_dev); px.tiles_dev = nullptr; }
+    HIP_CHECK(hipMalloc(&px.global_dev, (size_t)3 * G * G * 4));
+    const size_t nbytes = (size_t)w * h * 3;
+    uint8_t* d_rgb = nbytes ? (uint8_t*)ws("pp_rgb", nbytes) : nullptr;
+    if (nbytes) HIP_CHECK(hipMemcpyAsync(d_rgb, rgb, nbytes, hipMemcpyHostToDevice, st));
+    auto upload_taps = [&](const ResampleCoeffs& rc, const char* name) -> std::pair<int*, int*> {
+        std::vector<int> b(rc.bounds.size() * 2);
+        for (size_t i = 0; i < rc.bounds.size(); ++i) { b[2 * i] = rc.bounds[i].first; b[2 * i + 1] = rc.bounds[i].second; }
+        int* db = (int*)ws(std::string(name) + "_b", b.size() * 4);
+        int* dc = (int*)ws(std::string(name) + "_c", rc.coeffs.size() * 4);
+        HIP_CHECK(hipMemcpyAsync(db, b.data(), b.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(dc, rc.coeffs.data(), rc.coeffs.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));  // the host tables die with this lambda
+        return {db, dc};
+    };
+    // ---- global view
+    PpOut g;
+    g.mode = 0; g.size = G; g.n_out = 1; g.out = px.global_dev;
+    if (w > 0 && h > 0) {
+        int nw, nh, xo, yo;
+        global_view_geometry(w, h, G, &nw, &nh, &xo, &yo);
+        const ResampleCoeffs cx = compute_resample_coeffs(w, nw), cy = compute_resample_coeffs(h, nh);
+        auto tx = upload_taps(cx, "pp_gx");
+        auto ty = upload_taps(cy, "pp_gy");
+        uint8_t* hz = (uint8_t*)ws("pp_hz", (size_t)h * nw * 3);
+        launch_pp_resize_h(d_rgb, w, h, tx.first, tx.second, cx.ksize, nw, hz, st);
+        g.hz = hz; g.dw = nw; g.bounds = ty.first; g.coeffs = ty.second; g.ksize = cy.ksize;
+        g.ox = xo; g.oy = yo; g.nw = nw; g.nh = nh;
+    }
+    launch_pp_resize_v_chw(g, st);
+    // ---- tiles (vision/preprocess.rs:67-138, PreprocessParams::ocr1: 2..9 tiles)
+    px.n_tiles = 0;
+    px.crop_w = px.crop_h = 1;
+    int gw = 1, gh = 1;
+    if (px.crop && w > 0 && h > 0 && choose_tile_grid(w, h, px.tile, 2, 9, &gw, &gh)) {
+        const int T = px.tile, tw = T * gw, th = T * gh;
+        px.crop_w = gw;
+        px.crop_h = gh;
+        px.n_tiles = gw * gh;
+        HIP_CHECK(hipMalloc(&px.tiles_dev, (size_t)px.n_tiles * 3 * T * T * 4));
+        const ResampleCoeffs cx = compute_resample_coeffs(w, tw), cy = compute_resample_coeffs(h, th);
+        auto tx = upload_taps(cx, "pp_tx");
+        auto ty = upload_taps(cy, "pp_ty");
+        uint8_t* hz = (uint8_t*)ws("pp_thz", (size_t)h * tw * 3);
+        launch_pp_resize_h(d_rgb, w, h, tx.first, tx.second, cx.ksize, tw, hz, st);
+        PpOut t;
+        t.mode = 1; t.size = T; t.n_out = px.n_tiles; t.grid_w = gw; t.out = px.tiles_dev;
+        t.hz = hz; t.dw = tw; t.bounds = ty.first; t.coeffs = ty.second; t.ksize = cy.ksize;
+        launch_pp_resize_v_chw(t, st);
+    }
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(st));
+    px.global_chw.clear();
+    px.tiles_chw.clear();
+    px.dev_ordinal = device_;
+    px.n_image_tokens = image_placeholder_count(px.base, px.tile, px.crop, px.crop_w, px.crop_h);
 }
 
 Engine::~Engine() {
@@ -797,7 +864,7 @@ std::vector<std::vector<float>> Engine::image_embeddings(const std::vector<const
     const int H = cfg_.proj_out;
     for (const PagePixels* p : pages) {
         // one page at a time keeps this helper simple; generate() batches pages.
-        float* gimg = upload("e_gimg", p->global_chw);
+        float* gimg = p->global_dev && p->dev_ordinal == device_ ? p->global_dev : upload("e_gimg", p->global_chw);
         float* gpost = vision_pass(gimg, 1, p->gsize, "e_gpost");
         const int gs = p->gsize / 64;
         std::vector<float> gh((size_t)gs * gs * H);
@@ -805,7 +872,7 @@ std::vector<std::vector<float>> Engine::image_embeddings(const std::vector<const
         std::vector<float> lh;
         int ls = 0;
         if (p->n_tiles > 0) {
-            float* timg = upload("e_timg", p->tiles_chw);
+            float* timg = p->tiles_dev && p->dev_ordinal == device_ ? p->tiles_dev : upload("e_timg", p->tiles_chw);
             float* lpost = vision_pass(timg, p->n_tiles, p->tile, "e_lpost");
             ls = p->tile / 64;
             lh.resize((size_t)p->n_tiles * ls * ls * H);
@@ -1193,29 +1260,29 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     std::vector<float*> pass_outputs;
     int pass_id = 0;
     // pixels of one size group as one contiguous device batch: device-to-device gathers of
-    // HBM-resident pages (dsocr_page_to_device), else one staged host upload
+    // HBM-resident pages (dsocr_page_to_device / dsocr_prepare_page_device), host uploads otherwise
     auto gather = [&](const std::vector<int>& pages, bool tiles, size_t n_floats) -> float* {
         const std::string name = "g_img" + std::to_string(pass_id);
-        bool resident = true;
-        for (int b : pages) resident &= (tiles ? reqs[b].page->tiles_dev : reqs[b].page->global_dev) != nullptr &&
-                                         reqs[b].page->dev_ordinal == device_;
-        if (!resident) {
-            std::vector<float> imgs;
-            imgs.reserve(n_floats);
-            for (int b : pages) {
-                const auto& v = tiles ? reqs[b].page->tiles_chw : reqs[b].page->global_chw;
-                imgs.insert(imgs.end(), v.begin(), v.end());
-            }
-            return upload(name, imgs);
-        }
         float* d = wsf(name, n_floats);
         size_t off = 0;
+        bool host_copy = false;
         for (int b : pages) {
-            const size_t nf = tiles ? reqs[b].page->tiles_chw.size() : reqs[b].page->global_chw.size();
-            HIP_CHECK(hipMemcpyAsync(d + off, tiles ? reqs[b].page->tiles_dev : reqs[b].page->global_dev, nf * 4,
-                                     hipMemcpyDeviceToDevice, st));
+            const PagePixels& pg = *reqs[b].page;
+            const size_t nf = tiles ? (size_t)pg.n_tiles * 3 * pg.tile * pg.tile : (size_t)3 * pg.gsize * pg.gsize;
+            const float* dev = tiles ? pg.tiles_dev : pg.global_dev;
+            const std::vector<float>& host = tiles ? pg.tiles_chw : pg.global_chw;
+            if (dev && pg.dev_ordinal == device_)
+                HIP_CHECK(hipMemcpyAsync(d + off, dev, nf * 4, hipMemcpyDeviceToDevice, st));
+            else if (host.size() == nf) {
+                HIP_CHECK(hipMemcpyAsync(d + off, host.data(), nf * 4, hipMemcpyHostToDevice, st));
+                host_copy = true;
+            }
+            else
+                throw std::runtime_error("EINVAL: page pixels live on another device");
             off += nf;
         }
+        if (off != n_floats) throw std::runtime_error("EINTERNAL: pixel batch size mismatch");
+        if (host_copy) HIP_CHECK(hipStreamSynchronize(st));  // host sources may be pageable temporaries
         return d;
     };
     for (auto& kv : gsz) {

@@ -145,6 +145,7 @@ class Engine {
     DecodeProfile profile_decode(int iters);
     hipStream_t stream() const { return stream_; }
     void upload_page(PagePixels& pg);
+    void prepare_page_device(const uint8_t* rgb, int w, int h, PagePixels& px);
 
   private:
     // ---- loading

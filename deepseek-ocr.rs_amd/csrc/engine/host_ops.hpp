@@ -120,17 +120,23 @@ inline double round_ties_to_even(double v) {
     return ((long)t % 2 == 0) ? t : t + (v > 0 ? 1.0 : -1.0);
 }
 
-// model/mod.rs:2308-2330
+// model/mod.rs:2308-2330: size and placement of the resized page on the base x base canvas
+inline void global_view_geometry(int w, int h, int base, int* nw, int* nh, int* xo, int* yo) {
+    double scale = std::min((double)base / w, (double)base / h);
+    *nw = (int)std::min(std::max(round_ties_to_even(w * scale), 1.0), (double)base);
+    *nh = (int)std::min(std::max(round_ties_to_even(h * scale), 1.0), (double)base);
+    *xo = (int)round_ties_to_even((base - *nw) * 0.5);
+    *yo = (int)round_ties_to_even((base - *nh) * 0.5);
+}
+
 inline std::vector<uint8_t> build_global_view(const uint8_t* rgb, int w, int h, int base) {
     const uint8_t mean = (uint8_t)(0.5 * 255.0);
     std::vector<uint8_t> canvas((size_t)base * base * 3, mean);
     if (w == 0 || h == 0) return canvas;
-    double scale = std::min((double)base / w, (double)base / h);
-    int nw = (int)std::min(std::max(round_ties_to_even(w * scale), 1.0), (double)base);
-    int nh = (int)std::min(std::max(round_ties_to_even(h * scale), 1.0), (double)base);
+    int nw, nh, xo, yo;
+    global_view_geometry(w, h, base, &nw, &nh, &xo, &yo);
     std::vector<uint8_t> rs((size_t)nw * nh * 3);
     resize_bicubic(rgb, w, h, rs.data(), nw, nh);
-    int xo = (int)round_ties_to_even((base - nw) * 0.5), yo = (int)round_ties_to_even((base - nh) * 0.5);
     for (int y = 0; y < nh; ++y) {
         int cyy = y + yo;
         if (cyy < 0 || cyy >= base) continue;
@@ -143,11 +149,10 @@ inline std::vector<uint8_t> build_global_view(const uint8_t* rgb, int w, int h, 
     return canvas;
 }
 
-// vision/preprocess.rs:67-138 -> tiles (row-major) and grid (w, h)
-inline std::vector<std::vector<uint8_t>> dynamic_preprocess(const uint8_t* rgb, int w, int h, int tile, int min_num,
-                                                            int max_num, int* grid_w, int* grid_h) {
-    std::vector<std::vector<uint8_t>> tiles;
-    if (w <= tile && h <= tile) { *grid_w = 1; *grid_h = 1; return tiles; }
+// vision/preprocess.rs:67-138: the tile grid (closest aspect ratio, larger grid on ties when the
+// page area exceeds half of it); false when the page needs no tiles
+inline bool choose_tile_grid(int w, int h, int tile, int min_num, int max_num, int* grid_w, int* grid_h) {
+    if (w <= tile && h <= tile) { *grid_w = 1; *grid_h = 1; return false; }
     const double aspect = (double)w / (double)h;
     std::set<std::pair<int, int>> ratios;
     for (int n = min_num; n <= max_num; ++n)
@@ -164,6 +169,17 @@ inline std::vector<std::vector<uint8_t>> dynamic_preprocess(const uint8_t* rgb, 
                  area > 0.5 * (double)((long)tile * tile * r.first * r.second))
             best = r;
     }
+    *grid_w = best.first;
+    *grid_h = best.second;
+    return true;
+}
+
+// vision/preprocess.rs:67-138 -> tiles (row-major) and grid (w, h)
+inline std::vector<std::vector<uint8_t>> dynamic_preprocess(const uint8_t* rgb, int w, int h, int tile, int min_num,
+                                                            int max_num, int* grid_w, int* grid_h) {
+    std::vector<std::vector<uint8_t>> tiles;
+    if (!choose_tile_grid(w, h, tile, min_num, max_num, grid_w, grid_h)) return tiles;
+    const std::pair<int, int> best{*grid_w, *grid_h};
     const int tw = tile * best.first, th = tile * best.second;
     std::vector<uint8_t> rs((size_t)tw * th * 3);
     resize_bicubic(rgb, w, h, rs.data(), tw, th);

@@ -300,4 +300,20 @@ constexpr int DSQ_F32 = 0, DSQ_F16 = 1, DSQ_Q8_0 = 8, DSQ_Q4K = 12, DSQ_Q6K = 14
 size_t dsq_payload_bytes(int qtype, long out_dim, long in_dim);
 void launch_dsq_dequant(int qtype, const void* src, long out_dim, long in_dim, void* out_f16, hipStream_t s);
 
+// Page preprocessing on the GPU (preprocess.hip): Pillow 22-bit bicubic (tap tables from the host),
+// then a vertical pass fused with canvas placement / tile cropping and the CHW normalisation
+struct PpOut {
+    const uint8_t* hz = nullptr; int dw = 0;                          // horizontal-pass rows [*][dw][3]
+    const int* bounds = nullptr; const int* coeffs = nullptr; int ksize = 0;  // vertical taps
+    int mode = 0;            // 0 global canvas, 1 tiles
+    int size = 0;            // G or T
+    int n_out = 1;           // 1 (global) or number of tiles
+    int ox = 0, oy = 0, nw = 0, nh = 0;  // global: resized image placement
+    int grid_w = 1;          // tiles per row
+    float* out = nullptr;    // [n_out][3][size][size]
+};
+void launch_pp_resize_h(const uint8_t* src, int sw, int sh, const int* bounds, const int* coeffs, int ksize, int dw,
+                        uint8_t* hz, hipStream_t s);
+void launch_pp_resize_v_chw(const PpOut& a, hipStream_t s);
+
 }  // namespace dsocr

@@ -74,7 +74,7 @@ EXPORTS = [
     "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
-    "dsocr_k_sample_greedy", "dsocr_k_dsq_dequant",
+    "dsocr_k_sample_greedy", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
 ]
 
 _lib = None
@@ -95,6 +95,8 @@ def lib():
     L.dsocr_engine_info.argtypes = [vp, C.POINTER(sz), C.POINTER(sz), C.POINTER(i64), C.POINTER(sz)]
     L.dsocr_prepare_page.argtypes = [vp, u32, u32, C.POINTER(VisionSettingsC), C.POINTER(vp)]
     L.dsocr_page_free.argtypes = [vp]
+    L.dsocr_prepare_page_device.argtypes = [vp, vp, u32, u32, C.POINTER(VisionSettingsC), C.POINTER(vp)]
+    L.dsocr_page_read_device.argtypes = [vp, vp, vp]
     L.dsocr_page_free.restype = None
     L.dsocr_page_to_device.argtypes = [vp, vp]
     L.dsocr_page_info.argtypes = [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(sz)]

@@ -99,9 +99,12 @@ def build_prompt_tokens(tokenizer, prompt: str, image_token_counts: Sequence[int
 
 
 class Page:
-    """Preprocessed page pixels (a1-a3, host C++): global view + crop tiles."""
+    """Preprocessed page pixels (a1-a3): global view + crop tiles.
 
-    def __init__(self, rgb, vision: VisionSettings):
+    ``engine=None``: host C++ (dsocr_prepare_page); with an engine: on that engine's GPU
+    (dsocr_prepare_page_device, bit-identical pixels, device-resident)."""
+
+    def __init__(self, rgb, vision: VisionSettings, engine=None):
         if hasattr(rgb, "convert"):  # PIL image
             rgb = np.asarray(rgb.convert("RGB"))
         rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
@@ -109,8 +112,13 @@ class Page:
             raise DsocrError(1, "page must be HxWx3 uint8")
         vs = VisionSettingsC(vision.base_size, vision.image_size, 1 if vision.crop_mode else 0)
         h = C.c_void_p()
-        check(lib().dsocr_prepare_page(rgb.ctypes.data_as(C.c_void_p), rgb.shape[1], rgb.shape[0], C.byref(vs),
-                                       C.byref(h)))
+        if engine is None:
+            check(lib().dsocr_prepare_page(rgb.ctypes.data_as(C.c_void_p), rgb.shape[1], rgb.shape[0], C.byref(vs),
+                                           C.byref(h)))
+        else:
+            check(lib().dsocr_prepare_page_device(engine._h, rgb.ctypes.data_as(C.c_void_p), rgb.shape[1],
+                                                  rgb.shape[0], C.byref(vs), C.byref(h)))
+        self.on_device = engine is not None
         self._h = h
         cw, ch, nt, ntok = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_size_t()
         check(lib().dsocr_page_info(h, C.byref(cw), C.byref(ch), C.byref(nt), C.byref(ntok)))
@@ -126,6 +134,12 @@ class Page:
     def pixels(self):
         g, gs, t, ts = C.c_void_p(), C.c_uint32(), C.c_void_p(), C.c_uint32()
         check(lib().dsocr_page_pixels_view(self._h, C.byref(g), C.byref(gs), C.byref(t), C.byref(ts)))
+        if self.on_device:
+            glob = np.empty((3, gs.value, gs.value), np.float32)
+            tiles = np.empty((self.n_tiles, 3, ts.value, ts.value), np.float32) if self.n_tiles else None
+            check(lib().dsocr_page_read_device(self._h, glob.ctypes.data_as(C.c_void_p),
+                                               tiles.ctypes.data_as(C.c_void_p) if tiles is not None else None))
+            return glob, tiles
         glob = np.ctypeslib.as_array(C.cast(g, C.POINTER(C.c_float)), (3, gs.value, gs.value)).copy()
         tiles = None
         if self.n_tiles:

@@ -120,6 +120,14 @@ dsocr_status dsocr_engine_info(const dsocr_engine* e, size_t* hidden, size_t* vo
  *      preprocess.rs:67-138, image_to_tensor 2332-2347).  rgb: HWC uint8. */
 dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t width, uint32_t height,
                                 const dsocr_vision_settings* vs, dsocr_page_pixels** out);
+/* a1-a3 on the GPU of `e` (vision/resample.rs + preprocess.rs + model/mod.rs:2295-2347, the same
+ * results as dsocr_prepare_page bit for bit): only the RGB8 bytes cross PCIe, the f32 CHW tensors
+ * are produced in HBM.  The page's pixels are device-resident only (dsocr_page_pixels_view returns
+ * NULL arrays; dsocr_page_read_device copies them back). */
+dsocr_status dsocr_prepare_page_device(dsocr_engine* e, const uint8_t* rgb, uint32_t w, uint32_t h,
+                                       const dsocr_vision_settings* vs, dsocr_page_pixels** out);
+dsocr_status dsocr_page_read_device(const dsocr_page_pixels* p, float* global_out /* [3][G][G] */,
+                                    float* tiles_out /* [n_tiles][3][T][T] or NULL */);
 void dsocr_page_free(dsocr_page_pixels* p);
 /* Stage the page's preprocessed pixels in the engine's device memory (HBM) once, e.g. ahead of
  * a timed or latency-critical generate; later calls gather them device-to-device.  The device
