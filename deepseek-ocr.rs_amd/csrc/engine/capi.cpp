@@ -49,7 +49,10 @@ void check_hip(hipError_t e, const char* what) {
 
 dsocr::GenParams to_params(const dsocr_decode_params* p) {
     if (!p) throw std::runtime_error("EINVAL: decode params are NULL");
-    if (p->do_sample) throw std::runtime_error("EINVAL: do_sample is not supported by the MI355X engine (greedy only)");
+    // select_token_id samples only when do_sample && temperature > 0 (sampling.rs:67); otherwise it is the
+    // greedy path this engine runs.
+    if (p->do_sample && p->temperature > 0.0)
+        throw std::runtime_error("EINVAL: do_sample with temperature > 0 is not supported by the MI355X engine (greedy only)");
     if (!p->use_cache) throw std::runtime_error("EINVAL: use_cache=false is not supported (generate_without_cache)");
     dsocr::GenParams g;
     g.max_new = p->max_new_tokens;

@@ -280,7 +280,7 @@ class DeepseekOcrEngine:
     # ------------------------------------------------------------------ OcrEngine::decode
     def decode(self, tokenizer, prompt: str, images: Sequence, vision: VisionSettings,
                params: DecodeParameters, stream: Optional[Callable] = None) -> DecodeOutcome:
-        pages = [Page(im, vision) for im in images]
+        pages = [Page(im, vision, self) for im in images]
         ids, mask = build_prompt_tokens(tokenizer, prompt, [p.n_image_tokens for p in pages])
         if len(pages) > 1:
             raise DsocrError(1, "multiple images per prompt are not supported by this engine yet")

@@ -64,7 +64,7 @@ typedef struct {
 /* DecodeParameters (core/src/inference.rs:21-79) + generation options (model/mod.rs:177-218). */
 typedef struct {
     size_t max_new_tokens;
-    int do_sample;               /* sampling is not on this engine's path: must be 0 */
+    int do_sample;               /* with temperature > 0 sampling is requested: EINVAL (greedy engine); else greedy, as sampling.rs:67 */
     double temperature;
     double top_p;                /* <= 0 or >= 1: unset */
     size_t top_k;                /* 0: unset */
