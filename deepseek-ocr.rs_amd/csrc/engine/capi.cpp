@@ -51,8 +51,6 @@ dsocr::GenParams to_params(const dsocr_decode_params* p) {
     if (!p) throw std::runtime_error("EINVAL: decode params are NULL");
     // select_token_id samples only when do_sample && temperature > 0 (sampling.rs:67); otherwise it is the
     // greedy path this engine runs.
-    if (p->do_sample && p->temperature > 0.0)
-        throw std::runtime_error("EINVAL: do_sample with temperature > 0 is not supported by the MI355X engine (greedy only)");
     if (!p->use_cache) throw std::runtime_error("EINVAL: use_cache=false is not supported (generate_without_cache)");
     dsocr::GenParams g;
     g.max_new = p->max_new_tokens;
@@ -60,6 +58,14 @@ dsocr::GenParams to_params(const dsocr_decode_params* p) {
     g.ngram = p->no_repeat_ngram_size > 1 ? (int)p->no_repeat_ngram_size : 0;
     g.eos = p->eos_token_id;
     g.ignore_eos = p->ignore_eos != 0;
+    // select_token_id samples only when do_sample && temperature > 0 (sampling.rs:67); otherwise
+    // it is the greedy path
+    g.do_sample = p->do_sample != 0 && p->temperature > 0.0;
+    g.temperature = p->temperature;
+    g.top_p = p->top_p;
+    g.top_k = (long)p->top_k;
+    g.seed_set = p->has_seed != 0;
+    g.seed = p->seed;
     return g;
 }
 
@@ -512,6 +518,53 @@ dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, 
         hipError_t e = hipDeviceSynchronize();
         (void)hipFree(ridx); (void)hipFree(rval); (void)hipFree(done);
         check_hip(e, "sample");
+    });
+}
+
+dsocr_status dsocr_k_sample_stoch(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,
+                                  int ngram, float rep_penalty, double temperature, size_t top_k, double top_p,
+                                  uint64_t seed, int draws, int* out_tok) {
+    return guarded([&] {
+        if (B <= 0 || V <= 0 || draws <= 0 || !(temperature > 0.0)) throw std::runtime_error("EINVAL: bad sampling arguments");
+        const int rb = (int)dsocr::dec_sample_blocks(V);
+        std::vector<void*> bufs;
+        auto dalloc = [&](size_t bytes) {
+            void* p = nullptr;
+            check_hip(hipMalloc(&p, bytes), "hipMalloc");
+            bufs.push_back(p);
+            return p;
+        };
+        try {
+            int* ridx = (int*)dalloc(sizeof(int) * B * rb);
+            float* rval = (float*)dalloc(sizeof(float) * B * rb);
+            int* done = (int*)dalloc(sizeof(int) * B);
+            check_hip(hipMemset(done, 0, sizeof(int) * B), "hipMemset");
+            dsocr::SampleArgs p;
+            p.logits = logits; p.B = B; p.V = V; p.ld = V; p.ctx = ctx; p.ctx_cap = ctx_cap; p.ctx_len = ctx_len;
+            p.rep_penalty = rep_penalty;
+            dsocr::launch_rep_penalty(p, nullptr);
+            dsocr::DecSampleArgs a;
+            a.logits = logits; a.B = B; a.V = V; a.ld = V; a.ctx = const_cast<int*>(ctx); a.ctx_cap = ctx_cap;
+            a.ctx_len = const_cast<int*>(ctx_len); a.ngram = ngram; a.red_val = rval; a.red_idx = ridx; a.done = done;
+            a.do_sample = 1; a.temperature = temperature; a.top_k = (long)top_k; a.top_p = top_p; a.st_ld = V;
+            a.st_key = (uint32_t*)dalloc(sizeof(uint32_t) * 2 * (size_t)B * V);
+            a.st_idx = (int*)dalloc(sizeof(int) * 2 * (size_t)B * V);
+            a.st_w = (double*)dalloc(sizeof(double) * (size_t)B * V);
+            const std::vector<uint32_t> st = dsocr::rng_state_from_u64(seed);
+            a.rng = (uint32_t*)dalloc(sizeof(uint32_t) * dsocr::RNG_WORDS * B);
+            for (int b = 0; b < B; ++b)
+                check_hip(hipMemcpy(a.rng + (size_t)b * dsocr::RNG_WORDS, st.data(), sizeof(uint32_t) * dsocr::RNG_WORDS,
+                                    hipMemcpyHostToDevice), "hipMemcpy");
+            for (int d = 0; d < draws; ++d) {
+                a.out_tok = out_tok + (size_t)d * B;
+                dsocr::launch_dec_sample(a, nullptr);
+            }
+            check_hip(hipDeviceSynchronize(), "sample");
+        } catch (...) {
+            for (void* q : bufs) (void)hipFree(q);
+            throw;
+        }
+        for (void* q : bufs) (void)hipFree(q);
     });
 }
 

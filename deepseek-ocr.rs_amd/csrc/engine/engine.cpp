@@ -3,6 +3,7 @@
 #include "engine.hpp"
 
 #include <chrono>
+#include <random>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -1219,6 +1220,21 @@ void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
     launch_dec_sample(sa, st);
 }
 
+// rand_core 0.6.4 SeedableRng::seed_from_u64 for ChaCha12Rng (rand 0.8.5 StdRng): the 32-byte key
+// is filled by PCG32 (state advanced first, XSH-RR output, little-endian words); block counter 0,
+// stream 0, empty result buffer (sampling.hip reads this layout)
+std::vector<uint32_t> rng_state_from_u64(uint64_t state) {
+    std::vector<uint32_t> st(RNG_WORDS, 0u);
+    for (int i = 0; i < 8; ++i) {
+        state = state * 6364136223846793005ull + 11634580027462260723ull;
+        const uint32_t xorshifted = (uint32_t)(((state >> 18) ^ state) >> 27);
+        const uint32_t rot = (uint32_t)(state >> 59);
+        st[RNG_KEY + i] = (xorshifted >> rot) | (xorshifted << ((32 - rot) & 31));
+    }
+    st[RNG_IDX] = 64;
+    return st;
+}
+
 // ============================================================================ generate
 std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>& reqs, const GenParams& p, TokenCb cb,
                                                    void* user) {
@@ -1480,7 +1496,25 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     sa.out_tok = d_tok; sa.out_ids = d_out; sa.out_len = d_outlen; sa.out_cap = (long)p.max_new; sa.done = d_done;
     sa.eos = p.ignore_eos ? -1 : (int)p.eos;
     sa.table = embed_; sa.table_dt = embed_dt_; sa.H = H; sa.x_next = SX; sa.kv_pos = d_kvpos; sa.kv_len = d_kvlen;
-    if (screen_applies(B, p.rep_penalty)) {
+    if (p.do_sample) {
+        // stochastic selection (sampling.hip): StdRng::seed_from_u64(seed) per page — every page starts
+        // from init_rng(seed) like a single-page generate call (model/mod.rs:1917) — or entropy
+        sa.do_sample = 1; sa.temperature = p.temperature; sa.top_p = p.top_p; sa.top_k = p.top_k;
+        sa.st_ld = L.vocab;
+        sa.st_key = reinterpret_cast<uint32_t*>(wsi("s_stkey", (size_t)B * 2 * L.vocab));
+        sa.st_idx = wsi("s_stidx", (size_t)B * 2 * L.vocab);
+        sa.st_w = reinterpret_cast<double*>(wsf("s_stw", (size_t)B * 2 * L.vocab));
+        uint64_t seed = p.seed;
+        if (!p.seed_set) {
+            std::random_device rd;
+            seed = ((uint64_t)rd() << 32) ^ rd();
+        }
+        const std::vector<uint32_t> st = rng_state_from_u64(seed);
+        std::vector<int> all((size_t)B * RNG_WORDS);
+        for (int b = 0; b < B; ++b) memcpy(&all[(size_t)b * RNG_WORDS], st.data(), sizeof(uint32_t) * RNG_WORDS);
+        sa.rng = reinterpret_cast<uint32_t*>(upload("s_rng", all));
+    }
+    if (!p.do_sample && screen_applies(B, p.rep_penalty)) {
         // the screened head reads the n-gram ban list each selection kernel leaves for the next step
         sa.ban_ld = ctx_cap + 1;
         sa.ban_out = wsi("s_ban", (size_t)B * sa.ban_ld);

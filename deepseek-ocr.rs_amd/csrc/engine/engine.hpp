@@ -116,8 +116,16 @@ struct GenParams {
     int ngram = 20;
     long eos = -1;
     bool ignore_eos = false;
+    // sampling (do_sample && temperature > 0, sampling.rs:67-86); rng = init_rng(seed) per call
+    bool do_sample = false;
+    double temperature = 0.0, top_p = -1.0;
+    long top_k = 0;
+    bool seed_set = false;
+    uint64_t seed = 0;
 };
 typedef void (*TokenCb)(size_t, const int64_t*, void*);
+// rand_core seed_from_u64 for rand 0.8.5 StdRng, in the layout sampling.hip reads (RNG_WORDS words)
+std::vector<uint32_t> rng_state_from_u64(uint64_t seed);
 
 class Engine {
   public:

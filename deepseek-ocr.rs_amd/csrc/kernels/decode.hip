@@ -2753,7 +2753,7 @@ __global__ __launch_bounds__(NT) void dec_sample_final_kernel(DecSampleArgs a) {
 void launch_dec_sample(const DecSampleArgs& a0, hipStream_t s) {
     DecSampleArgs a = a0;
     a.red_blocks = (int)dec_sample_blocks(a.V);
-    const bool screen = a.blk_cnt && a.blk_t && a.cand && a.cand_hi && a.w_exact && a.xn && a.nblk > 0;
+    const bool screen = !a.do_sample && a.blk_cnt && a.blk_t && a.cand && a.cand_hi && a.w_exact && a.xn && a.nblk > 0;
     if (a.ban_out && a.ban_ld < a.ctx_cap + 1) throw std::runtime_error("EINVAL: ban list shorter than the context");
     if (screen) {
         if (a.K % 8 || a.K > 1536) throw std::runtime_error("EINVAL: screened selection needs K % 8 == 0, K <= 1536");
@@ -2761,7 +2761,8 @@ void launch_dec_sample(const DecSampleArgs& a0, hipStream_t s) {
         hipLaunchKernelGGL((dec_screen_final_kernel<1024>), dim3(a.B), dim3(1024), lds, s, a);
         return;
     }
-    if (a.ctx_cap <= 16384) hipLaunchKernelGGL((dec_argmax_partial_kernel<true>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), sizeof(int) * a.ctx_cap, s, a);
+    if (a.do_sample) launch_dec_stoch_select(a, s);  // sampling.hip: the chosen id in selection slot 0
+    else if (a.ctx_cap <= 16384) hipLaunchKernelGGL((dec_argmax_partial_kernel<true>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), sizeof(int) * a.ctx_cap, s, a);
     else hipLaunchKernelGGL((dec_argmax_partial_kernel<false>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), 0, s, a);
     hipLaunchKernelGGL((dec_sample_final_kernel<SP_BLOCK>), dim3(a.B), dim3(SP_BLOCK), 0, s, a);
 }

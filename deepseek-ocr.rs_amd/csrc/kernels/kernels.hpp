@@ -272,8 +272,16 @@ struct DecSampleArgs {
     int nblk = 0; long slot = 0;
     const void* w_exact = nullptr; const float* xn = nullptr; int K = 0;
     unsigned long long* stats = nullptr;  // [steps, kept rows, survivors] accumulated (diagnostics)
+    // stochastic selection (sampling.hip; do_sample && temperature > 0): per-page rand StdRng state
+    // ([B][RNG_WORDS]), top-k (0: off), top-p (active in [0, 1)), scratch of st_ld >= V entries
+    // per page (keys / indices double-buffered: [B][2][st_ld]; f64 weights [B][st_ld])
+    int do_sample = 0; double temperature = 0.0, top_p = -1.0; long top_k = 0;
+    uint32_t* rng = nullptr; uint32_t* st_key = nullptr; int* st_idx = nullptr; double* st_w = nullptr; long st_ld = 0;
 };
+// rand StdRng state words per page: ChaCha12 key, 64-bit block counter, buffer index, 64-word buffer
+constexpr int RNG_KEY = 0, RNG_CTR = 8, RNG_IDX = 10, RNG_BUF = 16, RNG_WORDS = 80;
 void launch_dec_sample(const DecSampleArgs& a, hipStream_t s);
+void launch_dec_stoch_select(const DecSampleArgs& a, hipStream_t s);
 size_t dec_sample_blocks(int V);
 // Screened lm_head (lmhead.hip): int8 rows + per-row scale / error bound give every row an
 // interval [lo, hi] that provably contains the exact kernel's logit; each block keeps the best

@@ -34,7 +34,7 @@ class DecodeParamsC(C.Structure):
     _fields_ = [("max_new_tokens", C.c_size_t), ("do_sample", C.c_int), ("temperature", C.c_double),
                 ("top_p", C.c_double), ("top_k", C.c_size_t), ("repetition_penalty", C.c_float),
                 ("no_repeat_ngram_size", C.c_size_t), ("seed", C.c_uint64), ("use_cache", C.c_int),
-                ("eos_token_id", C.c_int64), ("ignore_eos", C.c_int)]
+                ("eos_token_id", C.c_int64), ("ignore_eos", C.c_int), ("has_seed", C.c_int)]
 
 
 class RequestC(C.Structure):
@@ -74,7 +74,7 @@ EXPORTS = [
     "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
-    "dsocr_k_sample_greedy", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
+    "dsocr_k_sample_greedy", "dsocr_k_sample_stoch", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
 ]
 
 _lib = None
@@ -123,6 +123,8 @@ def lib():
     L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]
     L.dsocr_k_sample_greedy.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, vp]
+    L.dsocr_k_sample_stoch.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, C.c_double, C.c_size_t, C.c_double,
+                                       C.c_uint64, i32, vp]
     _lib = L
     return L
 

@@ -10,9 +10,9 @@ shared flags of crates/config/src/args.rs:9-92.  What differs, and why:
   and shapes), selected by `--synthetic-seed`.
 * `--device` accepts `hip` / `hip:N` (also the reference spellings `cuda` / `cuda:N`, mapped
   to the HIP ordinal); `cpu` / `metal` are refused — the product path has no CPU engine.
-* Sampling flags are parsed like the reference's; the engine runs greedy selection, which is
-  what the reference does unless `do_sample` and `temperature > 0` (sampling.rs:67).  That
-  combination is refused with EINVAL (dsocr_generate), never silently downgraded.
+* Sampling flags behave as the reference's: `--do-sample true --temperature T [--top-k K]
+  [--top-p P] [--seed S]` samples on the GPU with the reference's RNG (sampling.hip); without a
+  positive temperature selection is greedy (sampling.rs:67).
 
 Usage: python -m dsocr.cli --prompt "<image>\\nConvert the document to markdown." --image page.png
 """

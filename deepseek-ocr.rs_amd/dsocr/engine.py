@@ -158,10 +158,11 @@ class Page:
 
 def _params_c(p: DecodeParameters, eos: int, ignore_eos: bool) -> DecodeParamsC:
     return DecodeParamsC(max_new_tokens=p.max_new_tokens, do_sample=1 if p.do_sample else 0,
-                         temperature=p.temperature, top_p=p.top_p if p.top_p is not None else 0.0,
+                         temperature=p.temperature, top_p=p.top_p if p.top_p is not None else -1.0,
                          top_k=p.top_k or 0, repetition_penalty=p.repetition_penalty,
                          no_repeat_ngram_size=p.no_repeat_ngram_size or 0, seed=p.seed or 0,
-                         use_cache=1 if p.use_cache else 0, eos_token_id=eos, ignore_eos=1 if ignore_eos else 0)
+                         use_cache=1 if p.use_cache else 0, eos_token_id=eos, ignore_eos=1 if ignore_eos else 0,
+                         has_seed=0 if p.seed is None else 1)
 
 
 class DeepseekOcrEngine:

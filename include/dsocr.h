@@ -64,16 +64,17 @@ typedef struct {
 /* DecodeParameters (core/src/inference.rs:21-79) + generation options (model/mod.rs:177-218). */
 typedef struct {
     size_t max_new_tokens;
-    int do_sample;               /* with temperature > 0 sampling is requested: EINVAL (greedy engine); else greedy, as sampling.rs:67 */
+    int do_sample;               /* sampling iff do_sample && temperature > 0 (sampling.rs:67), else greedy */
     double temperature;
-    double top_p;                /* <= 0 or >= 1: unset */
+    double top_p;                /* active in [0, 1) (apply_top_p); otherwise unset */
     size_t top_k;                /* 0: unset */
     float repetition_penalty;    /* 1.0: off */
     size_t no_repeat_ngram_size; /* 0 or 1: off (reference default 20) */
-    uint64_t seed;
+    uint64_t seed;               /* StdRng::seed_from_u64(seed) when has_seed, else entropy */
     int use_cache;               /* must be 1 */
     int64_t eos_token_id;        /* < 0: none (reference: config eos_token_id) */
     int ignore_eos;              /* benchmark mode: always produce max_new_tokens */
+    int has_seed;                /* DecodeParameters::seed is Some */
 } dsocr_decode_params;
 
 /* stream callback: invoked after each generated token (model/mod.rs:1980-1982). */
@@ -235,6 +236,13 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
  * logits; ctx [B][ctx_cap] int32 with ctx_len[B]. */
 dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,
                                    int ngram, float rep_penalty, int* out_tok);
+/* Stochastic selection (select_token_id's do_sample branch: top-k, top-p, WeightedIndex over rand's
+ * StdRng seeded by seed_from_u64(seed)) on device logits [B][V] after the repetition penalty and the
+ * n-gram ban; `draws` successive selections on the same logits with the RNG state carried over
+ * (out_tok [draws][B]).  Device pointers, like dsocr_k_sample_greedy. */
+dsocr_status dsocr_k_sample_stoch(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,
+                                  int ngram, float rep_penalty, double temperature, size_t top_k, double top_p,
+                                  uint64_t seed, int draws, int* out_tok);
 
 #ifdef __cplusplus
 }

@@ -201,8 +201,9 @@ def banned_ngram_tokens(seq, n):
     return banned
 
 
-def select_token_id(logits, context, repetition_penalty=1.0, no_repeat_ngram_size=None):
-    """select_token_id core/src/sampling.rs:34-96 (greedy branch)."""
+def select_token_id(logits, context, repetition_penalty=1.0, no_repeat_ngram_size=None, do_sample=False,
+                    temperature=0.0, top_k=None, top_p=None, rng=None):
+    """select_token_id core/src/sampling.rs:34-96 (the sampling branch: oracle/sampling.py)."""
     logits = np.asarray(logits, F32)
     adjusted = logits.copy()
     if repetition_penalty > 0.0 and abs(repetition_penalty - 1.0) > np.finfo(np.float32).eps:
@@ -217,6 +218,11 @@ def select_token_id(logits, context, repetition_penalty=1.0, no_repeat_ngram_siz
                 filtered[t] = -np.inf
     if not np.any(np.isfinite(filtered)):
         filtered = adjusted
+    if do_sample and temperature > 0.0:
+        from .sampling import sample_token
+        tok = sample_token(filtered, temperature, top_k, top_p, rng)
+        if tok is not None:
+            return tok
     for arr in (filtered, adjusted, logits):
         idx = argmax_first(arr)
         if idx is not None:

@@ -78,8 +78,15 @@ class OracleModel:
         return e.astype(F32)
 
     def generate(self, ids, mask, image_rows, max_new_tokens, eos_token_id=None,
-                 repetition_penalty=1.0, no_repeat_ngram_size=20, record_logits=False, ignore_eos=False):
-        """DeepseekOcrModel::generate model/mod.rs:1870-2048 (greedy, use_cache)."""
+                 repetition_penalty=1.0, no_repeat_ngram_size=20, record_logits=False, ignore_eos=False,
+                 do_sample=False, temperature=0.0, top_k=None, top_p=None, seed=None):
+        """DeepseekOcrModel::generate model/mod.rs:1870-2048 (use_cache; rng = init_rng(seed) per call,
+        model/mod.rs:1917)."""
+        from .sampling import StdRng
+        rng = StdRng(seed) if (do_sample and temperature > 0.0 and seed is not None) else None
+        if rng is None and do_sample and temperature > 0.0:
+            raise ValueError("oracle sampling needs a seed")
+        sel = dict(do_sample=do_sample, temperature=temperature, top_k=top_k, top_p=top_p, rng=rng)
         self.dec.reset()
         ctx = [int(t) for t in ids]
         logits_log = []
@@ -88,7 +95,7 @@ class OracleModel:
         lg = self.dec.forward(self.prefill_embeddings(ids, mask, image_rows))[0]
         if record_logits:
             logits_log.append(lg)
-        cur = select_token_id(lg, ctx, repetition_penalty, no_repeat_ngram_size)
+        cur = select_token_id(lg, ctx, repetition_penalty, no_repeat_ngram_size, **sel)
         if eos_token_id is not None and cur == eos_token_id and not ignore_eos:
             return [], logits_log
         out = []
@@ -100,7 +107,7 @@ class OracleModel:
             lg = self.dec.forward(self.dec.embed([cur]))[0]
             if record_logits:
                 logits_log.append(lg)
-            cur = select_token_id(lg, ctx, repetition_penalty, no_repeat_ngram_size)
+            cur = select_token_id(lg, ctx, repetition_penalty, no_repeat_ngram_size, **sel)
             if eos_token_id is not None and cur == eos_token_id and not ignore_eos:
                 break
         return out, logits_log

@@ -283,7 +283,7 @@ def test_cli_quiet_and_slot_mismatch(monkeypatch, tmp_path):
 
 
 # ---------------------------------------------------------------- the same bridges over the MI355X engine
-def _oracle_ids(img, prompt, max_new):
+def _oracle_ids(img, prompt, max_new, **sampling):
     from oracle.model import OracleModel
     from oracle.weights import Weights
     from dsocr import Page, build_prompt_tokens
@@ -291,7 +291,7 @@ def _oracle_ids(img, prompt, max_new):
     vs = VisionSettings(256, 128, True)
     ids, mask = build_prompt_tokens(SyntheticTokenizer(512), prompt, [Page(img, vs).n_image_tokens])
     emb, _ = orc.image_embeddings(img, 256, 128, True)
-    ref, _ = orc.generate(ids, mask, emb, max_new, eos_token_id=1)
+    ref, _ = orc.generate(ids, mask, emb, max_new, eos_token_id=1, **sampling)
     return ref
 
 
@@ -329,8 +329,13 @@ def test_gpu_server_chat_matches_oracle(gpu):
                                                        "stream": True}).text)
         assert "".join(e["choices"][0]["delta"].get("content", "") for e in ev[1:-1]) == \
             SyntheticTokenizer(512).decode(ref)
-        r = c.post("/v1/chat/completions", json={"model": "deepseek-ocr", "messages": msg, "do_sample": True,
-                                                 "temperature": 0.7})
-        assert r.status_code == 500 and "do_sample" in r.json()["error"]["message"]
+        # sampling fields flatten into the request (DecodeParametersPatch), seeded -> reproducible
+        req = {"model": "deepseek-ocr", "messages": msg, "do_sample": True, "temperature": 0.7, "top_k": 30,
+               "seed": 99}
+        r = c.post("/v1/chat/completions", json=req)
+        assert r.status_code == 200
+        ref = _oracle_ids(arr, "<image>\nConvert the document to markdown.", 10, do_sample=True, temperature=0.7,
+                          top_k=30, top_p=None, seed=99)
+        assert r.json()["choices"][0]["message"]["content"] == SyntheticTokenizer(512).decode(ref)
     finally:
         eng.close()
