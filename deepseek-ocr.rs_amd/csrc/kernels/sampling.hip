@@ -107,34 +107,87 @@ __device__ int block_excl_scan(int v, int* lds16, int* total) {
 
 __device__ __forceinline__ bool is_banned(const uint32_t* ban, int v) { return (ban[v >> 5] >> (v & 31)) & 1u; }
 
-// sequential f64 left fold over w[0..n) (the reference's order); if cum, w[i-1] <- the running
-// total before w[i] is added (WeightedIndex's cumulative_weights).  Loads run a chunk ahead.
-__device__ double serial_fold(double* w, int n, bool cum) {
+// In-order f64 scan over n values produced by load(g) (the reference's sequential loops, bit for
+// bit).  The block stages ST_TILE values at a time in LDS (waves 1.. fetch tile t+1 while lane 0 of
+// wave 0 folds tile t out of LDS), so the serial chain pays LDS, not HBM/L2, latency.
+// stop(S) is a predicate on the running sum that can only turn true as S grows; the fold ends at
+// the first g with stop(S_g) and calls on_stop(g) on thread 0.  If cum_out is set, cum_out[g]
+// receives the running total S_g (WeightedIndex's cumulative weights are S_0..S_{n-2}).  The
+// total is returned on thread 0.  Terms must be non-negative (weights, shares).
+constexpr int ST_TILE = 4096;
+template <class Load, class Stop, class OnStop>
+__device__ double block_serial_fold(int n, double* tiles, int* stop_s, double* cum_out, Load load, Stop stop,
+                                    OnStop on_stop) {
+    const int tid = threadIdx.x;
     double total = 0.0;
-    constexpr int CH = 16;
-    double cur[CH], nxt[CH];
-    for (int j = 0; j < CH; ++j) cur[j] = j < n ? w[j] : 0.0;
-    for (int c = 0; c < n; c += CH) {
-        for (int j = 0; j < CH; ++j) nxt[j] = (c + CH + j) < n ? w[c + CH + j] : 0.0;
-        for (int j = 0; j < CH && c + j < n; ++j) {
-            const int i = c + j;
-            if (i == 0) total = cur[j];
-            else {
-                if (cum) w[i - 1] = total;
-                total = __dadd_rn(total, cur[j]);
-            }
+    const int ntile = (n + ST_TILE - 1) / ST_TILE;
+    for (int i = tid; i < min(n, ST_TILE); i += ST_NT) tiles[i] = load(i);
+    if (tid == 0) *stop_s = 0;
+    __syncthreads();
+    for (int t = 0; t < ntile; ++t) {
+        double* cur = tiles + (t & 1) * ST_TILE;
+        double* nxt = tiles + ((t + 1) & 1) * ST_TILE;
+        const int g0 = t * ST_TILE, len = min(ST_TILE, n - g0);
+        if (tid >= 64 && t + 1 < ntile) {
+            const int g1 = g0 + ST_TILE, len1 = min(ST_TILE, n - g1);
+            for (int i = tid - 64; i < len1; i += ST_NT - 64) nxt[i] = load(g1 + i);
         }
-        for (int j = 0; j < CH; ++j) cur[j] = nxt[j];
+        if (tid == 0 && !*stop_s) {
+            // 16-value register batches, the next batch's LDS reads in flight while this one folds;
+            // the chain is one f64 add per value (0 + v is exact for the non-negative terms, so the
+            // first value needs no special case) and the stop test runs once per batch: the running
+            // sums never decrease, so `stop` can only turn true and its first index is searched in
+            // the batch that crossed
+            constexpr int RB = 16;
+            double nb[RB];
+#pragma unroll
+            for (int j = 0; j < RB; ++j) nb[j] = cur[min(j, len - 1)];
+            int stop_at = -1;
+            for (int i0 = 0; i0 < len; i0 += RB) {
+                double v[RB];
+#pragma unroll
+                for (int j = 0; j < RB; ++j) v[j] = nb[j];
+#pragma unroll
+                for (int j = 0; j < RB; ++j) nb[j] = cur[min(i0 + RB + j, len - 1)];
+                const int cnt = min(RB, len - i0);
+                if (cnt == RB) {
+#pragma unroll
+                    for (int j = 0; j < RB; ++j) { total = total + v[j]; v[j] = total; }
+                } else {
+                    for (int j = 0; j < cnt; ++j) { total = total + v[j]; v[j] = total; }
+                }
+                if (cum_out) {
+#pragma unroll
+                    for (int j = 0; j < RB; ++j)
+                        if (j < cnt) cur[i0 + j] = v[j];
+                }
+                if (stop(total)) {
+                    for (int j = 0; j < cnt; ++j)
+                        if (stop(v[j])) { stop_at = g0 + i0 + j; break; }
+                    break;
+                }
+            }
+            if (stop_at >= 0) { *stop_s = 1; on_stop(stop_at); }
+        }
+        __syncthreads();
+        if (cum_out)
+            for (int i = tid; i < len; i += ST_NT) cum_out[g0 + i] = cur[i];
+        const bool stop = *stop_s != 0;
+        __syncthreads();
+        if (stop) break;
     }
     return total;
 }
 
 __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a) {
     extern __shared__ uint32_t ban[];  // (V + 31) / 32 words: n-gram ban, later the kept set
-    __shared__ int hist[ST_DIG * ST_NT];
+    __shared__ double lds_big[ST_DIG * ST_NT / 2];  // radix histograms, later two fold tiles
+    int* hist = reinterpret_cast<int*>(lds_big);
+    __shared__ int stop_s;
     __shared__ int lds16[ST_NT / 64];
     __shared__ float fmax_s[ST_NT / 64];
     __shared__ int keep_s, tok_s;
+    __shared__ double total_s;
     const int b = blockIdx.x, tid = threadIdx.x, V = a.V;
     const int nwords = (V + 31) >> 5;
     const float* lg = a.logits + (long)b * a.ld;
@@ -187,13 +240,19 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     }
     int nc;
     int off = block_excl_scan(c, lds16, &nc);
-    for (int v = v0; v < v1; ++v) {
-        const float x = lg[v];
-        const double q = (double)x / T;
-        if (q > -INFINITY && q < INFINITY && !(use_ban && is_banned(ban, v))) {
-            sk0[off] = desc_key(x);
-            si0[off] = v;
-            ++off;
+    for (int u0 = v0; u0 < v1; u0 += 8) {  // loads batched ahead of the stores
+        float xx[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xx[j] = u0 + j < v1 ? lg[u0 + j] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int v = u0 + j;
+            const double q = (double)xx[j] / T;
+            if (v < v1 && q > -INFINITY && q < INFINITY && !(use_ban && is_banned(ban, v))) {
+                sk0[off] = desc_key(xx[j]);
+                si0[off] = v;
+                ++off;
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o, 64));
@@ -222,7 +281,14 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
         for (int pass = 0; pass < 8; ++pass) {
             const int sh = pass * 4;
             for (int d = 0; d < ST_DIG; ++d) hist[d * ST_NT + tid] = 0;
-            for (int i = s0; i < s1; ++i) hist[((ks[i] >> sh) & 15) * ST_NT + tid] += 1;
+            for (int i0 = s0; i0 < s1; i0 += 8) {  // 8 loads in flight per round
+                uint32_t kk[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) kk[j] = i0 + j < s1 ? ks[i0 + j] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (i0 + j < s1) hist[((kk[j] >> sh) & 15) * ST_NT + tid] += 1;
+            }
             __syncthreads();
             // exclusive scan over (digit, thread): thread t owns flattened entries [16t, 16t+16)
             int loc[ST_DIG], sum = 0;
@@ -231,11 +297,21 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
             int base = block_excl_scan(sum, lds16, &tot);
             for (int j = 0; j < ST_DIG; ++j) { hist[tid * ST_DIG + j] = base; base += loc[j]; }
             __syncthreads();
-            for (int i = s0; i < s1; ++i) {
-                const uint32_t k = ks[i];
-                const int p = hist[((k >> sh) & 15) * ST_NT + tid]++;
-                kd[p] = k;
-                id[p] = is[i];
+            for (int i0 = s0; i0 < s1; i0 += 8) {  // loads batched ahead of the scattered stores
+                uint32_t kk[8];
+                int ii[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    kk[j] = i0 + j < s1 ? ks[i0 + j] : 0u;
+                    ii[j] = i0 + j < s1 ? is[i0 + j] : 0;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (i0 + j < s1) {
+                        const int p = hist[((kk[j] >> sh) & 15) * ST_NT + tid]++;
+                        kd[p] = kk[j];
+                        id[p] = ii[j];
+                    }
             }
             __syncthreads();
             uint32_t* tk = ks; ks = kd; kd = tk;
@@ -244,21 +320,22 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
         // 8 passes: sorted data is back in (sk0, si0)
         int m = topk ? (int)a.top_k : nc;
         if (topp) {
-            // apply_top_p: weights exp(q - qmax) in sorted order, total and cumulative share on one thread
-            for (int j = tid; j < m; j += ST_NT) sw[j] = exp((double)lg[si0[j]] / T - qmax);
+            // apply_top_p: weights exp(q - qmax) in sorted order; the total, then the cumulative share
+            // until it exceeds top_p, both as in-order folds (sampling.rs:195-211)
+            auto wsorted = [&](int j) { return exp((double)lg[si0[j]] / T - qmax); };
+            auto never = [](double) { return false; };
+            auto none = [](int) {};
+            const double total = block_serial_fold(m, lds_big, &stop_s, nullptr, wsorted, never, none);
+            if (tid == 0) { total_s = total; keep_s = m; }
             __syncthreads();
-            if (tid == 0) {
-                const double total = serial_fold(sw, m, false);
-                int keep = m;
-                if (total > 0.0) {
-                    double cumv = 0.0;
-                    for (int j = 0; j < m; ++j) {
-                        cumv = __dadd_rn(cumv, sw[j] / total);
-                        if (cumv > a.top_p) { keep = j + 1; break; }
-                    }
-                }
-                keep_s = keep < 1 ? 1 : keep;
+            const double tot = total_s;
+            if (tot > 0.0) {
+                const double tp = a.top_p;
+                (void)block_serial_fold(m, lds_big, &stop_s, nullptr, [&](int j) { return wsorted(j) / tot; },
+                                        [&](double cumv) { return cumv > tp; }, [&](int j) { keep_s = j + 1; });
             }
+            __syncthreads();
+            if (keep_s < 1) keep_s = 1;
             __syncthreads();
             m = keep_s;
         }
@@ -286,14 +363,15 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
         __syncthreads();
     }
 
-    // ---- 4. sample_from_logits over the kept candidates in index order
-    for (int i = tid; i < nk; i += ST_NT) {
+    // ---- 4. sample_from_logits over the kept candidates in index order: weights, WeightedIndex's
+    // cumulative left fold (sw[0..nk-1) = cumulative_weights) and the total
+    auto wkept = [&](int i) {
         const double w = exp((double)lg[kept[i]] / T - qmax);
-        sw[i] = (w < INFINITY && w > 0.0) ? w : 0.0;
-    }
-    __syncthreads();
+        return (w < INFINITY && w > 0.0) ? w : 0.0;
+    };
+    const double total = block_serial_fold(nk, lds_big, &stop_s, sw, wkept, [](double) { return false; }, [](int) {});
+    __syncthreads();  // cumulative weights visible to thread 0's search
     if (tid == 0) {
-        const double total = serial_fold(sw, nk, true);  // sw[0..nk-1) = cumulative_weights
         int tok;
         if (!(total > 0.0)) {
             // every weight zero: Iterator::max_by over the logits (the LAST maximum)
