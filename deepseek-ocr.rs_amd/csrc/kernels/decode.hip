@@ -8,6 +8,7 @@
 // Every reduction keeps the reference's f32 order where it is observable
 // (top-k weighted sum in top-k order, then + shared, then the residual add).
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "dev_common.hpp"
@@ -1772,6 +1773,13 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
     extern __shared__ float smem[];
     gateup_slot_body<WT, MT, false>(a, blockIdx.x, smem);
 }
+// the shared-expert blocks of the slot grid on their own (bid offset past the routed slots), so the
+// routed launch carries single-token registers and LDS (B > 1: MT = T only where it is needed)
+template <typename WT, int MT>
+__global__ __launch_bounds__(256) void moe_gateup_shared_kernel(MoeDec2Args a, int bid0) {
+    extern __shared__ float smem[];
+    gateup_slot_body<WT, MT, false>(a, bid0 + blockIdx.x, smem);
+}
 
 // ------------------------------------------------------------------ MoE down + combine + residual
 // A wave owns output row j of every token: v = sum_k h~[row(t,k)] . Wd_{e_k}[j]
@@ -2286,6 +2294,26 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
     const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
     dim3 grid(a.slots * units_r + units_s);
+    if (a.slot_mode && a.K <= 64 * 3 * 8 && a.T > 2 && a.T <= 8 && !(getenv("DSOCR_SLOT_ONE") && atoi(getenv("DSOCR_SLOT_ONE")))) {
+        // routed slots (one token each) with MT = 1, then the shared expert over the T tokens
+        MoeDec2Args r = a;
+        r.sWgu = nullptr;
+        const int mt = a.T <= 4 ? 4 : 8;
+        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_slot_kernel<bf16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
+        else hipLaunchKernelGGL((moe_gateup_slot_kernel<f16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
+        if (units_s) {
+            const size_t lds = stage_bytes(mt, a.K);
+            const int bid0 = a.slots * units_r;
+            if (a.wdtype == WDT_BF16) {
+                if (mt == 4) hipLaunchKernelGGL((moe_gateup_shared_kernel<bf16_t, 4>), dim3(units_s), dim3(256), lds, s, a, bid0);
+                else hipLaunchKernelGGL((moe_gateup_shared_kernel<bf16_t, 8>), dim3(units_s), dim3(256), lds, s, a, bid0);
+            } else {
+                if (mt == 4) hipLaunchKernelGGL((moe_gateup_shared_kernel<f16_t, 4>), dim3(units_s), dim3(256), lds, s, a, bid0);
+                else hipLaunchKernelGGL((moe_gateup_shared_kernel<f16_t, 8>), dim3(units_s), dim3(256), lds, s, a, bid0);
+            }
+        }
+        return;
+    }
     if (a.slot_mode && a.K <= 64 * 3 * 8 && a.T <= 8) {
         const int mt = a.T == 1 ? 1 : (a.T <= 2 ? 2 : (a.T <= 4 ? 4 : 8));
         const size_t lds = stage_bytes(mt, a.K);

@@ -284,8 +284,12 @@ class DeepseekOcrEngine:
         pages = [Page(im, vision, self) for im in images]
         ids, mask = build_prompt_tokens(tokenizer, prompt, [p.n_image_tokens for p in pages])
         if len(pages) > 1:
-            raise DsocrError(1, "multiple images per prompt are not supported by this engine yet")
-        gen = self.generate(ids, mask, pages[0] if pages else None, None, params, stream)
+            # several <image> slots: the pages' rows in image order (compute_image_embeddings over the
+            # list, model/mod.rs:2387), injected at the mask positions in that order
+            rows = np.concatenate(self.image_embeddings(pages), axis=0)
+            gen = self.generate(ids, mask, None, rows, params, stream)
+        else:
+            gen = self.generate(ids, mask, pages[0] if pages else None, None, params, stream)
         text = ""
         if hasattr(tokenizer, "decode"):
             try:

@@ -339,3 +339,26 @@ def test_gpu_server_chat_matches_oracle(gpu):
         assert r.json()["choices"][0]["message"]["content"] == SyntheticTokenizer(512).decode(ref)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_two_images_matches_oracle(gpu):
+    """OcrEngine::decode with two <image> slots: rows of both pages injected in image order."""
+    from dsocr import ModelLoadArgs, Page, build_prompt_tokens, load_model
+    from oracle.model import OracleModel
+    from oracle.weights import Weights
+    vs = VisionSettings(256, 128, True)
+    a = np.random.default_rng(21).integers(0, 256, (300, 420, 3), dtype=np.uint8)
+    b = np.random.default_rng(22).integers(0, 256, (200, 200, 3), dtype=np.uint8)
+    prompt = "<image>\nfirst page\n<image>\nsecond page"
+    tok = SyntheticTokenizer(512)
+    eng = load_model(ModelLoadArgs(config_path=TINY, synthetic_seed=7, dtype="f16"))
+    try:
+        out = eng.decode(tok, prompt, [a, b], vs, DecodeParameters(max_new_tokens=12))
+    finally:
+        eng.close()
+    orc = OracleModel(json.load(open(TINY)), Weights(seed=7, dtype="f16"))
+    ids, mask = build_prompt_tokens(tok, prompt, [Page(a, vs).n_image_tokens, Page(b, vs).n_image_tokens])
+    rows = np.concatenate([orc.image_embeddings(x, 256, 128, True)[0] for x in (a, b)], axis=0)
+    ref, _ = orc.generate(ids, mask, rows, 12, eos_token_id=1)
+    assert out.generated_tokens == ref and out.prompt_tokens == len(ids)
