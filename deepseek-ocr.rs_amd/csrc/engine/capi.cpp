@@ -3,6 +3,8 @@
 #include "../../../include/dsocr.h"
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -555,11 +557,23 @@ dsocr_status dsocr_k_sample_stoch(int B, int V, float* logits, const int* ctx, i
             for (int b = 0; b < B; ++b)
                 check_hip(hipMemcpy(a.rng + (size_t)b * dsocr::RNG_WORDS, st.data(), sizeof(uint32_t) * dsocr::RNG_WORDS,
                                     hipMemcpyHostToDevice), "hipMemcpy");
+            const bool stamps = getenv("DSOCR_SAMPLE_STAMPS") != nullptr;  // diagnostics: phase clocks to stderr
+            if (stamps) {
+                a.st_stamps = (unsigned long long*)dalloc(sizeof(unsigned long long) * 8);
+                check_hip(hipMemset(a.st_stamps, 0, sizeof(unsigned long long) * 8), "hipMemset");
+            }
             for (int d = 0; d < draws; ++d) {
                 a.out_tok = out_tok + (size_t)d * B;
                 dsocr::launch_dec_sample(a, nullptr);
             }
             check_hip(hipDeviceSynchronize(), "sample");
+            if (stamps) {
+                unsigned long long h[8];
+                check_hip(hipMemcpy(h, a.st_stamps, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy");
+                fprintf(stderr, "[sample stamps] phase clocks (shader cycles) from start:");
+                for (int i = 1; i < 8; ++i) fprintf(stderr, " %lld", h[i] ? (long long)(h[i] - h[0]) : -1LL);
+                fprintf(stderr, "\n");
+            }
         } catch (...) {
             for (void* q : bufs) (void)hipFree(q);
             throw;

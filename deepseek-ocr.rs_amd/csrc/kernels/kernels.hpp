@@ -277,6 +277,7 @@ struct DecSampleArgs {
     // per page (keys / indices double-buffered: [B][2][st_ld]; f64 weights [B][st_ld])
     int do_sample = 0; double temperature = 0.0, top_p = -1.0; long top_k = 0;
     uint32_t* rng = nullptr; uint32_t* st_key = nullptr; int* st_idx = nullptr; double* st_w = nullptr; long st_ld = 0;
+    unsigned long long* st_stamps = nullptr;  // diagnostics: shader clock at the sampler's phase points (page 0)
 };
 // rand StdRng state words per page: ChaCha12 key, 64-bit block counter, buffer index, 64-word buffer
 constexpr int RNG_KEY = 0, RNG_CTR = 8, RNG_IDX = 10, RNG_BUF = 16, RNG_WORDS = 80;

@@ -197,6 +197,9 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     int* si1 = si0 + a.st_ld;
     double* sw = a.st_w + (long)b * a.st_ld;
     const double T = a.temperature;
+#define ST_STAMP(i) \
+    if (a.st_stamps && b == 0 && tid == 0) a.st_stamps[i] = __builtin_amdgcn_s_memtime();
+    ST_STAMP(0)
 
     // ---- 1. n-gram ban (sampling.rs:141-158) over the whole vocabulary
     for (int i = tid; i < nwords; i += ST_NT) ban[i] = 0u;
@@ -224,6 +227,7 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     int nvalid;
     (void)block_excl_scan(nv, lds16, &nvalid);
     const bool use_ban = nvalid > 0;
+    ST_STAMP(1)
 
     // ---- 2. candidates in index order: finite logit / T (f64), contiguous range per thread
     const int chunk = (V + ST_NT - 1) / ST_NT;
@@ -262,6 +266,7 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     for (int w = 1; w < ST_NT / 64; ++w) lmax = fmaxf(lmax, fmax_s[w]);
     // max of the kept logits64 (top-k / top-p keep the largest): the division is monotonic
     const double qmax = (double)lmax / T;
+    ST_STAMP(2)
 
     if (nc == 0) {  // sample_from_logits -> None: the argmax chain of the final kernel decides
         for (int j = tid; j < a.red_blocks; j += ST_NT) a.red_idx[(long)b * a.red_blocks + j] = 0x7fffffff;
@@ -318,6 +323,7 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
             int* ti = is; is = id; id = ti;
         }
         // 8 passes: sorted data is back in (sk0, si0)
+        ST_STAMP(3)
         int m = topk ? (int)a.top_k : nc;
         if (topp) {
             // apply_top_p: weights exp(q - qmax) in sorted order; the total, then the cumulative share
@@ -339,6 +345,7 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
             __syncthreads();
             m = keep_s;
         }
+        ST_STAMP(4)
         // kept set back in index order (bitmap, then per-thread word ranges)
         for (int i = tid; i < nwords; i += ST_NT) ban[i] = 0u;
         __syncthreads();
@@ -361,16 +368,22 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
         kept = si1;
         nk = tot;
         __syncthreads();
+        ST_STAMP(5)
     }
 
     // ---- 4. sample_from_logits over the kept candidates in index order: weights, WeightedIndex's
     // cumulative left fold (sw[0..nk-1) = cumulative_weights) and the total
-    auto wkept = [&](int i) {
+    // weights first, by the whole block (coalesced), then the in-order fold reads them back
+    for (int i = tid; i < nk; i += ST_NT) {
         const double w = exp((double)lg[kept[i]] / T - qmax);
-        return (w < INFINITY && w > 0.0) ? w : 0.0;
-    };
-    const double total = block_serial_fold(nk, lds_big, &stop_s, sw, wkept, [](double) { return false; }, [](int) {});
+        sw[i] = (w < INFINITY && w > 0.0) ? w : 0.0;
+    }
+    __syncthreads();
+    ST_STAMP(5)
+    const double total = block_serial_fold(nk, lds_big, &stop_s, sw, [&](int i) { return sw[i]; },
+                                           [](double) { return false; }, [](int) {});
     __syncthreads();  // cumulative weights visible to thread 0's search
+    ST_STAMP(6)
     if (tid == 0) {
         int tok;
         if (!(total > 0.0)) {
@@ -400,6 +413,8 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
         tok_s = tok;
     }
     __syncthreads();
+    ST_STAMP(7)
+#undef ST_STAMP
     // ---- 5. hand the id to the final selection kernel
     for (int j = tid; j < a.red_blocks; j += ST_NT) {
         a.red_idx[(long)b * a.red_blocks + j] = j == 0 ? tok_s : 0x7fffffff;
