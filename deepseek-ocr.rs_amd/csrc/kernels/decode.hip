@@ -266,6 +266,70 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
         }
 }
 
+// Several tokens (M = 3..8, x already normalised): the x rows are read straight from L2 per chunk
+// instead of being staged through LDS, so a block needs no LDS (the 8-row staging window capped
+// residency at 3 blocks per CU and made the launch two rounds deep).  Same per-row arithmetic as
+// dec_gemv_kernel (chunk u-major, then j), so the results are bit-identical.
+template <typename WT, int MT, int RB>
+__global__ __launch_bounds__(256) void dec_gemv_direct_kernel(DecGemvArgs a) {
+    constexpr int U = 3;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = (blockIdx.x * 4 + wave) * RB;
+    if (n0 >= a.N) return;  // whole wave: nothing below synchronises the block
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    uint4 wq[U][RB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int n = min(n0 + r, a.N - 1);
+            wq[u][r] = ldg_nt16(W + (long)n * a.ldw + (min(c, chunks - 1) << 3));
+        }
+    }
+    float acc[RB][MT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        const int cc = min(c, chunks - 1);
+        float xv[MT][8];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) ld_x8(a.x + (long)min(m, a.M - 1) * a.ldx + (cc << 3), xv[m]);
+        if (c < chunks) {
+            float w8[RB][8];
+#pragma unroll
+            for (int r = 0; r < RB; ++r) unpack8<WT>(wq[u][r], w8[r]);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                if (m < a.M) {
+#pragma unroll
+                    for (int r = 0; r < RB; ++r)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc[r][m] = fmaf(xv[m][j], w8[r][j], acc[r][m]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            float v = wave_sum(acc[r][m]);
+            const int n = n0 + r;
+            if (lane == 0 && m < a.M && n < a.N) {
+                v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
+                float* yp = a.y + (long)m * a.ldy + n;
+                if (a.accumulate) v = *yp + v;
+                *yp = v;
+            }
+        }
+}
+
 // Large-N variant (lm_head: 129280 rows): a fixed grid of waves walks the row groups with a
 // two-deep register pipeline (the loads of group i+1 are in flight while group i is
 // reduced), so the per-block x staging / norm prologue is paid once per ~8 row groups.
@@ -356,6 +420,13 @@ __global__ __launch_bounds__(256) void dec_gemv_stream_kernel(DecGemvArgs a) {
 template <typename WT, int MT>
 static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     const size_t lds = stage_bytes(a.M, a.K);
+    if constexpr (MT >= 4 && MT <= 8) {  // several tokens, x already normalised: no LDS staging
+        static const bool direct = !(getenv("DSOCR_GEMV_DIRECT") && atoi(getenv("DSOCR_GEMV_DIRECT")) == 0);
+        if (direct && a.N <= 16384 && !a.norm_w && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
+            hipLaunchKernelGGL((dec_gemv_direct_kernel<WT, MT, 1>), dim3((a.N + 3) / 4), dim3(256), 0, s, a);
+            return;
+        }
+    }
     // small N: one row per wave so the whole matrix is in flight at once; large N: RB rows per wave
     // (DSOCR_GEMV_STREAM=G: small N on the streaming kernel with at most G blocks, experiment)
     static const int stream_blocks = getenv("DSOCR_GEMV_STREAM") ? atoi(getenv("DSOCR_GEMV_STREAM")) : 0;
