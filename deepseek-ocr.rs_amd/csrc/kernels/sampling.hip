@@ -278,6 +278,7 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     const int* kept = si0;
     int nk = nc;
     if (topk || topp) {
+      if (topp) {
         // ---- 3. stable LSD radix sort of (key, index) by key ascending = logit descending
         uint32_t *ks = sk0, *kd = sk1;
         int *is = si0, *id = si1;
@@ -351,6 +352,52 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
         __syncthreads();
         for (int j = tid; j < m; j += ST_NT) atomicOr(&ban[si0[j] >> 5], 1u << (si0[j] & 31));
         __syncthreads();
+      } else {
+        // top-k alone needs the kept SET, not its order: radix-select the k-th smallest key (8-bit
+        // digits from the top), keep every key below it and, of the keys equal to it, the first ones
+        // in index order — exactly the first k of the stable sort
+        for (int i = tid; i < nwords; i += ST_NT) ban[i] = 0u;
+        uint32_t prefix = 0u, pmask = 0u;
+        int need = (int)a.top_k;
+        for (int sh = 24; sh >= 0; sh -= 8) {
+            for (int d = tid; d < 256; d += ST_NT) hist[d] = 0;
+            __syncthreads();
+            for (int i = tid; i < nc; i += ST_NT) {
+                const uint32_t k = sk0[i];
+                if ((k & pmask) == prefix) atomicAdd(&hist[(k >> sh) & 255], 1);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int cum = 0, d = 0;
+                for (; d < 255; ++d) {
+                    if (cum + hist[d] >= need) break;
+                    cum += hist[d];
+                }
+                keep_s = d;
+                tok_s = need - cum;
+            }
+            __syncthreads();
+            prefix |= (uint32_t)keep_s << sh;
+            pmask |= 255u << sh;
+            need = tok_s;
+            __syncthreads();
+        }
+        // mark: keys < threshold, then the first `need` keys == threshold in index order
+        const int sc = (nc + ST_NT - 1) / ST_NT;
+        const int s0 = min(nc, tid * sc), s1 = min(nc, s0 + sc);
+        int eq = 0;
+        for (int i = s0; i < s1; ++i) eq += sk0[i] == prefix ? 1 : 0;
+        int eq_tot;
+        int rank = block_excl_scan(eq, lds16, &eq_tot);
+        for (int i = s0; i < s1; ++i) {
+            const uint32_t k = sk0[i];
+            bool keep = k < prefix;
+            if (k == prefix) keep = rank++ < need;
+            if (keep) atomicOr(&ban[si0[i] >> 5], 1u << (si0[i] & 31));
+        }
+        __syncthreads();
+        ST_STAMP(3)
+      }
         const int wc = (nwords + ST_NT - 1) / ST_NT;
         const int w0 = min(nwords, tid * wc), w1 = min(nwords, w0 + wc);
         int cnt = 0;
