@@ -1703,11 +1703,11 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
 // the rest are the shared experts over all T tokens (MT >= T).
 // FUSED: the block is a producer inside moe_fused_slot_kernel: every store of h (and of the
 // picks) is write-through (sc1) so the down blocks of the same launch can read it (Guideline 16 R1).
-template <typename WT, int MT, bool FUSED>
+template <typename WT, int MT, bool FUSED, int RB = 2>
 __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int bid, float* smem) {
     __shared__ int sel_e;
     __shared__ float sel_w;
-    constexpr int RB = 2, U = 3, XR = 2;  // K <= 1536
+    constexpr int U = 3, XR = 2;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
     // dev stamps: [0] wall clock (100 MHz) at entry, [1..7] shader clock at phase points
@@ -1846,10 +1846,10 @@ __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
 }
 // the shared-expert blocks of the slot grid on their own (bid offset past the routed slots), so the
 // routed launch carries single-token registers and LDS (B > 1: MT = T only where it is needed)
-template <typename WT, int MT>
+template <typename WT, int MT, int RB>
 __global__ __launch_bounds__(256) void moe_gateup_shared_kernel(MoeDec2Args a, int bid0) {
     extern __shared__ float smem[];
-    gateup_slot_body<WT, MT, false>(a, bid0 + blockIdx.x, smem);
+    gateup_slot_body<WT, MT, false, RB>(a, bid0 + blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------------ MoE down + combine + residual
@@ -2373,15 +2373,22 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
         if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_slot_kernel<bf16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
         else hipLaunchKernelGGL((moe_gateup_slot_kernel<f16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
         if (units_s) {
+            // shared expert alone (slots = 0: every block is a shared block), one row per wave so the
+            // M-token blocks are twice as many and half as long (same per-row arithmetic)
             const size_t lds = stage_bytes(mt, a.K);
-            const int bid0 = a.slots * units_r;
+            MoeDec2Args sh = a;
+            sh.slots = 0;
+            static const int srb = getenv("DSOCR_SHARED_RB") ? atoi(getenv("DSOCR_SHARED_RB")) : 1;
+            const int ns = srb == 1 ? (a.Is + 3) / 4 : units_s;
+#define DSOCR_SH(WTY, MTV) \
+    if (srb == 1) hipLaunchKernelGGL((moe_gateup_shared_kernel<WTY, MTV, 1>), dim3(ns), dim3(256), lds, s, sh, 0); \
+    else hipLaunchKernelGGL((moe_gateup_shared_kernel<WTY, MTV, 2>), dim3(ns), dim3(256), lds, s, sh, 0);
             if (a.wdtype == WDT_BF16) {
-                if (mt == 4) hipLaunchKernelGGL((moe_gateup_shared_kernel<bf16_t, 4>), dim3(units_s), dim3(256), lds, s, a, bid0);
-                else hipLaunchKernelGGL((moe_gateup_shared_kernel<bf16_t, 8>), dim3(units_s), dim3(256), lds, s, a, bid0);
+                if (mt == 4) { DSOCR_SH(bf16_t, 4) } else { DSOCR_SH(bf16_t, 8) }
             } else {
-                if (mt == 4) hipLaunchKernelGGL((moe_gateup_shared_kernel<f16_t, 4>), dim3(units_s), dim3(256), lds, s, a, bid0);
-                else hipLaunchKernelGGL((moe_gateup_shared_kernel<f16_t, 8>), dim3(units_s), dim3(256), lds, s, a, bid0);
+                if (mt == 4) { DSOCR_SH(f16_t, 4) } else { DSOCR_SH(f16_t, 8) }
             }
+#undef DSOCR_SH
         }
         return;
     }
