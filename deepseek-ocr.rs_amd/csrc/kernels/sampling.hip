@@ -187,7 +187,7 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     __shared__ int lds16[ST_NT / 64];
     __shared__ float fmax_s[ST_NT / 64];
     __shared__ int keep_s, tok_s;
-    __shared__ double total_s;
+    __shared__ double total_s, chosen_s;
     const int b = blockIdx.x, tid = threadIdx.x, V = a.V;
     const int nwords = (V + 31) >> 5;
     const float* lg = a.logits + (long)b * a.ld;
@@ -427,18 +427,20 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
     }
     __syncthreads();
     ST_STAMP(5)
-    const double total = block_serial_fold(nk, lds_big, &stop_s, sw, [&](int i) { return sw[i]; },
-                                           [](double) { return false; }, [](int) {});
-    __syncthreads();  // cumulative weights visible to thread 0's search
-    ST_STAMP(6)
+    // the total (one fold), the draw, then a second fold of the same terms that stops at the first
+    // running sum above the chosen weight: that index is WeightedIndex's partition point over
+    // cumulative_weights = S_0..S_{n-2} (n - 1 when none exceeds it), without storing the sums
+    auto wload = [&](int i) { return sw[i]; };
+    const double total = block_serial_fold(nk, lds_big, &stop_s, nullptr, wload, [](double) { return false; },
+                                           [](int) {});
     if (tid == 0) {
-        int tok;
+        total_s = total;
         if (!(total > 0.0)) {
             // every weight zero: Iterator::max_by over the logits (the LAST maximum)
             int best = kept[0];
             for (int i = 1; i < nk; ++i)
                 if (!(lg[kept[i]] < lg[best])) best = kept[i];
-            tok = best;
+            tok_s = best;
         } else {
             // UniformFloat::<f64>::new(0, total): shrink scale until scale * max_rand < total
             const double max_rand = 1.0 - 0x1p-52;
@@ -448,16 +450,18 @@ __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a
             uint32_t* st = a.rng + (long)b * RNG_WORDS;
             const uint64_t u = rng_next_u64(st);
             const double v12 = __longlong_as_double((long long)((u >> 12) | 0x3FF0000000000000ull));
-            const double chosen = __dadd_rn(__dmul_rn(v12 - 1.0, scale), 0.0);
-            int lo = 0, hi = nk - 1;  // partition point of (cum <= chosen)
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (sw[mid] <= chosen) lo = mid + 1;
-                else hi = mid;
-            }
-            tok = kept[lo];
+            chosen_s = __dadd_rn(__dmul_rn(v12 - 1.0, scale), 0.0);
         }
-        tok_s = tok;
+        keep_s = nk - 1;
+    }
+    __syncthreads();
+    ST_STAMP(6)
+    if (total_s > 0.0) {
+        const double chosen = chosen_s;
+        (void)block_serial_fold(nk, lds_big, &stop_s, nullptr, wload, [&](double S) { return S > chosen; },
+                                [&](int g) { keep_s = min(g, nk - 1); });
+        __syncthreads();
+        if (tid == 0) tok_s = kept[keep_s];
     }
     __syncthreads();
     ST_STAMP(7)
