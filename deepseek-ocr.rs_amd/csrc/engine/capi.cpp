@@ -51,10 +51,8 @@ void check_hip(hipError_t e, const char* what) {
 
 dsocr::GenParams to_params(const dsocr_decode_params* p) {
     if (!p) throw std::runtime_error("EINVAL: decode params are NULL");
-    // select_token_id samples only when do_sample && temperature > 0 (sampling.rs:67); otherwise it is the
-    // greedy path this engine runs.
-    if (!p->use_cache) throw std::runtime_error("EINVAL: use_cache=false is not supported (generate_without_cache)");
     dsocr::GenParams g;
+    g.use_cache = p->use_cache != 0;  // false: generate_without_cache (model/mod.rs:2051-2283)
     g.max_new = p->max_new_tokens;
     g.rep_penalty = p->repetition_penalty;
     g.ngram = p->no_repeat_ngram_size > 1 ? (int)p->no_repeat_ngram_size : 0;
@@ -126,7 +124,7 @@ dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t w, uint32_t h, cons
                                 dsocr_page_pixels** out) {
     return guarded([&] {
         if (!rgb || !vs || !out) throw std::runtime_error("EINVAL: NULL argument");
-        auto* p = new dsocr_page_pixels;
+        std::unique_ptr<dsocr_page_pixels> p(new dsocr_page_pixels);  // released only on success
         dsocr::PagePixels& px = p->px;
         px.base = (int)vs->base_size;
         px.tile = (int)vs->image_size;
@@ -147,7 +145,7 @@ dsocr_status dsocr_prepare_page(const uint8_t* rgb, uint32_t w, uint32_t h, cons
                 dsocr::image_to_chw(tiles[i].data(), px.tile, px.tile, px.tiles_chw.data() + (size_t)i * 3 * px.tile * px.tile);
         }
         px.n_image_tokens = dsocr::image_placeholder_count(px.base, px.tile, px.crop, px.crop_w, px.crop_h);
-        *out = p;
+        *out = p.release();
     });
 }
 
@@ -216,7 +214,10 @@ dsocr_status dsocr_image_embeddings(dsocr_engine* e, const dsocr_page_pixels* co
     return guarded([&] {
         if (!e || (!pages && n)) throw std::runtime_error("EINVAL: NULL argument");
         std::vector<const dsocr::PagePixels*> ps;
-        for (size_t i = 0; i < n; ++i) ps.push_back(&pages[i]->px);
+        for (size_t i = 0; i < n; ++i) {
+            if (!pages[i]) throw std::runtime_error("EINVAL: page " + std::to_string(i) + " is NULL");
+            ps.push_back(&pages[i]->px);
+        }
         auto rows = e->impl->image_embeddings(ps);
         const size_t H = e->impl->cfg().lang.hidden;
         size_t off = 0;
@@ -249,6 +250,25 @@ dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request
         std::vector<dsocr::GenRequest> rq;
         for (size_t i = 0; i < n; ++i) rq.push_back(to_request(reqs[i]));
         auto r = e->impl->generate(rq, to_params(params), nullptr, nullptr);
+        for (size_t i = 0; i < n; ++i) {
+            results[i].status = DSOCR_OK;
+            size_t m = std::min(r[i].size(), results[i].cap);
+            if (results[i].out_ids) std::memcpy(results[i].out_ids, r[i].data(), m * sizeof(int64_t));
+            results[i].n_out = m;
+            if (m < r[i].size()) results[i].status = DSOCR_EINVAL;
+        }
+    });
+}
+
+dsocr_status dsocr_generate_trace(dsocr_engine* e, size_t n, const dsocr_request* reqs,
+                                  const dsocr_decode_params* params, dsocr_result* results, float* logits_out) {
+    return guarded([&] {
+        if (!e || (!reqs && n) || (!results && n) || !logits_out) throw std::runtime_error("EINVAL: NULL argument");
+        std::vector<dsocr::GenRequest> rq;
+        for (size_t i = 0; i < n; ++i) rq.push_back(to_request(reqs[i]));
+        dsocr::GenParams g = to_params(params);
+        g.trace = logits_out;
+        auto r = e->impl->generate(rq, g, nullptr, nullptr);
         for (size_t i = 0; i < n; ++i) {
             results[i].status = DSOCR_OK;
             size_t m = std::min(r[i].size(), results[i].cap);
@@ -294,6 +314,8 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
         out->router = cp(p.router);
         out->layers_step = cp(p.layers_step);
         out->lm_head_screened = cp(p.lm_head_screened);
+        out->moe_gateup_kernel = p.gateup_kernel;
+        out->moe_down_kernel = p.down_kernel;
     });
 }
 
@@ -437,10 +459,7 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
                          const void* sWd, int wdtype, int norm_topk, float scaling, float* out, int* ids_out,
                          float* w_out) {
     return guarded([&] {
-        if (H % 8 || I % 8 || (Is && Is % 8)) throw std::runtime_error("EINVAL: dims must be multiples of 8");
-        if (E > 256 || topk > 8 || topk > E || T * topk > 512)
-            throw std::runtime_error("EINVAL: E <= 256, topk <= min(8, E), T*topk <= 512");
-        const int TK = T * topk;
+        if (T <= 0 || H <= 0 || E <= 0 || topk <= 0 || I <= 0) throw std::runtime_error("EINVAL: bad MoE shape");
         std::vector<void*> bufs;
         auto alloc = [&](size_t b) {
             void* p = nullptr;
@@ -448,54 +467,102 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
             bufs.push_back(p);
             return p;
         };
-        float* log = (float*)alloc(sizeof(float) * T * E);
-        dsocr::DecGemvArgs ra;
-        ra.M = T; ra.N = E; ra.K = H; ra.x = x; ra.ldx = H; ra.W = router; ra.ldw = H; ra.wdtype = wdtype;
-        ra.y = log; ra.ldy = E; ra.norm_w = norm_w; ra.eps = eps;
-        // same dispatch as Engine::moe_decode_args: slot mode for T <= 8, grouped by expert above
-        dsocr::MoeDec2Args m;
-        m.T = T; m.topk = topk; m.E = E; m.K = H; m.I = I; m.Hout = H;
-        m.x = x; m.norm_w = norm_w; m.eps = eps; m.Wgu = Wgu; m.Wd = Wd; m.wdtype = wdtype; m.out = out;
-        m.h = (float*)alloc(sizeof(float) * (size_t)TK * I);
-        int* ids = (int*)alloc(sizeof(int) * TK);
-        float* wts = (float*)alloc(sizeof(float) * TK);
-        m.ids = ids;
-        if (sWgu && sWd && Is > 0) {
-            m.Is = Is; m.sWgu = sWgu; m.sWd = sWd; m.hs = (float*)alloc(sizeof(float) * (size_t)T * Is);
+        try {
+            const int TK = T * topk;
+            // the engine's own dispatch (Engine::decode_step -> launch_moe_decode): mix kernels at one
+            // token, slot kernels at two, the grouped (expert-deduplicated) kernels at 3..8, sorted groups above
+            dsocr::MoeDecodeArgs a;
+            a.T = T; a.H = H; a.E = E; a.topk = topk; a.I = I;
+            a.x = x; a.norm_w = norm_w; a.eps = eps; a.out = out;
+            a.router = router; a.router_wdt = wdtype; a.Wgu = Wgu; a.Wd = Wd; a.wdtype = wdtype;
+            if (sWgu && sWd && Is > 0) {
+                a.Is = Is; a.sWgu = sWgu; a.sWd = sWd; a.hs = (float*)alloc(sizeof(float) * (size_t)T * Is);
+            }
+            a.softmax_scoring = 1; a.norm_topk = norm_topk; a.scaling = scaling;
+            a.xn = (float*)alloc(sizeof(float) * (size_t)T * H);
+            a.xn_router = (float*)alloc(sizeof(float) * (size_t)T * H);
+            a.logits = (float*)alloc(sizeof(float) * (size_t)T * E);
+            a.ids = (int*)alloc(sizeof(int) * TK);
+            a.wts = (float*)alloc(sizeof(float) * TK);
+            a.h = (float*)alloc(sizeof(float) * (size_t)TK * I);
+            a.grp = (int*)alloc(sizeof(int) * dsocr::moe_grp_ints(E, T, topk));
+            a.route_cnt = (int*)alloc(sizeof(int) * 16);
+            check_hip(hipMemset(a.route_cnt, 0, sizeof(int) * 16), "hipMemset");
+            if (T > 8) {
+                a.eoff = (int*)alloc(sizeof(int) * (E + 1)); a.arow = (int*)alloc(sizeof(int) * TK);
+                a.apos = (int*)alloc(sizeof(int) * TK); a.active = (int*)alloc(sizeof(int) * E);
+                a.aw = (float*)alloc(sizeof(float) * TK); a.n_active = (int*)alloc(sizeof(int));
+            }
+            dsocr::launch_moe_decode(a, nullptr);
+            check_hip(hipGetLastError(), "moe launch");
+            check_hip(hipDeviceSynchronize(), "moe");
+            if (ids_out) check_hip(hipMemcpy(ids_out, a.ids, sizeof(int) * TK, hipMemcpyDeviceToHost), "d2h");
+            if (w_out) check_hip(hipMemcpy(w_out, a.wts, sizeof(float) * TK, hipMemcpyDeviceToHost), "d2h");
+        } catch (...) {
+            for (void* p : bufs) (void)hipFree(p);
+            throw;
         }
-        const char* epi = getenv("DSOCR_ROUTER_EPI");
-        if (T <= 8 && epi && atoi(epi) && dsocr::dec_router_ok(T, E, H, topk)) {
-            int* cnt = (int*)alloc(sizeof(int) * 16);
-            check_hip(hipMemset(cnt, 0, sizeof(int) * 16), "hipMemset");
-            dsocr::DecRouteEpi re;
-            re.topk = topk; re.softmax_scoring = 1; re.norm_topk = norm_topk; re.scaling = scaling;
-            re.ids = ids; re.w = wts; re.counter = cnt;
-            dsocr::launch_dec_router(ra, re, nullptr);
-            m.slot_mode = 1; m.slots = TK; m.logits = nullptr; m.aw = wts;
-        } else if (T <= 8) {  // engine default: gate/up blocks route themselves
-            dsocr::launch_dec_gemv(ra, nullptr);
-            m.slot_mode = 1; m.slots = TK; m.logits = log; m.softmax_scoring = 1; m.norm_topk = norm_topk;
-            m.scaling = scaling; m.ids_out = ids; m.w_out = wts;
-        } else {
-            dsocr::launch_dec_gemv(ra, nullptr);
-            dsocr::MoeRouteArgs r;
-            r.logits = log; r.T = T; r.E = E; r.topk = topk; r.softmax_scoring = 1; r.norm_topk = norm_topk;
-            r.scaling = scaling; r.ids = ids; r.w = wts;
-            r.eoff = (int*)alloc(sizeof(int) * (E + 1)); r.arow = (int*)alloc(sizeof(int) * TK);
-            r.apos = (int*)alloc(sizeof(int) * TK); r.active = (int*)alloc(sizeof(int) * E);
-            r.aw = (float*)alloc(sizeof(float) * TK); r.n_active = (int*)alloc(sizeof(int));
-            dsocr::launch_moe_route(r, nullptr);
-            m.slots = std::min(E, TK);
-            m.eoff = r.eoff; m.arow = r.arow; m.apos = r.apos; m.active = r.active; m.n_active = r.n_active;
-            m.aw = r.aw;
-        }
-        dsocr::launch_moe_gateup2(m, nullptr);
-        dsocr::launch_moe_down2(m, nullptr);
-        hipError_t e = hipDeviceSynchronize();
-        if (e == hipSuccess && ids_out) e = hipMemcpy(ids_out, ids, sizeof(int) * TK, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && w_out) e = hipMemcpy(w_out, wts, sizeof(float) * TK, hipMemcpyDeviceToHost);
         for (void* p : bufs) (void)hipFree(p);
-        check_hip(e, "moe");
+    });
+}
+dsocr_status dsocr_k_moe_kernels(int T, int H, int E, int topk, int I, int Is, int has_norm, const char** gateup,
+                                 const char** down) {
+    return guarded([&] {
+        dsocr::MoeDecodeArgs a;
+        a.T = T; a.H = H; a.E = E; a.topk = topk; a.I = I; a.Is = Is;
+        int dummy = 0;
+        float fd = 0.f;
+        a.x = &fd; a.out = &fd; a.norm_w = has_norm ? &fd : nullptr;
+        if (Is > 0) { a.sWgu = &dummy; a.sWd = &dummy; a.hs = &fd; }
+        a.xn = a.xn_router = a.logits = a.wts = a.h = &fd;
+        a.ids = a.grp = a.route_cnt = &dummy;
+        if (T > 8) { a.eoff = a.arow = a.apos = a.active = a.n_active = &dummy; a.aw = &fd; }
+        dsocr::moe_decode_kernel_names(a, gateup, down);
+    });
+}
+dsocr_status dsocr_k_lmhead_screened(int B, int V, int K, const float* x, const float* norm_w, float eps,
+                                     const void* W, const int* ban, int ban_ld, int* out_tok) {
+    return guarded([&] {
+        if (B <= 0 || V <= 0 || K % 16 || K > 1536 || !x || !norm_w || !W || !out_tok)
+            throw std::runtime_error("EINVAL: screened lm_head needs B, V > 0, K % 16 == 0, K <= 1536, x / norm / W / out");
+        if (ban && ban_ld < 2) throw std::runtime_error("EINVAL: ban list stride < 2");
+        std::vector<void*> bufs;
+        auto alloc = [&](size_t b) {
+            void* p = nullptr;
+            check_hip(hipMalloc(&p, b ? b : 16), "hipMalloc");
+            bufs.push_back(p);
+            return p;
+        };
+        try {
+            // the engine's load-time quantisation and its per-step launches (Engine::decode_head)
+            void* q = alloc((size_t)V * K);
+            float* scale = (float*)alloc(sizeof(float) * V);
+            float* bound = (float*)alloc(sizeof(float) * V);
+            dsocr::launch_lmhead_quantize(W, V, K, q, scale, bound, nullptr);
+            dsocr::LmHeadQ8Args a;
+            a.x = x; a.ldx = K; a.norm_w = norm_w; a.eps = eps; a.q = q; a.scale = scale; a.bound = bound;
+            a.B = B; a.N = V; a.K = K; a.ban = ban; a.ban_ld = ban ? ban_ld : 0;
+            dsocr::lmhead_q8_grid(V, K, B, &a.nblk, &a.slot);
+            a.blk_cnt = (int*)alloc(sizeof(int) * B * a.nblk);
+            a.blk_t = (float*)alloc(sizeof(float) * B * a.nblk);
+            a.cand = (int*)alloc(sizeof(int) * B * a.nblk * a.slot);
+            a.cand_hi = (float*)alloc(sizeof(float) * B * a.nblk * a.slot);
+            a.xn_out = (float*)alloc(sizeof(float) * B * K);
+            dsocr::launch_lmhead_q8(a, nullptr);
+            dsocr::DecSampleArgs ss;  // selection only: empty contexts, no bookkeeping
+            ss.B = B; ss.V = V; ss.ld = V; ss.ctx = (int*)alloc(sizeof(int) * 64); ss.ctx_cap = 64;
+            ss.ctx_len = (int*)alloc(sizeof(int) * B); ss.ngram = 0; ss.out_tok = out_tok;
+            check_hip(hipMemset(ss.ctx_len, 0, sizeof(int) * B), "hipMemset");
+            ss.blk_cnt = a.blk_cnt; ss.blk_t = a.blk_t; ss.cand = a.cand; ss.cand_hi = a.cand_hi; ss.nblk = a.nblk;
+            ss.slot = a.slot; ss.w_exact = W; ss.xn = a.xn_out; ss.K = K;
+            dsocr::launch_dec_sample(ss, nullptr);
+            check_hip(hipGetLastError(), "screened lm_head launch");
+            check_hip(hipDeviceSynchronize(), "screened lm_head");
+        } catch (...) {
+            for (void* p : bufs) (void)hipFree(p);
+            throw;
+        }
+        for (void* p : bufs) (void)hipFree(p);
     });
 }
 dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,

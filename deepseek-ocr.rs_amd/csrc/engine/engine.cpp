@@ -986,39 +986,34 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     launch_moe_combine(Y, APOS, WTS, YS, T, K, H, X, 1, st);
 }
 
-// Decode MoE arguments of layer l for B pages (shared by decode_step and profile_decode).
-// B <= 8: slot mode (gate/up blocks route themselves from s_log); else grouped by expert.
-MoeDec2Args Engine::moe_decode_args(int l, int B, const float* x, const float* norm, float* out) {
+// Decode MoE arguments of layer l for B pages (shared by decode_step and profile_decode): the
+// layer's weights and the named workspaces; launch_moe_decode (decode.hip) picks the kernels.
+MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     const LangConfig& L = cfg_.lang;
     DecLayer& d = layers_[l];
     const int H = L.hidden, E = L.n_routed, K = L.topk, I = L.moe_inter, TK = B * K;
-    MoeDec2Args m;
-    m.T = B; m.K = H; m.Hout = H; m.x = x; m.norm_w = norm; m.eps = L.rms_eps; m.out = out;
-    m.topk = K; m.E = E; m.I = I;
-    m.Wgu = d.e_gu; m.Wd = d.e_d; m.wdtype = d.e_wdt;
-    m.h = wsf("s_ehh", (size_t)TK * I);
-    m.ids = wsi("s_ids", TK);
+    MoeDecodeArgs a;
+    a.T = B; a.H = H; a.E = E; a.topk = K; a.I = I;
+    a.x = X; a.norm_w = d.post_norm.w; a.eps = L.rms_eps; a.out = X;
+    a.router = d.router.W; a.router_wdt = d.router.wdt; a.router_bias = d.router.b;
+    a.Wgu = d.e_gu; a.Wd = d.e_d; a.wdtype = d.e_wdt;
     if (d.has_shared) {
         if (d.s_gu.wdt != d.e_wdt) throw std::runtime_error("EINTERNAL: shared/routed expert dtype mismatch");
-        m.Is = d.s_d.K; m.sWgu = d.s_gu.W; m.sWd = d.s_d.W; m.hs = wsf("s_shh", (size_t)B * m.Is);
+        a.Is = d.s_d.K; a.sWgu = d.s_gu.W; a.sWd = d.s_d.W; a.hs = wsf("s_shh", (size_t)B * a.Is);
     }
-    static const bool router_epi = getenv("DSOCR_ROUTER_EPI") && atoi(getenv("DSOCR_ROUTER_EPI"));
-    if (B <= 8 && router_epi && dec_router_ok(B, E, H, K)) {
-        // slot mode routed by dec_router's last-block epilogue (measured +1.6 us / layer on
-        // MI355X vs self-routing: the write-through + ticket hand-off costs more than it saves)
-        m.slot_mode = 1; m.slots = TK; m.logits = nullptr; m.aw = wsf("s_wts", TK);
-    } else if (B <= 8) {
-        // slot mode: every gate/up block routes itself from the router logits in s_log
-        m.slot_mode = 1; m.slots = TK; m.logits = wsf("s_log", (size_t)B * E);
-        m.softmax_scoring = L.scoring == "softmax"; m.norm_topk = L.norm_topk; m.scaling = L.routed_scaling;
-        m.ids_out = wsi("s_ids", TK); m.w_out = wsf("s_wts", TK);
-        if (const char* dbg = getenv("DSOCR_DBG_GU")) m.dbg = atoi(dbg);
-    } else {
-        m.slots = std::min(E, TK);
-        m.eoff = wsi("s_eoff", E + 1); m.arow = wsi("s_arow", TK); m.apos = wsi("s_apos", TK);
-        m.aw = wsf("s_aw", TK); m.active = wsi("s_active", E); m.n_active = wsi("s_nact", 1);
+    a.softmax_scoring = L.scoring == "softmax"; a.norm_topk = L.norm_topk; a.scaling = L.routed_scaling;
+    a.xn = wsf("s_xn", (size_t)B * H);
+    a.xn_router = wsf("s_xn_router", (size_t)B * H);
+    a.logits = wsf("s_log", (size_t)B * E);
+    a.ids = wsi("s_ids", TK); a.wts = wsf("s_wts", TK);
+    a.h = wsf("s_ehh", (size_t)TK * I);
+    a.grp = wsi("s_grp", moe_grp_ints(E, B, K));
+    a.route_cnt = wsi("s_route_cnt", 16);
+    if (B > 8) {
+        a.eoff = wsi("s_eoff", E + 1); a.arow = wsi("s_arow", TK); a.apos = wsi("s_apos", TK);
+        a.aw = wsf("s_aw", TK); a.active = wsi("s_active", E); a.n_active = wsi("s_nact", 1);
     }
-    return m;
+    return a;
 }
 
 void Engine::decode_step(int B, int Lmax) {
@@ -1034,13 +1029,7 @@ void Engine::decode_step(int B, int Lmax) {
     float* CTX = wsf("s_ctx", (size_t)B * H);
     float* part = wsf("s_part", dec_attn_workspace(B, L.heads, hd, Lmax) / 4 + 16);
     if (L.heads % L.kv_heads) throw std::runtime_error("EINVAL: num_attention_heads must be a multiple of num_key_value_heads");
-    // in-launch hand-off counters of the fused kernels: one block of SYNC_INTS per layer, zeroed
-    // by one memset node at the head of every step (a multiple of 16 bytes from the allocation start)
-    // (experiment, off by default: measured slower on MI355X at B = 1)
-    static const bool fused_moe = getenv("DSOCR_FUSED_MOE") && atoi(getenv("DSOCR_FUSED_MOE")) != 0;
-    int* sync = wsi("s_sync", (size_t)L.layers * SYNC_INTS);
     int* err = wsi("s_err", 4);
-    if (fused_moe) HIP_CHECK(hipMemsetAsync(sync, 0, sizeof(int) * L.layers * SYNC_INTS, st));
     for (int l = 0; l < L.layers; ++l) {
         DecLayer& d = layers_[l];
         const int QKVN = d.qkv.N;
@@ -1100,12 +1089,12 @@ void Engine::decode_step(int B, int Lmax) {
         if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
         else launch_dec_gemv(go, st);
         // MLP / MoE
-        const float* mx = X;
-        const float* mnorm = d.post_norm.w;
-        if (!fuse_norm) { launch_rmsnorm(X, H, XN, H, B, H, d.post_norm.w, L.rms_eps, st); mx = XN; mnorm = nullptr; }
-        MoeDec2Args m;
-        m.T = B; m.K = H; m.Hout = H; m.x = mx; m.norm_w = mnorm; m.eps = L.rms_eps; m.out = X;
         if (!d.moe) {
+            const float* mx = X;
+            const float* mnorm = d.post_norm.w;
+            if (!fuse_norm) { launch_rmsnorm(X, H, XN, H, B, H, d.post_norm.w, L.rms_eps, st); mx = XN; mnorm = nullptr; }
+            MoeDec2Args m;
+            m.T = B; m.K = H; m.Hout = H; m.x = mx; m.norm_w = mnorm; m.eps = L.rms_eps; m.out = X;
             m.topk = 0; m.E = 0; m.slots = 0; m.I = 8; m.Is = L.inter;
             m.sWgu = d.gu.W; m.sWd = d.down.W; m.wdtype = d.gu.wdt;
             m.hs = wsf("s_hh", (size_t)B * L.inter);
@@ -1114,46 +1103,7 @@ void Engine::decode_step(int B, int Lmax) {
             launch_moe_down2(m, st);
             continue;
         }
-        const int E = L.n_routed, K = L.topk, TK = B * K;
-        if (TK > 512 || E > 256 || K > 8) throw std::runtime_error("EINVAL: decode MoE supports batch*top_k <= 512, <= 256 experts, top_k <= 8");
-        float* LOG = wsf("s_log", (size_t)B * E);
-        DecGemvArgs gr;
-        gr.M = B; gr.N = E; gr.K = H; gr.x = mx; gr.ldx = H; gr.W = d.router.W; gr.ldw = H; gr.wdtype = d.router.wdt;
-        gr.bias = d.router.b; gr.y = LOG; gr.ldy = E; gr.norm_w = mnorm; gr.eps = L.rms_eps;
-        m = moe_decode_args(l, B, mx, mnorm, X);
-        static const bool gu_mix = !(getenv("DSOCR_GU_MIX") && atoi(getenv("DSOCR_GU_MIX")) == 0);
-        const bool mix = gu_mix && fuse_norm && moe_gateup_mix_ok(m);
-        float* XNR = wsf("s_xn_router", (size_t)B * H);
-        if (mix) gr.xn_out = XNR;  // the router hands its normalised row to the gate/up waves
-        if (m.slot_mode && !m.logits) {
-            DecRouteEpi re;
-            re.topk = K; re.softmax_scoring = L.scoring == "softmax"; re.norm_topk = L.norm_topk;
-            re.scaling = L.routed_scaling; re.ids = const_cast<int*>(m.ids); re.w = const_cast<float*>(m.aw);
-            re.counter = wsi("s_route_cnt", 16);
-            launch_dec_router(gr, re, st);
-        } else {
-            launch_dec_gemv(gr, st);
-        }
-        if (!m.slot_mode) {  // B > 8: one block sorts the assignments by expert
-            MoeRouteArgs ra;
-            ra.logits = LOG; ra.T = B; ra.E = E; ra.topk = K; ra.softmax_scoring = L.scoring == "softmax";
-            ra.norm_topk = L.norm_topk; ra.scaling = L.routed_scaling;
-            ra.ids = const_cast<int*>(m.ids); ra.w = wsf("s_wts", TK); ra.eoff = const_cast<int*>(m.eoff);
-            ra.arow = const_cast<int*>(m.arow); ra.apos = const_cast<int*>(m.apos); ra.aw = const_cast<float*>(m.aw);
-            ra.active = const_cast<int*>(m.active); ra.n_active = const_cast<int*>(m.n_active);
-            launch_moe_route(ra, st);
-        }
-        m.sync = sync + (size_t)l * SYNC_INTS;
-        m.err = err;
-        if (fused_moe && moe_fused_ok(m)) {
-            launch_moe_fused(m, st);
-            continue;
-        }
-        if (mix) launch_moe_gateup_mix(m, XNR, st);
-        else launch_moe_gateup2(m, st);
-        static const bool dn_mix = !(getenv("DSOCR_DN_MIX") && atoi(getenv("DSOCR_DN_MIX")) == 0);
-        if (dn_mix && moe_down_mix_ok(m)) launch_moe_down_mix(m, st);
-        else launch_moe_down2(m, st);
+        launch_moe_decode(moe_args(l, B, X), st);
     }
 }
 
@@ -1216,6 +1166,7 @@ void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
         g.x = SXN; g.ldx = H;
     }
     launch_dec_gemv(g, st);
+    if (trace_) launch_trace_logits(sa.logits, B, L.vocab, sa.ld, sa.out_len, sa.done, trace_, trace_steps_, st);
     launch_rep_penalty(pen, st);
     launch_dec_sample(sa, st);
 }
@@ -1325,9 +1276,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipEventRecord(ev[1], st));
 
-    // ---------------- 2. prefill input rows (embed + inject, model/mod.rs:1208-1239)
-    std::vector<int> kind(T), index(T), row_page(T), row_pos(T);
-    std::vector<long> q_off(B), kv_off(B), o_off(B);
+    // ---------------- 2. image rows for the injection (model/mod.rs:1208-1239)
     // host image rows of all pages concatenated (kind 1), device vision rows via per-row pointers:
     // we copy them into one contiguous device buffer per kind to keep the assemble kernel simple.
     std::vector<float> host_rows;
@@ -1357,11 +1306,11 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
             HIP_CHECK(hipMemcpyAsync(vis_rows + (vis_base[b] + vis_local_rows[b]) * H, gpost[b],
                                      vis_global_rows[b] * H * 4, hipMemcpyDeviceToDevice, st));
         }
-    long r0 = 0;
+    // image-row sequence of every page (format_local_tokens / format_global_tokens /
+    // assemble_artifacts order, model/mod.rs:656-709,879-923): (kind, index) per <image> slot
+    std::vector<std::vector<std::pair<int, long>>> img(B);
     for (int b = 0; b < B; ++b) {
         const GenRequest& rq = reqs[b];
-        // image token sequence for this page: list of (kind, index)
-        std::vector<std::pair<int, long>> img;
         if (rq.page) {
             const PagePixels* pg = rq.page;
             if (pg->n_tiles > 0) {
@@ -1369,44 +1318,28 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
                 for (int R = 0; R < pg->crop_h * ls; ++R) {
                     for (int Cc = 0; Cc < pg->crop_w * ls; ++Cc) {
                         int crop = (R / ls) * pg->crop_w + (Cc / ls);
-                        img.push_back({2, vis_base[b] + ((long)crop * ls + R % ls) * ls + Cc % ls});
+                        img[b].push_back({2, vis_base[b] + ((long)crop * ls + R % ls) * ls + Cc % ls});
                     }
-                    img.push_back({3, 0});
+                    img[b].push_back({3, 0});
                 }
             }
             const int gs = pg->gsize / 64;
             for (int R = 0; R < gs; ++R) {
-                for (int Cc = 0; Cc < gs; ++Cc) img.push_back({2, vis_base[b] + vis_local_rows[b] + (long)R * gs + Cc});
-                img.push_back({3, 0});
+                for (int Cc = 0; Cc < gs; ++Cc) img[b].push_back({2, vis_base[b] + vis_local_rows[b] + (long)R * gs + Cc});
+                img[b].push_back({3, 0});
             }
-            img.push_back({4, 0});
+            img[b].push_back({4, 0});
         } else if (rq.image_rows) {
-            for (size_t i = 0; i < rq.n_image_rows; ++i) img.push_back({1, host_row_base[b] + (long)i});
+            for (size_t i = 0; i < rq.n_image_rows; ++i) img[b].push_back({1, host_row_base[b] + (long)i});
         }
         size_t n_mask = 0;
         for (int i = 0; i < prompt_len[b]; ++i) n_mask += (!rq.mask.empty() && rq.mask[i]) ? 1 : 0;
-        if (n_mask != img.size())
+        if (n_mask != img[b].size())
             throw std::runtime_error("EINVAL: prompt/image embedding mismatch: image embeddings provide " +
-                                     std::to_string(img.size()) + " tokens but mask requires " + std::to_string(n_mask));
-        size_t j = 0;
-        for (int i = 0; i < prompt_len[b]; ++i) {
-            const long r = r0 + i;
-            if (!rq.mask.empty() && rq.mask[i]) {
-                kind[r] = img[j].first;
-                index[r] = (int)img[j].second;
-                ++j;
-            } else {
-                const int id = rq.ids[i];
-                if (id < 0 || id >= L.vocab) throw std::runtime_error("EINVAL: token id out of bounds for vocab size");
-                kind[r] = 0;
-                index[r] = id;
-            }
-            row_page[r] = b;
-            row_pos[r] = i;
-        }
-        q_off[b] = 0;  // set below once strides are known
-        o_off[b] = r0 * H;
-        r0 += prompt_len[b];
+                                     std::to_string(img[b].size()) + " tokens but mask requires " + std::to_string(n_mask));
+        for (int i = 0; i < prompt_len[b]; ++i)
+            if ((rq.mask.empty() || !rq.mask[i]) && (rq.ids[i] < 0 || rq.ids[i] >= L.vocab))
+                throw std::runtime_error("EINVAL: token id out of bounds for vocab size");
     }
     const int Lmax = max_p + (int)p.max_new + 1;
     ensure_rope(Lmax + 1);
@@ -1422,47 +1355,68 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
     HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     const int QKVN = layers_[0].qkv.N;
-    r0 = 0;
-    for (int b = 0; b < B; ++b) {
-        q_off[b] = r0 * QKVN;
-        kv_off[b] = (long)b * page_stride_;
-        r0 += prompt_len[b];
-    }
-    float* X = wsf("d_x", (size_t)T * H);
-    {
-        int* dk = upload("g_kind", kind);
-        int* di = upload("g_index", index);
-        float* hr = host_rows.empty() ? nullptr : upload("g_hostrows", host_rows);
-        launch_assemble_rows(dk, di, (int)T, H, embed_, embed_dt_, hr, vis_rows, newline_, separator_, X, H, st);
-    }
-    int* d_row_page = upload("g_rowpage", row_page);
-    int* d_row_pos = upload("g_rowpos", row_pos);
-    long* d_q_off = upload("g_qoff", q_off);
-    long* d_kv_off = upload("g_kvoff", kv_off);
-    long* d_o_off = upload("g_ooff", o_off);
-    int* d_plen = upload("g_plen", prompt_len);
-
-    // ---------------- 3. prefill (decode.prefill)
-    HIP_CHECK(hipEventRecord(ev[2], st));
-    for (int l = 0; l < L.layers; ++l)
-        layer_forward_prefill(l, (int)T, B, d_row_page, d_row_pos, d_q_off, d_kv_off, d_o_off, d_plen, max_p, Lmax);
-    // last row of every page -> final norm -> lm_head (the reference projects every
-    // position, transformer/model.rs:243-270; only the last row is ever read)
-    std::vector<int> last_rows(B);
-    r0 = 0;
-    for (int b = 0; b < B; ++b) { r0 += prompt_len[b]; last_rows[b] = (int)(r0 - 1); }
     float* SX = wsf("s_x", (size_t)B * H);
     float* SXN = wsf("s_xn", (size_t)B * H);
     float* LOGITS = wsf("s_logits", (size_t)B * L.vocab);
-    {
-        std::vector<int> zero(B, 0);
-        std::vector<int> lr_kind(B, 1);
-        int* dk = upload("g_lrkind", lr_kind);
-        int* di = upload("g_lrindex", last_rows);
-        launch_assemble_rows(dk, di, B, H, nullptr, 0, X, nullptr, nullptr, nullptr, SX, H, st);
-    }
-    launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
-    linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
+
+    // ---------------- 3. the forward over whole token sequences (DeepseekOcrModel::forward,
+    // model/mod.rs:1181-1251): embed + inject (1208-1239), every layer, final norm + lm_head on the
+    // last row of each page (the reference projects every position, transformer/model.rs:243-270;
+    // only the last row is ever read).  The prefill runs it once on the prompts; use_cache = false
+    // (generate_without_cache, model/mod.rs:2051-2283) re-runs it on prompt + generated every step.
+    auto forward_rows = [&](const std::vector<int>& lens, const std::vector<std::vector<int>>& extra) {
+        long Tn = 0;
+        int maxl = 0;
+        for (int b = 0; b < B; ++b) { Tn += lens[b]; maxl = std::max(maxl, lens[b]); }
+        std::vector<int> kind(Tn), index(Tn), row_page(Tn), row_pos(Tn);
+        std::vector<long> q_off(B), kv_off(B), o_off(B);
+        long r0 = 0;
+        for (int b = 0; b < B; ++b) {
+            const GenRequest& rq = reqs[b];
+            size_t j = 0;
+            for (int i = 0; i < lens[b]; ++i) {
+                const long r = r0 + i;
+                if (i < prompt_len[b] && !rq.mask.empty() && rq.mask[i]) {
+                    kind[r] = img[b][j].first;
+                    index[r] = (int)img[b][j].second;
+                    ++j;
+                } else {
+                    kind[r] = 0;
+                    index[r] = i < prompt_len[b] ? rq.ids[i] : extra[b][i - prompt_len[b]];
+                }
+                row_page[r] = b;
+                row_pos[r] = i;
+            }
+            q_off[b] = r0 * QKVN;
+            kv_off[b] = (long)b * page_stride_;
+            o_off[b] = r0 * H;
+            r0 += lens[b];
+        }
+        float* X = wsf("d_x", (size_t)Tn * H);
+        int* dk = upload("g_kind", kind);
+        int* di = upload("g_index", index);
+        float* hr = host_rows.empty() ? nullptr : upload("g_hostrows", host_rows);
+        launch_assemble_rows(dk, di, (int)Tn, H, embed_, embed_dt_, hr, vis_rows, newline_, separator_, X, H, st);
+        int* d_row_page = upload("g_rowpage", row_page);
+        int* d_row_pos = upload("g_rowpos", row_pos);
+        long* d_q_off = upload("g_qoff", q_off);
+        long* d_kv_off = upload("g_kvoff", kv_off);
+        long* d_o_off = upload("g_ooff", o_off);
+        int* d_plen = upload("g_plen", lens);
+        for (int l = 0; l < L.layers; ++l)
+            layer_forward_prefill(l, (int)Tn, B, d_row_page, d_row_pos, d_q_off, d_kv_off, d_o_off, d_plen, maxl, Lmax);
+        std::vector<int> last_rows(B), lr_kind(B, 1);
+        r0 = 0;
+        for (int b = 0; b < B; ++b) { r0 += lens[b]; last_rows[b] = (int)(r0 - 1); }
+        int* lk = upload("g_lrkind", lr_kind);
+        int* li = upload("g_lrindex", last_rows);
+        launch_assemble_rows(lk, li, B, H, nullptr, 0, X, nullptr, nullptr, nullptr, SX, H, st);
+        launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+        linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
+    };
+    HIP_CHECK(hipEventRecord(ev[2], st));
+    std::vector<std::vector<int>> extra(B);
+    forward_rows(prompt_len, extra);
 
     // sampling state: context = prompt ids (+ generated), sampling.rs:34-96
     const long ctx_cap = max_p + (long)p.max_new + 1;
@@ -1514,12 +1468,21 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         for (int b = 0; b < B; ++b) memcpy(&all[(size_t)b * RNG_WORDS], st.data(), sizeof(uint32_t) * RNG_WORDS);
         sa.rng = reinterpret_cast<uint32_t*>(upload("s_rng", all));
     }
-    if (!p.do_sample && screen_applies(B, p.rep_penalty)) {
+    if (!p.do_sample && !p.trace && screen_applies(B, p.rep_penalty)) {
         // the screened head reads the n-gram ban list each selection kernel leaves for the next step
         sa.ban_ld = ctx_cap + 1;
         sa.ban_out = wsi("s_ban", (size_t)B * sa.ban_ld);
         reserve_head_ws(B);
         if (getenv("DSOCR_SCREEN_STATS")) HIP_CHECK(hipMemsetAsync(wsi("s_scrstats", 32), 0, 128, st));
+    }
+    // parity trace: the raw logits of every step of every page ([B][max_new][V], index = tokens
+    // emitted so far), copied before the repetition penalty like the reference's debug dump
+    // (crates/infer-deepseek/src/debug.rs) — the exact lm_head runs (no screening) while tracing
+    trace_ = p.trace ? wsf("s_trace", (size_t)B * p.max_new * L.vocab) : nullptr;
+    trace_steps_ = (long)p.max_new;
+    if (trace_) {
+        HIP_CHECK(hipMemsetAsync(trace_, 0, sizeof(float) * B * p.max_new * L.vocab, st));
+        launch_trace_logits(LOGITS, B, L.vocab, L.vocab, d_outlen, d_done, trace_, trace_steps_, st);
     }
     // the fused selection kernel advances the KV position; after the prefill the first
     // decode position must be P, so start one behind
@@ -1533,7 +1496,57 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         HIP_CHECK(hipStreamSynchronize(st));
     }
     HIP_CHECK(hipEventRecord(ev[3], st));
-
+    std::vector<int> h_done(B), h_outlen(B);
+    std::vector<int> h_out;
+    size_t steps = 0;
+    int* pin_done = nullptr;
+    HIP_CHECK(hipHostMalloc((void**)&pin_done, sizeof(int) * (3 * B + 1)));
+    // stream callback with the tokens so far (B = 1; model/mod.rs:1980-1982 calls it after every token)
+    int streamed = 0;
+    auto stream_tokens = [&](int n) {
+        if (n <= streamed) return;  // no new token (EOS selected, or the page is done)
+        streamed = n;
+        std::vector<int> tmp(n);
+        if (n) HIP_CHECK(hipMemcpy(tmp.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+        std::vector<int64_t> t64(tmp.begin(), tmp.end());
+        cb(t64.size(), t64.data(), user);
+    };
+    auto poll = [&]() {  // done flags, output lengths and the last tokens of every page
+        HIP_CHECK(hipMemcpyAsync(pin_done, d_done, B * 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(pin_done + B, d_outlen, B * 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(pin_done + 2 * B, d_tok, B * 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        bool all = true;
+        for (int b = 0; b < B; ++b) all &= pin_done[b] != 0;
+        return all;
+    };
+    if (cb && B == 1 && p.max_new > 0) {
+        poll();
+        if (pin_done[B] > 0) stream_tokens(pin_done[B]);
+    }
+    if (!p.use_cache) {
+        // ---------------- 4'. generate_without_cache (model/mod.rs:2051-2283): every step re-runs the
+        // whole forward on prompt + generated tokens (image rows re-injected at the same slots), then
+        // the same selection / bookkeeping kernels as the cached loop
+        HIP_CHECK(hipEventRecord(ev[4], st));
+        std::vector<int> lens = prompt_len;
+        for (size_t i = 1; i < p.max_new; ++i) {
+            if (poll()) break;
+            for (int b = 0; b < B; ++b)
+                if (!pin_done[b]) { extra[b].push_back(pin_done[2 * B + b]); ++lens[b]; }
+            forward_rows(lens, extra);
+            if (trace_) launch_trace_logits(LOGITS, B, L.vocab, L.vocab, d_outlen, d_done, trace_, trace_steps_, st);
+            launch_rep_penalty(pen, st);
+            launch_dec_sample(sa, st);
+            ++steps;
+            if (cb && B == 1) {
+                poll();
+                stream_tokens(pin_done[B]);
+            }
+        }
+        HIP_CHECK(hipEventRecord(ev[5], st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    } else {
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
@@ -1562,34 +1575,22 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
 
     HIP_CHECK(hipEventRecord(ev[4], st));
-    std::vector<int> h_done(B), h_outlen(B);
-    std::vector<int> h_out;
-    size_t steps = 0;
-    int* pin_done = nullptr;
-    HIP_CHECK(hipHostMalloc((void**)&pin_done, sizeof(int) * (2 * B + 1)));
     for (size_t i = 1; i < p.max_new; ++i) {
         if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
         else step_body();
         ++steps;
         const bool check = cb != nullptr || (!p.ignore_eos && (i % 8 == 0 || i + 1 == p.max_new));
         if (check) {
-            HIP_CHECK(hipMemcpyAsync(pin_done, d_done, B * 4, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipMemcpyAsync(pin_done + B, d_outlen, B * 4, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            if (cb && B == 1) {
-                int n = pin_done[B];
-                std::vector<int> tmp(n);
-                HIP_CHECK(hipMemcpy(tmp.data(), d_out, n * 4, hipMemcpyDeviceToHost));
-                std::vector<int64_t> t64(tmp.begin(), tmp.end());
-                cb(t64.size(), t64.data(), user);
-            }
-            bool all = true;
-            for (int b = 0; b < B; ++b) all &= pin_done[b] != 0;
+            const bool all = poll();
+            if (cb && B == 1) stream_tokens(pin_done[B]);
             if (all) break;
         }
     }
     HIP_CHECK(hipEventRecord(ev[5], st));
     HIP_CHECK(hipStreamSynchronize(st));
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    }  // cached decode loop
     HIP_CHECK(hipHostFree(pin_done));
     {
         int e = 0;
@@ -1604,9 +1605,6 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         for (int k = 0; k < 7; ++k) fprintf(stderr, " %.2f", h[4 + k] / st / 100.0);  // wall clock: 100 MHz
         fprintf(stderr, "\n");
     }
-    if (gexec) (void)hipGraphExecDestroy(gexec);
-    if (graph) (void)hipGraphDestroy(graph);
-
     h_out.resize((size_t)B * p.max_new);
     HIP_CHECK(hipMemcpy(h_out.data(), d_out, h_out.size() * 4, hipMemcpyDeviceToHost));
     HIP_CHECK(hipMemcpy(h_outlen.data(), d_outlen, B * 4, hipMemcpyDeviceToHost));
@@ -1617,6 +1615,9 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     timings_.iterative_ms = ms_between(ev[4], ev[5]);
     timings_.generate_ms = ms_between(ev[2], ev[3]) + ms_between(ev[4], ev[5]);
     timings_.steps = steps;
+    if (trace_ && p.trace)
+        HIP_CHECK(hipMemcpy(p.trace, trace_, sizeof(float) * B * p.max_new * L.vocab, hipMemcpyDeviceToHost));
+    trace_ = nullptr;
     last_B_ = B;
     last_Lmax_ = Lmax;
     (void)t0;
@@ -1696,38 +1697,14 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         // replay on a scratch copy of the residual stream so the engine state is untouched
         float* Xs = wsf("p_x", (size_t)B * H);
         HIP_CHECK(hipMemcpyAsync(Xs, Xc, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
-        auto args = [&](int l) { return moe_decode_args(l, B, Xs, B <= 2 ? layers_[l].post_norm.w : nullptr, Xs); };
+        // the gate/up and down launches of decode_step's dispatch (launch_moe_decode), replayed
+        // alone on the routing state the last step left (logits, normalised rows, expert groups)
+        auto args = [&](int l) { return moe_args(l, B, Xs); };
         const int n = iters * (int)moe_layers.size();
+        moe_decode_kernel_names(args(moe_layers[0]), &prof.gateup_kernel, &prof.down_kernel);
         // rotating over the layers (~55 MB each) defeats the 256 MB Infinity Cache
-        static const bool gu_mix = !(getenv("DSOCR_GU_MIX") && atoi(getenv("DSOCR_GU_MIX")) == 0);
-        float* XNR = wsf("s_xn_router", (size_t)B * H);
-        timed(prof.moe_gateup, n, [&](int i) {
-            const MoeDec2Args m = args(moe_layers[i % moe_layers.size()]);
-            if (gu_mix && B <= 2 && moe_gateup_mix_ok(m)) launch_moe_gateup_mix(m, XNR, st);
-            else launch_moe_gateup2(m, st);
-        });
-        timed(prof.moe_down, n, [&](int i) {
-            const MoeDec2Args m = args(moe_layers[i % moe_layers.size()]);
-            static const bool dn_mix = !(getenv("DSOCR_DN_MIX") && atoi(getenv("DSOCR_DN_MIX")) == 0);
-            if (dn_mix && moe_down_mix_ok(m)) launch_moe_down_mix(m, st);
-            else launch_moe_down2(m, st);
-        });
-        if (const char* path = getenv("DSOCR_STAMPS_OUT")) {
-            // dev: per-block phase clocks of one gate/up launch (moe_gateup_slot_kernel)
-            const size_t nstamp = 4096 * 8;
-            auto* d_st = (unsigned long long*)ws("p_stamps", nstamp * 8);
-            HIP_CHECK(hipMemsetAsync(d_st, 0, nstamp * 8, st));
-            MoeDec2Args m = args(moe_layers[0]);
-            m.stamps = d_st;
-            launch_moe_gateup2(m, st);
-            std::vector<unsigned long long> h(nstamp);
-            HIP_CHECK(hipMemcpyAsync(h.data(), d_st, nstamp * 8, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            if (FILE* f = fopen(path, "wb")) {
-                fwrite(h.data(), 8, nstamp, f);
-                fclose(f);
-            }
-        }
+        timed(prof.moe_gateup, n, [&](int i) { launch_moe_decode(args(moe_layers[i % moe_layers.size()]), st, MOE_GATEUP); });
+        timed(prof.moe_down, n, [&](int i) { launch_moe_decode(args(moe_layers[i % moe_layers.size()]), st, MOE_DOWN); });
         const DecLayer& d0 = layers_[moe_layers[0]];
         const double Is = d0.has_shared ? d0.s_d.K : 0;
         const double touched = (double)prof.experts_touched;
@@ -1825,7 +1802,6 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         const float* SX = wsf("s_x", (size_t)B * H);
         float* Y = wsf("p_qkv", (size_t)B * QKVN);
         float* XO = wsf("p_xo", (size_t)B * H);
-        float* LG = wsf("p_rlog", (size_t)B * std::max(1, L.n_routed));
         const int n = iters * L.layers;
         const bool fuse_norm = B <= 2;
         timed(prof.qkv, n, [&](int i) {
@@ -1851,23 +1827,11 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         for (int l = 0; l < L.layers; ++l)
             if (layers_[l].moe) moe_l.push_back(l);
         if (!moe_l.empty()) {
+            // the routing launches of the dispatch ([RMSNorm +] router GEMV [+ routing / grouping])
             timed(prof.router, iters * (int)moe_l.size(), [&](int i) {
-                const int l = moe_l[i % moe_l.size()];
-                const DecLayer& d = layers_[l];
-                DecGemvArgs gr;
-                gr.M = B; gr.N = L.n_routed; gr.K = H; gr.x = SX; gr.ldx = H; gr.W = d.router.W; gr.ldw = H;
-                gr.wdtype = d.router.wdt; gr.bias = d.router.b; gr.y = LG; gr.ldy = L.n_routed;
-                if (fuse_norm) { gr.norm_w = d.post_norm.w; gr.eps = L.rms_eps; }
-                const MoeDec2Args m = moe_decode_args(l, B, SX, fuse_norm ? d.post_norm.w : nullptr, XO);
-                if (m.slot_mode && !m.logits) {  // the router kernel also routes (as in decode_step)
-                    DecRouteEpi re;
-                    re.topk = L.topk; re.softmax_scoring = L.scoring == "softmax"; re.norm_topk = L.norm_topk;
-                    re.scaling = L.routed_scaling; re.ids = wsi("p_ids", (size_t)B * L.topk);
-                    re.w = wsf("p_w", (size_t)B * L.topk); re.counter = wsi("s_route_cnt", 16);
-                    launch_dec_router(gr, re, st);
-                } else {
-                    launch_dec_gemv(gr, st);
-                }
+                MoeDecodeArgs ma = moe_args(moe_l[i % moe_l.size()], B, XO);
+                ma.x = SX;
+                launch_moe_decode(ma, st, MOE_ROUTE);
             });
             prof.router.bytes = (double)L.n_routed * H * 2.0 + (double)B * (H + L.n_routed) * 4.0;
             prof.router.flops = 2.0 * B * (double)L.n_routed * H;

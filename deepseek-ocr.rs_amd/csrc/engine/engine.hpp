@@ -122,6 +122,8 @@ struct GenParams {
     long top_k = 0;
     bool seed_set = false;
     uint64_t seed = 0;
+    bool use_cache = true;  // false: generate_without_cache (model/mod.rs:2051-2283)
+    float* trace = nullptr; // host [B][max_new][vocab]: raw logits of every step (parity hook)
 };
 typedef void (*TokenCb)(size_t, const int64_t*, void*);
 // rand_core seed_from_u64 for rand 0.8.5 StdRng, in the layout sampling.hip reads (RNG_WORDS words)
@@ -149,6 +151,8 @@ class Engine {
     struct DecodeProfile {
         KernelProfile moe_gateup, moe_down, attention, lm_head, qkv, o_proj, router, layers_step, lm_head_screened;
         int experts_touched = 0, tokens = 0, kv_len = 0;
+        const char* gateup_kernel = "";  // kernels the dispatch picked at this batch size
+        const char* down_kernel = "";
     };
     DecodeProfile profile_decode(int iters);
     hipStream_t stream() const { return stream_; }
@@ -188,7 +192,7 @@ class Engine {
     float* vision_pass(const float* imgs, int n, int S, const std::string& out);
     void prefill(int B, const std::vector<int>& rows_per_page, const float* x0, int Lmax);
     void decode_step(int B, int Lmax);
-    MoeDec2Args moe_decode_args(int l, int B, const float* x, const float* norm, float* out);
+    MoeDecodeArgs moe_args(int l, int B, float* X);
     void decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen);
     void reserve_head_ws(int B);
     bool screen_applies(int B, float rep_penalty) const;
@@ -232,6 +236,8 @@ class Engine {
     std::map<std::string, std::pair<void*, size_t>> pinned_;
     std::map<std::pair<int, int>, std::pair<int*, int*>> winmaps_;  // (n, grid) -> tok2win, win2tok
     int last_Lmax_ = 0;
+    float* trace_ = nullptr;  // device logits trace of the running generate (parity hook)
+    long trace_steps_ = 0;
 
     void* dev_alloc(size_t bytes);
     void ensure_rope(int len);

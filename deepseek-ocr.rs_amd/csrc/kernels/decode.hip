@@ -880,12 +880,54 @@ __global__ __launch_bounds__(256) void dec_router_kernel(DecGemvArgs a, DecRoute
     // every logit was stored sc1 and is read back with sc1 loads: no acquire fence needed
     // (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!r.grp) {
+        for (int t = wave; t < a.M; t += 4)
+            topk_write(a.y + (long)t * a.ldy, a.N, r.topk, r.softmax_scoring, r.norm_topk, r.scaling,
+                       r.ids + t * r.topk, r.w + t * r.topk, true);
+        return;
+    }
+    // picks into LDS, then wave 0 groups them by expert (records in increasing expert order, the
+    // tokens of a record in increasing order: the h rows t*topk + k are scanned in order)
+    __shared__ int ids_s[64];
+    __shared__ float w_s[64];
     for (int t = wave; t < a.M; t += 4)
-        topk_write(a.y + (long)t * a.ldy, a.N, r.topk, r.softmax_scoring, r.norm_topk, r.scaling, r.ids + t * r.topk,
-                   r.w + t * r.topk, true);
+        topk_write(a.y + (long)t * a.ldy, a.N, r.topk, r.softmax_scoring, r.norm_topk, r.scaling, ids_s + t * r.topk,
+                   w_s + t * r.topk, true);
+    __syncthreads();
+    const int TK = a.M * r.topk;
+    if (threadIdx.x < TK) {
+        r.ids[threadIdx.x] = ids_s[threadIdx.x];
+        r.w[threadIdx.x] = w_s[threadIdx.x];
+    }
+    if (wave == 0) {
+        int base = 0;
+        for (int e0 = 0; e0 < a.N; e0 += 64) {
+            const int e = e0 + lane;
+            int cnt = 0;
+            for (int i = 0; i < TK; ++i) cnt += ids_s[i] == e ? 1 : 0;
+            const unsigned long long act = __ballot(cnt > 0 && e < a.N);
+            const int s = base + __popcll(act & ((1ull << lane) - 1ull));
+            if (cnt > 0 && e < a.N) {
+                int* rec = r.grp + MOE_GRP_REC * (1 + s);
+                rec[0] = e;
+                rec[1] = cnt;
+                int n = 0;
+                for (int i = 0; i < TK; ++i)
+                    if (ids_s[i] == e) {
+                        rec[2 + n] = i;
+                        rec[10 + n] = __float_as_int(w_s[i]);
+                        ++n;
+                    }
+            }
+            base += __popcll(act);
+        }
+        if (lane == 0) r.grp[0] = base;
+    }
 }
 
-bool dec_router_ok(int T, int E, int K, int topk) { return T <= 8 && E <= 256 && K <= 64 * 3 * 8 && topk <= 8; }
+bool dec_router_ok(int T, int E, int K, int topk) {
+    return T <= 8 && E <= 256 && K <= 64 * 3 * 8 && topk <= 8 && T * topk <= 64;
+}
 
 void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s) {
     if (!dec_router_ok(a.M, a.N, a.K, r.topk) || !r.counter) throw std::runtime_error("EINVAL: dec_router out of range");
@@ -2441,6 +2483,367 @@ void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
     } else {
         if (stage) hipLaunchKernelGGL((moe_down2_kernel<f16_t, true>), grid, dim3(256), lds, s, a);
         else hipLaunchKernelGGL((moe_down2_kernel<f16_t, false>), grid, dim3(256), 0, s, a);
+    }
+}
+
+// ------------------------------------------------------------------ grouped decode MoE (3..8 tokens)
+// At 3..8 pages the slot kernels stream an expert once per (token, pick): 48 picks at 8 pages read
+// ~2.8x the bytes of the distinct experts.  Here the router epilogue's records (MOE_GRP_*) give each
+// distinct expert once with its tokens.
+//
+// Gate/up: blocks [0, units_s) are the shared expert over all T tokens, then (record s, unit u)
+// s-major (records past n_active exit before any barrier).  Per block: the record (one scalar round
+// trip), the activation rows of its tokens into registers, the RB gate + RB up rows per wave
+// (16-byte nontemporal loads), then the rows are staged in LDS and every weight chunk is FMA'd
+// against each token's row — the per-row arithmetic of the slot kernels (chunk u-major, then j).
+template <typename WT, int RB>
+__global__ __launch_bounds__(256) void moe_gateup_grp_kernel(MoeDec2Args a) {
+    extern __shared__ float smem[];
+    constexpr int U = 3, XR = 2, MT = 8;  // K <= 1536, T <= 8
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
+    const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
+    int bid = blockIdx.x;
+    const bool shared = bid < units_s;
+    int s = 0, u = bid;
+    if (!shared) {
+        bid -= units_s;
+        s = bid / units_r;
+        u = bid % units_r;
+    }
+    const int* rec = a.grp + MOE_GRP_REC * (1 + s);
+    int e = 0, cnt = a.T;
+    int rows[MT];
+    float wts[MT];
+    if (!shared) {
+        if (s >= a.grp[0]) return;  // block-uniform, before any barrier
+        e = rec[0];
+        cnt = rec[1];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            rows[m] = rec[2 + min(m, cnt - 1)];
+            wts[m] = __int_as_float(rec[10 + min(m, cnt - 1)]);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) { rows[m] = min(m, cnt - 1); wts[m] = 1.f; }
+    }
+    // 1. activation rows (token t = row / topk for routed picks) into registers
+    float4 xr[MT][XR];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int t = shared ? rows[m] : rows[m] / a.topk;
+        const float* xp = a.x + (long)t * a.K;
+#pragma unroll
+        for (int i = 0; i < XR; ++i) xr[m][i] = *reinterpret_cast<const float4*>(xp + min((tid + i * 256) * 4, a.K - 4));
+    }
+    // 2. the weight stream
+    const int rows_I = shared ? a.Is : a.I;
+    const WT* Wg = shared ? reinterpret_cast<const WT*>(a.sWgu) : reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
+    const WT* Wu = Wg + (long)rows_I * a.K;
+    const int i0 = (u * 4 + wave) * RB;
+    const int chunks = a.K >> 3;
+    uint4 qg[U][RB], qu[U][RB];
+#pragma unroll
+    for (int uu = 0; uu < U; ++uu) {
+        const int cc = min(uu * 64 + lane, chunks - 1);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int i = min(i0 + r, rows_I - 1);
+            qg[uu][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
+            qu[uu][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
+        }
+    }
+    // 3. stage the rows (waits for the activation loads only)
+    float* xs = smem;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+        if (m < cnt)
+#pragma unroll
+            for (int i = 0; i < XR; ++i) {
+                const int k = (tid + i * 256) * 4;
+                if (k < a.K) *reinterpret_cast<float4*>(xs + m * a.K + k) = xr[m][i];
+            }
+    __syncthreads();
+    if (i0 >= rows_I) return;
+    float ag[RB][MT], au[RB][MT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) { ag[r][m] = 0.f; au[r][m] = 0.f; }
+#pragma unroll
+    for (int uu = 0; uu < U; ++uu) {
+        const int c = uu * 64 + lane;
+        if (c >= chunks) continue;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            float wg[8], wu[8];
+            unpack8<WT>(qg[uu][r], wg);
+            unpack8<WT>(qu[uu][r], wu);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                if (m < cnt) {
+                    float xv[8];
+                    ld_x8(xs + m * a.K + (c << 3), xv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        ag[r][m] = fmaf(xv[j], wg[j], ag[r][m]);
+                        au[r][m] = fmaf(xv[j], wu[j], au[r][m]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            if (m < cnt) {
+                const float gs = wave_sum(ag[r][m]);
+                const float us = wave_sum(au[r][m]);
+                const int i = i0 + r;
+                if (lane == 0 && i < rows_I) {
+                    float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
+                    if (shared) a.hs[(long)m * a.Is + i] = hv;
+                    else a.h[(long)rows[m] * a.I + i] = hv * wts[m];
+                }
+            }
+        }
+}
+
+// Down + combine + residual: block owns RPB output rows j of every token.  The K axis is
+// [I chunks of each active expert in record order | Is chunks of the shared expert], cut in 4
+// contiguous ranges (one per wave); a lane FMAs each 8-weight chunk of row j against the h rows of
+// the tokens that picked that expert (h~ already carries w_k), one accumulator per token; the
+// 4 wave partials meet once in LDS: out[t][j] += (p0 + p1) + (p2 + p3).
+template <typename WT, int RPB, int U>
+__global__ __launch_bounds__(256) void moe_down_grp_kernel(MoeDec2Args a) {
+    constexpr int MT = 8;
+    __shared__ int exp_s[64];
+    __shared__ int row_s[64][MT];  // record s: h row of token t, or -1
+    __shared__ float part[4][RPB][MT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_act = a.grp[0];
+    for (int i = tid; i < n_act * MT; i += 256) {
+        const int s = i / MT, t = i % MT;
+        const int* rec = a.grp + MOE_GRP_REC * (1 + s);
+        const int cnt = rec[1];
+        int row = -1;
+        for (int m = 0; m < cnt; ++m) {
+            const int rw = rec[2 + m];
+            if (rw / a.topk == t) row = rw;
+        }
+        row_s[s][t] = row;
+        if (t == 0) exp_s[s] = rec[0];
+    }
+    __syncthreads();
+    const int j0 = blockIdx.x * RPB;
+    const int cpi = a.I >> 3, cps = a.sWd ? (a.Is >> 3) : 0;
+    const int nr = n_act * cpi, nch = nr + cps;
+    const int per = (nch + 3) / 4;
+    const int c0 = wave * per, c1 = min(nch, c0 + per);
+    float acc[MT][RPB];
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < RPB; ++r) acc[t][r] = 0.f;
+    for (int base = c0; base < c1; base += 64 * U) {
+        uint4 q[U][RPB];
+        int seg[U], off[U];
+#pragma unroll
+        for (int uu = 0; uu < U; ++uu) {
+            const int g = min(base + uu * 64 + lane, c1 - 1);
+            const bool rt = g < nr;
+            seg[uu] = rt ? g / cpi : -1;
+            off[uu] = (rt ? g % cpi : g - nr) << 3;
+            const int e = rt ? exp_s[seg[uu]] : 0;
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) {
+                const int j = min(j0 + r, a.Hout - 1);
+                const WT* W = rt ? reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + j) * a.I + off[uu]
+                                 : reinterpret_cast<const WT*>(a.sWd) + (long)j * a.Is + off[uu];
+                q[uu][r] = ldg_nt16(W);
+            }
+        }
+#pragma unroll
+        for (int uu = 0; uu < U; ++uu) {
+            if (base + uu * 64 + lane >= c1) continue;
+            float w8[RPB][8];
+#pragma unroll
+            for (int r = 0; r < RPB; ++r) unpack8<WT>(q[uu][r], w8[r]);
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                if (t >= a.T) continue;
+                const int row = seg[uu] >= 0 ? row_s[seg[uu]][t] : t;
+                if (row < 0) continue;
+                const float* hp = seg[uu] >= 0 ? a.h + (long)row * a.I + off[uu] : a.hs + (long)t * a.Is + off[uu];
+                float hv[8];
+                ld_x8(hp, hv);
+#pragma unroll
+                for (int r = 0; r < RPB; ++r)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) acc[t][r] = fmaf(hv[k], w8[r][k], acc[t][r]);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        if (t >= a.T) continue;
+#pragma unroll
+        for (int r = 0; r < RPB; ++r) {
+            const float v = wave_sum(acc[t][r]);
+            if (lane == 0) part[wave][r][t] = v;
+        }
+    }
+    __syncthreads();
+    if (tid < RPB * MT) {
+        const int r = tid / MT, t = tid % MT;
+        if (t < a.T && j0 + r < a.Hout) {
+            const float v = (part[0][r][t] + part[1][r][t]) + (part[2][r][t] + part[3][r][t]);
+            float* xp = a.out + (long)t * a.Hout + j0 + r;
+            *xp = *xp + v;
+        }
+    }
+}
+
+bool moe_grp_ok(const MoeDec2Args& a) {
+    return a.grp && a.T >= 1 && a.T <= 8 && a.topk <= 8 && a.T * a.topk <= 64 && a.E <= 256 && a.K % 8 == 0 &&
+           a.K <= 64 * 3 * 8 && a.I % 8 == 0 && (!a.sWd || a.Is % 8 == 0) && !a.norm_w && (!a.sWgu) == (!a.sWd);
+}
+
+void launch_moe_gateup_grp(const MoeDec2Args& a, hipStream_t s) {
+    if (!moe_grp_ok(a)) throw std::runtime_error("EINVAL: grouped decode gate/up outside its range");
+    constexpr int RB = 2;
+    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
+    const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
+    const int slots = std::min(a.E, a.T * a.topk);
+    const size_t lds = sizeof(float) * 8 * (size_t)a.K;
+    dim3 grid(units_s + slots * units_r);
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_grp_kernel<bf16_t, RB>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((moe_gateup_grp_kernel<f16_t, RB>), grid, dim3(256), lds, s, a);
+}
+
+void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s) {
+    if (!moe_grp_ok(a)) throw std::runtime_error("EINVAL: grouped decode down outside its range");
+    constexpr int RPB = 2, U = 8;
+    dim3 grid((a.Hout + RPB - 1) / RPB);
+    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down_grp_kernel<bf16_t, RPB, U>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((moe_down_grp_kernel<f16_t, RPB, U>), grid, dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ decode MoE layer dispatch
+static bool env_flag(const char* name, bool dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) != 0 : dflt;
+}
+
+namespace {
+struct MoePlan {
+    MoeDec2Args m;
+    DecGemvArgs router;
+    int mode = 0;  // 0 mix (T = 1), 1 slot (T <= 2), 2 grouped (3..8), 3 sorted (T > 8)
+    bool epi = false, mix_dn = false;
+};
+
+MoePlan moe_plan(const MoeDecodeArgs& a) {
+    const int T = a.T, E = a.E, K = a.topk, TK = T * K;
+    if (T <= 0 || TK > 512 || E > 256 || K > 8 || K > E)
+        throw std::runtime_error("EINVAL: decode MoE supports batch*top_k <= 512, <= 256 experts, top_k <= min(8, E)");
+    if (a.H % 8 || a.I % 8 || (a.Is && a.Is % 8)) throw std::runtime_error("EINVAL: MoE dims must be multiples of 8");
+    // experiment switches, read per plan (host-side, once per layer when a step is captured)
+    const bool router_epi = env_flag("DSOCR_ROUTER_EPI", false);
+    const bool gu_mix = env_flag("DSOCR_GU_MIX", true);
+    const bool dn_mix = env_flag("DSOCR_DN_MIX", true);
+    const bool grouped = env_flag("DSOCR_MOE_GRP", true);
+    MoePlan p;
+    const bool fuse_norm = T <= 2;  // T > 2: the rows are normalised once (launch_rmsnorm into xn)
+    const float* mx = (fuse_norm || !a.norm_w) ? a.x : a.xn;
+    const float* mnorm = fuse_norm ? a.norm_w : nullptr;
+    MoeDec2Args& m = p.m;
+    m.T = T; m.K = a.H; m.Hout = a.H; m.x = mx; m.norm_w = mnorm; m.eps = a.eps; m.out = a.out;
+    m.topk = K; m.E = E; m.I = a.I; m.Wgu = a.Wgu; m.Wd = a.Wd; m.wdtype = a.wdtype; m.h = a.h; m.ids = a.ids;
+    if (a.sWgu && a.sWd && a.Is > 0) { m.Is = a.Is; m.sWgu = a.sWgu; m.sWd = a.sWd; m.hs = a.hs; }
+    DecGemvArgs& gr = p.router;
+    gr.M = T; gr.N = E; gr.K = a.H; gr.x = mx; gr.ldx = a.H; gr.W = a.router; gr.ldw = a.H; gr.wdtype = a.router_wdt;
+    gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps;
+    const bool rt_ok = dec_router_ok(T, E, a.H, K) && a.route_cnt;
+    if (T >= 3 && T <= 8 && grouped && rt_ok && a.grp) {
+        p.mode = 2;
+        m.slot_mode = 1; m.slots = TK; m.grp = a.grp; m.aw = a.wts;
+        if (!moe_grp_ok(m)) p.mode = 1;
+    }
+    if (p.mode == 2) {
+        p.epi = true;
+    } else if (T <= 8) {
+        m.grp = nullptr;
+        m.slot_mode = 1; m.slots = TK;
+        if (router_epi && rt_ok) {
+            // routed by dec_router's last-block epilogue (measured +1.6 us / layer on MI355X at T = 1
+            // vs self-routing: the write-through + ticket hand-off costs more than it saves)
+            p.epi = true; m.logits = nullptr; m.aw = a.wts;
+        } else {
+            // every gate/up block routes itself from the router logits
+            m.logits = a.logits; m.softmax_scoring = a.softmax_scoring; m.norm_topk = a.norm_topk;
+            m.scaling = a.scaling; m.ids_out = a.ids; m.w_out = a.wts;
+        }
+        p.mode = (gu_mix && fuse_norm && moe_gateup_mix_ok(m) && a.xn_router) ? 0 : 1;
+        if (p.mode == 0) gr.xn_out = a.xn_router;  // the router hands its normalised row to gate/up
+        p.mix_dn = dn_mix && moe_down_mix_ok(m);
+    } else {
+        p.mode = 3;
+        if (!(a.eoff && a.arow && a.apos && a.active && a.n_active && a.aw))
+            throw std::runtime_error("EINVAL: decode MoE over 8 tokens needs the grouping workspaces");
+        m.slots = std::min(E, TK);
+        m.eoff = a.eoff; m.arow = a.arow; m.apos = a.apos; m.aw = a.aw; m.active = a.active; m.n_active = a.n_active;
+    }
+    return p;
+}
+}  // namespace
+
+void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down) {
+    const MoePlan p = moe_plan(a);
+    const char* gu = "moe_gateup2_kernel";
+    const char* dn = "moe_down2_kernel";
+    if (p.mode == 0) gu = "moe_gateup_mix_kernel";
+    else if (p.mode == 1) gu = (a.T > 2 && a.Is) ? "moe_gateup_slot_kernel+moe_gateup_shared_kernel" : "moe_gateup_slot_kernel";
+    else if (p.mode == 2) gu = "moe_gateup_grp_kernel";
+    if (p.mode == 2) dn = "moe_down_grp_kernel";
+    else if (p.mode <= 1) dn = p.mix_dn ? "moe_down_mix_kernel" : "moe_down_slot_kernel";
+    if (gateup) *gateup = gu;
+    if (down) *down = dn;
+}
+
+void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
+    const MoePlan p = moe_plan(a);
+    const MoeDec2Args& m = p.m;
+    if (parts & MOE_ROUTE) {
+        if (a.T > 2 && a.norm_w) launch_rmsnorm(a.x, a.H, a.xn, a.H, a.T, a.H, a.norm_w, a.eps, s);
+        if (p.epi) {
+            DecRouteEpi re;
+            re.topk = a.topk; re.softmax_scoring = a.softmax_scoring; re.norm_topk = a.norm_topk;
+            re.scaling = a.scaling; re.ids = a.ids; re.w = a.wts; re.counter = a.route_cnt;
+            if (p.mode == 2) re.grp = a.grp;
+            launch_dec_router(p.router, re, s);
+        } else {
+            launch_dec_gemv(p.router, s);
+        }
+        if (p.mode == 3) {
+            MoeRouteArgs ra;
+            ra.logits = a.logits; ra.T = a.T; ra.E = a.E; ra.topk = a.topk; ra.softmax_scoring = a.softmax_scoring;
+            ra.norm_topk = a.norm_topk; ra.scaling = a.scaling; ra.ids = a.ids; ra.w = a.wts; ra.eoff = a.eoff;
+            ra.arow = a.arow; ra.apos = a.apos; ra.aw = a.aw; ra.active = a.active; ra.n_active = a.n_active;
+            launch_moe_route(ra, s);
+        }
+    }
+    if (parts & MOE_GATEUP) {
+        if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
+        else if (p.mode == 2) launch_moe_gateup_grp(m, s);
+        else launch_moe_gateup2(m, s);
+    }
+    if (parts & MOE_DOWN) {
+        if (p.mode == 2) launch_moe_down_grp(m, s);
+        else if (p.mix_dn) launch_moe_down_mix(m, s);
+        else launch_moe_down2(m, s);
     }
 }
 

@@ -117,6 +117,9 @@ void launch_concat_clip_sam(const float* clip, const float* sam, int n, int S, i
 void launch_assemble_rows(const int* kind, const int* index, int rows, int H, const void* table, int table_dt,
                           const float* srcA, const float* srcB, const float* vecA, const float* vecB, float* dst,
                           long ld_dst, hipStream_t s);
+// logits [B][ld] -> trace[b][out_len[b]][V] for pages not done (out_len < steps): the parity trace
+void launch_trace_logits(const float* logits, int B, int V, long ld, const int* out_len, const int* done, float* trace,
+                         long steps, hipStream_t s);
 void launch_embed_tokens(const void* table, int table_dt, const int* ids, int n, int H, float* out, long ld,
                          hipStream_t s);
 // Repetition penalty over the context tokens (sampling.rs:34-96), in place on the logits.
@@ -152,7 +155,18 @@ struct DecRouteEpi {
     float scaling = 1.f;
     int* ids = nullptr; float* w = nullptr;   // [T][topk]
     int* counter = nullptr;                   // zero between launches
+    // optional: the picks grouped by expert (MOE_GRP_* layout below) for the grouped decode kernels
+    int* grp = nullptr;
 };
+// Expert groups of one decode MoE layer (T <= 8 tokens): grp[0] = number of distinct experts picked,
+// record s (s < grp[0]) at grp + MOE_GRP_REC * (1 + s): [0] expert id, [1] picks (tokens) n,
+// [2 .. 2+n) the h rows t*topk + k in increasing token order, [10 .. 10+n) their routing weights
+// (f32 bits).  Records are in increasing expert order.
+constexpr int MOE_GRP_REC = 32;
+inline size_t moe_grp_ints(int E, int T, int topk) {
+    const int slots = E < T * topk ? E : T * topk;
+    return (size_t)MOE_GRP_REC * (1 + slots);
+}
 void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s);
 bool dec_router_ok(int T, int E, int K, int topk);
 // RoPE on q / new k + KV-cache append + flash-decoding over 64-key chunks + combine.
@@ -235,6 +249,9 @@ struct MoeDec2Args {
     // fused launch (moe_fused_slot_kernel): arrival counters (SYNC_SHARDS lines, zeroed before
     // the launch), arrivals to wait for (set by the launcher), give-up flag
     int* sync = nullptr; int sync_target = 0; int* err = nullptr;
+    // grouped mode (3 <= T <= 8): expert groups written by the router epilogue (MOE_GRP_* layout);
+    // h rows stay in slot order (t*topk + k)
+    const int* grp = nullptr;
 };
 constexpr int SYNC_SHARDS = 8, SYNC_STRIDE = 32;  // counters per hand-off, ints between counters
 constexpr int SYNC_INTS = SYNC_SHARDS * SYNC_STRIDE;  // ints of one hand-off's counter block
@@ -251,6 +268,42 @@ void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_fused(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
+// Grouped decode MoE (3 <= T <= 8): every distinct routed expert's rows are streamed once per layer
+// (gate/up: routed groups + the shared expert in one launch; down: per output row over the
+// concatenated [active experts | shared] K axis, per-token accumulators).
+bool moe_grp_ok(const MoeDec2Args& a);
+void launch_moe_gateup_grp(const MoeDec2Args& a, hipStream_t s);
+void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s);
+
+// One decode MoE layer for T tokens (block.rs:1215-1395): [RMSNorm] -> router GEMV (+ routing /
+// grouping) -> gate/up -> down + weighted combine + shared experts + residual:
+// out[T][H] += moe(rmsnorm(x)).  The single dispatch shared by Engine::decode_step and the
+// kernel-level entry dsocr_k_moe.  Workspaces are device buffers sized as commented.
+struct MoeDecodeArgs {
+    int T = 0, H = 0, E = 0, topk = 0, I = 0, Is = 0;
+    const float* x = nullptr; const float* norm_w = nullptr; float eps = 0.f;  // x: [T][H] (may equal out)
+    const void* router = nullptr; int router_wdt = WDT_F16; const float* router_bias = nullptr;
+    const void* Wgu = nullptr; const void* Wd = nullptr;    // [E][2I][H], [E][H][I]
+    const void* sWgu = nullptr; const void* sWd = nullptr;  // [2Is][H], [H][Is] (or null)
+    int wdtype = WDT_F16;
+    int softmax_scoring = 1, norm_topk = 0; float scaling = 1.f;
+    float* out = nullptr;
+    // workspaces
+    float* xn = nullptr;        // [T][H]     normalised rows (T > 2)
+    float* xn_router = nullptr; // [T][H]     normalised row handed from the router to gate/up (T = 1)
+    float* logits = nullptr;    // [T][E]
+    int* ids = nullptr; float* wts = nullptr;   // [T*topk] picks (outputs)
+    float* h = nullptr;         // [T*topk][I]
+    float* hs = nullptr;        // [T][Is]
+    int* grp = nullptr;         // moe_grp_ints(E, T, topk)
+    int* route_cnt = nullptr;   // [16], zero between launches (router epilogue ticket)
+    int* eoff = nullptr; int* arow = nullptr; int* apos = nullptr; int* active = nullptr;  // T > 8:
+    int* n_active = nullptr; float* aw = nullptr;                                          // [E+1],[TK],[TK],[E],[1],[TK]
+};
+enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
+// kernel names of the gate/up and down launches the dispatch picks for these arguments
+void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down);
+void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts = MOE_ALL);
 // Greedy selection (ngram ban evaluated in-kernel) + step bookkeeping + KV advance.
 struct DecSampleArgs {
     const float* logits = nullptr; int B = 0, V = 0; long ld = 0;

@@ -159,6 +159,23 @@ void launch_embed_tokens(const void* table, int table_dt, const int* ids, int n,
     hipLaunchKernelGGL(embed_tokens_kernel, dim3(n), dim3(256), 0, s, table, table_dt, ids, n, H, out, ld);
 }
 
+// ------------------------------------------------------------------ parity trace
+// grid (chunks, B): page b's raw logits row -> trace[b][out_len[b]] while the page is running
+__global__ void trace_logits_kernel(const float* lg, int V, long ld, const int* out_len, const int* done, float* trace,
+                                    long steps) {
+    const int b = blockIdx.y;
+    const int n = out_len[b];
+    if (done[b] || n >= steps) return;
+    float* dst = trace + ((long)b * steps + n) * V;
+    const float* src = lg + (long)b * ld;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < V; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+void launch_trace_logits(const float* logits, int B, int V, long ld, const int* out_len, const int* done, float* trace,
+                         long steps, hipStream_t s) {
+    if (B == 0 || V == 0) return;
+    hipLaunchKernelGGL(trace_logits_kernel, dim3(64, B), dim3(256), 0, s, logits, V, ld, out_len, done, trace, steps);
+}
+
 // ------------------------------------------------------------------ repetition penalty
 // sampling.rs:34-96: every distinct context token's logit is divided (>0) or multiplied
 // (<=0) by the penalty once.  Selection itself is dec_argmax_partial / dec_sample_final (decode.hip).

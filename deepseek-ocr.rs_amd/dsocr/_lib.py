@@ -62,7 +62,8 @@ class DecodeProfileC(C.Structure):
     _fields_ = [("moe_gateup", KernelProfileC), ("moe_down", KernelProfileC), ("attention", KernelProfileC),
                 ("lm_head", KernelProfileC), ("experts_touched", C.c_int), ("tokens", C.c_int), ("kv_len", C.c_int),
                 ("qkv", KernelProfileC), ("o_proj", KernelProfileC), ("router", KernelProfileC),
-                ("layers_step", KernelProfileC), ("lm_head_screened", KernelProfileC)]
+                ("layers_step", KernelProfileC), ("lm_head_screened", KernelProfileC),
+                ("moe_gateup_kernel", C.c_char_p), ("moe_down_kernel", C.c_char_p)]
 
 
 STREAM_CB = C.CFUNCTYPE(None, C.c_size_t, C.POINTER(C.c_int64), C.c_void_p)
@@ -75,6 +76,7 @@ EXPORTS = [
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
     "dsocr_k_sample_greedy", "dsocr_k_sample_stoch", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
+    "dsocr_generate_trace", "dsocr_k_moe_kernels", "dsocr_k_lmhead_screened",
 ]
 
 _lib = None
@@ -105,6 +107,9 @@ def lib():
     L.dsocr_generate.argtypes = [vp, C.POINTER(RequestC), C.POINTER(DecodeParamsC), STREAM_CB, vp, vp, sz,
                                  C.POINTER(sz)]
     L.dsocr_generate_batch.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC)]
+    L.dsocr_generate_trace.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC), vp]
+    L.dsocr_k_lmhead_screened.argtypes = [i32, i32, i32, vp, vp, f32, vp, vp, i32, vp]
+    L.dsocr_k_moe_kernels.argtypes = [i32, i32, i32, i32, i32, i32, i32, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
     L.dsocr_last_timings.argtypes = [vp, C.POINTER(TimingsC)]
     L.dsocr_profile_decode.argtypes = [vp, i32, C.POINTER(DecodeProfileC)]
     L.dsocr_device_count.argtypes = [C.POINTER(i32)]

@@ -260,6 +260,20 @@ class DeepseekOcrEngine:
         check(lib().dsocr_generate_batch(self._h, len(requests), reqs, C.byref(pc), res))
         return [outs[i][:res[i].n_out].tolist() for i in range(len(requests))]
 
+    def generate_trace(self, requests, params: DecodeParameters = DecodeParameters(), ignore_eos: bool = False):
+        """generate_batch + the raw logits of every step (dsocr_generate_trace): returns
+        (ids per page, logits [n][max_new][vocab] float32; rows past a page's last token are 0)."""
+        keep = []
+        reqs = (RequestC * len(requests))(*[self._request(*r, keep) for r in requests])
+        outs = [np.empty(max(params.max_new_tokens, 1), np.int64) for _ in requests]
+        res = (ResultC * len(requests))(*[ResultC(o.ctypes.data_as(C.POINTER(C.c_int64)), len(o), 0, 0)
+                                          for o in outs])
+        logits = np.zeros((len(requests), max(params.max_new_tokens, 1), self.vocab), np.float32)
+        pc = _params_c(params, self.eos_token_id, ignore_eos)
+        check(lib().dsocr_generate_trace(self._h, len(requests), reqs, C.byref(pc), res,
+                                         logits.ctypes.data_as(C.c_void_p)))
+        return [outs[i][:res[i].n_out].tolist() for i in range(len(requests))], logits
+
     def last_timings(self) -> dict:
         t = TimingsC()
         check(lib().dsocr_last_timings(self._h, C.byref(t)))
@@ -275,7 +289,9 @@ class DeepseekOcrEngine:
                   "lm_head_screened"):
             kp = getattr(p, k)
             out[k] = {"avg_us": kp.avg_us, "bytes": kp.bytes, "flops": kp.flops, "launches": kp.launches}
-        out.update(experts_touched=p.experts_touched, tokens=p.tokens, kv_len=p.kv_len)
+        out.update(experts_touched=p.experts_touched, tokens=p.tokens, kv_len=p.kv_len,
+                   moe_gateup_kernel=(p.moe_gateup_kernel or b"").decode(),
+                   moe_down_kernel=(p.moe_down_kernel or b"").decode())
         return out
 
     # ------------------------------------------------------------------ OcrEngine::decode

@@ -71,7 +71,8 @@ typedef struct {
     float repetition_penalty;    /* 1.0: off */
     size_t no_repeat_ngram_size; /* 0 or 1: off (reference default 20) */
     uint64_t seed;               /* StdRng::seed_from_u64(seed) when has_seed, else entropy */
-    int use_cache;               /* must be 1 */
+    int use_cache;               /* 0: generate_without_cache (model/mod.rs:2051-2283): the whole forward re-runs
+                                    on prompt + generated tokens every step (same ids, O(n^2) work) */
     int64_t eos_token_id;        /* < 0: none (reference: config eos_token_id) */
     int ignore_eos;              /* benchmark mode: always produce max_new_tokens */
     int has_seed;                /* DecodeParameters::seed is Some */
@@ -154,6 +155,15 @@ dsocr_status dsocr_generate(dsocr_engine* e, const dsocr_request* req, const dso
 dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request* reqs,
                                   const dsocr_decode_params* params, dsocr_result* results);
 dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t);
+/* Parity hook: dsocr_generate_batch plus the raw logits (before repetition penalty and n-gram ban) of
+ * every step of every page, logits_out [n][max_new_tokens][vocab] host f32, step s = the logits the
+ * s-th generated token was selected from (step 0 = the prefill's last row).  The reference's
+ * counterparts: the cli-debug top-2 logits dump (crates/infer-deepseek/src/debug.rs:17-21,
+ * model/mod.rs:1937-1949) and the teacher-forcing logits its baseline tests compare
+ * (tests/baseline.rs:1108).  Selection runs on the exact lm_head while tracing (the screened head
+ * never forms the full logits; its ids equal the exact head's). */
+dsocr_status dsocr_generate_trace(dsocr_engine* e, size_t n, const dsocr_request* reqs,
+                                  const dsocr_decode_params* params, dsocr_result* results, float* logits_out);
 
 /* Decode-kernel profile (bench roofline): replays the dominant decode kernels of the
  * last generate() call on its final routing / KV state, each timed with HIP events on
@@ -166,10 +176,11 @@ typedef struct dsocr_kernel_profile {
     int launches;
 } dsocr_kernel_profile;
 typedef struct dsocr_decode_profile {
-    dsocr_kernel_profile moe_gateup;  /* moe_gateup2_kernel: routed + shared gate/up, one MoE layer */
-    dsocr_kernel_profile moe_down;    /* moe_down2_kernel: routed + shared down + combine + residual */
-    dsocr_kernel_profile attention;   /* dec_attn_kernel + combine: one layer, all pages */
-    dsocr_kernel_profile lm_head;     /* dec_gemv over the 129280 x 1280 lm_head */
+    dsocr_kernel_profile moe_gateup;  /* decode MoE gate/up launch(es) of one layer (routed + shared): the kernel
+                                         the dispatch picks at this batch size, named in moe_gateup_kernel */
+    dsocr_kernel_profile moe_down;    /* routed + shared down + combine + residual (moe_down_kernel) */
+    dsocr_kernel_profile attention;   /* dec_attn_kernel (RoPE / KV append / flash-decoding / combine): one layer */
+    dsocr_kernel_profile lm_head;     /* exact lm_head: dec_gemv over the 129280 x 1280 rows */
     int experts_touched;              /* routed experts active in the replayed step (per layer, summed / layers) */
     int tokens;                       /* pages in the batch */
     int kv_len;                       /* keys attended by page 0 */
@@ -178,6 +189,8 @@ typedef struct dsocr_decode_profile {
     dsocr_kernel_profile router;      /* MoE router logits (+ top-k when routed by the router kernel) */
     dsocr_kernel_profile layers_step; /* every decoder layer of one decode step, replayed as one hipGraph */
     dsocr_kernel_profile lm_head_screened; /* int8 screened lm_head + exact rescoring selection (B <= 2, no penalty) */
+    const char* moe_gateup_kernel;    /* static strings: kernel names of the two MoE entries above */
+    const char* moe_down_kernel;
 } dsocr_decode_profile;
 dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out);
 
@@ -225,13 +238,25 @@ dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, in
                                       const int* kv_pos, float* o);
 /* Decode MoE layer (the north-star kernel chain, block.rs:1215-1395): [RMSNorm] + router GEMV +
  * softmax top-k + grouping + grouped SwiGLU experts + shared experts + weighted combine,
- * out[T][H] += moe(xn), xn = rmsnorm(x; norm_w, eps) if norm_w != NULL else x.
+ * out[T][H] += moe(xn), xn = rmsnorm(x; norm_w, eps) if norm_w != NULL else x.  Runs exactly the
+ * engine's decode dispatch for T tokens (the same launches Engine::decode_step issues).
  * Wgu: [E][2I][H] (gate rows then up rows), Wd: [E][H][I], router [E][H], shared Wgu [2Is][H],
  * shared Wd [H][Is] (shared may be NULL), all 16-bit (wdtype). */
 dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const float* norm_w,
                          float eps, const void* router,
                          const void* Wgu, const void* Wd, const void* sWgu, const void* sWd, int wdtype,
                          int norm_topk, float scaling, float* out, int* topk_ids_out, float* topk_w_out);
+/* Kernel names launch_moe_decode picks for a decode MoE of T tokens (static strings), e.g. the bench's
+ * roofline label: "moe_gateup_mix_kernel" at T = 1, "moe_gateup_grp_kernel" at T = 3..8. */
+dsocr_status dsocr_k_moe_kernels(int T, int H, int E, int topk, int I, int Is, int has_norm, const char** gateup,
+                                 const char** down);
+/* Screened greedy selection (the engine's decode head at B <= 2 without repetition penalty): the
+ * int8 copy of W (bf16 [V][K], quantised as at engine load) gives every row an interval that holds
+ * the exact logit, the surviving rows are rescored with the exact kernel's arithmetic; out_tok[b] =
+ * the first-index argmax of rmsnorm(x_b; norm_w, eps) . W^T over the rows not in page b's ban list
+ * (ban [B][ban_ld]: count then tokens, or NULL), as argmax_index (sampling.rs:104-118). */
+dsocr_status dsocr_k_lmhead_screened(int B, int V, int K, const float* x, const float* norm_w, float eps,
+                                     const void* W, const int* ban, int ban_ld, int* out_tok);
 /* Greedy selection with repetition penalty + n-gram ban (sampling.rs:34-158) over B rows of V
  * logits; ctx [B][ctx_cap] int32 with ctx_len[B]. */
 dsocr_status dsocr_k_sample_greedy(int B, int V, float* logits, const int* ctx, int ctx_cap, const int* ctx_len,

@@ -77,6 +77,35 @@ class OracleModel:
             e[m] = image_rows
         return e.astype(F32)
 
+    def generate_without_cache(self, ids, mask, image_rows, max_new_tokens, eos_token_id=None,
+                               repetition_penalty=1.0, no_repeat_ngram_size=20):
+        """DeepseekOcrModel::generate_without_cache model/mod.rs:2051-2283 (greedy): every step runs the
+        whole forward on prompt + generated tokens (image mask extended with 0, rows re-injected) and
+        selects from the last position's logits with the tokens so far as context."""
+        tokens = [int(t) for t in ids]
+        msk = list(mask) if mask is not None else [0] * len(tokens)
+        if max_new_tokens == 0:
+            return []
+
+        def last_logits():
+            self.dec.reset()
+            return self.dec.forward(self.prefill_embeddings(tokens, msk, image_rows))[0]
+
+        cur = select_token_id(last_logits(), tokens, repetition_penalty, no_repeat_ngram_size)
+        if eos_token_id is not None and cur == eos_token_id:
+            return []
+        out = []
+        for step in range(max_new_tokens):
+            out.append(cur)
+            if step + 1 == max_new_tokens:
+                break
+            tokens.append(cur)
+            msk.append(0)
+            cur = select_token_id(last_logits(), tokens, repetition_penalty, no_repeat_ngram_size)
+            if eos_token_id is not None and cur == eos_token_id:
+                break
+        return out
+
     def generate(self, ids, mask, image_rows, max_new_tokens, eos_token_id=None,
                  repetition_penalty=1.0, no_repeat_ngram_size=20, record_logits=False, ignore_eos=False,
                  do_sample=False, temperature=0.0, top_k=None, top_p=None, seed=None):

@@ -62,3 +62,11 @@ def test_engine_reproduces_golden(gpu):
             assert got == p["generated"]
     finally:
         eng.close()
+
+
+def test_oracle_generate_without_cache_matches_cached(oracle_model):
+    """The oracle's generate_without_cache restatement gives the cached path's ids (text-only prompt)."""
+    ids = [0] + list(range(40, 70))
+    a = oracle_model.generate_without_cache(ids, None, None, 8, eos_token_id=1, no_repeat_ngram_size=20)
+    b, _ = oracle_model.generate(ids, [0] * len(ids), None, 8, eos_token_id=1, no_repeat_ngram_size=20)
+    assert a == b

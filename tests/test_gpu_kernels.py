@@ -277,3 +277,64 @@ def test_sample_greedy(gpu, ngram, pen):
     for b in range(B):
         ref = select_token_id(logits[b], ctx[b, : lens[b]].tolist(), pen, ngram if ngram > 1 else None)
         assert got[b] == ref, (b, got[b], ref)
+
+
+# ---------------------------------------------------------------- decode MoE: the production dispatch
+@pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(1, 1280, 64, 6, 896, 2, True),   # mix kernels (bench, 1 page)
+                                                  (2, 1280, 64, 6, 896, 2, True),   # slot kernels
+                                                  (3, 1280, 64, 6, 896, 2, True),   # grouped kernels ...
+                                                  (8, 1280, 64, 6, 896, 2, True),   # ... at 8 pages (configs[2])
+                                                  (5, 256, 16, 6, 64, 2, True),     # many tokens per expert
+                                                  (8, 256, 8, 3, 32, 1, False)])    # every record full (8 tokens)
+def test_moe_decode_full_size_dispatch(gpu, T, H, E, topk, I, ns, norm):
+    """dsocr_k_moe runs the engine's own decode dispatch (launch_moe_decode): at full size
+    (H 1280, 64 experts, I 896, 2 shared = Is 1792) one token takes moe_gateup_mix + moe_down_mix,
+    3..8 tokens the grouped kernels (each distinct expert streamed once) - vs the oracle's run_moe
+    (block.rs:1215-1395), ids exact, outputs <= 1e-4."""
+    test_moe_decode_layer(gpu, _NoEnv(), T, H, E, topk, I, ns, norm, 0)
+
+
+class _NoEnv:
+    def setenv(self, *a):
+        pass
+
+
+# ---------------------------------------------------------------- screened lm_head: ties / near ties
+def test_screened_head_ties_first_index(gpu):
+    """The screened selection (int8 intervals + exact rescoring) against the exact lm_head GEMV's
+    first-index argmax (argmax_index, sampling.rs:104-118) on rows built to tie: two identical
+    dominant rows (first index wins), a row one bf16 ulp away in one element (a near tie far below
+    the int8 quantisation error), and a ban list that removes the first of the tied rows."""
+    rng = np.random.default_rng(99)
+    B, V, K = 3, 20000, 1280
+    x = rng.standard_normal((B, K)).astype(np.float32)
+    nw = (1.0 + 0.05 * rng.standard_normal(K)).astype(np.float32)
+    w = (rng.standard_normal((V, K)) * 0.02).astype(np.float32)
+    xn = rms_norm(x, nw, 1e-6)
+    dom = (xn[0] / np.linalg.norm(xn[0]) * 0.5).astype(np.float32)
+    bits = bf16_round(w)
+    dbits = bf16_round(dom)
+    A, Bt, Cn = 777, 15000, 300
+    bits[A] = dbits
+    bits[Bt] = dbits                       # exact tie with A
+    bits[Cn] = dbits
+    j = int(np.argmax(np.abs(dom)))
+    bits[Cn, j] = dbits[j] + 1             # one ulp in one element: a near tie
+    bits[:, :][4000] = dbits               # a third copy (after A)
+    ban_ld = 8
+    ban = np.zeros((B, ban_ld), np.int32)
+    ban[1, 0], ban[1, 1] = 2, A            # page 1: A banned
+    ban[1, 2] = Cn
+    dx, dn, dW, dban, dt = Dev(x), Dev(nw), Dev(bits), Dev(ban), Dev.zeros(B, np.int32)
+    check(lib().dsocr_k_lmhead_screened(B, V, K, dx.ptr, dn.ptr, 1e-6, dW.ptr, dban.ptr, ban_ld, dt.ptr))
+    got = dt.get()
+    # the exact path: dec_gemv over the same rows (the engine's exact lm_head kernel for V > 16384)
+    dy = Dev.zeros((B, V))
+    check(lib().dsocr_k_gemv(B, V, K, dx.ptr, dn.ptr, 1e-6, dW.ptr, 0, None, dy.ptr, 0, 0))
+    ex = dy.get()
+    for b in range(B):
+        row = ex[b].copy()
+        for t in ban[b, 1:1 + ban[b, 0]]:
+            row[t] = -np.inf
+        assert got[b] == int(np.argmax(row)), (b, got[b], int(np.argmax(row)), row[[A, Bt, Cn, 4000]])
+    assert got[1] != A and got[1] != Cn

@@ -233,3 +233,35 @@ def test_full_screened_selection_equals_exact(full_engine, monkeypatch):
     monkeypatch.setenv("DSOCR_SCREEN", "0")
     exact = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
     assert screened == exact, (screened, exact)
+
+
+def test_tiny_generate_without_cache(tiny_engine, tiny_oracle):
+    """use_cache = false (generate_without_cache, model/mod.rs:2051-2283): every step re-runs the whole
+    forward on prompt + generated tokens; ids equal the oracle's no-cache restatement and the cached path."""
+    img = _img(21, 300, 420)
+    tok = SyntheticTokenizer(512)
+    page = Page(img, TINY_VS)
+    ids, mask = _prompt(tok, page)
+    emb, _ = tiny_oracle.image_embeddings(img, 256, 128, True)
+    seen = []
+    got = tiny_engine.generate(ids, mask, page, None, DecodeParameters(max_new_tokens=12, use_cache=False),
+                               stream=lambda n, toks: seen.append(list(toks)))
+    ref = tiny_oracle.generate_without_cache(ids, mask, emb, 12, eos_token_id=1, no_repeat_ngram_size=20)
+    assert got == ref
+    assert got == tiny_engine.generate(ids, mask, page, None, DecodeParameters(max_new_tokens=12))
+    assert [len(s) for s in seen] == list(range(1, len(got) + 1)) and seen[-1] == got
+    # batch of two pages without cache == per-page
+    page2 = Page(_img(22, 256, 256), TINY_VS)
+    ids2, mask2 = _prompt(tok, page2)
+    p = DecodeParameters(max_new_tokens=10, use_cache=False)
+    bat = tiny_engine.generate_batch([(ids, mask, page, None), (ids2, mask2, page2, None)], p)
+    assert bat == [tiny_engine.generate(ids, mask, page, None, p), tiny_engine.generate(ids2, mask2, page2, None, p)]
+
+
+def test_tiny_stream_callback_every_token(tiny_engine):
+    """The stream callback runs after every token, the first one included (model/mod.rs:1980-1982)."""
+    ids = [0] + list(range(30, 50))
+    seen = []
+    got = tiny_engine.generate(ids, None, None, None, DecodeParameters(max_new_tokens=6),
+                               stream=lambda n, toks: seen.append((n, list(toks))), ignore_eos=True)
+    assert [n for n, _ in seen] == list(range(1, 7)) and seen[-1][1] == got

@@ -199,3 +199,16 @@ def test_engine_load_errors_without_gpu_are_loud():
     from dsocr import DsocrError, ModelLoadArgs, load_model
     with pytest.raises(DsocrError):
         load_model(ModelLoadArgs(config_path="/nonexistent/config.json"))
+
+
+def test_moe_dispatch_kernel_names():
+    """Which kernels the dispatch picks (host-only query; the bench labels its roofline with it)."""
+    import ctypes as C
+    from dsocr._lib import check, lib
+    want = {1: ("moe_gateup_mix_kernel", "moe_down_mix_kernel"), 2: ("moe_gateup_slot_kernel", "moe_down_slot_kernel"),
+            3: ("moe_gateup_grp_kernel", "moe_down_grp_kernel"), 8: ("moe_gateup_grp_kernel", "moe_down_grp_kernel"),
+            9: ("moe_gateup2_kernel", "moe_down2_kernel")}
+    for T, (gu, dn) in want.items():
+        g, d = C.c_char_p(), C.c_char_p()
+        check(lib().dsocr_k_moe_kernels(T, 1280, 64, 6, 896, 1792, 1, C.byref(g), C.byref(d)))
+        assert (g.value.decode(), d.value.decode()) == (gu, dn), T

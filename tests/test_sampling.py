@@ -98,12 +98,14 @@ def _oracle_draws(logits, ctx, pen, ngram, T, k, p, seed, draws):
     (5000, 0.8, 0, 0.9, 0, 1.3),      # top-p with the repetition penalty
     (5000, 1.2, 50, 0.5, 20, 1.0),    # both
     (129280, 0.6, 0, 0.95, 20, 1.0),  # full vocabulary, top-p
+    (129280, 0.7, 0, -1.0, 0, 1.0),   # full vocabulary, temperature only: the early-stop fold crosses many tiles
+    (129280, 1.1, 64, -1.0, 20, 1.0), # full vocabulary, top-k only (radix select of the k-th key)
 ])
 def test_sample_stoch_matches_oracle(gpu, V, T, k, p, ngram, pen):
     from dsocr._lib import check, lib
     from _dev import Dev
     rng = np.random.default_rng(V + k)
-    B, cap, draws = 2, 64, 6
+    B, cap, draws = 2, 64, (12 if V > 100000 else 6)
     logits = (rng.standard_normal((B, V)) * 3).astype(np.float32)
     logits[0, 5] = -np.inf
     logits[1, 7] = np.nan

@@ -8,10 +8,14 @@ export TMPDIR=/tmp
 run() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; echo "rc=$rc :: $*" >> gpurun_out/rc.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; return 0; }
 for step in "$@"; do
   case $step in
-    kernels) run 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider > gpurun_out/kernels.log 2>&1 ;;
-    model_tiny) run 600 python -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider -k "tiny or eos or mask or safetensors" > gpurun_out/model_tiny.log 2>&1 ;;
-    model_full) run 900 python -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider -k "full" > gpurun_out/model_full.log 2>&1 ;;
-    gpu_all) run 1100 python -m pytest tests -q -m gpu -rf -p no:cacheprovider > gpurun_out/gpu_all.log 2>&1 ;;
+    kernels) run 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/kernels.log 2>&1 ;;
+    model_tiny) run 600 python -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread -k "tiny or eos or mask or safetensors" > gpurun_out/model_tiny.log 2>&1 ;;
+    model_full) run 900 python -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread -k "full" > gpurun_out/model_full.log 2>&1 ;;
+    parity) DSOCR_PARITY_OUT=gpurun_out/parity.jsonl run 900 python -u -m pytest tests/test_full_parity.py -q -m gpu -rf -p no:cacheprovider --timeout 400 --timeout-method thread > gpurun_out/parity.log 2>&1 ;;
+    nocache) run 600 python -u -m pytest tests/test_gpu_model.py -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread -k "without_cache or stream" > gpurun_out/nocache.log 2>&1 ;;
+    sampling) run 600 python -u -m pytest tests/test_sampling.py -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/sampling.log 2>&1 ;;
+    bench8) run 900 python bench.py --pages-per-gpu 8 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench8.log 2>&1 ;;
+    gpu_all) run 1100 python -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
     bench_full) run 1100 python bench.py > gpurun_out/bench_full.log 2>&1 ;;
