@@ -27,7 +27,6 @@ for _p in (ROOT, PKG):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-GATEUP_KERNEL = "moe_gateup_mix_kernel"  # the decode MoE grouped GEMM at B = 1 (decode.hip)
 
 
 def log(*a):
@@ -205,11 +204,12 @@ def main():
     if rank == 0:
         prof = eng.profile_decode(args.roofline_iters)
         gu = prof["moe_gateup"]
+        kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
         achieved = gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(GATEUP_KERNEL),
-                    "kernel": GATEUP_KERNEL + " (decode MoE gate/up: shared-expert waves + self-routed top-6 waves, one layer)",
+                    "traffic": pmc_traffic(kernel),
+                    "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts + shared experts)",
                     "avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
                     "experts_touched": prof["experts_touched"],
                     "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],

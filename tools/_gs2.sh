@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_session.sh gprof
+echo "session rc=$?" >> gpurun_out/rc.log
