@@ -120,6 +120,101 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
                       f"extrapolated to {max_new} tokens"}
 
 
+def dots_flops(cfg, N):
+    """Algorithmic FLOPs of the dots.ocr vision tower on N patch tokens (one frame): per block the
+    qkv / proj / fc1 / fc3 / fc2 GEMMs 2 N D (3D + D + 3 I) and the attention 4 N^2 D (QK^T and P.V);
+    patch embed 2 N (3 p^2) D; merger 2 (N/4) (G^2 + G H)."""
+    D, I, L = cfg["embed_dim"], cfg["intermediate_size"], cfg["num_hidden_layers"]
+    G = D * cfg["spatial_merge_size"] ** 2
+    gemm_block = 2.0 * N * D * (3 * D + D + 3 * I)
+    attn_block = 4.0 * N * N * D
+    other = 2.0 * N * 3 * cfg["patch_size"] ** 2 * D + 2.0 * (N / 4) * (G * G + G * cfg["hidden_size"])
+    return gemm_block * L, attn_block * L, other
+
+
+def run_dots(args, rank, world, local, dist):
+    """BASELINE configs[3]: dots.ocr (bf16) vision tower on a 2048-px class page per GPU per step
+    (2044 x 2044: the reference's smart_resize keeps it, grid 146 x 146 = 21316 patch tokens)."""
+    import ctypes as C
+
+    import numpy as np
+
+    from dsocr._lib import check, lib
+    from dsocr.dots import DOTS_CONFIG, DotsVision, preprocess
+    from dsocr.synth import synthetic_page
+    L = lib()
+    t_load = time.time()
+    eng = DotsVision(DOTS_CONFIG, synthetic_seed=0, device=local)
+    log(f"[rank {rank}] dots vision tower loaded on hip:{local} in {time.time() - t_load:.1f}s")
+    cfg = json.load(open(DOTS_CONFIG))["vision_config"]
+    size = args.dots_size
+    ppg = args.pages_per_gpu
+
+    def dev(arr):
+        p = C.c_void_p()
+        check(L.dsocr_dev_alloc(arr.nbytes, C.byref(p)))
+        check(L.dsocr_memcpy_h2d(p, arr.ctypes.data_as(C.c_void_p), arr.nbytes))
+        return p
+
+    pages = []  # inputs resident in HBM before the timed region
+    for s in range(args.warmup + args.steps):
+        batch = []
+        for idx in page_indices(s, world, rank, ppg):
+            patches, grid = preprocess(DOTS_CONFIG, synthetic_page(idx, size, size))
+            batch.append((dev(patches), grid))
+        pages.append(batch)
+    N = grid[0] * grid[1] * grid[2]
+    groups = N // 4
+    out = C.c_void_p()
+    check(L.dsocr_dev_alloc(groups * eng.hidden * 4, C.byref(out)))
+    for s in range(args.warmup):
+        for p, g in pages[s]:
+            eng.embed_device(p, g, out)
+    check(L.dsocr_dev_sync())
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, args.warmup + args.steps):
+        for p, g in pages[s]:
+            eng.embed_device(p, g, out)
+    check(L.dsocr_dev_sync())
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed, _ = reduce_over_ranks(dist, elapsed, 0.0)
+    value = args.steps * ppg * world / elapsed
+    if rank != 0:
+        return None
+    # one more page with its first 4 layers' attention timed alone (events around each launch)
+    eng.embed_device(pages[-1][0][0], pages[-1][0][1], out, time_attention_layers=4)
+    tm = eng.last_timings()
+    gemm_f, attn_f, other_f = dots_flops(cfg, N)
+    attn_layer_ms = tm["attention_ms"] / 4
+    attn_tf = (attn_f / cfg["num_hidden_layers"]) / (attn_layer_ms * 1e-3) / 1e12
+    page_ms = elapsed / (args.steps * ppg) * 1e3
+    return {
+        "metric": "pages/sec, dots.ocr bf16 vision tower, 2048px page (BASELINE configs[3])",
+        "value": round(value, 4), "unit": "pages/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16 (reference semantics: bf16 tensors between ops; f32 attention math)",
+        "data": "synthetic document pages + seeded synthetic weights (no checkpoint offline)",
+        "config": {"workload": f"configs[3]: dots.ocr vision tower, {size}x{size} page, grid {grid[1]}x{grid[2]}, "
+                               f"{N} patch tokens, {groups} output rows", "pages_per_gpu": ppg,
+                   "global_batch": ppg * world, "parallelism": f"dp{world}"},
+        "stage_ms": {"page_ms": round(page_ms, 2), "blocks_ms": round(tm["blocks_ms"], 2),
+                     "patch_ms": round(tm["patch_ms"], 2), "merger_ms": round(tm["merger_ms"], 2)},
+        "roofline": {"bound": "mfma", "achieved": round(attn_tf, 2), "peak": 157.3, "unit": "TFLOP/s",
+                     "frac": round(attn_tf / 157.3, 4), "traffic": None,
+                     "kernel": "attention_fwd2_kernel<128> (bidirectional flash attention over the page's tokens, "
+                               "f32 MFMA v_mfma_f32_32x32x2_f32: the reference's f32 attention math)",
+                     "avg_launch_us": round(attn_layer_ms * 1e3, 1),
+                     "flops_per_launch": attn_f / cfg["num_hidden_layers"],
+                     "tower_tflops_total": round((gemm_f + attn_f + other_f) / 1e12, 2),
+                     "tower_achieved_tflops": round((gemm_f + attn_f + other_f) / (page_ms * 1e-3) / 1e12, 2)},
+        "cpu_baseline": None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,6 +225,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-decode-steps", type=int, default=2)
     ap.add_argument("--roofline-iters", type=int, default=20)
+    ap.add_argument("--workload", default="deepseek", choices=["deepseek", "dots2048"],
+                    help="deepseek: configs[1]/[2] (default); dots2048: configs[3], the dots.ocr vision tower")
+    ap.add_argument("--dots-size", type=int, default=2044)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -139,6 +237,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")   # host-side barrier / max only; the data path has no collective
+
+    if args.workload == "dots2048":
+        res = run_dots(args, rank, world, local, dist)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     import numpy as np
 

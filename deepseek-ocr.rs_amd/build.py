@@ -23,8 +23,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CLANG = os.environ.get("DSOCR_CXX", "/opt/rocm/llvm/bin/clang++")
 ARCH = "gfx950"
 
-KERNELS = ["gemm", "gemm_bf16", "moe", "norm", "attention", "misc", "decode", "lmhead", "dsq", "preprocess", "sampling"]
-HOST = ["engine", "capi"]
+KERNELS = ["gemm", "gemm_bf16", "moe", "norm", "attention", "misc", "decode", "lmhead", "dsq", "preprocess", "sampling",
+           "dots_ops"]
+HOST = ["engine", "dots", "capi"]
 
 
 def sources():

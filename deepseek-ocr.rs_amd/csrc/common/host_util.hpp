@@ -100,7 +100,7 @@ inline uint64_t mix64(uint64_t z) {
 inline void synth_init_rule(const std::string& name, double* mean, double* stdv) {
     auto ends = [&](const char* s) { size_t n = strlen(s); return name.size() >= n && name.compare(name.size() - n, n, s) == 0; };
     bool norm_w = ends(".weight") && (name.find("norm") != std::string::npos || name.find(".neck.1.") != std::string::npos ||
-                                      name.find(".neck.3.") != std::string::npos);
+                                      name.find(".neck.3.") != std::string::npos || name.find(".ln_q.") != std::string::npos);
     *mean = norm_w ? 1.0 : 0.0;
     *stdv = norm_w ? 0.05 : 0.02;
 }

@@ -6,9 +6,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
 #include <string>
 
 #include "../common/host_util.hpp"
+#include "dots.hpp"
 #include "engine.hpp"
 #include "host_ops.hpp"
 
@@ -17,6 +21,9 @@ struct dsocr_engine {
 };
 struct dsocr_page_pixels {
     dsocr::PagePixels px;
+};
+struct dsocr_dots {
+    std::unique_ptr<dsocr::DotsVision> impl;
 };
 
 namespace {
@@ -646,6 +653,78 @@ dsocr_status dsocr_k_sample_stoch(int B, int V, float* logits, const int* ctx, i
             throw;
         }
         for (void* q : bufs) (void)hipFree(q);
+    });
+}
+
+// ---------------------------------------------------------------- dots.ocr vision tower
+dsocr_status dsocr_dots_load(const char* config_path, const char* weights_path, uint64_t seed, int device,
+                             dsocr_dots** out) {
+    return guarded([&] {
+        if (!config_path || !out) throw std::runtime_error("EINVAL: NULL argument");
+        std::unique_ptr<dsocr_dots> d(new dsocr_dots);
+        d->impl.reset(new dsocr::DotsVision(config_path, weights_path ? weights_path : "", seed, device));
+        *out = d.release();
+    });
+}
+void dsocr_dots_free(dsocr_dots* d) { delete d; }
+dsocr_status dsocr_dots_info(const dsocr_dots* d, size_t* hidden, size_t* embed, size_t* layers, size_t* patch_dim) {
+    return guarded([&] {
+        if (!d) throw std::runtime_error("EINVAL: NULL handle");
+        const dsocr::DotsConfig& c = d->impl->cfg();
+        if (hidden) *hidden = c.hidden;
+        if (embed) *embed = c.embed;
+        if (layers) *layers = c.layers;
+        if (patch_dim) *patch_dim = (size_t)c.channels * c.patch * c.patch;
+    });
+}
+dsocr_status dsocr_dots_preprocess(const char* config_path, const uint8_t* rgb, uint32_t w, uint32_t h, float* patches,
+                                   size_t cap, size_t* n_patches, uint32_t* grid) {
+    return guarded([&] {
+        if (!config_path || !rgb || !n_patches) throw std::runtime_error("EINVAL: NULL argument");
+        std::ifstream f(config_path);
+        if (!f) throw std::runtime_error(std::string("ENOENT: cannot read config ") + config_path);
+        std::stringstream ss;
+        ss << f.rdbuf();
+        const dsocr::DotsConfig c = dsocr::parse_dots_config(dsocr::Json::parse(ss.str()));
+        const dsocr::DotsPatches p = dsocr::dots_preprocess(c, rgb, (int)w, (int)h);
+        const size_t n = (size_t)p.grid_t * p.grid_h * p.grid_w;
+        *n_patches = n;
+        if (grid) { grid[0] = p.grid_t; grid[1] = p.grid_h; grid[2] = p.grid_w; }
+        if (patches) {
+            if (n > cap) throw std::runtime_error("EINVAL: patch capacity too small");
+            std::memcpy(patches, p.data.data(), p.data.size() * 4);
+        }
+    });
+}
+dsocr_status dsocr_dots_embed(dsocr_dots* d, const uint8_t* rgb, uint32_t w, uint32_t h, float* out, size_t cap_rows,
+                              size_t* n_rows, uint32_t* grid) {
+    return guarded([&] {
+        if (!d || !rgb || !n_rows) throw std::runtime_error("EINVAL: NULL argument");
+        const dsocr::DotsConfig& c = d->impl->cfg();
+        const dsocr::DotsPatches p = dsocr::dots_preprocess(c, rgb, (int)w, (int)h);
+        const size_t groups = (size_t)p.grid_t * p.grid_h * p.grid_w / (c.merge * c.merge);
+        *n_rows = groups;
+        if (grid) { grid[0] = p.grid_t; grid[1] = p.grid_h; grid[2] = p.grid_w; }
+        if (groups > cap_rows) throw std::runtime_error("EINVAL: output capacity too small");
+        std::vector<float> r = d->impl->embed(p);
+        if (out) std::memcpy(out, r.data(), r.size() * 4);
+    });
+}
+dsocr_status dsocr_dots_embed_device(dsocr_dots* d, const float* patches, uint32_t gt, uint32_t gh, uint32_t gw,
+                                     float* out, int time_attention_layers) {
+    return guarded([&] {
+        if (!d || !patches || !out || !gt || !gh || !gw) throw std::runtime_error("EINVAL: bad arguments");
+        d->impl->time_layers = std::max(0, time_attention_layers);
+        d->impl->embed_device(patches, (int)gt, (int)gh, (int)gw, out);
+        d->impl->time_layers = 0;
+    });
+}
+dsocr_status dsocr_dots_last_timings(const dsocr_dots* d, dsocr_dots_timings* t) {
+    return guarded([&] {
+        if (!d || !t) throw std::runtime_error("EINVAL: NULL argument");
+        const dsocr::DotsTimings x = d->impl->last_timings();
+        t->total_ms = x.total_ms; t->patch_ms = x.patch_ms; t->blocks_ms = x.blocks_ms;
+        t->attention_ms = x.attention_ms; t->merger_ms = x.merger_ms; t->tokens = x.tokens; t->groups = x.groups;
     });
 }
 

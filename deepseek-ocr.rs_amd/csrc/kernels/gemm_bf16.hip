@@ -46,6 +46,19 @@ __device__ __forceinline__ bf16x8_v frag(const uint16_t* lds, int r, int kc) {
     return *reinterpret_cast<const bf16x8_v*>(lds + r * TB_K + c * 8);
 }
 
+__device__ __forceinline__ float rnd_bf16(float v) { return (float)(__bf16)v; }
+
+// bf16-output epilogue: each reference op rounds to bf16 on its own (matmul, + bias, activation,
+// + residual), so the rounding chain is rnd(rnd(rnd(acc) + b) ...)
+__device__ __forceinline__ void bf16_store_epilogue(const GemmBf16Args& g, long orow, int col, float acc, float bv) {
+    float v = rnd_bf16(acc);
+    if (g.bias) v = rnd_bf16(v + bv);
+    if (g.act) v = rnd_bf16(apply_act(v, g.act));
+    __bf16* cp = reinterpret_cast<__bf16*>(g.C) + orow * (long)g.ldc + col;
+    if (g.accumulate) v = rnd_bf16((float)*cp + v);
+    *cp = (__bf16)v;
+}
+
 __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
     __shared__ __attribute__((aligned(16))) uint16_t smem[2 * TB_STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -136,6 +149,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
                 if (row >= g.M) continue;
                 const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;
                 if (orow < 0) continue;
+                if (g.out_bf16) {
+                    bf16_store_epilogue(g, orow, col, acc[i][j][r], bv);
+                    continue;
+                }
                 float v = apply_act(acc[i][j][r] + bv, g.act);
                 float* cp = g.C + orow * (long)g.ldc + col;
                 if (g.accumulate) v += *cp;
@@ -154,6 +171,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmBf16Args g) {
     for (int sp = 0; sp < g.splits; ++sp) v += g.part[(long)sp * g.M * g.N + i];
     const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;
     if (orow < 0) return;
+    if (g.out_bf16) {
+        bf16_store_epilogue(g, orow, col, v, g.bias ? g.bias[col] : 0.f);
+        return;
+    }
     v = apply_act(v + (g.bias ? g.bias[col] : 0.f), g.act);
     float* cp = g.C + orow * g.ldc + col;
     if (g.accumulate) v += *cp;

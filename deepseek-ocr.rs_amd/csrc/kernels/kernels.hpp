@@ -21,6 +21,10 @@ struct GemmBf16Args {
     const int* c_rows = nullptr;      // optional row scatter for C (-1 drops the row)
     int act = 0, accumulate = 0;
     int splits = 1; float* part = nullptr;  // split-K: [splits][M][N] f32 partials (reduced in order)
+    // bf16 output (the dots.ocr tower's bf16 tensors): C is then uint16_t [M][ldc] and every op of the
+    // epilogue rounds to bf16 as the reference's separate bf16 ops do (quant.rs:141-150):
+    // v = rnd(acc); bias: v = rnd(v + b); act: v = rnd(act(v)); accumulate: v = rnd(C + v)
+    int out_bf16 = 0;
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
 int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)

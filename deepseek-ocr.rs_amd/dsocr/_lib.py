@@ -66,6 +66,11 @@ class DecodeProfileC(C.Structure):
                 ("moe_gateup_kernel", C.c_char_p), ("moe_down_kernel", C.c_char_p)]
 
 
+class DotsTimingsC(C.Structure):
+    _fields_ = [("total_ms", C.c_double), ("patch_ms", C.c_double), ("blocks_ms", C.c_double),
+                ("attention_ms", C.c_double), ("merger_ms", C.c_double), ("tokens", C.c_size_t), ("groups", C.c_size_t)]
+
+
 STREAM_CB = C.CFUNCTYPE(None, C.c_size_t, C.POINTER(C.c_int64), C.c_void_p)
 
 # every symbol include/dsocr.h declares (tests check the library exports all of them)
@@ -77,6 +82,8 @@ EXPORTS = [
     "dsocr_k_gemm", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
     "dsocr_k_sample_greedy", "dsocr_k_sample_stoch", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
     "dsocr_generate_trace", "dsocr_k_moe_kernels", "dsocr_k_lmhead_screened",
+    "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
+    "dsocr_dots_embed_device", "dsocr_dots_last_timings",
 ]
 
 _lib = None
@@ -108,6 +115,14 @@ def lib():
                                  C.POINTER(sz)]
     L.dsocr_generate_batch.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC)]
     L.dsocr_generate_trace.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC), vp]
+    L.dsocr_dots_load.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64, i32, C.POINTER(vp)]
+    L.dsocr_dots_free.argtypes = [vp]
+    L.dsocr_dots_free.restype = None
+    L.dsocr_dots_info.argtypes = [vp, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
+    L.dsocr_dots_preprocess.argtypes = [C.c_char_p, vp, u32, u32, vp, sz, C.POINTER(sz), C.POINTER(u32)]
+    L.dsocr_dots_embed.argtypes = [vp, vp, u32, u32, vp, sz, C.POINTER(sz), C.POINTER(u32)]
+    L.dsocr_dots_embed_device.argtypes = [vp, vp, u32, u32, u32, vp, i32]
+    L.dsocr_dots_last_timings.argtypes = [vp, C.POINTER(DotsTimingsC)]
     L.dsocr_k_lmhead_screened.argtypes = [i32, i32, i32, vp, vp, f32, vp, vp, i32, vp]
     L.dsocr_k_moe_kernels.argtypes = [i32, i32, i32, i32, i32, i32, i32, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
     L.dsocr_last_timings.argtypes = [vp, C.POINTER(TimingsC)]

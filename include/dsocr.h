@@ -269,6 +269,33 @@ dsocr_status dsocr_k_sample_stoch(int B, int V, float* logits, const int* ctx, i
                                   int ngram, float rep_penalty, double temperature, size_t top_k, double top_p,
                                   uint64_t seed, int draws, int* out_tok);
 
+/* ---- dots.ocr vision tower (BASELINE configs[3]; crates/infer-dots/src/vision/dots_vit.rs
+ *      DotsVisionModel::load / forward, vision/preprocess.rs preprocess_image).  The tower runs in the
+ *      reference's bf16 semantics (every op's output rounded to bf16; attention scores / softmax /
+ *      probs.V in f32).  config_path: the dots config.json (its `vision_config`, plus an optional
+ *      `preprocessor_config` object with the preprocessor_config.json fields); weights_path NULL
+ *      selects the seeded synthetic checkpoint (tensor names `vision_tower.*`). */
+typedef struct dsocr_dots dsocr_dots;
+dsocr_status dsocr_dots_load(const char* config_path, const char* weights_path, uint64_t synthetic_seed, int device,
+                             dsocr_dots** out);
+void dsocr_dots_free(dsocr_dots* d);
+dsocr_status dsocr_dots_info(const dsocr_dots* d, size_t* hidden, size_t* embed_dim, size_t* layers, size_t* patch_dim);
+/* preprocess_image (host): RGB8 HWC -> patches [N][3*p*p] in merge-group order; grid_thw = (t, h, w) */
+dsocr_status dsocr_dots_preprocess(const char* config_path, const uint8_t* rgb, uint32_t width, uint32_t height,
+                                   float* patches, size_t cap_patches, size_t* n_patches, uint32_t* grid_thw);
+/* preprocess + tower for one page: out [groups][hidden] f32 (bf16 values), groups = N / merge^2 */
+dsocr_status dsocr_dots_embed(dsocr_dots* d, const uint8_t* rgb, uint32_t width, uint32_t height, float* out,
+                              size_t cap_rows, size_t* n_rows, uint32_t* grid_thw);
+/* tower on device-resident patches (device pointers; the bench's inputs-in-HBM form); the first
+ * time_attention_layers layers' attention launches are timed alone (0: no per-layer sync) */
+dsocr_status dsocr_dots_embed_device(dsocr_dots* d, const float* patches, uint32_t grid_t, uint32_t grid_h,
+                                     uint32_t grid_w, float* out, int time_attention_layers);
+typedef struct {
+    double total_ms, patch_ms, blocks_ms, attention_ms, merger_ms;
+    size_t tokens, groups;
+} dsocr_dots_timings;
+dsocr_status dsocr_dots_last_timings(const dsocr_dots* d, dsocr_dots_timings* t);
+
 #ifdef __cplusplus
 }
 #endif

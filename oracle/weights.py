@@ -49,7 +49,7 @@ def _lib():
 def init_rule(name: str):
     """Synthetic init (same rule as the product's csrc/common/synth.hpp)."""
     is_norm_w = name.endswith(".weight") and (
-        "norm" in name or ".neck.1." in name or ".neck.3." in name)
+        "norm" in name or ".neck.1." in name or ".neck.3." in name or ".ln_q." in name)
     if is_norm_w:
         return 1.0, 0.05
     return 0.0, 0.02

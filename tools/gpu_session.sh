@@ -17,6 +17,8 @@ for step in "$@"; do
     bench8) run 900 python bench.py --pages-per-gpu 8 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench8.log 2>&1 ;;
     gprof) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof.log 2>&1 ;;
     gprof8) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8 -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8.log 2>&1 ;;
+    dots) run 900 python -u -m pytest tests/test_dots.py -q -m gpu -rf -p no:cacheprovider --timeout 600 --timeout-method thread -s > gpurun_out/dots.log 2>&1 ;;
+    benchdots) run 900 python bench.py --workload dots2048 --steps 2 --warmup 1 > gpurun_out/benchdots.log 2>&1 ;;
     gpu_all) run 1100 python -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
