@@ -306,7 +306,7 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
         auto p = e->impl->profile_decode(iters);
         auto cp = [](const dsocr::Engine::KernelProfile& k) {
             dsocr_kernel_profile r;
-            r.avg_us = k.avg_us; r.bytes = k.bytes; r.flops = k.flops; r.launches = k.launches;
+            r.avg_us = k.avg_us; r.bytes = k.bytes; r.flops = k.flops; r.launches = k.launches; r.replay_us = k.replay_us;
             return r;
         };
         out->moe_gateup = cp(p.moe_gateup);
@@ -434,6 +434,22 @@ dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale,
         hipError_t e = hipDeviceSynchronize();
         if (rb) (void)hipFree(rb);
         check_hip(e, "attention");
+    });
+}
+dsocr_status dsocr_k_attention_bf16(int n_seq, int L, int heads, int hd, float scale, const void* qkv, long ld,
+                                    void* o, long o_ld, int o_bf16) {
+    return guarded([&] {
+        if (!qkv || !o || n_seq <= 0 || L <= 0 || heads <= 0) throw std::runtime_error("EINVAL: bad attention arguments");
+        const long D = (long)heads * hd;
+        if (ld < 3 * D || o_ld < D) throw std::runtime_error("EINVAL: row strides too small");
+        dsocr::AttnBf16Args a;
+        a.q = (const uint16_t*)qkv; a.k = (const uint16_t*)qkv + D; a.v = (const uint16_t*)qkv + 2 * D;
+        a.q_rs = a.k_rs = a.v_rs = ld; a.q_hs = a.k_hs = a.v_hs = hd;
+        a.o = o; a.o_rs = o_ld; a.o_hs = hd; a.o_bf16 = o_bf16;
+        a.n_seq = n_seq; a.L = L; a.heads = heads; a.kv_heads = heads; a.hd = hd; a.scale = scale;
+        dsocr::launch_attention_bf16(a, nullptr);
+        check_hip(hipGetLastError(), "attention_bf16 launch");
+        check_hip(hipDeviceSynchronize(), "attention_bf16");
     });
 }
 dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, int rope_dim, int max_len, float scale,

@@ -20,8 +20,8 @@ namespace dsocr {
 void launch_dots_rmsnorm(const void* x, int in_f32, long rows, int D, const float* w, float eps, void* y, hipStream_t s);
 void launch_dots_layernorm(const void* x, long rows, int D, const float* w, const float* b, float eps, void* y,
                            hipStream_t s);
-void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, float* out,
-                      hipStream_t s);
+void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
+                      int out_bf16, hipStream_t s);
 void launch_dots_swiglu(const void* gu, long N, int I, void* h, hipStream_t s);
 void launch_dots_gelu(void* x, long n, hipStream_t s);
 void launch_dots_to_bf16(const float* x, long N, int D, long ldi, void* y, int ldo, hipStream_t s);
@@ -311,8 +311,11 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
     void* X = ws("d_x", (size_t)N * D * 2);
     void* XN = ws("d_xn", (size_t)N * D * 2);
     void* QKV = ws("d_qkv", (size_t)N * 3 * D * 2);
-    float* QKVf = (float*)ws("d_qkvf", (size_t)N * 3 * D * 4);
-    float* CTX = (float*)ws("d_ctx", (size_t)N * D * 4);
+    // DSOCR_DOTS_ATTN=f32 selects the f32-MFMA attention (f32 copies of q / k / v) for comparison
+    const bool attn_f32 = getenv("DSOCR_DOTS_ATTN") && std::string(getenv("DSOCR_DOTS_ATTN")) == "f32";
+    float* QKVf = attn_f32 ? (float*)ws("d_qkvf", (size_t)N * 3 * D * 4) : nullptr;
+    float* CTX = attn_f32 ? (float*)ws("d_ctx", (size_t)N * D * 4) : nullptr;
+    void* QKVr = attn_f32 ? nullptr : ws("d_qkvr", (size_t)N * 3 * D * 2);
     void* CTXb = ws("d_ctxb", (size_t)N * D * 2);
     void* GU = ws("d_gu", (size_t)N * 2 * I * 2);
     void* HB = ws("d_h", (size_t)N * I * 2);
@@ -334,25 +337,39 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
         // DotsVisionBlock::forward (305-315) / VisionAttention::forward (364-431)
         launch_dots_rmsnorm(X, 0, N, D, b.n1, (float)c_.eps, XN, st);
         gemm(XN, D, (int)N, 3 * D, D, b.qkv, b.b_qkv, QKV, 3 * D, 0);
-        launch_dots_rope(QKV, N, H, hd, d_cos, d_sin, QKVf, st);
-        AttnArgs a;
-        a.q = {QKVf, 3L * D, hd, nullptr};
-        a.k = {QKVf + D, 3L * D, hd, nullptr};
-        a.v = {QKVf + 2 * D, 3L * D, hd, nullptr};
-        a.o = CTX; a.o_row_stride = D; a.o_head_stride = hd;
-        a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd;
-        a.scale = (float)(1.0 / std::sqrt((double)hd));
         const bool timed = l < time_layers;
-        if (timed) HIP_CHECK(hipEventRecord(a0, st));
-        launch_attention(a, st);
+        const float scale = (float)(1.0 / std::sqrt((double)hd));
+        if (attn_f32) {
+            // f32 flash attention on f32 copies of the bf16 q / k / v (f32 MFMA; the comparison path)
+            launch_dots_rope(QKV, N, H, hd, d_cos, d_sin, QKVf, 0, st);
+            AttnArgs a;
+            a.q = {QKVf, 3L * D, hd, nullptr};
+            a.k = {QKVf + D, 3L * D, hd, nullptr};
+            a.v = {QKVf + 2 * D, 3L * D, hd, nullptr};
+            a.o = CTX; a.o_row_stride = D; a.o_head_stride = hd;
+            a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
+            if (timed) HIP_CHECK(hipEventRecord(a0, st));
+            launch_attention(a, st);
+            if (timed) HIP_CHECK(hipEventRecord(a1, st));
+            launch_dots_to_bf16(CTX, N, D, D, CTXb, D, st);
+        } else {
+            // bf16 matrix cores with the same f32 math (attention_bf16.hip): rotated q / k stay bf16
+            // (exactly the reference's rounding), the context is written as the bf16 tensor it becomes
+            launch_dots_rope(QKV, N, H, hd, d_cos, d_sin, QKVr, 1, st);
+            AttnBf16Args a;
+            a.q = (const uint16_t*)QKVr; a.k = (const uint16_t*)QKVr + D; a.v = (const uint16_t*)QKVr + 2 * D;
+            a.q_rs = a.k_rs = a.v_rs = 3L * D; a.q_hs = a.k_hs = a.v_hs = hd;
+            a.o = CTXb; a.o_rs = D; a.o_hs = hd; a.o_bf16 = 1;
+            a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
+            if (timed) prof_events() = ProfEvents{a0, a1};  // the launch's own dispatch timestamps
+            launch_attention_bf16(a, st);
+        }
         if (timed) {
-            HIP_CHECK(hipEventRecord(a1, st));
             HIP_CHECK(hipEventSynchronize(a1));
             float ms = 0.f;
             HIP_CHECK(hipEventElapsedTime(&ms, a0, a1));
             attn_ms += ms;
         }
-        launch_dots_to_bf16(CTX, N, D, D, CTXb, D, st);
         gemm(CTXb, D, (int)N, D, D, b.proj, b.b_proj, X, D, 1);
         launch_dots_rmsnorm(X, 0, N, D, b.n2, (float)c_.eps, XN, st);
         gemm(XN, D, (int)N, 2 * I, D, b.fc13, b.b_fc13, GU, 2 * I, 0);

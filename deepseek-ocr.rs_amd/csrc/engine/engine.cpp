@@ -1646,23 +1646,36 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     // engine stream: per-launch time = span / n = device time + the dependent-kernel boundary
     // (eager launches go host-bound below ~3.5 us per kernel, MI355X_MICROARCH.md
     // graph-replay-floor, so they cannot time the short decode kernels)
+    // Two figures per kernel:
+    //  * avg_us: every launch carries its own start / stop events on its dispatch packet
+    //    (hipExtLaunchKernelGGL through DSOCR_LAUNCH: the begin / end timestamps rocprofv3's kernel
+    //    trace reports), eager, one launch at a time — the figure the committed rocprof summaries
+    //    corroborate;
+    //  * replay_us: n launches back to back in one hipGraph replay, span / n - the kernel inside a
+    //    dependent chain as the decode loop runs it (duration + the ~1.2 us kernel boundary, minus
+    //    whatever startup the chained dispatch hides).
     auto timed = [&](KernelProfile& kp, int n, const std::function<void(int)>& body) {
+        body(0);  // warm (code objects, TLB) and every workspace allocated before capture
+        std::vector<hipEvent_t> ev(2 * n);
+        for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+        for (int i = 0; i < n; ++i) {
+            prof_events() = ProfEvents{ev[2 * i], ev[2 * i + 1]};  // the body's first launch times itself
+            body(i);
+            if (prof_events().start) {  // the body launched nothing through DSOCR_LAUNCH: bracket it
+                prof_events() = ProfEvents();
+                throw std::runtime_error("EINTERNAL: profiled body made no instrumented launch");
+            }
+        }
+        HIP_CHECK(hipEventSynchronize(ev[2 * n - 1]));
+        double sum = 0;
+        for (int i = 0; i < n; ++i) sum += ms_between(ev[2 * i], ev[2 * i + 1]);
+        for (auto& e : ev) (void)hipEventDestroy(e);
+        kp.avg_us = 1000.0 * sum / n;
+        kp.launches = n;
+        if (getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0) return;
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
-        body(0);  // warm (code objects, TLB) and every workspace allocated before capture
-        if (getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0) {
-            // eager (profiler runs: rocprofv3 kernel tracing of graph capture is unreliable here)
-            HIP_CHECK(hipEventRecord(e0, st));
-            for (int i = 0; i < n; ++i) body(i);
-            HIP_CHECK(hipEventRecord(e1, st));
-            HIP_CHECK(hipEventSynchronize(e1));
-            kp.avg_us = 1000.0 * ms_between(e0, e1) / n;
-            kp.launches = n;
-            (void)hipEventDestroy(e0);
-            (void)hipEventDestroy(e1);
-            return;
-        }
         hipGraph_t graph = nullptr;
         hipGraphExec_t gexec = nullptr;
         capturing_ = true;
@@ -1676,8 +1689,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         HIP_CHECK(hipGraphLaunch(gexec, st));
         HIP_CHECK(hipEventRecord(e1, st));
         HIP_CHECK(hipEventSynchronize(e1));
-        kp.avg_us = 1000.0 * ms_between(e0, e1) / n;
-        kp.launches = n;
+        kp.replay_us = 1000.0 * ms_between(e0, e1) / n;
         (void)hipGraphExecDestroy(gexec);
         (void)hipGraphDestroy(graph);
         (void)hipEventDestroy(e0);

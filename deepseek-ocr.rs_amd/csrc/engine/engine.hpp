@@ -147,6 +147,7 @@ class Engine {
     struct KernelProfile {
         double avg_us = 0, bytes = 0, flops = 0;
         int launches = 0;
+        double replay_us = 0;
     };
     struct DecodeProfile {
         KernelProfile moe_gateup, moe_down, attention, lm_head, qkv, o_proj, router, layers_step, lm_head_screened;

@@ -1,0 +1,200 @@
+// Bidirectional flash attention on the bf16 matrix cores for bf16-valued q / k / v with the
+// reference's f32 math (dots.ocr VisionAttention::forward_uniform, crates/infer-dots/src/vision/
+// dots_vit.rs:433-498: q_heads . k^T in f32, * scale, softmax, probs . v in f32; compute_dtype_for
+// 584-589 widens bf16 to f32).
+//
+// Exactness: q, k, v hold bf16 values, so every product of QK^T is exact in the f32 accumulator of
+// v_mfma_f32_32x32x16_bf16 (only the summation order differs from an f32 matmul).  The softmax
+// probabilities p are f32: each is split exactly into three bf16 planes p = hi + mid + lo (RNE at
+// each step, the residuals exact), and P.V runs as three MFMA passes (lo, mid, hi) against the bf16
+// V: again exact products summed in f32.  16x the f32-MFMA rate per pass (MI355X_MICROARCH.md
+// Matrix cores), so the 3 + 1 passes cost a quarter of the f32-MFMA kernel's cycles.
+//
+// Layout: S^T = K . Q^T (the accumulator's column is the lane's own query: the online-softmax
+// rescale needs no cross-lane traffic), O^T = V^T . P^T with V staged transposed in LDS; the key
+// order inside each 16-key MFMA step is permuted (bits 2 and 3 of the key index swapped) so that the
+// 8 keys a lane's P registers hold are 8 contiguous LDS columns of V^T (one 16-byte read).
+// 4 waves x 32 queries per block, 64-key tiles in LDS, the next tile's global loads in registers
+// while the current one is consumed.
+#include <stdexcept>
+
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int AB_Q = 32;   // queries per wave
+constexpr int AB_KT = 64;  // keys per LDS tile
+
+// LDS column of key k (0..63) inside a V^T tile: within each 16-key step swap bits 2 and 3
+__device__ __forceinline__ int vt_col(int k) { return (k & ~15) | ((k & 4) << 1) | ((k & 8) >> 1) | (k & 3); }
+
+__device__ __forceinline__ uint16_t bf_bits(float v) {
+    const __bf16 b = (__bf16)v;
+    uint16_t u;
+    __builtin_memcpy(&u, &b, 2);
+    return u;
+}
+
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) {
+    constexpr int KP = HD + 8, VP = AB_KT + 8;   // LDS row pitches (bf16 elements)
+    constexpr int C8 = HD / 8;                    // 16-byte chunks per row
+    constexpr int NCH = AB_KT * C8 / 256;         // chunks per thread per operand per tile
+    constexpr int QS = HD / 16;                   // MFMA k-steps of the QK product
+    constexpr int DC = HD / 32;                   // 32-dim output chunks
+    __shared__ __attribute__((aligned(16))) uint16_t Ks[AB_KT][KP];
+    __shared__ __attribute__((aligned(16))) uint16_t Vt[HD][VP];
+    const int s = blockIdx.z, h = blockIdx.y;
+    const int len = a.L;
+    const int qb0 = blockIdx.x * (4 * AB_Q);
+    if (qb0 >= len) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = lane >> 5, l32 = lane & 31;
+    const int kvh = h / (a.heads / a.kv_heads);
+    const uint16_t* Q = a.q + (long)s * a.L * a.q_rs + (long)h * a.q_hs;
+    const uint16_t* K = a.k + (long)s * a.L * a.k_rs + (long)kvh * a.k_hs;
+    const uint16_t* V = a.v + (long)s * a.L * a.v_rs + (long)kvh * a.v_hs;
+    const int q_lane = qb0 + wave * AB_Q + l32;
+    const bool q_valid = q_lane < len;
+    // this lane's query: dims 16 st + 8 half .. + 8 for every k-step st
+    bf16x8_t qreg[QS];
+    {
+        const uint16_t* qr = Q + (long)(q_valid ? q_lane : 0) * a.q_rs + 8 * half;
+#pragma unroll
+        for (int st = 0; st < QS; ++st) qreg[st] = *reinterpret_cast<const bf16x8_t*>(qr + 16 * st);
+    }
+    uint4 rk[NCH], rv[NCH];
+#define AB_GLOAD(K0)                                                                            \
+    _Pragma("unroll") for (int j = 0; j < NCH; ++j) {                                           \
+        const int f = tid + 256 * j;                                                            \
+        const int key = min((K0) + f / C8, len - 1);                                            \
+        const int c8 = f % C8;                                                                  \
+        rk[j] = *reinterpret_cast<const uint4*>(K + (long)key * a.k_rs + c8 * 8);               \
+        rv[j] = *reinterpret_cast<const uint4*>(V + (long)key * a.v_rs + c8 * 8);               \
+    }
+#define AB_LSTORE()                                                                             \
+    _Pragma("unroll") for (int j = 0; j < NCH; ++j) {                                           \
+        const int f = tid + 256 * j;                                                            \
+        const int kr = f / C8, c8 = f % C8;                                                     \
+        *reinterpret_cast<uint4*>(&Ks[kr][c8 * 8]) = rk[j];                                     \
+        const int col = vt_col(kr);                                                             \
+        const uint32_t w4[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};                            \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                         \
+            Vt[c8 * 8 + 2 * i][col] = (uint16_t)(w4[i] & 0xffffu);                              \
+            Vt[c8 * 8 + 2 * i + 1][col] = (uint16_t)(w4[i] >> 16);                              \
+        }                                                                                       \
+    }
+    f32x16 o[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    AB_GLOAD(0);
+    AB_LSTORE();
+    __syncthreads();
+    for (int k0 = 0; k0 < len; k0 += AB_KT) {
+        AB_GLOAD(k0 + AB_KT);  // unconditional (clamped keys): the next tile's loads in flight
+        // S^T for the two 32-key halves of the tile
+        f32x16 sc[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[u][r] = 0.f;
+#pragma unroll
+            for (int st = 0; st < QS; ++st) {
+                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(&Ks[u * 32 + l32][16 * st + 8 * half]);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qreg[st], sc[u], 0, 0, 0);
+            }
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                float v = sc[u][r] * a.scale;
+                if (key >= len) v = -INFINITY;
+                sc[u][r] = v;
+                tmax = fmaxf(tmax, v);
+            }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = (m_new == -INFINITY) ? 0.f : expf(sc[u][r] - m_new);
+                sc[u][r] = p;
+                psum += p;
+            }
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+        // O^T += V^T . P^T: per 16-key step t of half u, the lane's P registers 8t .. 8t+7 (keys
+        // 32u + 16t + 4 half + {0..3, 8..11}) as three exact bf16 planes
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                bf16x8_t ph, pm, pl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float p = sc[u][8 * t + j];
+                    const __bf16 hi = (__bf16)p;
+                    const float r1 = p - (float)hi;
+                    const __bf16 mi = (__bf16)r1;
+                    ph[j] = hi;
+                    pm[j] = mi;
+                    pl[j] = (__bf16)(r1 - (float)mi);
+                }
+#pragma unroll
+                for (int c = 0; c < DC; ++c) {
+                    const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(&Vt[c * 32 + l32][u * 32 + 16 * t + 8 * half]);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pm, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, ph, o[c], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // every wave is done with the tile before it is refilled
+        AB_LSTORE();
+        __syncthreads();
+    }
+    if (q_valid) {
+        const long orow = (long)s * a.L * a.o_rs + (long)q_lane * a.o_rs + (long)h * a.o_hs;
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = c * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const float v = o[c][r] / l_run;
+                if (a.o_bf16) reinterpret_cast<uint16_t*>(a.o)[orow + d] = bf_bits(v);
+                else reinterpret_cast<float*>(a.o)[orow + d] = v;
+            }
+    }
+#undef AB_GLOAD
+#undef AB_LSTORE
+}
+
+void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s) {
+    if (a.n_seq <= 0 || a.L <= 0) return;
+    if (a.hd != 64 && a.hd != 128) throw std::runtime_error("EINVAL: attention_bf16 supports head_dim 64 / 128");
+    if (a.kv_heads <= 0 || a.heads % a.kv_heads) throw std::runtime_error("EINVAL: heads must be a multiple of kv_heads");
+    if ((a.q_rs | a.k_rs | a.v_rs | a.q_hs | a.k_hs | a.v_hs) % 8)
+        throw std::runtime_error("EINVAL: attention_bf16 needs 16-byte aligned rows");
+    dim3 grid((a.L + 4 * AB_Q - 1) / (4 * AB_Q), a.heads, a.n_seq);
+    if (a.hd == 128) DSOCR_LAUNCH(attention_bf16_kernel<128>, grid, dim3(256), 0, s, a);
+    else DSOCR_LAUNCH(attention_bf16_kernel<64>, grid, dim3(256), 0, s, a);
+}
+
+}  // namespace dsocr

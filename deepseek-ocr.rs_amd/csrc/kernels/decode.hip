@@ -16,6 +16,11 @@
 
 namespace dsocr {
 
+ProfEvents& prof_events() {
+    static thread_local ProfEvents p;
+    return p;
+}
+
 // ------------------------------------------------------------------ helpers
 // Dynamic LDS of the GEMV-type kernels: [XS_RED floats of row partial sums][M][K staged rows].
 constexpr int XS_RED = 128;  // >= M * (blockDim / 64)
@@ -423,7 +428,7 @@ static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     if constexpr (MT >= 4 && MT <= 8) {  // several tokens, x already normalised: no LDS staging
         static const bool direct = !(getenv("DSOCR_GEMV_DIRECT") && atoi(getenv("DSOCR_GEMV_DIRECT")) == 0);
         if (direct && a.N <= 16384 && !a.norm_w && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
-            hipLaunchKernelGGL((dec_gemv_direct_kernel<WT, MT, 1>), dim3((a.N + 3) / 4), dim3(256), 0, s, a);
+            DSOCR_LAUNCH((dec_gemv_direct_kernel<WT, MT, 1>), dim3((a.N + 3) / 4), dim3(256), 0, s, a);
             return;
         }
     }
@@ -434,10 +439,10 @@ static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
         constexpr int RB = 2;
         const int groups = (a.N + RB - 1) / RB;
         const int blocks = std::max(1, std::min((groups + 3) / 4, stream_blocks));
-        hipLaunchKernelGGL((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
+        DSOCR_LAUNCH((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
     } else if (a.N <= 16384) {
         constexpr int RB = 1;
-        hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
+        DSOCR_LAUNCH((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
     } else if (a.K <= 64 * 3 * 8 && MT <= 2) {
         constexpr int RB = 4;
         // exactly one resident wave of blocks (no tail of late-starting blocks)
@@ -451,10 +456,10 @@ static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
         }
         const int groups = (a.N + RB - 1) / RB;
         const int blocks = std::min((groups + 3) / 4, resident);
-        hipLaunchKernelGGL((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
+        DSOCR_LAUNCH((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
     } else {
         constexpr int RB = MT <= 2 ? 4 : 2;
-        hipLaunchKernelGGL((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
+        DSOCR_LAUNCH((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
     }
 }
 template <typename WT>
@@ -626,12 +631,12 @@ void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t 
     // (off by default: every wave re-reading x and the norm weight from L2 measured +0.75 us/layer)
     static const bool wn = getenv("DSOCR_WAVENORM") && atoi(getenv("DSOCR_WAVENORM")) != 0;
     if (wn && a.norm_w) {
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((dec_qkv_rope_kernel<bf16_t, true>), grid, dim3(256), 0, s, a, r);
-        else hipLaunchKernelGGL((dec_qkv_rope_kernel<f16_t, true>), grid, dim3(256), 0, s, a, r);
+        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_rope_kernel<bf16_t, true>), grid, dim3(256), 0, s, a, r);
+        else DSOCR_LAUNCH((dec_qkv_rope_kernel<f16_t, true>), grid, dim3(256), 0, s, a, r);
         return;
     }
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((dec_qkv_rope_kernel<bf16_t, false>), grid, dim3(256), lds, s, a, r);
-    else hipLaunchKernelGGL((dec_qkv_rope_kernel<f16_t, false>), grid, dim3(256), lds, s, a, r);
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_rope_kernel<bf16_t, false>), grid, dim3(256), lds, s, a, r);
+    else DSOCR_LAUNCH((dec_qkv_rope_kernel<f16_t, false>), grid, dim3(256), lds, s, a, r);
 }
 
 // ------------------------------------------------------------------ attention combine + o_proj
@@ -741,7 +746,7 @@ void launch_dec_oproj_comb(const DecGemvArgs& a, const DecCombArgs& cb, hipStrea
     if (!dec_oproj_comb_ok(a, cb)) throw std::runtime_error("EINVAL: dec_oproj_comb outside its range");
     static const int rw = getenv("DSOCR_OC_RW") ? atoi(getenv("DSOCR_OC_RW")) : 1;
 #define DSOCR_OC(WTY, R, NC, E) \
-    hipLaunchKernelGGL((dec_oproj_comb_kernel<WTY, R, NC, E>), dim3((a.N + 4 * R - 1) / (4 * R)), dim3(256), 0, s, a, cb)
+    DSOCR_LAUNCH((dec_oproj_comb_kernel<WTY, R, NC, E>), dim3((a.N + 4 * R - 1) / (4 * R)), dim3(256), 0, s, a, cb)
 #define DSOCR_OC2(WTY, NC, E) do { if (rw == 2) DSOCR_OC(WTY, 2, NC, E); else DSOCR_OC(WTY, 1, NC, E); } while (0)
 #define DSOCR_OC3(WTY) do { \
         if (cb.cm <= 20 && a.K <= 1280) DSOCR_OC2(WTY, 20, 5); else if (cb.cm <= 20) DSOCR_OC2(WTY, 20, 6); \
@@ -934,7 +939,7 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
     const int mt = a.M == 1 ? 1 : (a.M <= 2 ? 2 : (a.M <= 4 ? 4 : 8));
     const size_t lds = stage_bytes(mt, a.K);
     dim3 grid((a.N + 3) / 4);
-#define DSOCR_RT(WTY, MTV) hipLaunchKernelGGL((dec_router_kernel<WTY, MTV>), grid, dim3(256), lds, s, a, r)
+#define DSOCR_RT(WTY, MTV) DSOCR_LAUNCH((dec_router_kernel<WTY, MTV>), grid, dim3(256), lds, s, a, r)
     if (a.wdtype == WDT_BF16) {
         if (mt == 1) DSOCR_RT(bf16_t, 1); else if (mt == 2) DSOCR_RT(bf16_t, 2);
         else if (mt == 4) DSOCR_RT(bf16_t, 4); else DSOCR_RT(bf16_t, 8);
@@ -1361,8 +1366,8 @@ void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s) {
     const int chunks = (a.max_len + 63) / 64;
     dim3 g1(chunks, a.heads, a.B);
     const size_t lds = stage_bytes(1, a.K);
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
+    else DSOCR_LAUNCH((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
 }
 
 static int dec_attn_ch() {
@@ -1384,8 +1389,8 @@ void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     const bool prerot = a.prerot != 0;
 #define DSOCR_DA(HDV, CHV)                                                                          \
     do {                                                                                             \
-        if (prerot) hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, true>), g1, dim3(256), 0, s, a);  \
-        else hipLaunchKernelGGL((dec_attn_kernel<HDV, CHV, false>), g1, dim3(256), 0, s, a);        \
+        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true>), g1, dim3(256), 0, s, a);  \
+        else DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, false>), g1, dim3(256), 0, s, a);        \
     } while (0)
     if (ch == 64) {
         if (a.hd == 128) DSOCR_DA(128, 64); else if (a.hd == 64) DSOCR_DA(64, 64); else DSOCR_DA(32, 64);
@@ -1518,7 +1523,7 @@ __global__ __launch_bounds__(256) void moe_route_kernel(MoeRouteArgs a) {
 
 void launch_moe_route(const MoeRouteArgs& a, hipStream_t s) {
     if (a.T > RT_MAXT || a.E > 256 || a.topk > 8) throw std::runtime_error("EINVAL: routing supports T <= 64, E <= 256, top_k <= 8");
-    hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(256), 0, s, a);
+    DSOCR_LAUNCH(moe_route_kernel, dim3(1), dim3(256), 0, s, a);
 }
 
 // One wave: greedy top-k of E router logits (softmax or sigmoid scores, stable: ties -> lower
@@ -2351,7 +2356,7 @@ bool moe_down_mix_ok(const MoeDec2Args& a) {
 void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s) {
     if (!moe_down_mix_ok(a)) throw std::runtime_error("EINVAL: moe_down_mix outside its range");
     static const int rpb = getenv("DSOCR_DN_RPB") ? atoi(getenv("DSOCR_DN_RPB")) : 2;  // 2: measured best
-#define DSOCR_DM(WTY, R) hipLaunchKernelGGL((moe_down_mix_kernel<WTY, R>), dim3((a.Hout + R - 1) / R), dim3(256), 0, s, a)
+#define DSOCR_DM(WTY, R) DSOCR_LAUNCH((moe_down_mix_kernel<WTY, R>), dim3((a.Hout + R - 1) / R), dim3(256), 0, s, a)
     if (a.wdtype == WDT_BF16) {
         if (rpb == 4) DSOCR_DM(bf16_t, 4); else if (rpb == 1) DSOCR_DM(bf16_t, 1); else DSOCR_DM(bf16_t, 2);
     } else {
@@ -2371,8 +2376,8 @@ void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s)
     const int n_sh = a.sWgu ? (a.Is + RB - 1) / RB : 0;
     const int n_rt = a.topk * ((a.I + RB - 1) / RB);
     dim3 grid(std::max(n_sh, (n_rt + 2) / 3));
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL(moe_gateup_mix_kernel<bf16_t>, grid, dim3(256), 0, s, a, xn);
-    else hipLaunchKernelGGL(moe_gateup_mix_kernel<f16_t>, grid, dim3(256), 0, s, a, xn);
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH(moe_gateup_mix_kernel<bf16_t>, grid, dim3(256), 0, s, a, xn);
+    else DSOCR_LAUNCH(moe_gateup_mix_kernel<f16_t>, grid, dim3(256), 0, s, a, xn);
 }
 
 bool moe_fused_ok(const MoeDec2Args& a) {
@@ -2391,7 +2396,7 @@ void launch_moe_fused(const MoeDec2Args& a, hipStream_t s) {
     MoeDec2Args b = a;
     b.sync_target = NG;
     const size_t lds = std::max(stage_bytes(a.T == 1 ? 1 : 2, a.K), (size_t)256 * DN_HREG * 16);
-#define DSOCR_FU(WTY, MTV, KTV) hipLaunchKernelGGL((moe_fused_slot_kernel<WTY, MTV, KTV>), dim3(NG + ND), dim3(256), lds, s, b, NG)
+#define DSOCR_FU(WTY, MTV, KTV) DSOCR_LAUNCH((moe_fused_slot_kernel<WTY, MTV, KTV>), dim3(NG + ND), dim3(256), lds, s, b, NG)
     if (a.wdtype == WDT_BF16) {
         if (a.T == 1) { if (a.topk == 6) DSOCR_FU(bf16_t, 1, 6); else DSOCR_FU(bf16_t, 1, 3); }
         else { if (a.topk == 6) DSOCR_FU(bf16_t, 2, 6); else DSOCR_FU(bf16_t, 2, 3); }
@@ -2412,8 +2417,8 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
         MoeDec2Args r = a;
         r.sWgu = nullptr;
         const int mt = a.T <= 4 ? 4 : 8;
-        if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_slot_kernel<bf16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
-        else hipLaunchKernelGGL((moe_gateup_slot_kernel<f16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
+        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_slot_kernel<bf16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
+        else DSOCR_LAUNCH((moe_gateup_slot_kernel<f16_t, 1>), dim3(a.slots * units_r), dim3(256), stage_bytes(1, a.K), s, r);
         if (units_s) {
             // shared expert alone (slots = 0: every block is a shared block), one row per wave so the
             // M-token blocks are twice as many and half as long (same per-row arithmetic)
@@ -2423,8 +2428,8 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
             static const int srb = getenv("DSOCR_SHARED_RB") ? atoi(getenv("DSOCR_SHARED_RB")) : 1;
             const int ns = srb == 1 ? (a.Is + 3) / 4 : units_s;
 #define DSOCR_SH(WTY, MTV) \
-    if (srb == 1) hipLaunchKernelGGL((moe_gateup_shared_kernel<WTY, MTV, 1>), dim3(ns), dim3(256), lds, s, sh, 0); \
-    else hipLaunchKernelGGL((moe_gateup_shared_kernel<WTY, MTV, 2>), dim3(ns), dim3(256), lds, s, sh, 0);
+    if (srb == 1) DSOCR_LAUNCH((moe_gateup_shared_kernel<WTY, MTV, 1>), dim3(ns), dim3(256), lds, s, sh, 0); \
+    else DSOCR_LAUNCH((moe_gateup_shared_kernel<WTY, MTV, 2>), dim3(ns), dim3(256), lds, s, sh, 0);
             if (a.wdtype == WDT_BF16) {
                 if (mt == 4) { DSOCR_SH(bf16_t, 4) } else { DSOCR_SH(bf16_t, 8) }
             } else {
@@ -2437,7 +2442,7 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
     if (a.slot_mode && a.K <= 64 * 3 * 8 && a.T <= 8) {
         const int mt = a.T == 1 ? 1 : (a.T <= 2 ? 2 : (a.T <= 4 ? 4 : 8));
         const size_t lds = stage_bytes(mt, a.K);
-#define DSOCR_SLOT(WTY, MTV) hipLaunchKernelGGL((moe_gateup_slot_kernel<WTY, MTV>), grid, dim3(256), lds, s, a)
+#define DSOCR_SLOT(WTY, MTV) DSOCR_LAUNCH((moe_gateup_slot_kernel<WTY, MTV>), grid, dim3(256), lds, s, a)
         if (a.wdtype == WDT_BF16) {
             if (mt == 1) DSOCR_SLOT(bf16_t, 1); else if (mt == 2) DSOCR_SLOT(bf16_t, 2);
             else if (mt == 4) DSOCR_SLOT(bf16_t, 4); else DSOCR_SLOT(bf16_t, 8);
@@ -2452,13 +2457,13 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
     const size_t lds = stage_bytes(mt, a.K);
     if (lds > STAGE_LDS_MAX) throw std::runtime_error("EINVAL: moe_gateup2 hidden size too large for LDS staging");
     if (a.wdtype == WDT_BF16) {
-        if (mt == 1) hipLaunchKernelGGL((moe_gateup2_kernel<bf16_t, 1>), grid, dim3(256), lds, s, a);
-        else if (mt == 4) hipLaunchKernelGGL((moe_gateup2_kernel<bf16_t, 4>), grid, dim3(256), lds, s, a);
-        else hipLaunchKernelGGL((moe_gateup2_kernel<bf16_t, 8>), grid, dim3(256), lds, s, a);
+        if (mt == 1) DSOCR_LAUNCH((moe_gateup2_kernel<bf16_t, 1>), grid, dim3(256), lds, s, a);
+        else if (mt == 4) DSOCR_LAUNCH((moe_gateup2_kernel<bf16_t, 4>), grid, dim3(256), lds, s, a);
+        else DSOCR_LAUNCH((moe_gateup2_kernel<bf16_t, 8>), grid, dim3(256), lds, s, a);
     } else {
-        if (mt == 1) hipLaunchKernelGGL((moe_gateup2_kernel<f16_t, 1>), grid, dim3(256), lds, s, a);
-        else if (mt == 4) hipLaunchKernelGGL((moe_gateup2_kernel<f16_t, 4>), grid, dim3(256), lds, s, a);
-        else hipLaunchKernelGGL((moe_gateup2_kernel<f16_t, 8>), grid, dim3(256), lds, s, a);
+        if (mt == 1) DSOCR_LAUNCH((moe_gateup2_kernel<f16_t, 1>), grid, dim3(256), lds, s, a);
+        else if (mt == 4) DSOCR_LAUNCH((moe_gateup2_kernel<f16_t, 4>), grid, dim3(256), lds, s, a);
+        else DSOCR_LAUNCH((moe_gateup2_kernel<f16_t, 8>), grid, dim3(256), lds, s, a);
     }
 }
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
@@ -2468,7 +2473,7 @@ void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
     if (a.slot_mode && !a.apos && (a.topk == 6 || a.topk == 3) && a.I <= 1024 && (!a.sWd || a.Is <= 2048) &&
         n4 <= 256L * DN_HREG) {
         const size_t lds = (size_t)256 * DN_HREG * 16;
-#define DSOCR_DSLOT(WTY, KTV) hipLaunchKernelGGL((moe_down_slot_kernel<WTY, KTV>), grid, dim3(256), lds, s, a)
+#define DSOCR_DSLOT(WTY, KTV) DSOCR_LAUNCH((moe_down_slot_kernel<WTY, KTV>), grid, dim3(256), lds, s, a)
         if (a.wdtype == WDT_BF16) { if (a.topk == 6) DSOCR_DSLOT(bf16_t, 6); else DSOCR_DSLOT(bf16_t, 3); }
         else { if (a.topk == 6) DSOCR_DSLOT(f16_t, 6); else DSOCR_DSLOT(f16_t, 3); }
 #undef DSOCR_DSLOT
@@ -2478,11 +2483,11 @@ void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
     const bool stage = f4 <= 256L * DN_HREG && f4 * 16 <= (long)STAGE_LDS_MAX;
     const size_t lds = stage ? (size_t)f4 * 16 : 0;
     if (a.wdtype == WDT_BF16) {
-        if (stage) hipLaunchKernelGGL((moe_down2_kernel<bf16_t, true>), grid, dim3(256), lds, s, a);
-        else hipLaunchKernelGGL((moe_down2_kernel<bf16_t, false>), grid, dim3(256), 0, s, a);
+        if (stage) DSOCR_LAUNCH((moe_down2_kernel<bf16_t, true>), grid, dim3(256), lds, s, a);
+        else DSOCR_LAUNCH((moe_down2_kernel<bf16_t, false>), grid, dim3(256), 0, s, a);
     } else {
-        if (stage) hipLaunchKernelGGL((moe_down2_kernel<f16_t, true>), grid, dim3(256), lds, s, a);
-        else hipLaunchKernelGGL((moe_down2_kernel<f16_t, false>), grid, dim3(256), 0, s, a);
+        if (stage) DSOCR_LAUNCH((moe_down2_kernel<f16_t, true>), grid, dim3(256), lds, s, a);
+        else DSOCR_LAUNCH((moe_down2_kernel<f16_t, false>), grid, dim3(256), 0, s, a);
     }
 }
 
@@ -2719,16 +2724,16 @@ void launch_moe_gateup_grp(const MoeDec2Args& a, hipStream_t s) {
     const int slots = std::min(a.E, a.T * a.topk);
     const size_t lds = sizeof(float) * 8 * (size_t)a.K;
     dim3 grid(units_s + slots * units_r);
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_gateup_grp_kernel<bf16_t, RB>), grid, dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((moe_gateup_grp_kernel<f16_t, RB>), grid, dim3(256), lds, s, a);
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_grp_kernel<bf16_t, RB>), grid, dim3(256), lds, s, a);
+    else DSOCR_LAUNCH((moe_gateup_grp_kernel<f16_t, RB>), grid, dim3(256), lds, s, a);
 }
 
 void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s) {
     if (!moe_grp_ok(a)) throw std::runtime_error("EINVAL: grouped decode down outside its range");
     constexpr int RPB = 2, U = 8;
     dim3 grid((a.Hout + RPB - 1) / RPB);
-    if (a.wdtype == WDT_BF16) hipLaunchKernelGGL((moe_down_grp_kernel<bf16_t, RPB, U>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((moe_down_grp_kernel<f16_t, RPB, U>), grid, dim3(256), 0, s, a);
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_down_grp_kernel<bf16_t, RPB, U>), grid, dim3(256), 0, s, a);
+    else DSOCR_LAUNCH((moe_down_grp_kernel<f16_t, RPB, U>), grid, dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ decode MoE layer dispatch
@@ -3267,13 +3272,13 @@ void launch_dec_sample(const DecSampleArgs& a0, hipStream_t s) {
     if (screen) {
         if (a.K % 8 || a.K > 1536) throw std::runtime_error("EINVAL: screened selection needs K % 8 == 0, K <= 1536");
         const size_t lds = sizeof(float) * a.K + sizeof(int) * SP_LIST;
-        hipLaunchKernelGGL((dec_screen_final_kernel<1024>), dim3(a.B), dim3(1024), lds, s, a);
+        DSOCR_LAUNCH((dec_screen_final_kernel<1024>), dim3(a.B), dim3(1024), lds, s, a);
         return;
     }
     if (a.do_sample) launch_dec_stoch_select(a, s);  // sampling.hip: the chosen id in selection slot 0
-    else if (a.ctx_cap <= 16384) hipLaunchKernelGGL((dec_argmax_partial_kernel<true>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), sizeof(int) * a.ctx_cap, s, a);
-    else hipLaunchKernelGGL((dec_argmax_partial_kernel<false>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), 0, s, a);
-    hipLaunchKernelGGL((dec_sample_final_kernel<SP_BLOCK>), dim3(a.B), dim3(SP_BLOCK), 0, s, a);
+    else if (a.ctx_cap <= 16384) DSOCR_LAUNCH((dec_argmax_partial_kernel<true>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), sizeof(int) * a.ctx_cap, s, a);
+    else DSOCR_LAUNCH((dec_argmax_partial_kernel<false>), dim3(a.red_blocks, a.B), dim3(SP_BLOCK), 0, s, a);
+    DSOCR_LAUNCH((dec_sample_final_kernel<SP_BLOCK>), dim3(a.B), dim3(SP_BLOCK), 0, s, a);
 }
 
 }  // namespace dsocr

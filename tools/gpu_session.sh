@@ -19,6 +19,9 @@ for step in "$@"; do
     gprof8) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8 -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8.log 2>&1 ;;
     dots) run 900 python -u -m pytest tests/test_dots.py -q -m gpu -rf -p no:cacheprovider --timeout 600 --timeout-method thread -s > gpurun_out/dots.log 2>&1 ;;
     benchdots) run 900 python bench.py --workload dots2048 --steps 2 --warmup 1 > gpurun_out/benchdots.log 2>&1 ;;
+    prof1) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o b1 --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof1.log 2>&1 ;;
+    prof8) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o b8 --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof8.log 2>&1 ;;
+    profdots) run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profdots -o dots --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 1 > gpurun_out/profdots.log 2>&1 ;;
     gpu_all) run 1100 python -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
