@@ -1081,7 +1081,8 @@ void Engine::decode_step(int B, int Lmax) {
             DecGemvArgs g;
             g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
             g.y = QKV; g.ldy = QKVN;
-            if (fuse_norm) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
+            // the input RMSNorm rides in the projection (B <= 2: block-staged; 3..8: dec_gemv_lds)
+            if (fuse_norm || B <= 8) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
             else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
             launch_dec_gemv(g, st);
             launch_dec_attn(da, st);

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
     }
     // REL: the block's 128 query rows of the rel-pos table staged once into LDS (row pitch R + 1:
     // the lanes of a wave read 32 different rows at one column without bank conflicts)
-    extern __shared__ float rbs[];
+    extern __shared__ __attribute__((aligned(16))) float rbs[];
     const int R = a.rel_h + a.rel_w, RP = R + 1;
     const float* rb = nullptr;
     if (REL) {
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void sam_relbias_kernel(const float* q, long q
 template <int HD>
 __global__ __launch_bounds__(256) void sam_relbias2_kernel(const float* q, long q_rs, int n_seq, int gh, int gw,
                                                            int heads, const float* Rh, const float* Rw, float* out) {
-    extern __shared__ float tabs[];
+    extern __shared__ __attribute__((aligned(16))) float tabs[];
     constexpr int P = HD + 1;
     const int nh = 2 * gh - 1, nw = 2 * gw - 1;
     float* th = tabs;

@@ -191,7 +191,7 @@ constexpr size_t STAGE_LDS_MAX = 64 * 1024;
 // stream overlaps the norm prologue; K <= 64*U*8 is a single batch.
 template <typename WT, int MT, int RB, int U>
 __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = (blockIdx.x * 4 + wave) * RB;
     const bool active = n0 < a.N;
@@ -335,6 +335,102 @@ __global__ __launch_bounds__(256) void dec_gemv_direct_kernel(DecGemvArgs a) {
         }
 }
 
+// Several tokens (M = 3..8): blocks of 4 waves, RB weight rows per wave (issued first), the M
+// activation rows staged once per block in LDS — wave w stages rows w and w + 4 in the GEMV chunk
+// layout (lane: chunks lane, lane+64, lane+128), RMS-normalising them when NORM (its squares summed
+// u-major then j, one wave sum, x / den * w: dec_route_grp's form), so the standalone RMSNorm
+// launch disappears.  Per-row arithmetic that of dec_gemv (chunk u-major, then j; wave sum; + bias,
+// act, y); rows past M are clamped to row M-1 and discarded, so the MT x RB FMA chains interleave.
+template <typename WT, int MT, int RB, bool NORM>
+__global__ __launch_bounds__(256) void dec_gemv_lds_kernel(DecGemvArgs a) {
+    constexpr int U = 3;
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // [MT][K]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = (blockIdx.x * 4 + wave) * RB;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    const int chunks = a.K >> 3;
+    uint4 wq[U][RB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int cc = min(u * 64 + lane, chunks - 1);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) wq[u][r] = ldg_nt16(W + (long)min(n0 + r, a.N - 1) * a.ldw + (cc << 3));
+    }
+#pragma unroll
+    for (int h = 0; h < (MT + 3) / 4; ++h) {
+        const int m = wave + 4 * h;
+        if (m < a.M) {
+            float xv[U][8], nw[U][8];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int cc = min(u * 64 + lane, chunks - 1);
+                ld_x8(a.x + (long)m * a.ldx + (cc << 3), xv[u]);
+                if (NORM) ld_x8(a.norm_w + (cc << 3), nw[u]);
+            }
+            if (NORM) {
+                float q = 0.f;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (u * 64 + lane < chunks)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) q += xv[u][j] * xv[u][j];
+                const float den = sqrtf(wave_sum(q) / (float)a.K + a.eps);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xv[u][j] = (xv[u][j] / den) * nw[u][j];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = u * 64 + lane;
+                if (c < chunks) {
+                    float* d = xs + (long)m * a.K + (c << 3);
+                    *reinterpret_cast<float4*>(d) = make_float4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]);
+                    *reinterpret_cast<float4*>(d + 4) = make_float4(xv[u][4], xv[u][5], xv[u][6], xv[u][7]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (n0 >= a.N) return;
+    float acc[RB][MT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        if (c < chunks) {
+            float w8[RB][8];
+#pragma unroll
+            for (int r = 0; r < RB; ++r) unpack8<WT>(wq[u][r], w8[r]);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                float xv[8];
+                ld_x8(xs + (long)min(m, a.M - 1) * a.K + (c << 3), xv);
+#pragma unroll
+                for (int r = 0; r < RB; ++r)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[r][m] = fmaf(xv[j], w8[r][j], acc[r][m]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            float v = wave_sum(acc[r][m]);
+            const int n = n0 + r;
+            if (lane == 0 && m < a.M && n < a.N) {
+                v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
+                float* yp = a.y + (long)m * a.ldy + n;
+                if (a.accumulate) v = *yp + v;
+                *yp = v;
+            }
+        }
+}
+
 // Large-N variant (lm_head: 129280 rows): a fixed grid of waves walks the row groups with a
 // two-deep register pipeline (the loads of group i+1 are in flight while group i is
 // reduced), so the per-block x staging / norm prologue is paid once per ~8 row groups.
@@ -398,7 +494,7 @@ __device__ __forceinline__ void gemv_finish(const uint4 (&q)[U][RB], const float
 
 template <typename WT, int MT, int RB>
 __global__ __launch_bounds__(256) void dec_gemv_stream_kernel(DecGemvArgs a) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int U = 3;  // K <= 1536: one batch per row
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const WT* W = reinterpret_cast<const WT*>(a.W);
@@ -425,7 +521,24 @@ __global__ __launch_bounds__(256) void dec_gemv_stream_kernel(DecGemvArgs a) {
 template <typename WT, int MT>
 static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     const size_t lds = stage_bytes(a.M, a.K);
-    if constexpr (MT >= 4 && MT <= 8) {  // several tokens, x already normalised: no LDS staging
+    if constexpr (MT >= 4 && MT <= 8) {  // several tokens: no LDS staging
+        // rows per wave of dec_gemv_lds (DSOCR_GEMV_RB: 1 / 2 / 4; 0 = the direct kernel); measured on
+        // MI355X at M = 8, K = 1280 (tools/kbench gemv8): RB 2 for N = 3840 (8.4 us vs 10.6 direct,
+        // 11.1 with the norm fused vs 5 + 10.6), RB 1 for N = 1280 (5.9 vs 6.8)
+        static const int env_rb = getenv("DSOCR_GEMV_RB") ? atoi(getenv("DSOCR_GEMV_RB")) : -1;
+        const int rows_rb = env_rb >= 0 ? env_rb : (a.N >= 2560 ? 2 : 1);
+        if (rows_rb > 0 && a.N <= 16384 && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
+            const size_t xl = sizeof(float) * MT * (size_t)a.K;
+#define DSOCR_GR(R)                                                                                                   \
+    do {                                                                                                              \
+        const dim3 g((a.N + 4 * R - 1) / (4 * R));                                                                    \
+        if (a.norm_w) DSOCR_LAUNCH((dec_gemv_lds_kernel<WT, MT, R, true>), g, dim3(256), xl, s, a);                   \
+        else DSOCR_LAUNCH((dec_gemv_lds_kernel<WT, MT, R, false>), g, dim3(256), xl, s, a);                           \
+    } while (0)
+            if (rows_rb == 1) DSOCR_GR(1); else if (rows_rb == 2) DSOCR_GR(2); else DSOCR_GR(4);
+#undef DSOCR_GR
+            return;
+        }
         static const bool direct = !(getenv("DSOCR_GEMV_DIRECT") && atoi(getenv("DSOCR_GEMV_DIRECT")) == 0);
         if (direct && a.N <= 16384 && !a.norm_w && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
             DSOCR_LAUNCH((dec_gemv_direct_kernel<WT, MT, 1>), dim3((a.N + 3) / 4), dim3(256), 0, s, a);
@@ -495,7 +608,7 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
 // dot-product chunks use, the sum of squares is one wave reduction): no LDS and no block barrier.
 template <typename WT, bool WAVENORM>
 __global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRopeEpi r) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int U = 3, XR = 2;
     if (WAVENORM) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -831,7 +944,7 @@ __device__ __forceinline__ void topk_write(const float* lg, int E, int K, int so
 
 template <typename WT, int MT>
 __global__ __launch_bounds__(256) void dec_router_kernel(DecGemvArgs a, DecRouteEpi r) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     __shared__ int last_s;
     constexpr int U = 3, XR = 2;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -932,6 +1045,253 @@ __global__ __launch_bounds__(256) void dec_router_kernel(DecGemvArgs a, DecRoute
 
 bool dec_router_ok(int T, int E, int K, int topk) {
     return T <= 8 && E <= 256 && K <= 64 * 3 * 8 && topk <= 8 && T * topk <= 64;
+}
+
+// Greedy top-k of one token by one wave, lane e holding expert e's logit (E <= 64): the picks of
+// topk_write (softmax / sigmoid scores, descending, ties -> lower expert id, weights summed in
+// pick order, optional renormalise + scaling), by rank: every lane counts the scores that beat its
+// own from a 64-float LDS copy (16 broadcast reads).  lds: 64 floats private to the wave.  Lane 0
+// writes ids[k], w[k].
+__device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softmax_scoring, int norm_topk, float scaling,
+                                            float* lds, int* ids, float* w) {
+    const int lane = threadIdx.x & 63;
+    float sc;
+    if (softmax_scoring) {
+        const float v = lane < E ? logit : -INFINITY;
+        const float mx = wave_max(v);
+        const float ex = lane < E ? expf(v - mx) : 0.f;
+        const float sum = wave_sum(ex);
+        sc = lane < E ? ex / sum : -INFINITY;
+    } else {
+        sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
+    }
+    lds[lane] = sc;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    int rank = 0;
+#pragma unroll
+    for (int j4 = 0; j4 < 16; ++j4) {
+        const float4 o = reinterpret_cast<const float4*>(lds)[j4];
+        const float oj[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = j4 * 4 + q;
+            rank += (oj[q] > sc || (oj[q] == sc && j < lane)) ? 1 : 0;
+        }
+    }
+    if (lane >= E) rank = 1 << 20;
+    float wsum = 0.f;
+    int pe[8];
+    float pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        pe[k] = 0;
+        pv[k] = 0.f;
+        if (k < K) {
+            const unsigned long long bm = __ballot(rank == k);
+            pe[k] = __builtin_ctzll(bm);
+            pv[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), pe[k]));
+            wsum += pv[k];
+        }
+    }
+    if (lane < K) {
+        float v = pv[0];
+        int e = pe[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (lane == k) { v = pv[k]; e = pe[k]; }
+        if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
+        if (scaling != 1.0f) v = v * scaling;
+        ids[lane] = e;
+        w[lane] = v;
+    }
+}
+
+// Decode router for T <= 8 tokens, E <= 64 experts: RMSNorm + router logits + greedy top-k +
+// expert records in one launch.  Blocks of 8 waves, one expert row per wave.  Wave w normalises
+// token row w in the GEMV chunk layout (lane: chunks lane, lane+64, lane+128; its squares summed
+// u-major then j, one wave sum, x / den * w — dec_gemv_rows' NORM form) into LDS (block 0 also
+// hands the rows to the expert kernels: xn_out), then every wave dots its expert row with the T
+// rows (dec_gemv's per-row arithmetic).  Logits are stored write-through (sc1); the last block to
+// take its ticket reads them back with sc1 loads (MI355X_MICROARCH.md hand-offs, first row), routes
+// token w on wave w (topk_wave64) and wave 0 groups the picks by expert (MOE_GRP_* records).
+template <typename WT>
+__global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRouteEpi r) {
+    constexpr int U = 3, MT = 8;  // K <= 1536, T <= 8
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // [MT][K]
+    __shared__ float lg_s[MT][64];
+    __shared__ float rank_s[MT][64];
+    __shared__ int ids_s[64];
+    __shared__ float w_s[64];
+    __shared__ int last_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#define RG_STAMP(i)                                                      \
+    if (r.stamps && tid == 0 && (blockIdx.x == 0 || (i) >= 5)) r.stamps[i] = __builtin_amdgcn_s_memrealtime();
+    RG_STAMP(0);
+    const int n = blockIdx.x * MT + wave;
+    const int chunks = a.K >> 3;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    uint4 wq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        wq[u] = ldg_nt16(W + (long)min(n, a.N - 1) * a.ldw + (min(u * 64 + lane, chunks - 1) << 3));
+    if (wave < a.M) {
+        float xv[U][8], nw[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int cc = min(u * 64 + lane, chunks - 1);
+            ld_x8(a.x + (long)wave * a.ldx + (cc << 3), xv[u]);
+            if (a.norm_w) ld_x8(a.norm_w + (cc << 3), nw[u]);
+        }
+        if (a.norm_w) {
+            float q = 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (u * 64 + lane < chunks)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) q += xv[u][j] * xv[u][j];
+            const float den = sqrtf(wave_sum(q) / (float)a.K + a.eps);
+            RG_STAMP(1);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[u][j] = (xv[u][j] / den) * nw[u][j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = u * 64 + lane;
+            if (c < chunks) {
+                const float4 lo = make_float4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]);
+                const float4 hi = make_float4(xv[u][4], xv[u][5], xv[u][6], xv[u][7]);
+                float* d = xs + (long)wave * a.K + (c << 3);
+                *reinterpret_cast<float4*>(d) = lo;
+                *reinterpret_cast<float4*>(d + 4) = hi;
+                if (blockIdx.x == 0 && a.xn_out) {
+                    float* g = a.xn_out + (long)wave * a.K + (c << 3);
+                    *reinterpret_cast<float4*>(g) = lo;
+                    *reinterpret_cast<float4*>(g + 4) = hi;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    RG_STAMP(2);
+    float w8[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) unpack8<WT>(wq[u], w8[u]);
+    RG_STAMP(3);
+    // every token row unconditionally (rows past M clamp to row M-1, discarded): the 8 FMA chains and
+    // wave sums are independent and interleave
+    float acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        if (c < chunks) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                float xv[8];
+                ld_x8(xs + (long)min(m, a.M - 1) * a.K + (c << 3), xv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[m] = fmaf(xv[j], w8[u][j], acc[m]);
+            }
+        }
+    }
+    const float bias = a.bias ? a.bias[min(n, a.N - 1)] : 0.f;
+    float mine = 0.f;  // lane m keeps token m's logit
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const float v = wave_sum(acc[m]) + bias;
+        if (lane == m) mine = v;
+    }
+    RG_STAMP(4);
+    if (n < a.N && lane < a.M) __hip_atomic_store(a.y + (long)lane * a.ldy + n, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(r.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (int)gridDim.x - 1;
+        if (last) __hip_atomic_store(r.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
+    RG_STAMP(5);
+    {
+        const int m = tid >> 6, e = tid & 63;  // 512 threads: one logit each
+        lg_s[m][e] = (m < a.M && e < a.N)
+                         ? __hip_atomic_load(a.y + (long)m * a.ldy + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : -INFINITY;
+    }
+    __syncthreads();
+    if (wave < a.M)
+        topk_wave64(lg_s[wave][lane], a.N, r.topk, r.softmax_scoring, r.norm_topk, r.scaling, rank_s[wave],
+                    ids_s + wave * r.topk, w_s + wave * r.topk);
+    __syncthreads();
+    RG_STAMP(6);
+    const int TK = a.M * r.topk;
+    if (tid < TK) {
+        r.ids[tid] = ids_s[tid];
+        r.w[tid] = w_s[tid];
+    }
+    // wave 0, lane e: the tokens that picked expert e (a token's picks are distinct, so at most one
+    // per token), in increasing token order -> record s = number of picked experts below e
+    if (wave == 0 && r.grp) {
+        const int K = r.topk;
+        int pk[MT][8];  // picks, read unconditionally (clamped index) so the LDS reads batch
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pk[t][k] = ids_s[min(t * K + k, 63)];
+        int hit[MT];
+        int cnt = 0;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            hit[t] = -1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k < K && t < a.M && pk[t][k] == lane) hit[t] = t * K + k;
+            cnt += hit[t] >= 0 ? 1 : 0;
+        }
+        float hw[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) hw[t] = w_s[max(hit[t], 0)];
+        const bool act = cnt > 0 && lane < a.N;
+        const unsigned long long bm = __ballot(act);
+        const int sidx = __popcll(bm & ((1ull << lane) - 1ull));
+        if (act) {
+            int* rec = r.grp + MOE_GRP_REC * (1 + sidx);
+            rec[0] = lane;
+            rec[1] = cnt;
+            int q = 0;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                if (hit[t] >= 0) {
+                    rec[2 + q] = hit[t];
+                    rec[10 + q] = __float_as_int(hw[t]);
+                    ++q;
+                }
+        }
+        if (lane == 0) r.grp[0] = __popcll(bm);
+    }
+    RG_STAMP(7);
+#undef RG_STAMP
+}
+
+bool dec_route_grp_ok(int T, int E, int K, int topk) {
+    return T >= 1 && T <= 8 && E >= 1 && E <= 64 && K % 8 == 0 && K <= 64 * 3 * 8 && topk >= 1 && topk <= 8 &&
+           topk <= E && T * topk <= 64;
+}
+
+void launch_dec_route_grp(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s) {
+    if (!dec_route_grp_ok(a.M, a.N, a.K, r.topk) || !r.ids || !r.w || !r.counter || !a.y)
+        throw std::runtime_error("EINVAL: decode router (grouped) outside its range");
+    dim3 grid((a.N + 7) / 8);
+    const size_t lds = sizeof(float) * 8 * (size_t)a.K;
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_route_grp_kernel<bf16_t>), grid, dim3(512), lds, s, a, r);
+    else DSOCR_LAUNCH((dec_route_grp_kernel<f16_t>), grid, dim3(512), lds, s, a, r);
 }
 
 void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s) {
@@ -1352,7 +1712,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
 
 template <int HD, int CH>
 __global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecAttn2Args a) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     attn_body<HD, CH, false, true>(a, smem);
 }
 
@@ -1583,7 +1943,7 @@ __device__ __forceinline__ void topk_select(const float* lg, int E, int K, int s
 // the down kernel reduces every expert of a token into ONE accumulator.
 template <typename WT, int MT>
 __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int RB = 2, U = 3;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
@@ -1888,14 +2248,14 @@ __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int
 
 template <typename WT, int MT>
 __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     gateup_slot_body<WT, MT, false>(a, blockIdx.x, smem);
 }
 // the shared-expert blocks of the slot grid on their own (bid offset past the routed slots), so the
 // routed launch carries single-token registers and LDS (B > 1: MT = T only where it is needed)
 template <typename WT, int MT, int RB>
 __global__ __launch_bounds__(256) void moe_gateup_shared_kernel(MoeDec2Args a, int bid0) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     gateup_slot_body<WT, MT, false, RB>(a, bid0 + blockIdx.x, smem);
 }
 
@@ -1909,7 +2269,7 @@ constexpr int DN_HREG = 8;  // float4 activation registers per thread (topk*I + 
 
 template <typename WT, bool STAGE>
 __global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
-    extern __shared__ float hsm[];
+    extern __shared__ __attribute__((aligned(16))) float hsm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = blockIdx.x * 4 + wave;
     const bool active = j < a.Hout;
@@ -2115,7 +2475,7 @@ __device__ __forceinline__ void down_slot_body(const MoeDec2Args& a, const int b
 
 template <typename WT, int KT>
 __global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
-    extern __shared__ float hsm[];
+    extern __shared__ __attribute__((aligned(16))) float hsm[];
     down_slot_body<WT, KT, false>(a, blockIdx.x, hsm);
 }
 
@@ -2124,7 +2484,7 @@ __global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
 // block ids, so a resident down block only ever waits for blocks dispatched before it.
 template <typename WT, int MT, int KT>
 __global__ __launch_bounds__(256) void moe_fused_slot_kernel(MoeDec2Args a, int NG) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     const int bid = blockIdx.x;
     if (bid < NG) {
         gateup_slot_body<WT, MT, true>(a, bid, smem);
@@ -2503,7 +2863,7 @@ void launch_moe_down2(const MoeDec2Args& a, hipStream_t s) {
 // against each token's row — the per-row arithmetic of the slot kernels (chunk u-major, then j).
 template <typename WT, int RB>
 __global__ __launch_bounds__(256) void moe_gateup_grp_kernel(MoeDec2Args a) {
-    extern __shared__ float smem[];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int U = 3, XR = 2, MT = 8;  // K <= 1536, T <= 8
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
@@ -2748,6 +3108,7 @@ struct MoePlan {
     DecGemvArgs router;
     int mode = 0;  // 0 mix (T = 1), 1 slot (T <= 2), 2 grouped (3..8), 3 sorted (T > 8)
     bool epi = false, mix_dn = false;
+    bool route1 = false;  // grouped mode: dec_route_grp (norm + router + top-k + records, one block)
 };
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
@@ -2779,6 +3140,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     }
     if (p.mode == 2) {
         p.epi = true;
+        p.route1 = env_flag("DSOCR_ROUTE1", true) && a.route_cnt && dec_route_grp_ok(T, E, a.H, K);
     } else if (T <= 8) {
         m.grp = nullptr;
         m.slot_mode = 1; m.slots = TK;
@@ -2821,7 +3183,15 @@ void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const 
 void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     const MoePlan p = moe_plan(a);
     const MoeDec2Args& m = p.m;
-    if (parts & MOE_ROUTE) {
+    if ((parts & MOE_ROUTE) && p.route1) {
+        // norm + logits + top-k + records in one block (the grouped kernels read a.xn)
+        DecGemvArgs g = p.router;
+        g.x = a.x; g.norm_w = a.norm_w; g.xn_out = a.norm_w ? a.xn : nullptr;
+        DecRouteEpi re;
+        re.topk = a.topk; re.softmax_scoring = a.softmax_scoring; re.norm_topk = a.norm_topk;
+        re.scaling = a.scaling; re.ids = a.ids; re.w = a.wts; re.grp = a.grp; re.counter = a.route_cnt;
+        launch_dec_route_grp(g, re, s);
+    } else if (parts & MOE_ROUTE) {
         if (a.T > 2 && a.norm_w) launch_rmsnorm(a.x, a.H, a.xn, a.H, a.T, a.H, a.norm_w, a.eps, s);
         if (p.epi) {
             DecRouteEpi re;
@@ -2879,7 +3249,7 @@ __device__ __forceinline__ void block_argmax(float bv, int bi, float* sv, int* s
 
 template <bool LDSCTX>
 __global__ __launch_bounds__(SP_BLOCK) void dec_argmax_partial_kernel(DecSampleArgs a) {
-    extern __shared__ int ctx_s[];  // the page's context, staged once per block (LDSCTX)
+    extern __shared__ __attribute__((aligned(16))) int ctx_s[];  // the page's context, staged once per block (LDSCTX)
     __shared__ float sv[SP_BLOCK];
     __shared__ int si[SP_BLOCK];
     __shared__ unsigned ban[SP_PER_BLOCK / 32];  // banned-token bitmap of this block's vocab range

@@ -181,6 +181,7 @@ struct DecRouteEpi {
     int* counter = nullptr;                   // zero between launches
     // optional: the picks grouped by expert (MOE_GRP_* layout below) for the grouped decode kernels
     int* grp = nullptr;
+    unsigned long long* stamps = nullptr;  // dev: wall clock at dec_route_grp's phase points (profile only)
 };
 // Expert groups of one decode MoE layer (T <= 8 tokens): grp[0] = number of distinct experts picked,
 // record s (s < grp[0]) at grp + MOE_GRP_REC * (1 + s): [0] expert id, [1] picks (tokens) n,
@@ -193,6 +194,10 @@ inline size_t moe_grp_ints(int E, int T, int topk) {
 }
 void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s);
 bool dec_router_ok(int T, int E, int K, int topk);
+// One-block router for T <= 8 tokens, E <= 64 experts: [RMSNorm of x (rows -> a.xn_out)] + logits
+// (-> a.y when set) + greedy top-k (-> r.ids / r.w) + expert records (-> r.grp when set).
+bool dec_route_grp_ok(int T, int E, int K, int topk);
+void launch_dec_route_grp(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s);
 // RoPE on q / new k + KV-cache append + flash-decoding over 64-key chunks + combine.
 struct DecAttn2Args {
     const float* qkv = nullptr; long ld = 0;           // [B][(heads + 2 kv_heads) * hd]

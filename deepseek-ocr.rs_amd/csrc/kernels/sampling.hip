@@ -180,7 +180,7 @@ __device__ double block_serial_fold(int n, double* tiles, int* stop_s, double* c
 }
 
 __global__ __launch_bounds__(ST_NT) void dec_stoch_select_kernel(DecSampleArgs a) {
-    extern __shared__ uint32_t ban[];  // (V + 31) / 32 words: n-gram ban, later the kept set
+    extern __shared__ __attribute__((aligned(16))) uint32_t ban[];  // (V + 31) / 32 words: n-gram ban, later the kept set
     __shared__ double lds_big[ST_DIG * ST_NT / 2];  // radix histograms, later two fold tiles
     int* hist = reinterpret_cast<int*>(lds_big);
     __shared__ int stop_s;

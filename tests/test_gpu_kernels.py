@@ -55,7 +55,9 @@ def test_gemm(gpu, M, N, K, wdt, act, acc):
 @pytest.mark.parametrize("M,N,K,wdt,norm", [(1, 1280, 1280, 1, True), (1, 129280, 1280, 0, True),
                                             (2, 3840, 1280, 1, True), (3, 3840, 1280, 1, False),
                                             (8, 896, 1792, 1, False), (16, 100, 64, 0, False),
-                                            (21, 513, 128, 0, True), (1, 64, 1280, 1, True), (4, 9000, 256, 0, False)])
+                                            (21, 513, 128, 0, True), (1, 64, 1280, 1, True), (4, 9000, 256, 0, False),
+                                            (8, 3840, 1280, 1, True), (5, 1280, 1280, 1, True), (8, 1280, 1280, 1, False),
+                                            (7, 200, 512, 0, True)])
 def test_gemv(gpu, M, N, K, wdt, norm):
     """Decode linear (dec_gemv) with the optional fused RMSNorm prologue (block.rs:24-29)."""
     rng = np.random.default_rng(N + K + M)

@@ -27,6 +27,7 @@ for step in "$@"; do
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
     bench_full) run 1100 python bench.py > gpurun_out/bench_full.log 2>&1 ;;
     prof) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
+    kbench) run 300 ./tools/kbench $KB_CASES > gpurun_out/kbench.log 2>&1 ;;
     mb) run 120 ./tools/mb_stream > gpurun_out/mb_stream.log 2>&1 ;;
     pmc_fetch) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_fetch.log 2>&1 ;;
     pmc_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_write.log 2>&1 ;;

@@ -1,0 +1,295 @@
+// Dev microbenchmark of the decode kernels in isolation (full DeepSeek-OCR decoder shapes, random
+// weights), timed per launch from the dispatch-packet timestamps (prof_events / DSOCR_LAUNCH, the
+// figures rocprofv3's kernel trace reports) and as back-to-back hipGraph replays.  Weight buffers
+// rotate over more than the 256 MiB Infinity Cache so every launch streams from HBM.
+//   tools/build_kbench.sh && tools/kbench [case ...]
+//   cases: router8 moe1 moe8 gemv1 gemv8 attn1 attn8 lm8 (default: all)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../deepseek-ocr.rs_amd/csrc/kernels/kernels.hpp"
+
+using namespace dsocr;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(2);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+__global__ void fill_f16(uint16_t* p, size_t n, uint32_t seed, float amp) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+        const float u = ((h & 0xffffff) / 16777216.0f - 0.5f) * 2.f * amp;
+        _Float16 f = (_Float16)u;
+        uint16_t b;
+        __builtin_memcpy(&b, &f, 2);
+        p[i] = b;
+    }
+}
+__global__ void fill_f32(float* p, size_t n, uint32_t seed, float amp, float off) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+        p[i] = off + ((h & 0xffffff) / 16777216.0f - 0.5f) * 2.f * amp;
+    }
+}
+
+static uint32_t g_seed = 1;
+static void* dalloc(size_t bytes) {
+    void* p = nullptr;
+    CK(hipMalloc(&p, bytes ? bytes : 16));
+    CK(hipMemset(p, 0, bytes ? bytes : 16));
+    return p;
+}
+static uint16_t* rand_f16(size_t n, float amp = 0.05f) {
+    auto* p = (uint16_t*)dalloc(n * 2);
+    hipLaunchKernelGGL(fill_f16, dim3(1024), dim3(256), 0, 0, p, n, g_seed++ * 7919u, amp);
+    return p;
+}
+static float* rand_f32(size_t n, float amp = 1.f, float off = 0.f) {
+    auto* p = (float*)dalloc(n * 4);
+    hipLaunchKernelGGL(fill_f32, dim3(1024), dim3(256), 0, 0, p, n, g_seed++ * 104729u, amp, off);
+    return p;
+}
+
+struct Timing {
+    double avg_us = 0, replay_us = 0;
+};
+
+static double ms_between(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+}
+
+// per-launch dispatch timestamps (the body's first DSOCR_LAUNCH) + graph replay of n bodies
+static Timing timeit(int n, const std::function<void(int)>& body, hipStream_t s) {
+    Timing t;
+    body(0);
+    CK(hipStreamSynchronize(s));
+    std::vector<hipEvent_t> ev(2 * n);
+    for (auto& e : ev) CK(hipEventCreate(&e));
+    for (int i = 0; i < n; ++i) {
+        prof_events() = ProfEvents{ev[2 * i], ev[2 * i + 1]};
+        body(i);
+        if (prof_events().start) { fprintf(stderr, "body made no instrumented launch\n"); exit(3); }
+    }
+    CK(hipEventSynchronize(ev[2 * n - 1]));
+    double sum = 0;
+    for (int i = 0; i < n; ++i) sum += ms_between(ev[2 * i], ev[2 * i + 1]);
+    t.avg_us = 1000.0 * sum / n;
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < n; ++i) body(i);
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    CK(hipGraphLaunch(ge, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    t.replay_us = 1000.0 * ms_between(e0, e1) / n;
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    return t;
+}
+
+static void report(const char* name, const Timing& t, double bytes) {
+    printf("%-34s avg %8.2f us  (%6.3f TB/s)   replay %8.2f us  (%6.3f TB/s)   bytes %.2f MB\n", name, t.avg_us,
+           bytes / t.avg_us / 1e6, t.replay_us, bytes / t.replay_us / 1e6, bytes / 1e6);
+    fflush(stdout);
+}
+
+// DeepSeek-OCR decoder (deepseek-ocr.json language config)
+constexpr int H = 1280, E = 64, TOPK = 6, I = 896, IS = 1792, HEADS = 10, HD = 128, V = 129280;
+constexpr int NL = 11;  // MoE layers
+
+struct MoeLayerW {
+    uint16_t *router, *gu, *d, *sgu, *sd;
+    float* norm;
+};
+
+static std::vector<MoeLayerW> g_moe;
+static void moe_weights() {
+    if (!g_moe.empty()) return;
+    for (int l = 0; l < NL; ++l) {
+        MoeLayerW w;
+        w.router = rand_f16((size_t)E * H, 0.05f);
+        w.gu = rand_f16((size_t)E * 2 * I * H);
+        w.d = rand_f16((size_t)E * H * I);
+        w.sgu = rand_f16((size_t)2 * IS * H);
+        w.sd = rand_f16((size_t)H * IS);
+        w.norm = rand_f32(H, 0.2f, 1.0f);
+        g_moe.push_back(w);
+    }
+}
+
+static void case_moe(int T, hipStream_t s, bool route_only) {
+    moe_weights();
+    float* x = rand_f32((size_t)T * H);
+    MoeDecodeArgs a;
+    a.T = T; a.H = H; a.E = E; a.topk = TOPK; a.I = I; a.Is = IS;
+    a.x = x; a.eps = 1e-6f; a.out = x;
+    a.router_wdt = WDT_F16; a.wdtype = WDT_F16;
+    a.softmax_scoring = 1; a.norm_topk = 0; a.scaling = 1.f;
+    a.xn = (float*)dalloc((size_t)T * H * 4);
+    a.xn_router = (float*)dalloc((size_t)T * H * 4);
+    a.logits = (float*)dalloc((size_t)T * E * 4);
+    a.ids = (int*)dalloc((size_t)T * TOPK * 4);
+    a.wts = (float*)dalloc((size_t)T * TOPK * 4);
+    a.h = (float*)dalloc((size_t)T * TOPK * I * 4);
+    a.hs = (float*)dalloc((size_t)T * IS * 4);
+    a.grp = (int*)dalloc(moe_grp_ints(E, T, TOPK) * 4);
+    a.route_cnt = (int*)dalloc(64);
+    auto set = [&](int l) {
+        const MoeLayerW& w = g_moe[l % NL];
+        a.norm_w = w.norm; a.router = w.router; a.Wgu = w.gu; a.Wd = w.d; a.sWgu = w.sgu; a.sWd = w.sd;
+    };
+    const int n = 4 * NL;
+    set(0);
+    launch_moe_decode(a, s, MOE_ALL);
+    CK(hipStreamSynchronize(s));
+    std::vector<int> ids(T * TOPK);
+    CK(hipMemcpy(ids.data(), a.ids, ids.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<char> seen(E, 0);
+    int touched = 0;
+    for (int v : ids) if (v >= 0 && v < E && !seen[v]) { seen[v] = 1; ++touched; }
+    const char *gun, *dnn;
+    moe_decode_kernel_names(a, &gun, &dnn);
+    printf("moe T=%d: %d distinct experts, kernels %s / %s\n", T, touched, gun, dnn);
+    char nm[96];
+    snprintf(nm, sizeof nm, "moe%d route", T);
+    report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_ROUTE); }, s), (double)E * H * 2);
+    if (route_only) {
+        // phase clocks of the one-block router (wall clock, 100 MHz)
+        auto* st = (unsigned long long*)dalloc(128);
+        for (int it = 0; it < 3; ++it) {
+            CK(hipMemset(st, 0, 128));
+            set(it);
+            DecGemvArgs g;
+            g.M = T; g.N = E; g.K = H; g.x = x; g.ldx = H; g.W = a.router; g.ldw = H; g.wdtype = WDT_F16;
+            g.y = a.logits; g.ldy = E; g.norm_w = a.norm_w; g.eps = a.eps; g.xn_out = a.xn;
+            DecRouteEpi re;
+            re.topk = TOPK; re.ids = a.ids; re.w = a.wts; re.grp = a.grp; re.stamps = st; re.counter = a.route_cnt;
+            launch_dec_route_grp(g, re, s);
+            CK(hipStreamSynchronize(s));
+            unsigned long long h[16];
+            CK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
+            printf("route stamps (us from block 0 entry):");
+            for (int i = 1; i < 8; ++i) printf(" %d:%.2f", i, ((long long)h[i] - (long long)h[0]) / 100.0);
+            printf("\n");
+        }
+        return;
+    }
+    // gate/up / down rotate layers but keep layer 0's routing state (same expert set per layer)
+    set(0);
+    launch_moe_decode(a, s, MOE_ROUTE);
+    const double gub = ((double)touched * 2 * I + 2.0 * IS) * H * 2;
+    const double dnb = ((double)touched * I + IS) * H * 2;
+    snprintf(nm, sizeof nm, "moe%d gateup", T);
+    report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_GATEUP); }, s), gub);
+    snprintf(nm, sizeof nm, "moe%d down", T);
+    report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_DOWN); }, s), dnb);
+}
+
+static void case_gemv(int M, hipStream_t s) {
+    // q/k/v (3840 x 1280) and o_proj (1280 x 1280), 40 layers' worth (> the Infinity Cache)
+    constexpr int NB = 40;
+    std::vector<uint16_t*> wq(NB), wo(NB);
+    for (int i = 0; i < NB; ++i) { wq[i] = rand_f16((size_t)3 * H * H); wo[i] = rand_f16((size_t)H * H); }
+    float* x = rand_f32((size_t)M * H);
+    float* nw = rand_f32(H, 0.2f, 1.f);
+    float* y = (float*)dalloc((size_t)M * 3 * H * 4);
+    for (int norm = 0; norm < 2; ++norm) {
+        DecGemvArgs g;
+        g.M = M; g.K = H; g.x = x; g.ldx = H; g.wdtype = WDT_F16; g.y = y; g.ldw = H;
+        if (norm) { g.norm_w = nw; g.eps = 1e-6f; }
+        char nm[96];
+        g.N = 3 * H; g.ldy = 3 * H;
+        snprintf(nm, sizeof nm, "gemv M=%d N=3840%s", M, norm ? " +norm" : "");
+        report(nm, timeit(NB, [&](int i) { g.W = wq[i]; launch_dec_gemv(g, s); }, s), 3.0 * H * H * 2);
+        g.N = H; g.ldy = H;
+        snprintf(nm, sizeof nm, "gemv M=%d N=1280%s", M, norm ? " +norm" : "");
+        report(nm, timeit(NB, [&](int i) { g.W = wo[i]; launch_dec_gemv(g, s); }, s), 1.0 * H * H * 2);
+    }
+    for (int i = 0; i < NB; ++i) { (void)hipFree(wq[i]); (void)hipFree(wo[i]); }
+}
+
+static void case_attn(int B, int pos, hipStream_t s) {
+    const int max_len = 1218;
+    constexpr int NLA = 12;
+    const long head_stride = (long)max_len * HD, page_stride = (long)HEADS * head_stride;
+    std::vector<float*> kc(NLA), vc(NLA);
+    for (int l = 0; l < NLA; ++l) { kc[l] = rand_f32((size_t)B * page_stride); vc[l] = rand_f32((size_t)B * page_stride); }
+    float* qkv = rand_f32((size_t)B * 3 * HEADS * HD);
+    std::vector<int> hpos(B, pos);
+    int* kv_pos = (int*)dalloc(B * 4);
+    CK(hipMemcpy(kv_pos, hpos.data(), B * 4, hipMemcpyHostToDevice));
+    float* cs = rand_f32((size_t)max_len * HD, 1.f);
+    float* sn = rand_f32((size_t)max_len * HD, 1.f);
+    float* part = (float*)dalloc(dec_attn_workspace(B, HEADS, HD, max_len) + 64);
+    int* cnt = (int*)dalloc((size_t)B * HEADS * 4);
+    float* o = (float*)dalloc((size_t)B * HEADS * HD * 4);
+    DecAttn2Args a;
+    a.qkv = qkv; a.ld = 3 * HEADS * HD; a.kv_pos = kv_pos; a.B = B; a.heads = HEADS; a.kv_heads = HEADS; a.hd = HD;
+    a.rope_dim = HD; a.max_len = max_len; a.cos = cs; a.sin = sn; a.page_stride = page_stride; a.head_stride = head_stride;
+    a.scale = 1.f / sqrtf((float)HD); a.part = part; a.counters = cnt; a.o = o; a.o_ld = HEADS * HD; a.prerot = B == 1;
+    char nm[96];
+    snprintf(nm, sizeof nm, "attn B=%d L=%d", B, pos + 1);
+    const double bytes = 2.0 * B * (pos + 1) * HEADS * HD * 4;
+    report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
+    for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); }
+}
+
+static void case_lm(int M, hipStream_t s) {
+    constexpr int NB = 2;  // 2 x 331 MB > the Infinity Cache
+    std::vector<uint16_t*> w(NB);
+    for (int i = 0; i < NB; ++i) w[i] = rand_f16((size_t)V * H);
+    float* x = rand_f32((size_t)M * H);
+    float* y = (float*)dalloc((size_t)M * V * 4);
+    DecGemvArgs g;
+    g.M = M; g.N = V; g.K = H; g.x = x; g.ldx = H; g.wdtype = WDT_BF16; g.y = y; g.ldy = V; g.ldw = H;
+    char nm[96];
+    snprintf(nm, sizeof nm, "lm_head exact M=%d", M);
+    report(nm, timeit(8, [&](int i) { g.W = w[i % NB]; launch_dec_gemv(g, s); }, s), (double)V * H * 2);
+    for (int i = 0; i < NB; ++i) (void)hipFree(w[i]);
+}
+
+int main(int argc, char** argv) {
+    std::vector<std::string> cases;
+    for (int i = 1; i < argc; ++i) cases.push_back(argv[i]);
+    if (cases.empty()) cases = {"router8", "moe1", "moe8", "gemv1", "gemv8", "attn1", "attn8", "lm8"};
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (const auto& c : cases) {
+        if (c == "router8") case_moe(8, s, true);
+        else if (c == "moe1") case_moe(1, s, false);
+        else if (c == "moe8") case_moe(8, s, false);
+        else if (c == "gemv1") case_gemv(1, s);
+        else if (c == "gemv8") case_gemv(8, s);
+        else if (c == "attn1") { case_attn(1, 706, s); case_attn(1, 1216, s); }
+        else if (c == "attn8") { case_attn(8, 706, s); case_attn(8, 1216, s); }
+        else if (c == "lm8") case_lm(8, s);
+        else fprintf(stderr, "unknown case %s\n", c.c_str());
+        CK(hipStreamSynchronize(s));
+    }
+    printf("kbench done\n");
+    return 0;
+}
