@@ -511,6 +511,11 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
             a.grp = (int*)alloc(sizeof(int) * dsocr::moe_grp_ints(E, T, topk));
             a.route_cnt = (int*)alloc(sizeof(int) * 16);
             check_hip(hipMemset(a.route_cnt, 0, sizeof(int) * 16), "hipMemset");
+            if (T >= 3 && T <= 8) {
+                a.dn_part = (float*)alloc(sizeof(float) * dsocr::moe_down_mm_part_floats(E, T, topk, I, a.Is, H));
+                a.dn_tick = (int*)alloc(sizeof(int) * (H / 128 + 1));
+                check_hip(hipMemset(a.dn_tick, 0, sizeof(int) * (H / 128 + 1)), "hipMemset");
+            }
             if (T > 8) {
                 a.eoff = (int*)alloc(sizeof(int) * (E + 1)); a.arow = (int*)alloc(sizeof(int) * TK);
                 a.apos = (int*)alloc(sizeof(int) * TK); a.active = (int*)alloc(sizeof(int) * E);
@@ -539,6 +544,7 @@ dsocr_status dsocr_k_moe_kernels(int T, int H, int E, int topk, int I, int Is, i
         if (Is > 0) { a.sWgu = &dummy; a.sWd = &dummy; a.hs = &fd; }
         a.xn = a.xn_router = a.logits = a.wts = a.h = &fd;
         a.ids = a.grp = a.route_cnt = &dummy;
+        if (T >= 3 && T <= 8) { a.dn_part = &fd; a.dn_tick = &dummy; }
         if (T > 8) { a.eoff = a.arow = a.apos = a.active = a.n_active = &dummy; a.aw = &fd; }
         dsocr::moe_decode_kernel_names(a, gateup, down);
     });

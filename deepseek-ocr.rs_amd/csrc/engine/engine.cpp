@@ -1009,6 +1009,13 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     a.h = wsf("s_ehh", (size_t)TK * I);
     a.grp = wsi("s_grp", moe_grp_ints(E, B, K));
     a.route_cnt = wsi("s_route_cnt", 16);
+    if (B >= 3 && B <= 8) {  // matrix-core grouped kernels: fragment-ordered experts, down partials + tickets
+        a.dn_part = wsf("s_dnpart", moe_down_mm_part_floats(E, B, K, I, a.Is, H));
+        a.dn_tick = wsi("s_dntick", (size_t)H / 128 + 1);
+        if (d.e_gu_swz && (!d.has_shared || d.s_gu_swz)) {
+            a.Wgu_swz = d.e_gu_swz; a.Wd_swz = d.e_d_swz; a.sWgu_swz = d.s_gu_swz; a.sWd_swz = d.s_d_swz;
+        }
+    }
     if (B > 8) {
         a.eoff = wsi("s_eoff", E + 1); a.arow = wsi("s_arow", TK); a.apos = wsi("s_apos", TK);
         a.aw = wsf("s_aw", TK); a.active = wsi("s_active", E); a.n_active = wsi("s_nact", 1);
@@ -1122,6 +1129,38 @@ void Engine::reserve_head_ws(int B) {
     wsf("s_lmxn", (size_t)B * L.hidden);
 }
 
+// 3..8 pages: fragment-ordered copies of the lm_head and of every MoE layer's experts for the
+// matrix-core kernels (decode_mm.hip: every wave weight load one contiguous 1 KiB block; lm_head 6.0 vs
+// 4.6 TB/s row-major on MI355X, tools/kbench lm8), made once, outside any capture (HBM: + vocab x hidden
+// + the expert weights again, ~5.3 GB of the 288)
+void Engine::ensure_mm_weights(int B) {
+    if (B < 3 || B > 8 || lm_swz_ || capturing_) return;
+    if (getenv("DSOCR_MM_SWZ") && atoi(getenv("DSOCR_MM_SWZ")) == 0) return;
+    const LangConfig& L = cfg_.lang;
+    DecGemvArgs g;
+    g.M = B; g.N = L.vocab; g.K = L.hidden; g.ldw = L.hidden;
+    if (!dec_mm_ok(g)) return;
+    lm_swz_ = dev_alloc(mm_swizzle_elems(L.vocab, L.hidden) * 2);
+    launch_mm_swizzle(lm_head_.W, L.vocab, L.hidden, lm_swz_, stream_);
+    // the experts of every MoE layer (routed [E * 2I][H], [E * H][I]; shared [2Is][H], [H][Is])
+    const int H = L.hidden, E = L.n_routed, I = L.moe_inter;
+    for (DecLayer& d : layers_) {
+        if (!d.moe || d.e_wdt != WDT_F16 || H % 32 || I % 32) continue;
+        d.e_gu_swz = dev_alloc(mm_swizzle_elems(E * 2 * I, H) * 2);
+        launch_mm_swizzle(d.e_gu, E * 2 * I, H, d.e_gu_swz, stream_);
+        d.e_d_swz = dev_alloc(mm_swizzle_elems(E * H, I) * 2);
+        launch_mm_swizzle(d.e_d, E * H, I, d.e_d_swz, stream_);
+        if (d.has_shared && d.s_gu.wdt == WDT_F16) {
+            const int Is = d.s_d.K;
+            d.s_gu_swz = dev_alloc(mm_swizzle_elems(2 * Is, H) * 2);
+            launch_mm_swizzle(d.s_gu.W, 2 * Is, H, d.s_gu_swz, stream_);
+            d.s_d_swz = dev_alloc(mm_swizzle_elems(H, Is) * 2);
+            launch_mm_swizzle(d.s_d.W, H, Is, d.s_d_swz, stream_);
+        }
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
 // screened selection applies (lmhead.hip): int8 copy present, B <= 2, no repetition penalty
 // (DSOCR_SCREEN=0 forces the exact lm_head; read per generate call)
 bool Engine::screen_applies(int B, float rep_penalty) const {
@@ -1160,8 +1199,10 @@ void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
     DecGemvArgs g;
     g.M = B; g.N = L.vocab; g.K = H; g.W = lm_head_.W; g.ldw = H; g.wdtype = lm_head_.wdt; g.bias = lm_head_.b;
     g.y = const_cast<float*>(sa.logits); g.ldy = L.vocab;
-    if (B <= 2) { g.x = SX; g.ldx = H; g.norm_w = final_norm_; g.eps = L.rms_eps; }
-    else {
+    if (B <= 2 || (lm_swz_ && B <= 8)) {  // final RMSNorm fused (B 3..8: dec_mm on the fragment-ordered copy)
+        g.x = SX; g.ldx = H; g.norm_w = final_norm_; g.eps = L.rms_eps;
+        if (B > 2) g.w_swz = lm_swz_;
+    } else {
         float* SXN = wsf("s_xn", (size_t)B * H);
         launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
         g.x = SXN; g.ldx = H;
@@ -1353,6 +1394,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // arrival tickets of the decode-attention combine: zero here, every launch leaves them zero
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
+    HIP_CHECK(hipMemsetAsync(wsi("s_dntick", (size_t)H / 128 + 1), 0, sizeof(int) * (H / 128 + 1), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
     HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     const int QKVN = layers_[0].qkv.N;
@@ -1469,6 +1511,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         for (int b = 0; b < B; ++b) memcpy(&all[(size_t)b * RNG_WORDS], st.data(), sizeof(uint32_t) * RNG_WORDS);
         sa.rng = reinterpret_cast<uint32_t*>(upload("s_rng", all));
     }
+    ensure_mm_weights(B);
     if (!p.do_sample && !p.trace && screen_applies(B, p.rep_penalty)) {
         // the screened head reads the n-gram ban list each selection kernel leaves for the next step
         sa.ban_ld = ctx_cap + 1;
@@ -1774,13 +1817,17 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         float* LG = wsf("p_logits", (size_t)B * L.vocab);
         const float* SX = wsf("s_x", (size_t)B * H);
         float* SXN = wsf("p_xn", (size_t)B * H);
-        if (B > 2) launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
+        ensure_mm_weights(B);
+        const bool fused = B <= 2 || (lm_swz_ && B <= 8);
+        if (!fused) launch_rmsnorm(SX, H, SXN, H, B, H, final_norm_, L.rms_eps, st);
         timed(prof.lm_head, iters, [&](int) {
             DecGemvArgs g;
             g.M = B; g.N = L.vocab; g.K = H; g.W = lm_head_.W; g.ldw = H; g.wdtype = lm_head_.wdt; g.bias = lm_head_.b;
             g.y = LG; g.ldy = L.vocab;
-            if (B <= 2) { g.x = SX; g.ldx = H; g.norm_w = final_norm_; g.eps = L.rms_eps; }
-            else { g.x = SXN; g.ldx = H; }
+            if (fused) {
+                g.x = SX; g.ldx = H; g.norm_w = final_norm_; g.eps = L.rms_eps;
+                if (B > 2) g.w_swz = lm_swz_;
+            } else { g.x = SXN; g.ldx = H; }
             launch_dec_gemv(g, st);
         });
         prof.lm_head.bytes = (double)L.vocab * H * 2.0 + (double)B * (L.vocab + H) * 4.0;

@@ -79,6 +79,8 @@ struct DecLayer {
     int e_wdt = WDT_F16;
     bool has_shared = false;
     Lin s_gu, s_d;                // [2Is][H], [H][Is]
+    // fragment-ordered copies for the 3..8-page matrix-core kernels (Engine::ensure_mm_weights)
+    void* e_gu_swz = nullptr; void* e_d_swz = nullptr; void* s_gu_swz = nullptr; void* s_d_swz = nullptr;
 };
 
 struct PagePixels {
@@ -218,6 +220,8 @@ class Engine {
     std::vector<DecLayer> layers_;
     float* final_norm_ = nullptr;
     Lin lm_head_;
+    void* lm_swz_ = nullptr;         // lm_head in dec_mm fragment order (3..8 pages; made on first use)
+    void ensure_mm_weights(int B);
     void* lmq_ = nullptr;            // int8 [vocab][hidden] screening copy of lm_head
     float* lmq_scale_ = nullptr;     // per-row scale
     float* lmq_bound_ = nullptr;     // per-row error-bound factor (times ||x||)

@@ -522,6 +522,12 @@ template <typename WT, int MT>
 static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     const size_t lds = stage_bytes(a.M, a.K);
     if constexpr (MT >= 4 && MT <= 8) {  // several tokens: no LDS staging
+        // matrix-core form (decode_mm.hip): weights straight into MFMA, activations as 16-bit planes
+        static const bool use_mm = !(getenv("DSOCR_GEMV_MM") && atoi(getenv("DSOCR_GEMV_MM")) == 0);
+        if (use_mm && dec_mm_ok(a)) {
+            launch_dec_mm(a, s);
+            return;
+        }
         // rows per wave of dec_gemv_lds (DSOCR_GEMV_RB: 1 / 2 / 4; 0 = the direct kernel); measured on
         // MI355X at M = 8, K = 1280 (tools/kbench gemv8): RB 2 for N = 3840 (8.4 us vs 10.6 direct,
         // 11.1 with the norm fused vs 5 + 10.6), RB 1 for N = 1280 (5.9 vs 6.8)
@@ -3109,6 +3115,8 @@ struct MoePlan {
     int mode = 0;  // 0 mix (T = 1), 1 slot (T <= 2), 2 grouped (3..8), 3 sorted (T > 8)
     bool epi = false, mix_dn = false;
     bool route1 = false;  // grouped mode: dec_route_grp (norm + router + top-k + records, one block)
+    bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
+    bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
 };
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
@@ -3129,6 +3137,8 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     m.T = T; m.K = a.H; m.Hout = a.H; m.x = mx; m.norm_w = mnorm; m.eps = a.eps; m.out = a.out;
     m.topk = K; m.E = E; m.I = a.I; m.Wgu = a.Wgu; m.Wd = a.Wd; m.wdtype = a.wdtype; m.h = a.h; m.ids = a.ids;
     if (a.sWgu && a.sWd && a.Is > 0) { m.Is = a.Is; m.sWgu = a.sWgu; m.sWd = a.sWd; m.hs = a.hs; }
+    m.Wgu_swz = a.Wgu_swz; m.sWgu_swz = a.sWgu_swz; m.Wd_swz = a.Wd_swz; m.sWd_swz = a.sWd_swz;
+    m.dn_part = a.dn_part; m.dn_tick = a.dn_tick;
     DecGemvArgs& gr = p.router;
     gr.M = T; gr.N = E; gr.K = a.H; gr.x = mx; gr.ldx = a.H; gr.W = a.router; gr.ldw = a.H; gr.wdtype = a.router_wdt;
     gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps;
@@ -3141,6 +3151,8 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     if (p.mode == 2) {
         p.epi = true;
         p.route1 = env_flag("DSOCR_ROUTE1", true) && a.route_cnt && dec_route_grp_ok(T, E, a.H, K);
+        p.gu_mm = env_flag("DSOCR_MOE_MM", true) && moe_gateup_mm_ok(m);
+        p.dn_mm = env_flag("DSOCR_MOE_MM", true) && env_flag("DSOCR_DN_MM", true) && moe_down_mm_ok(m);
     } else if (T <= 8) {
         m.grp = nullptr;
         m.slot_mode = 1; m.slots = TK;
@@ -3173,8 +3185,8 @@ void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const 
     const char* dn = "moe_down2_kernel";
     if (p.mode == 0) gu = "moe_gateup_mix_kernel";
     else if (p.mode == 1) gu = (a.T > 2 && a.Is) ? "moe_gateup_slot_kernel+moe_gateup_shared_kernel" : "moe_gateup_slot_kernel";
-    else if (p.mode == 2) gu = "moe_gateup_grp_kernel";
-    if (p.mode == 2) dn = "moe_down_grp_kernel";
+    else if (p.mode == 2) gu = p.gu_mm ? "moe_gateup_mm_kernel" : "moe_gateup_grp_kernel";
+    if (p.mode == 2) dn = p.dn_mm ? "moe_down_mm_kernel" : "moe_down_grp_kernel";
     else if (p.mode <= 1) dn = p.mix_dn ? "moe_down_mix_kernel" : "moe_down_slot_kernel";
     if (gateup) *gateup = gu;
     if (down) *down = dn;
@@ -3211,12 +3223,16 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
         }
     }
     if (parts & MOE_GATEUP) {
+        if (const char* sp = getenv("DSOCR_MOE_STAMPS"))  // dev: per-block phase clocks (profile only)
+            const_cast<MoeDec2Args&>(m).stamps = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(sp, nullptr, 10));
         if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
+        else if (p.mode == 2 && p.gu_mm) launch_moe_gateup_mm(m, s);
         else if (p.mode == 2) launch_moe_gateup_grp(m, s);
         else launch_moe_gateup2(m, s);
     }
     if (parts & MOE_DOWN) {
-        if (p.mode == 2) launch_moe_down_grp(m, s);
+        if (p.mode == 2 && p.dn_mm) launch_moe_down_mm(m, s);
+        else if (p.mode == 2) launch_moe_down_grp(m, s);
         else if (p.mix_dn) launch_moe_down_mix(m, s);
         else launch_moe_down2(m, s);
     }

@@ -1,0 +1,718 @@
+// Multi-token decode projections on the matrix cores (3..8 pages decoding together: BASELINE
+// configs[2], 8 pages per GPU).  The reference computes every projection as an f32 matmul of f32
+// activations with the model's 16-bit weights widened to f32 (transformer/block.rs attention / MLP
+// linears at seq_len 1 per page); here the 16-bit weight rows go straight from HBM into
+// v_mfma_f32_16x16x32_{f16,bf16} as the A operand (16 output rows x 32 k per step), and the f32
+// activation rows become the B operand as three 16-bit planes x = p0 + p1 + p2:
+//   * bf16 weights: three bf16 planes represent every f32 exactly (8 + 8 + 8 significand bits);
+//   * f16 weights: each token row is first scaled by a power of two 2^s that puts its largest
+//     magnitude in [2^14, 2^15) (exact), then split into three f16 planes; the split leaves an
+//     absolute error below 2^-25 in scaled units (f16's subnormal half-step), i.e. 2^-39 of the row
+//     maximum — far below the f32 rounding of the dot product itself — and the result is scaled back
+//     by 2^-s (exact).
+// Every product is then exact in the f32 accumulator (16-bit x 16-bit significands) and only the
+// summation order differs from an f32 matmul.  The VALU does no per-weight work at all (the decode
+// GEMV spent a convert and M FMAs per weight plus one wave reduction per output), so the launch is
+// bound by the weight stream.
+//
+// Fragment maps (cdna_hip_programming.md §3, gfx950 16x16x32): lane l holds A[row l&15][k 8(l>>4)+j]
+// and B[k 8(l>>4)+j][col l&15], j < 8; C[row 4(l>>4)+i][col l&15], i < 4.  Columns are tokens
+// (8 staged; lanes of columns 8..15 read the rows of columns 0..7 and their results are dropped).
+#include <cstdlib>
+#include <stdexcept>
+
+#include "dev_common.hpp"
+#include "kernels.hpp"
+
+namespace dsocr {
+
+typedef _Float16 mm_f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 mm_b16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int MM_MT = 8;  // token rows staged (M <= 8)
+
+template <typename WT>
+struct MmT;
+template <>
+struct MmT<f16_t> {
+    typedef mm_f16x8 frag;
+    static constexpr bool scaled = true;
+    __device__ static uint16_t to_bits(float v, float& back) {
+        const _Float16 h = (_Float16)v;
+        back = (float)h;
+        uint16_t b;
+        __builtin_memcpy(&b, &h, 2);
+        return b;
+    }
+    __device__ static f32x4 mfma(const frag& a, const frag& b, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+};
+template <>
+struct MmT<bf16_t> {
+    typedef mm_b16x8 frag;
+    static constexpr bool scaled = false;
+    __device__ static uint16_t to_bits(float v, float& back) {
+        const __bf16 h = (__bf16)v;
+        back = (float)h;
+        uint16_t b;
+        __builtin_memcpy(&b, &h, 2);
+        return b;
+    }
+    __device__ static f32x4 mfma(const frag& a, const frag& b, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+
+// LDS row pitch of a plane row (16-bit elements): K + 16 puts consecutive rows 8 banks apart, which
+// makes the B-operand ds_read_b128 (rows l&7, k groups l>>4) conflict-free.
+__host__ __device__ inline int mm_pitch(int K) { return K + 16; }
+
+// Wave-level staging of token row m of x (f32, K <= 1536) as 3 planes in LDS (xp[(p * MT + m) * KP +
+// k]) with its inverse scale scl[m], in two halves so that the row's loads can be issued BEFORE the
+// weight stream (vmcnt retires in issue order: loads issued after a weight batch wait for it).
+// NORM: RMS-normalised first — the lane's chunks (lane, lane+64, lane+128; 8 floats each) squared and
+// summed u-major then j, one wave sum, x * (1 / den) * w.
+template <int U>
+struct MmRowU {
+    float v[U][8];
+    float w[U][8];
+};
+typedef MmRowU<3> MmRow;  // K <= 1536
+
+template <bool NORM, int U = 3>
+__device__ __forceinline__ void mm_row_load(MmRowU<U>& r, const float* xr, int K, const float* nw) {
+    const int lane = threadIdx.x & 63;
+    const int chunks = K >> 3;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int cc = min(u * 64 + lane, chunks - 1);
+        const float4 lo = *reinterpret_cast<const float4*>(xr + (cc << 3));
+        const float4 hi = *reinterpret_cast<const float4*>(xr + (cc << 3) + 4);
+        r.v[u][0] = lo.x; r.v[u][1] = lo.y; r.v[u][2] = lo.z; r.v[u][3] = lo.w;
+        r.v[u][4] = hi.x; r.v[u][5] = hi.y; r.v[u][6] = hi.z; r.v[u][7] = hi.w;
+        if (NORM) {
+            const float4 wl = *reinterpret_cast<const float4*>(nw + (cc << 3));
+            const float4 wh = *reinterpret_cast<const float4*>(nw + (cc << 3) + 4);
+            r.w[u][0] = wl.x; r.w[u][1] = wl.y; r.w[u][2] = wl.z; r.w[u][3] = wl.w;
+            r.w[u][4] = wh.x; r.w[u][5] = wh.y; r.w[u][6] = wh.z; r.w[u][7] = wh.w;
+        }
+    }
+}
+
+template <typename WT, bool NORM, int U = 3>
+__device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uint16_t* xp, int KP, float* scl, int m) {
+    const int lane = threadIdx.x & 63;
+    const int chunks = K >> 3;
+    if (NORM) {
+        float q = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u * 64 + lane < chunks)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) q += r.v[u][j] * r.v[u][j];
+        // one division per row: x * (1 / den) is within an ulp of the reference's x / den (the planes
+        // below are exact, the GEMM sums in its own order: this path is tolerance-pinned, not bitwise)
+        const float inv = 1.0f / sqrtf(wave_sum(q) / (float)K + eps);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r.v[u][j] = (r.v[u][j] * inv) * r.w[u][j];
+    }
+    float s_inv = 1.f;
+    if (MmT<WT>::scaled) {
+        float mx = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u * 64 + lane < chunks)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(r.v[u][j]));
+        mx = wave_max(mx);
+        int s = 0;
+        if (mx > 0.f) {
+            int e;
+            (void)frexpf(mx, &e);  // mx < 2^e
+            s = 15 - e;            // mx * 2^s < 2^15
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r.v[u][j] = ldexpf(r.v[u][j], s);
+        s_inv = ldexpf(1.f, -s);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        if (c < chunks) {
+            uint16_t pb[3][8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float b0, b1, b2;
+                pb[0][j] = MmT<WT>::to_bits(r.v[u][j], b0);
+                const float r1 = r.v[u][j] - b0;
+                pb[1][j] = MmT<WT>::to_bits(r1, b1);
+                const float r2 = r1 - b1;
+                pb[2][j] = MmT<WT>::to_bits(r2, b2);
+            }
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                uint4 q;
+                q.x = pb[p][0] | ((uint32_t)pb[p][1] << 16);
+                q.y = pb[p][2] | ((uint32_t)pb[p][3] << 16);
+                q.z = pb[p][4] | ((uint32_t)pb[p][5] << 16);
+                q.w = pb[p][6] | ((uint32_t)pb[p][7] << 16);
+                *reinterpret_cast<uint4*>(xp + ((long)(p * MM_MT + m) * KP + (c << 3))) = q;
+            }
+        }
+    }
+    if (lane == 0) scl[m] = s_inv;
+}
+
+// Y[m][n] (+)= act((norm?(X) . W^T)[m][n] * 1 + bias[n]) for m < M <= 8.  Block: WR x WK waves —
+// WR 16-row tiles side by side, each tile's K split in WK contiguous ranges whose partial tiles meet
+// once in LDS (summed in range order).  The block stages the planes once, then walks row tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ... (a persistent grid for the lm_head).  A fragments are
+// 16-byte nontemporal loads straight into registers, PF k-steps per batch, double-buffered.
+template <typename WT, int WR, int WK, int PF, int Q, bool NORM, bool SWZ>
+__global__ __launch_bounds__(64 * WR * WK) void dec_mm_kernel(DecGemvArgs a) {
+    typedef typename MmT<WT>::frag frag;
+    static_assert(PF % Q == 0, "a batch holds whole k groups");
+    // k order inside each group of Q steps: step Q T + s gives lane group g the 8 k's
+    // 32 Q T + 8 Q g + 8 s + j, so a lane's Q fragments of a group are 16 Q contiguous bytes of its row
+    auto koff = [](int i) { return 32 * Q * (i / Q) + 8 * (i % Q); };
+    extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
+    __shared__ float scl[MM_MT];
+    __shared__ f32x4 red[WK > 1 ? WK - 1 : 1][WR][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int KP = mm_pitch(a.K);
+    constexpr int NW = WR * WK;
+    const int wr = wave % WR, wk = wave / WR;
+    const int steps = a.K >> 5, per = steps / WK, t0 = wk * per;
+    const int nch = per / PF;  // host guarantees per % PF == 0 (and an even nch for several tiles per block)
+    const int ntiles = (a.N + 15) >> 4;
+    const int col = lane & 15, g = lane >> 4;
+    const WT* W = reinterpret_cast<const WT*>(a.W);
+    auto rowp = [&](int bt) {
+        if (SWZ) {  // fragment-ordered copy: [tile][step][lane][8], one 1 KiB block per wave load
+            const int tile = min(bt * WR + wr, ntiles - 1);
+            return W + ((long)tile * steps + t0) * 512 + lane * 8;
+        }
+        const int n = min((bt * WR + wr) * 16 + col, a.N - 1);
+        return W + (long)n * a.ldw + 8 * Q * g + 32 * t0;
+    };
+    frag fa[PF], fb[PF];
+    auto load = [&](frag(&f)[PF], const WT* wrow, int c) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint4 q = ldg_nt16(SWZ ? wrow + (long)(c * PF + i) * 512 : wrow + 32 * c * PF + koff(i));
+            __builtin_memcpy(&f[i], &q, 16);
+        }
+    };
+    // this wave's activation rows are loaded first, then the first weight batch goes out, then the rows
+    // are normalised / split into the LDS planes while the weights are in flight
+    static_assert(NW >= 4, "staging: at most two rows per wave");
+    MmRow r0, r1;
+    const int m0 = wave, m1 = wave + NW;
+    if (m0 < a.M) mm_row_load<NORM>(r0, a.x + (long)m0 * a.ldx, a.K, a.norm_w);
+    if (NW < MM_MT && m1 < a.M) mm_row_load<NORM>(r1, a.x + (long)m1 * a.ldx, a.K, a.norm_w);
+    int bt = blockIdx.x;
+    const WT* cur = rowp(bt);
+    load(fa, cur, 0);
+    if (m0 < a.M) mm_row_store<WT, NORM>(r0, a.K, a.eps, xp, KP, scl, m0);
+    if (NW < MM_MT && m1 < a.M) mm_row_store<WT, NORM>(r1, a.K, a.eps, xp, KP, scl, m1);
+    __syncthreads();
+    const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * Q * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const frag(&f)[PF], int c) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int k = 32 * (t0 + c * PF) + koff(i);
+#pragma unroll
+            for (int p = 2; p >= 0; --p) {
+                const frag b = *reinterpret_cast<const frag*>(bbase + (long)p * MM_MT * KP + k);
+                acc = MmT<WT>::mfma(f[i], b, acc);
+            }
+        }
+    };
+    auto finish = [&](int btile) {
+        const int tile = btile * WR + wr;
+        if (WK > 1) {
+            if (wk > 0) red[wk - 1][wr][lane] = acc;
+            __syncthreads();
+            if (wk == 0) {
+#pragma unroll
+                for (int q = 0; q < WK - 1; ++q) {
+                    const f32x4 o = red[q][wr][lane];
+                    acc[0] += o[0]; acc[1] += o[1]; acc[2] += o[2]; acc[3] += o[3];
+                }
+            }
+            __syncthreads();  // red reused by the next tile
+        }
+        if (wk == 0 && col < a.M && tile < ntiles) {
+            const float s = scl[col];
+            float* yr = a.y + (long)col * a.ldy;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int nn = tile * 16 + 4 * g + i;
+                if (nn < a.N) {
+                    float v = apply_act(acc[i] * s + (a.bias ? a.bias[nn] : 0.f), a.act);
+                    if (a.accumulate) v = yr[nn] + v;
+                    yr[nn] = v;
+                }
+            }
+        }
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    // one stream over (tile, chunk): the next batch (the next chunk, or the next tile's first) is
+    // always in flight while the current one is consumed
+    for (;;) {
+        const int nbt = bt + gridDim.x;
+        const bool more = nbt * WR < ntiles;
+        const WT* nxt = more ? rowp(nbt) : cur;
+        for (int c = 0; c < nch; c += 2) {
+            if (c + 1 < nch) load(fb, cur, c + 1);
+            else if (more) load(fb, nxt, 0);
+            compute(fa, c);
+            if (c + 1 >= nch) break;
+            if (c + 2 < nch) load(fa, cur, c + 2);
+            else if (more) load(fa, nxt, 0);
+            compute(fb, c + 1);
+        }
+        finish(bt);
+        if (!more) break;
+        bt = nbt;
+        cur = nxt;
+        if (nch & 1) {  // odd batch count: the next tile's first batch landed in fb
+#pragma unroll
+            for (int i = 0; i < PF; ++i) fa[i] = fb[i];
+        }
+    }
+}
+
+bool dec_mm_ok(const DecGemvArgs& a) {
+    return a.M >= 1 && a.M <= MM_MT && a.K % 32 == 0 && a.K <= 1536 && (a.K >> 5) % 40 == 0 && a.N >= 16 &&
+           !a.xn_out && a.ldw >= a.K && a.ldw % 8 == 0;
+}
+
+static int mm_resident_blocks(const void* kernel, int threads, size_t lds) {
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, per_cu) * std::max(1, cus);
+}
+
+template <typename WT, int WR, int WK, int PF, int Q, bool NORM, bool SWZ = false>
+static void mm_launch(const DecGemvArgs& a, hipStream_t s) {
+    const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.K);
+    const int ntiles = (a.N + 15) / 16;
+    int blocks = (ntiles + WR - 1) / WR;
+    if (WR > 1) {  // persistent: at most one resident round
+        static int resident = 0;
+        if (!resident) resident = mm_resident_blocks((const void*)dec_mm_kernel<WT, WR, WK, PF, Q, NORM, SWZ>, 64 * WR * WK, lds);
+        blocks = std::min(blocks, resident);
+    }
+    DSOCR_LAUNCH((dec_mm_kernel<WT, WR, WK, PF, Q, NORM, SWZ>), dim3(blocks), dim3(64 * WR * WK), lds, s, a);
+}
+
+// block shapes (K steps of 32 a multiple of 40: per-wave batches divide evenly); DSOCR_MM_CFG
+// (experiments) forces one: 0 = WR 8 persistent, 1 = WK 8, 2 = WK 4, 3 = WR 4 persistent,
+// 4 = WR 8 persistent with Q 5 (k-permuted A: measured 2x slower — keep Q 1)
+template <typename WT, bool NORM>
+static void mm_dispatch(const DecGemvArgs& a, hipStream_t s) {
+    static const int cfg_env = getenv("DSOCR_MM_CFG") ? atoi(getenv("DSOCR_MM_CFG")) : -1;
+    if (a.w_swz) {  // fragment-ordered weights (the lm_head's B > 2 copy)
+        DecGemvArgs b = a;
+        b.W = a.w_swz;
+        mm_launch<WT, 8, 1, 10, 1, NORM, true>(b, s);
+        return;
+    }
+    const int cfg = cfg_env >= 0 ? cfg_env : (a.N >= 16384 ? 0 : 1);
+    switch (cfg) {
+        case 0: mm_launch<WT, 8, 1, 10, 1, NORM>(a, s); break;
+        case 2: mm_launch<WT, 1, 4, 10, 1, NORM>(a, s); break;
+        case 3: mm_launch<WT, 4, 1, 10, 1, NORM>(a, s); break;
+        case 4: mm_launch<WT, 8, 1, 10, 5, NORM>(a, s); break;
+        default: mm_launch<WT, 1, 8, 5, 1, NORM>(a, s); break;
+    }
+}
+
+// W [N][K] row-major -> fragment order [N/16 tiles][K/32 steps][64 lanes][8]: lane l of step t of tile
+// T holds W[16 T + (l & 15)][32 t + 8 (l >> 4) .. + 7] (rows past N repeat row N-1)
+__global__ void mm_swizzle_kernel(const uint16_t* w, int N, int K, uint16_t* out) {
+    const int steps = K >> 5;
+    const long total = (long)((N + 15) >> 4) * steps * 64;
+    for (long f = blockIdx.x * (long)blockDim.x + threadIdx.x; f < total; f += (long)gridDim.x * blockDim.x) {
+        const int lane = (int)(f & 63);
+        const long ts = f >> 6;
+        const int t = (int)(ts % steps);
+        const long tile = ts / steps;
+        const int n = (int)std::min<long>(tile * 16 + (lane & 15), N - 1);
+        const uint4 q = *reinterpret_cast<const uint4*>(w + (long)n * K + 32 * t + 8 * (lane >> 4));
+        *reinterpret_cast<uint4*>(out + f * 8) = q;
+    }
+}
+
+size_t mm_swizzle_elems(int N, int K) { return (size_t)((N + 15) / 16) * 16 * (size_t)K; }
+
+void launch_mm_swizzle(const void* w, int N, int K, void* out, hipStream_t s) {
+    if (K % 32) throw std::runtime_error("EINVAL: mm_swizzle needs K % 32 == 0");
+    hipLaunchKernelGGL(mm_swizzle_kernel, dim3(2048), dim3(256), 0, s, (const uint16_t*)w, N, K, (uint16_t*)out);
+}
+
+void launch_dec_mm(const DecGemvArgs& a, hipStream_t s) {
+    if (!dec_mm_ok(a)) throw std::runtime_error("EINVAL: dec_mm outside its range");
+    if (a.wdtype == WDT_BF16) {
+        if (a.norm_w) mm_dispatch<bf16_t, true>(a, s); else mm_dispatch<bf16_t, false>(a, s);
+    } else {
+        if (a.norm_w) mm_dispatch<f16_t, true>(a, s); else mm_dispatch<f16_t, false>(a, s);
+    }
+}
+
+// ------------------------------------------------------------------ grouped decode MoE gate/up (3..8 tokens)
+// Work units of 16 intermediate rows: the shared expert's Is/16 units first, then (record s, tile t)
+// for the router's records (MOE_GRP_*: each distinct routed expert once, with its tokens).  A unit is
+// the 16 gate rows and the 16 up rows over the full K, streamed as MFMA A fragments (PF k-steps of
+// both per batch, double-buffered, the next unit's first batch in flight behind the current one's
+// last); the 8 normalised token rows (xn) are the B operand as three f16 planes staged once per
+// block.  Persistent grid (resident blocks only): unit u goes to block u % grid, wave (u / grid) % 8,
+// so every CU streams the same share (a second round of blocks, or two blocks' rows on one CU, set
+// the launch's length before).  Epilogue per (row, token): g, u scaled back, h = silu(g) * u (candle
+// silu: x / (1 + exp(-x))), times the pick's routing weight for routed experts, to h[slot row]
+// (slot = t * topk + k) or hs[t]; tokens outside a record are computed (a 16-column tile costs the
+// same) and dropped.
+template <typename WT, int PF, bool SWZ>
+__global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
+    typedef typename MmT<WT>::frag frag;
+    constexpr int NWV = 8;
+    extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
+    __shared__ float scl[MM_MT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+#define GM_STAMP(i) \
+    if (a.stamps && lane == 0) a.stamps[((long)blockIdx.x * NWV + wave) * 4 + (i)] = __builtin_amdgcn_s_memrealtime();
+    GM_STAMP(0);
+    const int tiles_r = a.I >> 4, tiles_s = a.sWgu ? a.Is >> 4 : 0;
+    const int n_units = tiles_s + a.grp[0] * tiles_r;
+    const int steps = a.K >> 5, nch = steps / PF;
+    const int stride = gridDim.x * NWV;
+    int unit = blockIdx.x + gridDim.x * wave;
+    // unit -> (shared?, expert, first row) and the lane's two fragment streams
+    struct Src {
+        const WT* pg;
+        const WT* pu;
+        int i0, s;
+        bool shared;
+    };
+    auto src = [&](int uu) {
+        Src r;
+        r.shared = uu < tiles_s;
+        int t = uu;
+        r.s = 0;
+        if (!r.shared) {
+            r.s = (uu - tiles_s) / tiles_r;
+            t = (uu - tiles_s) % tiles_r;
+        }
+        r.i0 = t * 16;
+        const int rows_I = r.shared ? a.Is : a.I;
+        const int e = r.shared ? 0 : a.grp[MOE_GRP_REC * (1 + r.s)];
+        if (SWZ) {
+            const WT* base = r.shared ? reinterpret_cast<const WT*>(a.sWgu_swz) : reinterpret_cast<const WT*>(a.Wgu_swz);
+            const long tg = (r.shared ? 0L : (long)e * (2 * a.I / 16)) + t;
+            r.pg = base + (tg * steps) * 512 + lane * 8;
+            r.pu = base + ((tg + rows_I / 16) * steps) * 512 + lane * 8;
+        } else {
+            const WT* Wg = r.shared ? reinterpret_cast<const WT*>(a.sWgu)
+                                    : reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
+            r.pg = Wg + (long)(r.i0 + col) * a.K + 8 * g;
+            r.pu = r.pg + (long)rows_I * a.K;
+        }
+        return r;
+    };
+    constexpr long FS = SWZ ? 512 : 32;  // elements between a lane's consecutive k-step fragments
+    frag ga[PF], ua[PF], gb[PF], ub[PF];
+    auto load = [&](frag(&fg)[PF], frag(&fu)[PF], const Src& r, int c) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint4 q0 = ldg_nt16(r.pg + FS * (c * PF + i));
+            const uint4 q1 = ldg_nt16(r.pu + FS * (c * PF + i));
+            __builtin_memcpy(&fg[i], &q0, 16);
+            __builtin_memcpy(&fu[i], &q1, 16);
+        }
+    };
+    MmRow xr;  // wave w stages token row w: its loads go out before the weight batch
+    if (wave < a.T) mm_row_load<false>(xr, a.x + (long)wave * a.K, a.K, nullptr);
+    Src cur = src(min(unit, max(n_units - 1, 0)));
+    // both weight batches of the first unit go out before the staging barrier (the stream would
+    // otherwise idle behind it)
+    if (unit < n_units) {
+        load(ga, ua, cur, 0);
+        if (nch > 1) load(gb, ub, cur, 1);
+    }
+    const int KP = mm_pitch(a.K);
+    if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
+    __syncthreads();
+    GM_STAMP(1);
+    const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
+    f32x4 accg = {0.f, 0.f, 0.f, 0.f}, accu = {0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const frag(&fg)[PF], const frag(&fu)[PF], int c) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int k = 32 * (c * PF + i);
+#pragma unroll
+            for (int p = 2; p >= 0; --p) {
+                const frag b = *reinterpret_cast<const frag*>(bbase + (long)p * MM_MT * KP + k);
+                accg = MmT<WT>::mfma(fg[i], b, accg);
+                accu = MmT<WT>::mfma(fu[i], b, accu);
+            }
+        }
+    };
+    bool first = true;
+    for (; unit < n_units; unit += stride) {
+        const int nu = unit + stride;
+        const bool more = nu < n_units;
+        const Src nxt = more ? src(nu) : cur;
+        for (int c = 0; c < nch; c += 2) {
+            if (c + 1 < nch) { if (!(first && c == 0)) load(gb, ub, cur, c + 1); }
+            else if (more) load(gb, ub, nxt, 0);
+            compute(ga, ua, c);
+            if (c + 1 >= nch) break;
+            if (c + 2 < nch) load(ga, ua, cur, c + 2);
+            else if (more) load(ga, ua, nxt, 0);
+            compute(gb, ub, c + 1);
+        }
+        // token col's slot row (routed: -1 when the token did not pick this expert) and weight
+        int slot = -1;
+        float wk = 1.f;
+        if (cur.shared) {
+            slot = col < a.T ? col : -1;
+        } else {
+            const int* rec = a.grp + MOE_GRP_REC * (1 + cur.s);
+            const int cnt = rec[1];
+            for (int q = 0; q < cnt; ++q) {
+                const int r = rec[2 + q];
+                if (r / a.topk == col) { slot = r; wk = __int_as_float(rec[10 + q]); }
+            }
+        }
+        if (slot >= 0) {
+            const float sc = scl[col];
+            float hv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float gs = accg[i] * sc, us = accu[i] * sc;
+                const float h = (gs / (1.0f + expf(-gs))) * us;
+                hv[i] = cur.shared ? h : h * wk;
+            }
+            float* dst = cur.shared ? a.hs + (long)slot * a.Is : a.h + (long)slot * a.I;
+            *reinterpret_cast<float4*>(dst + cur.i0 + 4 * g) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        }
+        accg = f32x4{0.f, 0.f, 0.f, 0.f};
+        accu = f32x4{0.f, 0.f, 0.f, 0.f};
+        cur = nxt;
+        if (nch & 1) {  // odd batch count: the next unit's first batch landed in the b buffers
+#pragma unroll
+            for (int i = 0; i < PF; ++i) { ga[i] = gb[i]; ua[i] = ub[i]; }
+        }
+        if (unit == blockIdx.x + gridDim.x * wave) GM_STAMP(2);  // first unit done
+        first = false;
+    }
+    GM_STAMP(3);
+#undef GM_STAMP
+}
+
+bool moe_gateup_mm_ok(const MoeDec2Args& a) {
+    const bool swz_ok = !a.Wgu_swz || !a.sWgu || a.sWgu_swz;
+    return a.grp && a.T >= 1 && a.T <= MM_MT && a.topk >= 1 && a.K % 32 == 0 && a.K <= 1536 && ((a.K >> 5) % 5) == 0 &&
+           a.I % 16 == 0 && (!a.sWgu || a.Is % 16 == 0) && !a.norm_w && a.x && swz_ok;
+}
+
+void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
+    if (!moe_gateup_mm_ok(a)) throw std::runtime_error("EINVAL: grouped decode gate/up (matrix cores) outside its range");
+    const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.K);
+    const int slots = std::min(a.E, a.T * a.topk);
+    const int max_units = (a.sWgu ? a.Is / 16 : 0) + slots * (a.I / 16);
+#define DSOCR_GM(WTY, SW)                                                                                       \
+    do {                                                                                                        \
+        static int resident = 0;                                                                                \
+        if (!resident) resident = mm_resident_blocks((const void*)moe_gateup_mm_kernel<WTY, 5, SW>, 512, lds);  \
+        const int blocks = std::max(1, std::min(resident, (max_units + 7) / 8));                               \
+        DSOCR_LAUNCH((moe_gateup_mm_kernel<WTY, 5, SW>), dim3(blocks), dim3(512), lds, s, a);                    \
+    } while (0)
+    if (a.wdtype == WDT_BF16) { if (a.Wgu_swz) DSOCR_GM(bf16_t, true); else DSOCR_GM(bf16_t, false); }
+    else { if (a.Wgu_swz) DSOCR_GM(f16_t, true); else DSOCR_GM(f16_t, false); }
+#undef DSOCR_GM
+}
+
+// ------------------------------------------------------------------ grouped decode MoE down (3..8 tokens)
+// out[t][j] += sum over the routed records s of Wd[e_s][j] . h~[slot(s, t)] + Wds[j] . hs[t] (h~ carries
+// the routing weight).  Segments: the n_act records, then the shared expert's K cut into Is / I
+// pseudo-experts of I.  Work unit = (segment, 128 output rows); a block streams its unit's 8 x 16 rows
+// as MFMA A fragments against the segment's token columns staged as three f16 planes (column t = the
+// h~ row of the token's pick, zero when the token did not pick the expert), stores the partial tile
+// write-through (sc1) to part[segment][t][j], and takes a ticket on the row tile; the block whose
+// ticket completes the tile (every segment stored) sums the segments in order (records by expert id,
+// then the shared pieces) with sc1 loads and adds to out (split-K seam: MI355X_MICROARCH.md price list
+// 'splitk-seam'; hand-off: the sc1-load table's first row).
+template <typename WT, int PF, bool SWZ>
+__global__ __launch_bounds__(512, 4) void moe_down_mm_kernel(MoeDec2Args a) {
+    typedef typename MmT<WT>::frag frag;
+    constexpr int NWV = 8, RT = 128, U = 2;  // waves, rows per unit, chunks per lane (I <= 1024)
+    extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
+    __shared__ float scl[MM_MT];
+    __shared__ int last_s;
+    __shared__ unsigned char mem_s[72][MM_MT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int n_act = a.grp[0];
+    const int n_sh = a.sWd ? a.Is / a.I : 0;
+    const int n_seg = n_act + n_sh;
+    const int tiles = a.Hout / RT;
+    const int unit = blockIdx.x;
+    if (unit >= n_seg * tiles) return;  // block-uniform, before any barrier
+    const int seg = unit / tiles, tile = unit % tiles;
+    const bool shared = seg >= n_act;
+    const int hpiece = seg - n_act;
+    const int* rec = a.grp + MOE_GRP_REC * (1 + (shared ? 0 : seg));
+    const int e = shared ? 0 : rec[0];
+    const int steps = a.I >> 5, nch = steps / PF;
+    const int j0 = tile * RT + 16 * wave;
+    // A stream: rows j0 .. j0 + 15 of the segment's down matrix over its I columns
+    const WT* pa;
+    long fs = 32;
+    if (SWZ) {
+        if (shared) {
+            const int steps_s = a.Is >> 5;
+            pa = reinterpret_cast<const WT*>(a.sWd_swz) + ((long)(j0 >> 4) * steps_s + hpiece * steps) * 512 + lane * 8;
+        } else {
+            pa = reinterpret_cast<const WT*>(a.Wd_swz) + (((long)e * a.Hout + j0) / 16 * steps) * 512 + lane * 8;
+        }
+        fs = 512;
+    } else if (shared) {
+        pa = reinterpret_cast<const WT*>(a.sWd) + (long)(j0 + col) * a.Is + (long)hpiece * a.I + 8 * g;
+    } else {
+        pa = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + j0 + col) * a.I + 8 * g;
+    }
+    frag fa[PF], fb[PF];
+    auto load = [&](frag(&f)[PF], int c) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint4 q = ldg_nt16(pa + fs * (c * PF + i));
+            __builtin_memcpy(&f[i], &q, 16);
+        }
+    };
+    // wave w stages token column w: the h~ row of its pick of this expert (shared: hs[w] piece)
+    const float* srcrow = nullptr;
+    if (wave < a.T) {
+        if (shared) {
+            srcrow = a.hs + (long)wave * a.Is + (long)hpiece * a.I;
+        } else {
+            const int cnt = rec[1];
+            for (int q = 0; q < cnt; ++q) {
+                const int r = rec[2 + q];
+                if (r / a.topk == wave) srcrow = a.h + (long)r * a.I;
+            }
+        }
+    }
+    MmRowU<U> xr;
+    if (srcrow) mm_row_load<false, U>(xr, srcrow, a.I, nullptr);
+    load(fa, 0);
+    if (nch > 1) load(fb, 1);
+    const int KP = mm_pitch(a.I);
+    if (!srcrow) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xr.v[u][j] = 0.f;
+    }
+    mm_row_store<WT, false, U>(xr, a.I, 0.f, xp, KP, scl, wave);
+    __syncthreads();
+    const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const frag(&f)[PF], int c) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int k = 32 * (c * PF + i);
+#pragma unroll
+            for (int p = 2; p >= 0; --p) {
+                const frag b = *reinterpret_cast<const frag*>(bbase + (long)p * MM_MT * KP + k);
+                acc = MmT<WT>::mfma(f[i], b, acc);
+            }
+        }
+    };
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch && c > 0) load(fb, c + 1);
+        compute(fa, c);
+        if (c + 1 >= nch) break;
+        if (c + 2 < nch) load(fa, c + 2);
+        compute(fb, c + 1);
+    }
+    // partial tile -> part[seg][t][j] (write-through); tokens outside the segment are zero columns
+    if (col < a.T) {
+        const float sc = scl[col];
+        float* dst = a.dn_part + ((long)seg * MM_MT + col) * a.Hout + j0 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) __hip_atomic_store(dst + i, acc[i] * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        int* tk = a.dn_tick + tile;
+        const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == n_seg - 1;
+        if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
+    // the last arriver: which segments carry token t, then the ordered sum over segments
+    for (int i = tid; i < n_seg * MM_MT; i += NWV * 64) {
+        const int sg = i / MM_MT, t = i % MM_MT;
+        unsigned char m = 0;
+        if (t < a.T) {
+            if (sg >= n_act) {
+                m = 1;
+            } else {
+                const int* rr = a.grp + MOE_GRP_REC * (1 + sg);
+                const int cnt = rr[1];
+                for (int q = 0; q < cnt; ++q) m |= (rr[2 + q] / a.topk == t) ? 1 : 0;
+            }
+        }
+        mem_s[sg][t] = m;
+    }
+    __syncthreads();
+    for (int i = tid; i < RT * MM_MT; i += NWV * 64) {
+        const int t = i / RT, j = tile * RT + i % RT;
+        if (t >= a.T) continue;
+        float v = 0.f;
+        for (int sg = 0; sg < n_seg; ++sg)
+            if (mem_s[sg][t])
+                v += __hip_atomic_load(a.dn_part + ((long)sg * MM_MT + t) * a.Hout + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float* op = a.out + (long)t * a.Hout + j;
+        *op = *op + v;
+    }
+}
+
+bool moe_down_mm_ok(const MoeDec2Args& a) {
+    const bool swz_ok = !a.Wd_swz || !a.sWd || a.sWd_swz;
+    return a.grp && a.dn_part && a.dn_tick && a.T >= 1 && a.T <= MM_MT && a.I % 32 == 0 && a.I <= 1024 &&
+           ((a.I >> 5) % 7) == 0 && a.Hout % 128 == 0 && (!a.sWd || (a.Is % a.I == 0 && a.Is / a.I <= 8)) &&
+           std::min(a.E, a.T * a.topk) + (a.sWd ? a.Is / a.I : 0) <= 72 && swz_ok;
+}
+
+size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H) {
+    return (size_t)(std::min(E, T * topk) + (I > 0 && Is > 0 ? Is / I : 0)) * MM_MT * H;
+}
+
+void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s) {
+    if (!moe_down_mm_ok(a)) throw std::runtime_error("EINVAL: grouped decode down (matrix cores) outside its range");
+    const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.I);
+    const int max_seg = std::min(a.E, a.T * a.topk) + (a.sWd ? a.Is / a.I : 0);
+    dim3 grid(max_seg * (a.Hout / 128));
+#define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW>), grid, dim3(512), lds, s, a)
+    if (a.wdtype == WDT_BF16) { if (a.Wd_swz) DSOCR_DM(bf16_t, true); else DSOCR_DM(bf16_t, false); }
+    else { if (a.Wd_swz) DSOCR_DM(f16_t, true); else DSOCR_DM(f16_t, false); }
+#undef DSOCR_DM
+}
+
+}  // namespace dsocr

@@ -171,8 +171,16 @@ struct DecGemvArgs {
     const float* norm_w = nullptr;
     float eps = 0.f;
     float* xn_out = nullptr;  // optional: block 0 writes the staged (normalised) rows [M][K] here
+    const void* w_swz = nullptr;  // optional: W in dec_mm's fragment order (launch_mm_swizzle), M = 3..8
 };
 void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s);
+// 3..8 tokens on the matrix cores (decode_mm.hip): weight rows as MFMA A operands, the (optionally
+// RMS-normalised) activation rows as three exact 16-bit planes (f16: per-row power-of-two scaled)
+bool dec_mm_ok(const DecGemvArgs& a);
+void launch_dec_mm(const DecGemvArgs& a, hipStream_t s);
+// W [N][K] -> dec_mm fragment order ([N/16][K/32][64][8] 16-bit): every wave weight load one 1 KiB block
+size_t mm_swizzle_elems(int N, int K);
+void launch_mm_swizzle(const void* w, int N, int K, void* out, hipStream_t s);
 // Router GEMV whose last-arriving block writes the greedy top-k of every token (T <= 8).
 struct DecRouteEpi {
     int topk = 0, softmax_scoring = 1, norm_topk = 0;
@@ -281,6 +289,13 @@ struct MoeDec2Args {
     // grouped mode (3 <= T <= 8): expert groups written by the router epilogue (MOE_GRP_* layout);
     // h rows stay in slot order (t*topk + k)
     const int* grp = nullptr;
+    // optional fragment-ordered copies (launch_mm_swizzle) for the matrix-core grouped kernels:
+    // routed [E * 2I][K], shared [2 Is][K]; routed down [E * H][I], shared down [H][Is]
+    const void* Wgu_swz = nullptr; const void* sWgu_swz = nullptr;
+    const void* Wd_swz = nullptr; const void* sWd_swz = nullptr;
+    // matrix-core grouped down: per-segment partial tiles [segments][8][Hout] and per-128-row
+    // arrival tickets [Hout / 128] (zero between launches; the last arriver resets them)
+    float* dn_part = nullptr; int* dn_tick = nullptr;
 };
 constexpr int SYNC_SHARDS = 8, SYNC_STRIDE = 32;  // counters per hand-off, ints between counters
 constexpr int SYNC_INTS = SYNC_SHARDS * SYNC_STRIDE;  // ints of one hand-off's counter block
@@ -303,6 +318,13 @@ void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
 bool moe_grp_ok(const MoeDec2Args& a);
 void launch_moe_gateup_grp(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s);
+// the grouped gate/up on the matrix cores (decode_mm.hip): expert rows as MFMA A fragments, the
+// token rows as three exact f16 planes
+bool moe_gateup_mm_ok(const MoeDec2Args& a);
+void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s);
+bool moe_down_mm_ok(const MoeDec2Args& a);
+size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H);
+void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s);
 
 // One decode MoE layer for T tokens (block.rs:1215-1395): [RMSNorm] -> router GEMV (+ routing /
 // grouping) -> gate/up -> down + weighted combine + shared experts + residual:
@@ -314,6 +336,8 @@ struct MoeDecodeArgs {
     const void* router = nullptr; int router_wdt = WDT_F16; const float* router_bias = nullptr;
     const void* Wgu = nullptr; const void* Wd = nullptr;    // [E][2I][H], [E][H][I]
     const void* sWgu = nullptr; const void* sWd = nullptr;  // [2Is][H], [H][Is] (or null)
+    const void* Wgu_swz = nullptr; const void* sWgu_swz = nullptr;  // optional fragment-ordered copies
+    const void* Wd_swz = nullptr; const void* sWd_swz = nullptr;
     int wdtype = WDT_F16;
     int softmax_scoring = 1, norm_topk = 0; float scaling = 1.f;
     float* out = nullptr;
@@ -326,6 +350,8 @@ struct MoeDecodeArgs {
     float* hs = nullptr;        // [T][Is]
     int* grp = nullptr;         // moe_grp_ints(E, T, topk)
     int* route_cnt = nullptr;   // [16], zero between launches (router epilogue ticket)
+    float* dn_part = nullptr;   // moe_down_mm_part_floats(...)  (grouped matrix-core down)
+    int* dn_tick = nullptr;     // [H / 128], zero between launches
     int* eoff = nullptr; int* arow = nullptr; int* apos = nullptr; int* active = nullptr;  // T > 8:
     int* n_active = nullptr; float* aw = nullptr;                                          // [E+1],[TK],[TK],[E],[1],[TK]
 };

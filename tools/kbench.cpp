@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <functional>
 #include <string>
 #include <vector>
@@ -123,8 +124,10 @@ constexpr int NL = 11;  // MoE layers
 
 struct MoeLayerW {
     uint16_t *router, *gu, *d, *sgu, *sd;
+    uint16_t *gu_s = nullptr, *sgu_s = nullptr, *d_s = nullptr, *sd_s = nullptr;  // fragment-ordered copies
     float* norm;
 };
+static bool g_swz = getenv("KB_SWZ") && atoi(getenv("KB_SWZ")) != 0;
 
 static std::vector<MoeLayerW> g_moe;
 static void moe_weights() {
@@ -137,6 +140,16 @@ static void moe_weights() {
         w.sgu = rand_f16((size_t)2 * IS * H);
         w.sd = rand_f16((size_t)H * IS);
         w.norm = rand_f32(H, 0.2f, 1.0f);
+        if (g_swz) {
+            w.gu_s = (uint16_t*)dalloc(mm_swizzle_elems(E * 2 * I, H) * 2);
+            launch_mm_swizzle(w.gu, E * 2 * I, H, w.gu_s, nullptr);
+            w.sgu_s = (uint16_t*)dalloc(mm_swizzle_elems(2 * IS, H) * 2);
+            launch_mm_swizzle(w.sgu, 2 * IS, H, w.sgu_s, nullptr);
+            w.d_s = (uint16_t*)dalloc(mm_swizzle_elems(E * H, I) * 2);
+            launch_mm_swizzle(w.d, E * H, I, w.d_s, nullptr);
+            w.sd_s = (uint16_t*)dalloc(mm_swizzle_elems(H, IS) * 2);
+            launch_mm_swizzle(w.sd, H, IS, w.sd_s, nullptr);
+        }
         g_moe.push_back(w);
     }
 }
@@ -158,9 +171,14 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     a.hs = (float*)dalloc((size_t)T * IS * 4);
     a.grp = (int*)dalloc(moe_grp_ints(E, T, TOPK) * 4);
     a.route_cnt = (int*)dalloc(64);
+    if (T >= 3 && T <= 8) {
+        a.dn_part = (float*)dalloc(moe_down_mm_part_floats(E, T, TOPK, I, IS, H) * 4);
+        a.dn_tick = (int*)dalloc(64);
+    }
     auto set = [&](int l) {
         const MoeLayerW& w = g_moe[l % NL];
         a.norm_w = w.norm; a.router = w.router; a.Wgu = w.gu; a.Wd = w.d; a.sWgu = w.sgu; a.sWd = w.sd;
+        a.Wgu_swz = w.gu_s; a.sWgu_swz = w.sgu_s; a.Wd_swz = w.d_s; a.sWd_swz = w.sd_s;
     };
     const int n = 4 * NL;
     set(0);
@@ -205,6 +223,41 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     const double dnb = ((double)touched * I + IS) * H * 2;
     snprintf(nm, sizeof nm, "moe%d gateup", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_GATEUP); }, s), gub);
+    if (getenv("KB_STAMPS")) {  // per-block phase clocks of the gate/up launch (wall clock, 100 MHz)
+        const int nb = 8192;
+        auto* st = (unsigned long long*)dalloc((size_t)nb * 4 * 8);
+        set(5);
+        MoeDecodeArgs b = a;
+        // stamps ride in the dispatch's MoeDec2Args through a global hook: DSOCR_STAMPS_PTR
+        char buf[64];
+        snprintf(buf, sizeof buf, "%llu", (unsigned long long)(uintptr_t)st);
+        setenv("DSOCR_MOE_STAMPS", buf, 1);
+        launch_moe_decode(b, s, MOE_GATEUP);
+        CK(hipStreamSynchronize(s));
+        unsetenv("DSOCR_MOE_STAMPS");
+        std::vector<unsigned long long> h((size_t)nb * 4);
+        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+        // per wave: [entry, staged, first unit done, end]
+        unsigned long long t0 = ~0ull;
+        for (int i = 0; i < nb; ++i)
+            if (h[i * 4]) t0 = std::min(t0, h[i * 4]);
+        std::vector<double> st1, fu, en;
+        for (int i = 0; i < nb; ++i) {
+            if (!h[i * 4] || !h[i * 4 + 3]) continue;
+            st1.push_back((h[i * 4 + 1] - t0) / 100.0);
+            if (h[i * 4 + 2]) fu.push_back((h[i * 4 + 2] - t0) / 100.0);
+            en.push_back((h[i * 4 + 3] - t0) / 100.0);
+        }
+        auto pr = [](const char* n, std::vector<double> v) {
+            if (v.empty()) return;
+            std::sort(v.begin(), v.end());
+            printf("  %s: n %zu p10 %.2f p50 %.2f p90 %.2f max %.2f us\n", n, v.size(), v[v.size() / 10], v[v.size() / 2],
+                   v[v.size() * 9 / 10], v.back());
+        };
+        pr("staged", st1);
+        pr("first unit done", fu);
+        pr("wave end", en);
+    }
     snprintf(nm, sizeof nm, "moe%d down", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_DOWN); }, s), dnb);
 }
@@ -269,7 +322,16 @@ static void case_lm(int M, hipStream_t s) {
     char nm[96];
     snprintf(nm, sizeof nm, "lm_head exact M=%d", M);
     report(nm, timeit(8, [&](int i) { g.W = w[i % NB]; launch_dec_gemv(g, s); }, s), (double)V * H * 2);
-    for (int i = 0; i < NB; ++i) (void)hipFree(w[i]);
+    // fragment-ordered copies
+    std::vector<uint16_t*> ws(NB);
+    for (int i = 0; i < NB; ++i) {
+        ws[i] = (uint16_t*)dalloc(mm_swizzle_elems(V, H) * 2);
+        launch_mm_swizzle(w[i], V, H, ws[i], s);
+    }
+    snprintf(nm, sizeof nm, "lm_head exact M=%d swizzled", M);
+    report(nm, timeit(8, [&](int i) { g.W = w[i % NB]; g.w_swz = ws[i % NB]; launch_dec_gemv(g, s); }, s), (double)V * H * 2);
+    g.w_swz = nullptr;
+    for (int i = 0; i < NB; ++i) { (void)hipFree(w[i]); (void)hipFree(ws[i]); }
 }
 
 int main(int argc, char** argv) {
