@@ -1422,7 +1422,7 @@ __device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, 
 // loads), then run the attention chunk exactly as the unfused kernel.
 // PREROT: the q / k rows arrive already rotated (dec_qkv_rope applied RoPE in its epilogue), so
 // q, k_new and v_new are loaded before the position and no RoPE table is read here.
-template <int HD, int CH, bool PREROT, bool FUSED>
+template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false>
 __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
@@ -1475,12 +1475,14 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         k_pre = row[a.heads * HD + kvh * HD + td];
         v_pre = row[(a.heads + a.kv_heads) * HD + kvh * HD + td];
     }
+    // EARLY (one page: latency-bound): the chunk's K / V loads go out before the position is known,
+    // clamped to the cache capacity (keys past pos are masked at use), overlapping the pos round trip
+    if (EARLY) issue_kv(kcap);
     const int pos = a.kv_pos[b];
     const int len = pos + 1;
     if (k0 >= len) return;
     const int kn = min(CH, len - k0);
-    issue_kv(k0 + kn - 1);
-    (void)kcap;
+    if (!EARLY) issue_kv(k0 + kn - 1);
     const bool own = pos >= k0 && pos < k0 + CH;
     const int nc = (len + CH - 1) / CH;
     if (FUSED) qkv_rows_for_head<HD>(a, b, h, c, nc, smem);
@@ -1711,9 +1713,9 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
 #undef AT_STAMP
 }
 
-template <int HD, int CH, bool PREROT>
+template <int HD, int CH, bool PREROT, bool EARLY>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
-    attn_body<HD, CH, PREROT, false>(a, nullptr);
+    attn_body<HD, CH, PREROT, false, EARLY>(a, nullptr);
 }
 
 template <int HD, int CH>
@@ -1753,10 +1755,14 @@ void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     const int chunks = (a.max_len + ch - 1) / ch;
     dim3 g1(chunks, a.heads, a.B);
     const bool prerot = a.prerot != 0;
+    static const bool early_env = !(getenv("DSOCR_ATT_EARLY") && atoi(getenv("DSOCR_ATT_EARLY")) == 0);
+    const bool early = early_env && a.B == 1;
 #define DSOCR_DA(HDV, CHV)                                                                          \
     do {                                                                                             \
-        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true>), g1, dim3(256), 0, s, a);  \
-        else DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, false>), g1, dim3(256), 0, s, a);        \
+        if (prerot && early) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true, true>), g1, dim3(256), 0, s, a);  \
+        else if (prerot) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true, false>), g1, dim3(256), 0, s, a);     \
+        else if (early) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, false, true>), g1, dim3(256), 0, s, a);      \
+        else DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, false, false>), g1, dim3(256), 0, s, a);                \
     } while (0)
     if (ch == 64) {
         if (a.hd == 128) DSOCR_DA(128, 64); else if (a.hd == 64) DSOCR_DA(64, 64); else DSOCR_DA(32, 64);
