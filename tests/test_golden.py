@@ -70,3 +70,35 @@ def test_oracle_generate_without_cache_matches_cached(oracle_model):
     a = oracle_model.generate_without_cache(ids, None, None, 8, eos_token_id=1, no_repeat_ngram_size=20)
     b, _ = oracle_model.generate(ids, [0] * len(ids), None, 8, eos_token_id=1, no_repeat_ngram_size=20)
     assert a == b
+
+
+# ---------------------------------------------------------------- a16: the product's prompt builder
+@pytest.mark.parametrize("prompt,counts", [
+    ("<image>\n<|grounding|>Convert the document to markdown.", [693]),
+    ("<image>\nFree OCR.", [273]),
+    ("Compare <image> with <image>, then summarise.", [100, 257]),
+    ("<image><image>", [5, 7]),
+    ("No image at all, just text.", []),
+])
+def test_product_prompt_builder_equals_oracle(prompt, counts):
+    """dsocr.build_prompt_tokens (the product's host builder) gives the oracle's ids and mask
+    (oracle/model.py build_prompt_tokens, model/mod.rs:2536-2603) for single, multiple and no images."""
+    from dsocr import build_prompt_tokens
+    from dsocr.synth import SyntheticTokenizer
+    from oracle.model import build_prompt_tokens as oracle_build
+    tok = SyntheticTokenizer(129280)
+    ids, mask = build_prompt_tokens(tok, prompt, counts)
+    segs = [list(tok.encode(s, add_special_tokens=False).ids) for s in prompt.split("<image>")]
+    rids, rmask = oracle_build(segs, tok.token_to_id("<image>"), counts)
+    assert ids == rids and mask == rmask
+    assert sum(mask) == sum(counts)
+
+
+def test_product_prompt_builder_mismatch_is_einval():
+    """slots != images -> the reference's 'prompt/image embedding mismatch' (400 class, DSOCR_EINVAL)."""
+    from dsocr import build_prompt_tokens
+    from dsocr._lib import DsocrError
+    from dsocr.synth import SyntheticTokenizer
+    with pytest.raises(DsocrError) as e:
+        build_prompt_tokens(SyntheticTokenizer(512), "<image> and <image>", [10])
+    assert "mismatch" in str(e.value)
