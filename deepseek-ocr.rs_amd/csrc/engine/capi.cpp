@@ -511,6 +511,19 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
             a.grp = (int*)alloc(sizeof(int) * dsocr::moe_grp_ints(E, T, topk));
             a.route_cnt = (int*)alloc(sizeof(int) * 16);
             check_hip(hipMemset(a.route_cnt, 0, sizeof(int) * 16), "hipMemset");
+            if (wdtype == 1 && H % 32 == 0 && I % 32 == 0 && T <= 8) {
+                // fragment-ordered expert copies, as Engine::ensure_mm_weights keeps them
+                a.Wgu_swz = alloc(sizeof(uint16_t) * dsocr::mm_swizzle_elems(E * 2 * I, H));
+                dsocr::launch_mm_swizzle(Wgu, E * 2 * I, H, const_cast<void*>(a.Wgu_swz), nullptr);
+                a.Wd_swz = alloc(sizeof(uint16_t) * dsocr::mm_swizzle_elems(E * H, I));
+                dsocr::launch_mm_swizzle(Wd, E * H, I, const_cast<void*>(a.Wd_swz), nullptr);
+                if (a.Is > 0 && a.Is % 32 == 0) {
+                    a.sWgu_swz = alloc(sizeof(uint16_t) * dsocr::mm_swizzle_elems(2 * a.Is, H));
+                    dsocr::launch_mm_swizzle(sWgu, 2 * a.Is, H, const_cast<void*>(a.sWgu_swz), nullptr);
+                    a.sWd_swz = alloc(sizeof(uint16_t) * dsocr::mm_swizzle_elems(H, a.Is));
+                    dsocr::launch_mm_swizzle(sWd, H, a.Is, const_cast<void*>(a.sWd_swz), nullptr);
+                }
+            }
             if (T >= 3 && T <= 8) {
                 a.dn_part = (float*)alloc(sizeof(float) * dsocr::moe_down_mm_part_floats(E, T, topk, I, a.Is, H));
                 a.dn_tick = (int*)alloc(sizeof(int) * (H / 128 + 1));
@@ -545,6 +558,9 @@ dsocr_status dsocr_k_moe_kernels(int T, int H, int E, int topk, int I, int Is, i
         a.xn = a.xn_router = a.logits = a.wts = a.h = &fd;
         a.ids = a.grp = a.route_cnt = &dummy;
         if (T >= 3 && T <= 8) { a.dn_part = &fd; a.dn_tick = &dummy; }
+        // the engine keeps fragment-ordered expert copies (Engine::ensure_mm_weights)
+        a.Wgu_swz = a.Wd_swz = &dummy;
+        if (Is > 0) a.sWgu_swz = a.sWd_swz = &dummy;
         if (T > 8) { a.eoff = a.arow = a.apos = a.active = a.n_active = &dummy; a.aw = &fd; }
         dsocr::moe_decode_kernel_names(a, gateup, down);
     });

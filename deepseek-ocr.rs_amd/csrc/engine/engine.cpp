@@ -1009,12 +1009,12 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     a.h = wsf("s_ehh", (size_t)TK * I);
     a.grp = wsi("s_grp", moe_grp_ints(E, B, K));
     a.route_cnt = wsi("s_route_cnt", 16);
-    if (B >= 3 && B <= 8) {  // matrix-core grouped kernels: fragment-ordered experts, down partials + tickets
+    if (B >= 3 && B <= 8) {  // matrix-core grouped kernels: down partials + tickets
         a.dn_part = wsf("s_dnpart", moe_down_mm_part_floats(E, B, K, I, a.Is, H));
         a.dn_tick = wsi("s_dntick", (size_t)H / 128 + 1);
-        if (d.e_gu_swz && (!d.has_shared || d.s_gu_swz)) {
-            a.Wgu_swz = d.e_gu_swz; a.Wd_swz = d.e_d_swz; a.sWgu_swz = d.s_gu_swz; a.sWd_swz = d.s_d_swz;
-        }
+    }
+    if (B <= 8 && d.e_gu_swz && (!d.has_shared || d.s_gu_swz)) {  // fragment-ordered experts
+        a.Wgu_swz = d.e_gu_swz; a.Wd_swz = d.e_d_swz; a.sWgu_swz = d.s_gu_swz; a.sWd_swz = d.s_d_swz;
     }
     if (B > 8) {
         a.eoff = wsi("s_eoff", E + 1); a.arow = wsi("s_arow", TK); a.apos = wsi("s_apos", TK);
@@ -1134,18 +1134,23 @@ void Engine::reserve_head_ws(int B) {
 // 4.6 TB/s row-major on MI355X, tools/kbench lm8), made once, outside any capture (HBM: + vocab x hidden
 // + the expert weights again, ~5.3 GB of the 288)
 void Engine::ensure_mm_weights(int B) {
-    if (B < 3 || B > 8 || lm_swz_ || capturing_) return;
+    if (B > 8 || capturing_) return;
     if (getenv("DSOCR_MM_SWZ") && atoi(getenv("DSOCR_MM_SWZ")) == 0) return;
     const LangConfig& L = cfg_.lang;
-    DecGemvArgs g;
-    g.M = B; g.N = L.vocab; g.K = L.hidden; g.ldw = L.hidden;
-    if (!dec_mm_ok(g)) return;
-    lm_swz_ = dev_alloc(mm_swizzle_elems(L.vocab, L.hidden) * 2);
-    launch_mm_swizzle(lm_head_.W, L.vocab, L.hidden, lm_swz_, stream_);
-    // the experts of every MoE layer (routed [E * 2I][H], [E * H][I]; shared [2Is][H], [H][Is])
+    if (B >= 3 && !lm_swz_) {
+        DecGemvArgs g;
+        g.M = B; g.N = L.vocab; g.K = L.hidden; g.ldw = L.hidden;
+        if (dec_mm_ok(g)) {
+            lm_swz_ = dev_alloc(mm_swizzle_elems(L.vocab, L.hidden) * 2);
+            launch_mm_swizzle(lm_head_.W, L.vocab, L.hidden, lm_swz_, stream_);
+        }
+    }
+    // the experts of every MoE layer (routed [E * 2I][H], [E * H][I]; shared [2Is][H], [H][Is]): the
+    // grouped matrix-core kernels stream them (one page: only with DSOCR_MIX_MM=1)
     const int H = L.hidden, E = L.n_routed, I = L.moe_inter;
+    if (B < 3 && !(getenv("DSOCR_MIX_MM") && atoi(getenv("DSOCR_MIX_MM")) != 0)) return;
     for (DecLayer& d : layers_) {
-        if (!d.moe || d.e_wdt != WDT_F16 || H % 32 || I % 32) continue;
+        if (!d.moe || d.e_gu_swz || d.e_wdt != WDT_F16 || H % 32 || I % 32) continue;
         d.e_gu_swz = dev_alloc(mm_swizzle_elems(E * 2 * I, H) * 2);
         launch_mm_swizzle(d.e_gu, E * 2 * I, H, d.e_gu_swz, stream_);
         d.e_d_swz = dev_alloc(mm_swizzle_elems(E * H, I) * 2);

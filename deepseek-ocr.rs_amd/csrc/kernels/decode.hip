@@ -3123,6 +3123,7 @@ struct MoePlan {
     bool route1 = false;  // grouped mode: dec_route_grp (norm + router + top-k + records, one block)
     bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
     bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
+    bool gu_mix_mm = false;  // one token: gate/up on the matrix cores (moe_gateup_mix_mm)
 };
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
@@ -3173,6 +3174,9 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
         }
         p.mode = (gu_mix && fuse_norm && moe_gateup_mix_ok(m) && a.xn_router) ? 0 : 1;
         if (p.mode == 0) gr.xn_out = a.xn_router;  // the router hands its normalised row to gate/up
+        // one-token gate/up on the matrix cores: equal to moe_gateup_mix on MI355X (9.7 us both, tools/kbench
+        // moe1: the routing round trip and the staging barrier eat the coalescing gain) -> off by default
+        p.gu_mix_mm = p.mode == 0 && env_flag("DSOCR_MIX_MM", false) && moe_gateup_mix_mm_ok(m);
         p.mix_dn = dn_mix && moe_down_mix_ok(m);
     } else {
         p.mode = 3;
@@ -3189,7 +3193,7 @@ void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const 
     const MoePlan p = moe_plan(a);
     const char* gu = "moe_gateup2_kernel";
     const char* dn = "moe_down2_kernel";
-    if (p.mode == 0) gu = "moe_gateup_mix_kernel";
+    if (p.mode == 0) gu = p.gu_mix_mm ? "moe_gateup_mix_mm_kernel" : "moe_gateup_mix_kernel";
     else if (p.mode == 1) gu = (a.T > 2 && a.Is) ? "moe_gateup_slot_kernel+moe_gateup_shared_kernel" : "moe_gateup_slot_kernel";
     else if (p.mode == 2) gu = p.gu_mm ? "moe_gateup_mm_kernel" : "moe_gateup_grp_kernel";
     if (p.mode == 2) dn = p.dn_mm ? "moe_down_mm_kernel" : "moe_down_grp_kernel";
@@ -3231,7 +3235,8 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     if (parts & MOE_GATEUP) {
         if (const char* sp = getenv("DSOCR_MOE_STAMPS"))  // dev: per-block phase clocks (profile only)
             const_cast<MoeDec2Args&>(m).stamps = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(sp, nullptr, 10));
-        if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
+        if (p.mode == 0 && p.gu_mix_mm) launch_moe_gateup_mix_mm(m, a.xn_router, s);
+        else if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
         else if (p.mode == 2 && p.gu_mm) launch_moe_gateup_mm(m, s);
         else if (p.mode == 2) launch_moe_gateup_grp(m, s);
         else launch_moe_gateup2(m, s);

@@ -322,6 +322,8 @@ void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s);
 // token rows as three exact f16 planes
 bool moe_gateup_mm_ok(const MoeDec2Args& a);
 void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s);
+bool moe_gateup_mix_mm_ok(const MoeDec2Args& a);
+void launch_moe_gateup_mix_mm(const MoeDec2Args& a, const float* xn, hipStream_t s);
 bool moe_down_mm_ok(const MoeDec2Args& a);
 size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H);
 void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s);

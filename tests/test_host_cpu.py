@@ -206,7 +206,7 @@ def test_moe_dispatch_kernel_names():
     import ctypes as C
     from dsocr._lib import check, lib
     want = {1: ("moe_gateup_mix_kernel", "moe_down_mix_kernel"), 2: ("moe_gateup_slot_kernel", "moe_down_slot_kernel"),
-            3: ("moe_gateup_grp_kernel", "moe_down_grp_kernel"), 8: ("moe_gateup_grp_kernel", "moe_down_grp_kernel"),
+            3: ("moe_gateup_mm_kernel", "moe_down_mm_kernel"), 8: ("moe_gateup_mm_kernel", "moe_down_mm_kernel"),
             9: ("moe_gateup2_kernel", "moe_down2_kernel")}
     for T, (gu, dn) in want.items():
         g, d = C.c_char_p(), C.c_char_p()

@@ -237,16 +237,15 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
         unsetenv("DSOCR_MOE_STAMPS");
         std::vector<unsigned long long> h((size_t)nb * 4);
         CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-        // per wave: [entry, staged, first unit done, end]
+        // per record: 4 wall-clock stamps (kernel-specific phase points), relative to the first entry
         unsigned long long t0 = ~0ull;
         for (int i = 0; i < nb; ++i)
             if (h[i * 4]) t0 = std::min(t0, h[i * 4]);
-        std::vector<double> st1, fu, en;
+        std::vector<double> ph[4];
         for (int i = 0; i < nb; ++i) {
             if (!h[i * 4] || !h[i * 4 + 3]) continue;
-            st1.push_back((h[i * 4 + 1] - t0) / 100.0);
-            if (h[i * 4 + 2]) fu.push_back((h[i * 4 + 2] - t0) / 100.0);
-            en.push_back((h[i * 4 + 3] - t0) / 100.0);
+            for (int k = 0; k < 4; ++k)
+                if (h[i * 4 + k]) ph[k].push_back(((long long)h[i * 4 + k] - (long long)t0) / 100.0);
         }
         auto pr = [](const char* n, std::vector<double> v) {
             if (v.empty()) return;
@@ -254,9 +253,10 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
             printf("  %s: n %zu p10 %.2f p50 %.2f p90 %.2f max %.2f us\n", n, v.size(), v[v.size() / 10], v[v.size() / 2],
                    v[v.size() * 9 / 10], v.back());
         };
-        pr("staged", st1);
-        pr("first unit done", fu);
-        pr("wave end", en);
+        pr("stamp0", ph[0]);
+        pr("stamp1", ph[1]);
+        pr("stamp2", ph[2]);
+        pr("stamp3", ph[3]);
     }
     snprintf(nm, sizeof nm, "moe%d down", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_DOWN); }, s), dnb);
