@@ -385,6 +385,25 @@ dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm
         check_hip(hipDeviceSynchronize(), "gemv");
     });
 }
+dsocr_status dsocr_k_gemv_splitk(int M, int N, int K, const float* x, const void* W, int wdtype, const float* bias,
+                                 float* y, int accumulate) {
+    return guarded([&] {
+        dsocr::DecGemvArgs a;
+        a.M = M; a.N = N; a.K = K; a.x = x; a.ldx = K; a.W = W; a.ldw = K; a.wdtype = wdtype; a.bias = bias;
+        a.y = y; a.ldy = N; a.accumulate = accumulate;
+        if (!dsocr::dec_mm_splitk_ok(a)) throw std::runtime_error("EINVAL: gemv_splitk needs M <= 8, K % 64 == 0");
+        float* part = nullptr;
+        int* tick = nullptr;
+        check_hip(hipMalloc(&part, sizeof(float) * dsocr::dec_mm_splitk_part_floats(N, K)), "hipMalloc");
+        check_hip(hipMalloc(&tick, sizeof(int) * dsocr::dec_mm_splitk_ticks(N)), "hipMalloc");
+        check_hip(hipMemset(tick, 0, sizeof(int) * dsocr::dec_mm_splitk_ticks(N)), "hipMemset");
+        dsocr::launch_dec_mm_splitk(a, part, tick, nullptr);
+        hipError_t e = hipDeviceSynchronize();
+        (void)hipFree(part);
+        (void)hipFree(tick);
+        check_hip(e, "gemv_splitk");
+    });
+}
 dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* w, const float* b, float eps, float* y) {
     return guarded([&] {
         if (cols % 4) throw std::runtime_error("EINVAL: cols must be a multiple of 4");

@@ -1023,6 +1023,17 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     return a;
 }
 
+// the dense MLP's matrix-core form at 3..8 pages (decode_mm.hip): q/k/v-sized K for gate|up, K % 64 for down
+bool Engine::dense_mm_ok(const DecLayer& d, int B) const {
+    if (getenv("DSOCR_DENSE_MM") && atoi(getenv("DSOCR_DENSE_MM")) == 0) return false;
+    const LangConfig& L = cfg_.lang;
+    DecGemvArgs g1;
+    g1.M = B; g1.N = 2 * L.inter; g1.K = L.hidden; g1.ldw = L.hidden;
+    DecGemvArgs g2;
+    g2.M = B; g2.N = L.hidden; g2.K = L.inter; g2.ldw = L.inter; g2.ldx = L.inter;
+    return d.gu.W && d.down.W && dec_mm_ok(g1) && dec_mm_splitk_ok(g2);
+}
+
 void Engine::decode_step(int B, int Lmax) {
     // One token for each of B pages: 8 launches per layer (decode.hip).  For B <= 2 the
     // RMSNorms are fused into the consuming GEMV / expert kernels (x normalised on the fly).
@@ -1097,6 +1108,23 @@ void Engine::decode_step(int B, int Lmax) {
         if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
         else launch_dec_gemv(go, st);
         // MLP / MoE
+        if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
+            // dense MLP (layer 0) on the matrix cores: gate|up with the post-attention RMSNorm fused,
+            // SwiGLU, down as a split-K launch accumulating into the residual
+            const int I = L.inter;
+            float* G = wsf("s_dg", (size_t)B * 2 * I);
+            float* HH = wsf("s_dhh", (size_t)B * I);
+            DecGemvArgs g1;
+            g1.M = B; g1.N = 2 * I; g1.K = H; g1.x = X; g1.ldx = H; g1.norm_w = d.post_norm.w; g1.eps = L.rms_eps;
+            g1.W = d.gu.W; g1.ldw = H; g1.wdtype = d.gu.wdt; g1.bias = d.gu.b; g1.y = G; g1.ldy = 2 * I;
+            launch_dec_gemv(g1, st);
+            launch_silu_mul(G, 2 * I, I, B, HH, I, st);
+            DecGemvArgs g2;
+            g2.M = B; g2.N = H; g2.K = I; g2.x = HH; g2.ldx = I; g2.W = d.down.W; g2.ldw = I; g2.wdtype = d.down.wdt;
+            g2.bias = d.down.b; g2.y = X; g2.ldy = H; g2.accumulate = 1;
+            launch_dec_mm_splitk(g2, wsf("s_dpart", dec_mm_splitk_part_floats(H, I)), wsi("s_dtick", dec_mm_splitk_ticks(H)), st);
+            continue;
+        }
         if (!d.moe) {
             const float* mx = X;
             const float* mnorm = d.post_norm.w;
@@ -1400,6 +1428,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_dntick", (size_t)H / 128 + 1), 0, sizeof(int) * (H / 128 + 1), st));
+    HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
     HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     const int QKVN = layers_[0].qkv.N;

@@ -222,6 +222,7 @@ class Engine {
     Lin lm_head_;
     void* lm_swz_ = nullptr;         // lm_head in dec_mm fragment order (3..8 pages; made on first use)
     void ensure_mm_weights(int B);
+    bool dense_mm_ok(const DecLayer& d, int B) const;
     void* lmq_ = nullptr;            // int8 [vocab][hidden] screening copy of lm_head
     float* lmq_scale_ = nullptr;     // per-row scale
     float* lmq_bound_ = nullptr;     // per-row error-bound factor (times ||x||)

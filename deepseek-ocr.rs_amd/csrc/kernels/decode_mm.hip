@@ -925,4 +925,115 @@ void launch_moe_gateup_mix_mm(const MoeDec2Args& a, const float* xn, hipStream_t
     else DSOCR_LAUNCH((moe_gateup_mix_mm_kernel<f16_t>), dim3(units), dim3(256), 0, s, a, xn);
 }
 
+// ------------------------------------------------------------------ long-K projection, 3..8 tokens
+// Y[m][n] (+)= X[m] . W[n]^T (+ bias) for K too long to stage whole (the dense layer-0 down
+// projection, K = 6848): K is cut in pieces of MMK_PIECE; unit = (piece, 64 output rows); a block
+// stages its piece of the token rows as three planes (one power-of-two scale per (row, piece)),
+// streams its 4 waves x 16 rows, stores the scaled partial tile write-through and takes a ticket on
+// its row tile; the last arriver sums the pieces in order, adds the bias and (+=) the output.
+constexpr int MMK_PIECE = 512;
+
+template <typename WT>
+__global__ __launch_bounds__(256) void dec_mm_splitk_kernel(DecGemvArgs a, float* part, int* tick) {
+    typedef typename MmT<WT>::frag frag;
+    constexpr int NWV = 4, RW = 64, U = 1;  // waves, rows per unit, chunks per lane (piece <= 512)
+    __shared__ __attribute__((aligned(16))) uint16_t xp[3 * MM_MT * (MMK_PIECE + 16)];
+    __shared__ float scl[MM_MT];
+    __shared__ int last_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, g = lane >> 4;
+    const int n_pieces = (a.K + MMK_PIECE - 1) / MMK_PIECE;
+    const int tiles = (a.N + RW - 1) / RW;
+    const int piece = blockIdx.x % n_pieces, tile = blockIdx.x / n_pieces;
+    const int k0 = piece * MMK_PIECE, klen = min(MMK_PIECE, a.K - k0);
+    const int steps = klen >> 5;  // host: every piece a multiple of 64
+    const int KP = MMK_PIECE + 16;
+    const int j0 = tile * RW + 16 * wave;
+    const WT* pa = reinterpret_cast<const WT*>(a.W) + (long)min(j0 + col, a.N - 1) * a.ldw + k0 + 8 * g;
+    // token rows of this piece: wave w stages rows w and w + 4 (loads before the weight stream)
+    MmRowU<U> r0, r1;
+    const int m0 = wave, m1 = wave + NWV;
+    if (m0 < a.M) mm_row_load<false, U>(r0, a.x + (long)m0 * a.ldx + k0, klen, nullptr);
+    if (m1 < a.M) mm_row_load<false, U>(r1, a.x + (long)m1 * a.ldx + k0, klen, nullptr);
+    frag fa[2], fb[2];
+    auto load = [&](frag(&f)[2], int c) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint4 q = ldg_nt16(pa + 32 * (2 * c + i));
+            __builtin_memcpy(&f[i], &q, 16);
+        }
+    };
+    const int nch = steps / 2;
+    load(fa, 0);
+    if (nch > 1) load(fb, 1);
+    if (m0 < a.M) mm_row_store<WT, false, U>(r0, klen, 0.f, xp, KP, scl, m0);
+    if (m1 < a.M) mm_row_store<WT, false, U>(r1, klen, 0.f, xp, KP, scl, m1);
+    __syncthreads();
+    const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const frag(&f)[2], int c) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int k = 32 * (2 * c + i);
+#pragma unroll
+            for (int p = 2; p >= 0; --p) {
+                const frag b = *reinterpret_cast<const frag*>(bbase + (long)p * MM_MT * KP + k);
+                acc = MmT<WT>::mfma(f[i], b, acc);
+            }
+        }
+    };
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch && c > 0) load(fb, c + 1);
+        compute(fa, c);
+        if (c + 1 >= nch) break;
+        if (c + 2 < nch) load(fa, c + 2);
+        compute(fb, c + 1);
+    }
+    if (col < a.M && j0 < a.N) {
+        const float sc = scl[col];
+        float* dst = part + ((long)piece * MM_MT + col) * a.N + j0 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (j0 + 4 * g + i < a.N) __hip_atomic_store(dst + i, acc[i] * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(tick + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == n_pieces - 1;
+        if (last) __hip_atomic_store(tick + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
+    for (int i = tid; i < RW * MM_MT; i += NWV * 64) {
+        const int m = i / RW, n = tile * RW + i % RW;
+        if (m >= a.M || n >= a.N) continue;
+        float v = 0.f;
+        for (int pc = 0; pc < n_pieces; ++pc)
+            v += __hip_atomic_load(part + ((long)pc * MM_MT + m) * a.N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
+        float* yp = a.y + (long)m * a.ldy + n;
+        if (a.accumulate) v = *yp + v;
+        *yp = v;
+    }
+    (void)tiles;
+}
+
+bool dec_mm_splitk_ok(const DecGemvArgs& a) {
+    return a.M >= 1 && a.M <= MM_MT && a.K % 64 == 0 && a.N >= 16 && !a.norm_w && !a.xn_out && a.ldw % 8 == 0 &&
+           a.ldx % 4 == 0;
+}
+
+size_t dec_mm_splitk_part_floats(int N, int K) { return (size_t)((K + MMK_PIECE - 1) / MMK_PIECE) * MM_MT * N; }
+size_t dec_mm_splitk_ticks(int N) { return (size_t)(N + 63) / 64; }
+
+void launch_dec_mm_splitk(const DecGemvArgs& a, float* part, int* tick, hipStream_t s) {
+    if (!dec_mm_splitk_ok(a) || !part || !tick) throw std::runtime_error("EINVAL: dec_mm_splitk outside its range");
+    const int n_pieces = (a.K + MMK_PIECE - 1) / MMK_PIECE, tiles = (a.N + 63) / 64;
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_mm_splitk_kernel<bf16_t>), dim3(n_pieces * tiles), dim3(256), 0, s, a, part, tick);
+    else DSOCR_LAUNCH((dec_mm_splitk_kernel<f16_t>), dim3(n_pieces * tiles), dim3(256), 0, s, a, part, tick);
+}
+
 }  // namespace dsocr

@@ -180,6 +180,13 @@ bool dec_mm_ok(const DecGemvArgs& a);
 void launch_dec_mm(const DecGemvArgs& a, hipStream_t s);
 // W [N][K] -> dec_mm fragment order ([N/16][K/32][64][8] 16-bit): every wave weight load one 1 KiB block
 size_t mm_swizzle_elems(int N, int K);
+// long-K form (K % 64 == 0, any length; the dense layer-0 down projection): split-K over pieces of 512
+// with write-through partial tiles and an in-launch last-arriver sum; part / tick sized below, tick
+// zero between launches (the last arriver resets it)
+bool dec_mm_splitk_ok(const DecGemvArgs& a);
+size_t dec_mm_splitk_part_floats(int N, int K);
+size_t dec_mm_splitk_ticks(int N);
+void launch_dec_mm_splitk(const DecGemvArgs& a, float* part, int* tick, hipStream_t s);
 void launch_mm_swizzle(const void* w, int N, int K, void* out, hipStream_t s);
 // Router GEMV whose last-arriving block writes the greedy top-k of every token (T <= 8).
 struct DecRouteEpi {

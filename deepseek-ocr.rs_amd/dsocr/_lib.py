@@ -84,7 +84,7 @@ EXPORTS = [
     "dsocr_k_sample_greedy", "dsocr_k_sample_stoch", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
     "dsocr_generate_trace", "dsocr_k_moe_kernels", "dsocr_k_lmhead_screened",
     "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
-    "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16",
+    "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16", "dsocr_k_gemv_splitk",
 ]
 
 _lib = None
@@ -138,6 +138,7 @@ def lib():
     L.dsocr_resize_bicubic.argtypes = [vp, u32, u32, vp, u32, u32]
     L.dsocr_k_gemm.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_gemv.argtypes = [i32, i32, i32, vp, vp, f32, vp, i32, vp, vp, i32, i32]
+    L.dsocr_k_gemv_splitk.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32]
     L.dsocr_k_layernorm.argtypes = [i32, i32, vp, vp, vp, f32, vp]
     L.dsocr_k_rmsnorm.argtypes = [i32, i32, vp, vp, f32, vp]
     L.dsocr_k_dsq_dequant.argtypes = [i32, vp, sz, sz, sz, vp]

@@ -216,6 +216,10 @@ dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, in
  * act(xn . W^T + bias) (+ y), xn = rmsnorm(x; norm_w, eps) when norm_w != NULL (block.rs:24-29), else x. */
 dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm_w, float eps, const void* W,
                           int wdtype, const float* bias, float* y, int act, int accumulate);
+/* Long-K decode linear for 1..8 rows on the matrix cores (the dense layer-0 down projection of the
+ * 3..8-page decode, K = 6848): y[M][N] (+)= x . W^T + bias, split-K with an in-launch ordered sum. */
+dsocr_status dsocr_k_gemv_splitk(int M, int N, int K, const float* x, const void* W, int wdtype, const float* bias,
+                                 float* y, int accumulate);
 dsocr_status dsocr_k_layernorm(int rows, int cols, const float* x, const float* w, const float* b, float eps,
                                float* y);
 /* DSQ record payload (device bytes, crates/dsq/src/lib.rs:60-110 dtype codes 0/1/8/12/14/16) ->

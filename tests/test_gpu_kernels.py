@@ -73,6 +73,21 @@ def test_gemv(gpu, M, N, K, wdt, norm):
     assert np.all(np.abs(dy.get() - ref) <= _bound(xn, w) + 1e-6 * np.abs(ref))
 
 
+@pytest.mark.parametrize("M,N,K,acc", [(8, 1280, 6848, True), (3, 1280, 6848, False), (5, 200, 640, True)])
+def test_gemv_splitk(gpu, M, N, K, acc):
+    """Long-K decode linear on the matrix cores (the dense layer-0 down projection at 3..8 pages):
+    split-K pieces of 512 with per-(row, piece) scaled f16 planes, in-launch ordered sum."""
+    rng = np.random.default_rng(N + K + M)
+    x = (rng.standard_normal((M, K)) * np.exp(rng.standard_normal((M, 1)) * 3)).astype(np.float32)
+    bits, w = _weights(rng, N, K, 1)
+    y0 = rng.standard_normal((M, N)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    dx, dW, dy, db = Dev(x), Dev(bits), Dev(y0 if acc else np.zeros((M, N), np.float32)), Dev(bias)
+    check(lib().dsocr_k_gemv_splitk(M, N, K, dx.ptr, dW.ptr, 1, db.ptr, dy.ptr, int(acc)))
+    ref = (x.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias + (y0 if acc else 0)
+    assert np.all(np.abs(dy.get() - ref) <= _bound(x, w) + 1e-6 * np.abs(ref))
+
+
 @pytest.mark.parametrize("rows,cols,eps", [(4096, 768, 1e-6), (257, 1024, 1e-5), (100, 256, 1e-6)])
 def test_layernorm(gpu, rows, cols, eps):
     rng = np.random.default_rng(rows)
