@@ -268,6 +268,9 @@ def main():
     ap.add_argument("--workload", default="deepseek", choices=["deepseek", "dots2048"],
                     help="deepseek: configs[1]/[2] (default); dots2048: configs[3], the dots.ocr vision tower")
     ap.add_argument("--dots-size", type=int, default=2044)
+    ap.add_argument("--snapshot", default=None, choices=["q4k"],
+                    help="q4k: configs[4], a full-size synthetic Q4_K DSQ snapshot loaded through the engine's "
+                         "dequant-on-load path (written to $TMPDIR first)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -299,9 +302,24 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    snap = None
+    if args.snapshot == "q4k":
+        import tempfile
+
+        from dsocr.synth import write_synthetic_snapshot
+        snap_path = os.path.join(tempfile.gettempdir(), f"dsocr_synth_q4k_r{rank}.dsq")
+        t = time.time()
+        snap = write_synthetic_snapshot(json.load(open(dsocr.FULL_CONFIG)), snap_path, seed=0)
+        snap["write_s"] = round(time.time() - t, 1)
+        log(f"[rank {rank}] synthetic Q4_K snapshot {snap} -> {snap_path}")
     t_load = time.time()
-    eng = load_model(ModelLoadArgs(config_path=dsocr.FULL_CONFIG, synthetic_seed=0, dtype="f16", device=local))
-    log(f"[rank {rank}] engine loaded on hip:{local} in {time.time() - t_load:.1f}s")
+    eng = load_model(ModelLoadArgs(config_path=dsocr.FULL_CONFIG, synthetic_seed=0, dtype="f16", device=local,
+                                   snapshot_path=snap_path if snap else None))
+    load_s = time.time() - t_load
+    log(f"[rank {rank}] engine loaded on hip:{local} in {load_s:.1f}s")
+    if snap:
+        snap["load_s"] = round(load_s, 1)
+        os.unlink(snap_path)  # the engine holds the dequantised weights in HBM
     tok = SyntheticTokenizer(eng.vocab)
     vs = VisionSettings(1024, 640, True)
     ppg = args.pages_per_gpu
@@ -371,7 +389,7 @@ def main():
                                if prof.get(k, {}).get("avg_us", 0) > 0},
                     "kv_len": prof["kv_len"]}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not snap:
             b = batches[args.warmup]
             try:
                 cpu = cpu_baseline(b[0], b[1][0][0], b[1][0][1], args.max_new_tokens, args.cpu_decode_steps)
@@ -389,13 +407,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (fp16-rounded decoder weights, bf16 vision/lm_head weights)",
-            "data": "synthetic 1024x1024 pages + seeded synthetic weights (no checkpoint offline)",
-            "config": {"workload": "configs[1]: deepseek-ocr, 1024x1024 page, crop (2,2), 706-token prefill, "
-                                   "512 greedy tokens" if ppg == 1 else f"deepseek-ocr, {ppg} pages/GPU batch",
+            "dtype": ("f32 (Q4_K / Q8_0 snapshot linears dequantised to fp16 at load)" if snap else
+                      "f32 (fp16-rounded decoder weights, bf16 vision/lm_head weights)"),
+            "data": "synthetic 1024x1024 pages + seeded synthetic weights (no checkpoint offline)"
+                    + ("; snapshot linears: random valid Q4_K / Q8_0 blocks" if snap else ""),
+            "config": {"workload": ("configs[4]: deepseek-ocr-q4k DSQ snapshot, dequant-on-load -> fp16 kernels, "
+                                    f"{ppg} pages/GPU batch") if snap else
+                                   ("configs[1]: deepseek-ocr, 1024x1024 page, crop (2,2), 706-token prefill, "
+                                    "512 greedy tokens" if ppg == 1 else f"deepseek-ocr, {ppg} pages/GPU batch"),
                        "pages_per_gpu": ppg, "global_batch": ppg * world, "prefill_tokens": len(batches[0][1][0][0]),
                        "max_new_tokens": args.max_new_tokens, "parallelism": f"dp{world}"},
             "stage_ms": {k: round(v, 2) for k, v in stage.items()},
+            "snapshot": snap,
             "host_prepare_ms_per_page": round(prep_ms, 2),
             "gpu_prepare_ms_per_page": round(gpu_prep_ms, 2),
             "roofline": roofline,

@@ -230,6 +230,33 @@ def test_adapter_discovery_full_config():
     assert specs[-2][:3] == ("lm_head.weight", 129280, 1280)
 
 
+def test_synthetic_snapshot_generator(tmp_path):
+    """dsocr.synth.write_synthetic_snapshot (the bench's configs[4] input): the adapter's record list,
+    the quantizer's dtype choice (lm_head / projector Q8_0, Q4_K unless in_dim % 256 falls back to
+    Q8_0), a container the reader accepts, values of the synthetic checkpoint's scale."""
+    import dsocr
+    from dsocr.synth import snapshot_dtype, snapshot_linears, write_synthetic_snapshot
+    for cfgp in (TINY256, dsocr.FULL_CONFIG):
+        cfg = json.load(open(cfgp))
+        assert [r[:3] for r in snapshot_linears(cfg)] == [r[:3] for r in dsq.discover_linears(cfg)]
+    assert snapshot_dtype("model.layers.1.mlp.experts.3.down_proj.weight", 896) == dsq.Q8_0
+    assert snapshot_dtype("model.layers.0.mlp.down_proj.weight", 6848) == dsq.Q8_0
+    assert snapshot_dtype("model.layers.1.mlp.shared_experts.down_proj.weight", 1792) == dsq.Q4K
+    assert snapshot_dtype("lm_head.weight", 1280) == dsq.Q8_0
+    cfg = json.load(open(TINY256))
+    path = str(tmp_path / "synth.dsq")
+    info = write_synthetic_snapshot(cfg, path, seed=3)
+    snap = dsq.Snapshot(path)
+    assert info["records"] == len(snap.records) and info["bytes"] == os.path.getsize(path)
+    assert snap.header["default_qdtype"] == dsq.Q4K and snap.header["block_size"] == 256
+    for name, out_dim, in_dim, bias in dsq.discover_linears(cfg):
+        r = snap.records[name]
+        assert (r["out_dim"], r["in_dim"], r["q_dtype"]) == (out_dim, in_dim, snapshot_dtype(name, in_dim))
+        w = snap.weight(name)
+        assert np.isfinite(w).all() and 0.01 < float(w.std()) < 0.04 and abs(float(w.mean())) < 0.005
+        assert (snap.bias_for(name) is not None) == name.startswith("model.projector")
+
+
 # ------------------------------------------------------------------ GPU
 def make_tiny256_snapshot(path):
     """Every linear of the tiny256 model from the seeded synthetic checkpoint (bf16 values), in
@@ -336,3 +363,39 @@ def test_snapshot_load_errors(gpu, snap_path, tmp_path):
     dsq.write_dsq(wrong, [("lm_head.weight", 256, 512, dsq.Q8_0, dsq.quantize(dsq.Q8_0, np.zeros((256, 512), np.float32)), None)])
     with pytest.raises(DsocrError, match="EINVAL"):
         load_model(ModelLoadArgs(config_path=TINY256, synthetic_seed=SEED, dtype="f16", snapshot_path=wrong))
+
+
+@pytest.mark.gpu
+def test_full_q4k_snapshot_engine_matches_oracle(gpu, tmp_path):
+    """configs[4] at its size: a full-size synthetic Q4_K snapshot (the bench's input: 1491 Q4_K and
+    707 Q8_0 records, 2.05 GB) loaded through the engine's dequant-on-load path; text prompts so the
+    oracle only dequantises the experts it routes to.  One page: ids and per-step logits (the same
+    2e-3 bar as tests/test_full_parity.py) vs the oracle; 8 pages (the matrix-core decode of the
+    configs[2]/[4] batch): ids vs the oracle per page."""
+    import dsocr
+    from dsocr import DecodeParameters, ModelLoadArgs, load_model
+    from dsocr.synth import write_synthetic_snapshot
+    from oracle.model import OracleModel
+    from oracle.weights import Weights
+    cfg = json.load(open(dsocr.FULL_CONFIG))
+    path = str(tmp_path / "full_q4k.dsq")
+    write_synthetic_snapshot(cfg, path, seed=0)
+    n_new = 12
+    rng = np.random.default_rng(9)
+    prompts = [rng.integers(16, 129000, int(rng.integers(6, 20))).astype(np.int64) for _ in range(8)]
+    eng = load_model(ModelLoadArgs(config_path=dsocr.FULL_CONFIG, synthetic_seed=0, dtype="f16", snapshot_path=path))
+    try:
+        params = DecodeParameters(max_new_tokens=n_new)
+        ids1, logits = eng.generate_trace([(prompts[0], None, None, None)], params, ignore_eos=True)
+        ids8 = eng.generate_batch([(p, None, None, None) for p in prompts], params, ignore_eos=True)
+    finally:
+        eng.close()
+    oracle = OracleModel(cfg, Weights(seed=0, dtype="f16", snapshot=dsq.Snapshot(path)))
+    for i, p in enumerate(prompts):
+        ref, lg = oracle.generate(p, np.zeros(len(p), np.uint8), None, n_new, eos_token_id=None,
+                                  record_logits=(i == 0), ignore_eos=True)
+        if i == 0:
+            assert ids1[0] == ref
+            err = max(float(np.max(np.abs(logits[0, s] - lg[s]))) for s in range(n_new))
+            assert err < 2e-3, err
+        assert ids8[i] == ref, (i, ids8[i], ref)
