@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "dev_common.hpp"
 #include "kernels.hpp"
@@ -1326,6 +1327,23 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 // CH keys per block (64 or 32: env DSOCR_ATT_CH); LPK = 256 / CH lanes score one key.
 constexpr int DA2_CH_MIN = 32;
 
+// an empty asm that takes N float4 registers as operands (4 at a time): the loads that produced them
+// stay above this point
+template <int N>
+__device__ __forceinline__ void keep_f4(const float4* r) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+        f4v t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 u = r[min(i + j, N - 1)];
+            t[j] = f4v{u.x, u.y, u.z, u.w};
+        }
+        asm volatile("" ::"v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]));
+    }
+}
+
 // sum over aligned groups of N lanes (N = 4 or 8), result in every lane of the group
 template <int N>
 __device__ __forceinline__ float group_sum(float v) {
@@ -1422,13 +1440,15 @@ __device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, 
 // loads), then run the attention chunk exactly as the unfused kernel.
 // PREROT: the q / k rows arrive already rotated (dec_qkv_rope applied RoPE in its epilogue), so
 // q, k_new and v_new are loaded before the position and no RoPE table is read here.
-template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false>
+template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false, int NSUB = 1>
 __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
     constexpr int DG = HD / 4, KG = 256 / DG, KPG = CH / KG;     // PV: float4 dim groups x key groups
+    constexpr int KB = CH * NSUB;                                // keys per block (NSUB sub-chunks of CH)
     static_assert(LPK == 4 || LPK == 8, "CH must be 64 or 32");
     static_assert(KPG >= 1 && DPL % 4 == 0, "unsupported head_dim / chunk");
+    static_assert(NSUB == 1 || !FUSED, "the fused q/k/v path runs one chunk per block");
     __shared__ float qs[HD];
     __shared__ float knew[HD];
     __shared__ float vnew[HD];
@@ -1444,7 +1464,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         a.stamps[sbid * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();                         \
     }
     AT_STAMP(0);
-    const int k0 = c * CH;
+    const int k0 = c * KB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvh = h / (a.heads / a.kv_heads);
     float* Kc = a.kc + (long)b * a.page_stride + (long)kvh * a.head_stride;
@@ -1457,13 +1477,29 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     const int dg = tid % DG, kg = tid / DG;
     float4 kreg[DPL / 4];
     float4 vreg[KPG];
-    auto issue_kv = [&](int klim) {
-        const float4* kp = reinterpret_cast<const float4*>(Kc + (long)min(k0 + key, klim) * HD + sub * DPL);
+    // TK (64-key chunks of 128-dim heads): K is loaded like V, instruction i of wave w reading keys
+    // w*16 + 2i and w*16 + 2i + 1 whole (1 KiB contiguous per instruction: 8 L2 lines, where one
+    // key per 4 lanes touched 64 lines per instruction); lane l holds dims 4 (l & 31) .. + 3 of key
+    // tk_key(i) = w*16 + 2i + (l >> 5), and the q.k dot products are finished by a transposing
+    // butterfly over the 32 lanes of a key (9 swizzle / DPP adds for 8 keys).
+    constexpr bool TK = CH == 64 && HD == 128;
+    const int tk_half = lane >> 5, tk_d4 = (lane & 31) * 4;
+    auto tk_key = [&](int i) { return wave * 16 + 2 * i + tk_half; };
+    auto issue_k = [&](int kb, int klim) {
+        if constexpr (TK) {
 #pragma unroll
-        for (int i = 0; i < DPL / 4; ++i) kreg[i] = kp[i];
+            for (int i = 0; i < 8; ++i)
+                kreg[i] = *reinterpret_cast<const float4*>(Kc + (long)min(kb + tk_key(i), klim) * HD + tk_d4);
+        } else {
+            const float4* kp = reinterpret_cast<const float4*>(Kc + (long)min(kb + key, klim) * HD + sub * DPL);
+#pragma unroll
+            for (int i = 0; i < DPL / 4; ++i) kreg[i] = kp[i];
+        }
+    };
+    auto issue_v = [&](int kb, int klim) {
 #pragma unroll
         for (int j = 0; j < KPG; ++j) {
-            const int kk = min(k0 + kg * KPG + j, klim);
+            const int kk = min(kb + (TK ? tk_key(j) : kg * KPG + j), klim);
             vreg[j] = *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4);
         }
     };
@@ -1477,14 +1513,21 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     }
     // EARLY (one page: latency-bound): the chunk's K / V loads go out before the position is known,
     // clamped to the cache capacity (keys past pos are masked at use), overlapping the pos round trip
-    if (EARLY) issue_kv(kcap);
     const int pos = a.kv_pos[b];
+    if (EARLY) {
+        issue_k(k0, kcap);
+        issue_v(k0, kcap);
+        // every loaded register is an operand here, so the compiler cannot sink a cache load below
+        // the position test (it did: two round trips instead of one); the test then waits for the
+        // loads, which left with the position load
+        keep_f4<DPL / 4>(kreg);
+        keep_f4<KPG>(vreg);
+    }
     const int len = pos + 1;
     if (k0 >= len) return;
-    const int kn = min(CH, len - k0);
-    if (!EARLY) issue_kv(k0 + kn - 1);
-    const bool own = pos >= k0 && pos < k0 + CH;
-    const int nc = (len + CH - 1) / CH;
+    if (!EARLY) { issue_k(k0, min(k0 + CH, len) - 1); issue_v(k0, min(k0 + CH, len) - 1); }
+    const bool own = pos >= k0 && pos < k0 + KB;
+    const int nc = (len + KB - 1) / KB;
     if (FUSED) qkv_rows_for_head<HD>(a, b, h, c, nc, smem);
     // 2. RoPE inputs
     const float* krow = row + a.heads * HD + kvh * HD;
@@ -1539,61 +1582,126 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     }
     __syncthreads();
     AT_STAMP(1);
-    // 4. scores: LPK lanes per key, wave w owns keys w*CH/4 .. (w+1)*CH/4 - 1
-    {
-        float acc = 0.f;
-        if (key < kn) {
-            if (k0 + key == pos) {
-#pragma unroll
-                for (int i = 0; i < DPL; ++i) acc = fmaf(qs[sub * DPL + i], knew[sub * DPL + i], acc);
-            } else {
-#pragma unroll
-                for (int i = 0; i < DPL / 4; ++i) {
-                    acc = fmaf(qs[sub * DPL + 4 * i + 0], kreg[i].x, acc);
-                    acc = fmaf(qs[sub * DPL + 4 * i + 1], kreg[i].y, acc);
-                    acc = fmaf(qs[sub * DPL + 4 * i + 2], kreg[i].z, acc);
-                    acc = fmaf(qs[sub * DPL + 4 * i + 3], kreg[i].w, acc);
-                }
-            }
-        }
-        acc = group_sum<LPK>(acc);
-        const float sc = key < kn ? acc * a.scale : -INFINITY;
-        if (sub == 0) p_s[key] = sc;
-        const float mw = wave_max(sc);
-        if (lane == 0) red[wave] = mw;
-    }
-    __syncthreads();
-    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (wave == 0) {  // whole wave active for the DPP reduction
-        const float p = (tid < CH && tid < kn) ? expf(p_s[tid] - m) : 0.f;
-        if (tid < CH) p_s[tid] = p;
-        const float l = wave_sum(p);
-        if (tid == 0) red[4] = l;
-    }
-    __syncthreads();
-    AT_STAMP(2);
-    // 5. P.V over this thread's KPG keys
+    // NSUB sub-chunks of CH keys, merged in registers by the online softmax (running max m, sum l,
+    // and this thread's P.V partial o, each rescaled by exp(m_old - m_new)); the next sub-chunk's K
+    // loads go out once the scores consumed kreg, its V loads once P.V consumed vreg.  NSUB = 1 is
+    // the one-chunk arithmetic exactly (the first sub-chunk assigns, it does not rescale).
+    float m = -INFINITY, l_run = 0.f;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < KPG; ++j) {
-        const int key2 = kg * KPG + j;
-        if (key2 >= kn) vreg[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // never 0 * (stale cache bits)
-        else if (k0 + key2 == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
-    }
+    for (int s = 0; s < NSUB; ++s) {
+        const int ks = k0 + s * CH;
+        if (s > 0 && ks >= len) break;  // block-uniform
+        const int kn = min(CH, len - ks);
+        const bool more = s + 1 < NSUB && ks + CH < len;
+        // 4. scores: LPK lanes per key, wave w owns keys w*CH/4 .. (w+1)*CH/4 - 1
+        if constexpr (TK) {
+            const float4 q4 = *reinterpret_cast<const float4*>(qs + tk_d4);
+            const float4 kn4 = *reinterpret_cast<const float4*>(knew + tk_d4);
+            float v[8];
 #pragma unroll
-    for (int j = 0; j < KPG; ++j) {
-        const float p = p_s[kg * KPG + j];
-        o.x = fmaf(p, vreg[j].x, o.x);
-        o.y = fmaf(p, vreg[j].y, o.y);
-        o.z = fmaf(p, vreg[j].z, o.z);
-        o.w = fmaf(p, vreg[j].w, o.w);
+            for (int i = 0; i < 8; ++i) {
+                const float4 k4 = ks + tk_key(i) == pos ? kn4 : kreg[i];
+                v[i] = fmaf(q4.w, k4.w, fmaf(q4.z, k4.z, fmaf(q4.y, k4.y, q4.x * k4.x)));
+            }
+            if (more) issue_k(ks + CH, len - 1);
+            // butterfly: after the xor-16 / 8 / 4 steps lane l holds key i = b2 + 2 b3 + 4 b4 (bits of l)
+            // summed over its 8 lanes of that bit pattern; the quad sum finishes the 32 lanes
+            const int b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1;
+            float u[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float keep = b4 ? v[j + 4] : v[j], send = b4 ? v[j] : v[j + 4];
+                u[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (16 << 10)));
+            }
+            float t[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float keep = b3 ? u[j + 2] : u[j], send = b3 ? u[j] : u[j + 2];
+                t[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (8 << 10)));
+            }
+            float r;
+            {
+                const float keep = b2 ? t[1] : t[0], send = b2 ? t[0] : t[1];
+                r = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (4 << 10)));
+            }
+            r = group_sum<4>(r);
+            const int kk = tk_key(b2 + 2 * b3 + 4 * b4);
+            const float sc = kk < kn ? r * a.scale : -INFINITY;
+            if ((lane & 3) == 0) p_s[kk] = sc;
+            const float mw = wave_max(sc);
+            if (lane == 0) red[wave] = mw;
+        } else {
+            float acc = 0.f;
+            if (key < kn) {
+                if (ks + key == pos) {
+#pragma unroll
+                    for (int i = 0; i < DPL; ++i) acc = fmaf(qs[sub * DPL + i], knew[sub * DPL + i], acc);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < DPL / 4; ++i) {
+                        acc = fmaf(qs[sub * DPL + 4 * i + 0], kreg[i].x, acc);
+                        acc = fmaf(qs[sub * DPL + 4 * i + 1], kreg[i].y, acc);
+                        acc = fmaf(qs[sub * DPL + 4 * i + 2], kreg[i].z, acc);
+                        acc = fmaf(qs[sub * DPL + 4 * i + 3], kreg[i].w, acc);
+                    }
+                }
+            }
+            if (more) issue_k(ks + CH, len - 1);
+            acc = group_sum<LPK>(acc);
+            const float sc = key < kn ? acc * a.scale : -INFINITY;
+            if (sub == 0) p_s[key] = sc;
+            const float mw = wave_max(sc);
+            if (lane == 0) red[wave] = mw;
+        }
+        __syncthreads();
+        const float mc = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        const float mn = s == 0 ? mc : fmaxf(m, mc);
+        if (wave == 0) {  // whole wave active for the DPP reduction
+            const float p = (tid < CH && tid < kn) ? expf(p_s[tid] - mn) : 0.f;
+            if (tid < CH) p_s[tid] = p;
+            const float l = wave_sum(p);
+            if (tid == 0) red[4] = l;
+        }
+        __syncthreads();
+        if (s == 0) AT_STAMP(2);
+        // 5. P.V over this thread's KPG keys
+        float4 oc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < KPG; ++j) {
+            const int key2 = TK ? tk_key(j) : kg * KPG + j;
+            if (key2 >= kn) vreg[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // never 0 * (stale cache bits)
+            else if (ks + key2 == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < KPG; ++j) {
+            const float p = p_s[TK ? tk_key(j) : kg * KPG + j];
+            oc.x = fmaf(p, vreg[j].x, oc.x);
+            oc.y = fmaf(p, vreg[j].y, oc.y);
+            oc.z = fmaf(p, vreg[j].z, oc.z);
+            oc.w = fmaf(p, vreg[j].w, oc.w);
+        }
+        if (more) issue_v(ks + CH, len - 1);
+        if (s == 0) {
+            o = oc;
+            l_run = red[4];
+        } else {
+            const float al = expf(m - mn);
+            o.x = fmaf(o.x, al, oc.x);
+            o.y = fmaf(o.y, al, oc.y);
+            o.z = fmaf(o.z, al, oc.z);
+            o.w = fmaf(o.w, al, oc.w);
+            l_run = fmaf(l_run, al, red[4]);
+        }
+        m = mn;
+        if (more) __syncthreads();  // p_s / red are rewritten by the next sub-chunk
     }
     o_s[tid] = o;
     __syncthreads();
     if (a.split) {
         // split mode: no in-kernel combine; per (page, head) [m[CM] | l[CM] | o[CM][HD]] for the o_proj
         // kernel's combine prologue (next launch: plain stores; o rows coalesce along d)
-        const int CM = (a.max_len + CH - 1) / CH;
+        const int CM = (a.max_len + KB - 1) / KB;
         float* Q = a.part + ((long)b * a.heads + h) * (2 + HD) * CM;
         if (tid < DG) {
             float4 t = o_s[tid];
@@ -1605,14 +1713,14 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         }
         if (tid == 0) {
             Q[c] = m;
-            Q[CM + c] = red[4];
+            Q[CM + c] = l_run;
         }
         return;
     }
     // partial record of chunk c: [m, l, -, -, o[HD]] (16-byte aligned), stored WRITE-THROUGH (sc1)
     // so the hand-off needs no L2-writeback release fence (cdna_hip_programming.md Guideline 16 R1)
     constexpr int PR = HD + 4;
-    const int chunks = (a.max_len + CH - 1) / CH;
+    const int chunks = (a.max_len + KB - 1) / KB;
     float* part0 = a.part + ((long)b * a.heads + h) * chunks * PR;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part0, (short)0, chunks * PR * 4, 0x00020000);
     if (tid < DG) {
@@ -1626,7 +1734,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (c * PR + 4 + tid * 4) * 4, 0, 16);
     }
     if (tid == 0) {
-        const float ml[4] = {m, red[4], 0.f, 0.f};
+        const float ml[4] = {m, l_run, 0.f, 0.f};
         u32x4 bits;
         __builtin_memcpy(&bits, ml, 16);
         __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
@@ -1718,6 +1826,13 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     attn_body<HD, CH, PREROT, false, EARLY>(a, nullptr);
 }
 
+// NSUB sub-chunks per block: at most 128 VGPRs (4 blocks per CU), so the grid of >= 600 blocks is
+// resident at once (without the cap the compiler hoists the next sub-chunk's loads to 132 VGPRs)
+template <int HD, int CH, bool PREROT, int NSUB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void dec_attn_sub_kernel(DecAttn2Args a) {
+    attn_body<HD, CH, PREROT, false, false, NSUB>(a, nullptr);
+}
+
 template <int HD, int CH>
 __global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecAttn2Args a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1747,16 +1862,43 @@ size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
     return (size_t)B * heads * ((max_len + DA2_CH_MIN - 1) / DA2_CH_MIN) * (hd + 4) * sizeof(float);
 }
 
+// Keys per block: NSUB sub-chunks of ch (env DSOCR_ATT_NSUB).  A block holds its chunk's K / V in
+// registers (90 VGPRs: 5 blocks per CU), so 8 pages at L 1217 (1600 blocks) run 1.25 rounds; NSUB 2
+// keeps the grid within one round but each block's second sub-chunk then waits behind the first.
+static int dec_attn_nsub(const DecAttn2Args& a, int chunks) {
+    const char* e = getenv("DSOCR_ATT_NSUB");
+    if (e) {
+        const int v = atoi(e);
+        return v >= 4 ? 4 : v >= 2 ? 2 : 1;
+    }
+    (void)a; (void)chunks;  // 2 / 4 measured slower at 8 pages (27.5 / 37.2 vs 26.0 us at L 1217)
+    return 1;
+}
+
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     if (!a.counters) throw std::runtime_error("EINTERNAL: dec_attn needs a zeroed counter array");
     const int ch = dec_attn_ch();
     if (a.max_len > 512 * ch) throw std::runtime_error("EINVAL: decode context too long for the attention combine");
     if (a.hd != 128 && a.hd != 64 && a.hd != 32) throw std::runtime_error("EINVAL: decode attention supports head_dim 32 / 64 / 128");
     const int chunks = (a.max_len + ch - 1) / ch;
-    dim3 g1(chunks, a.heads, a.B);
     const bool prerot = a.prerot != 0;
-    static const bool early_env = !(getenv("DSOCR_ATT_EARLY") && atoi(getenv("DSOCR_ATT_EARLY")) == 0);
+    // EARLY (K / V loads before the position, one page): measured slower once the loads really go
+    // out first (7.9 vs 8.7 us at L 707: the test then waits for the whole chunk), so opt-in
+    static const bool early_env = getenv("DSOCR_ATT_EARLY") && atoi(getenv("DSOCR_ATT_EARLY")) != 0;
     const bool early = early_env && a.B == 1;
+    const int nsub = (ch == 64 && a.hd == 128 && !a.split) ? dec_attn_nsub(a, chunks) : 1;
+    if (nsub > 1) {
+        dim3 g((chunks + nsub - 1) / nsub, a.heads, a.B);
+#define DSOCR_DAN(NS)                                                                                   \
+        do {                                                                                            \
+            if (prerot) DSOCR_LAUNCH((dec_attn_sub_kernel<128, 64, true, NS>), g, dim3(256), 0, s, a);      \
+            else DSOCR_LAUNCH((dec_attn_sub_kernel<128, 64, false, NS>), g, dim3(256), 0, s, a);            \
+        } while (0)
+        if (nsub == 2) DSOCR_DAN(2); else DSOCR_DAN(4);
+#undef DSOCR_DAN
+        return;
+    }
+    dim3 g1(chunks, a.heads, a.B);
 #define DSOCR_DA(HDV, CHV)                                                                          \
     do {                                                                                             \
         if (prerot && early) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true, true>), g1, dim3(256), 0, s, a);  \

@@ -170,15 +170,24 @@ def test_attention_sam_relpos(gpu, g, rel_len):
         assert np.max(np.abs(got[:, hl] - ref)) < 5e-5
 
 
-@pytest.mark.parametrize("B,heads,kvh,hd,max_len", [(1, 10, 10, 128, 1218), (3, 4, 4, 32, 300),
-                                                   (5, 12, 4, 64, 700), (2, 10, 10, 128, 257), (1, 10, 10, 128, 64)])
-@pytest.mark.parametrize("chunk", ["64", "32"])
-def test_decode_attention(gpu, B, heads, kvh, hd, max_len, chunk, monkeypatch):
+@pytest.mark.parametrize("B,heads,kvh,hd,max_len,chunk,nsub", [
+    (1, 10, 10, 128, 1218, "64", None), (3, 4, 4, 32, 300, "64", None), (5, 12, 4, 64, 700, "64", None),
+    (2, 10, 10, 128, 257, "64", None), (1, 10, 10, 128, 64, "64", None), (1, 10, 10, 128, 1218, "32", None),
+    (3, 4, 4, 32, 300, "32", None), (5, 12, 4, 64, 700, "32", None), (2, 10, 10, 128, 257, "32", None),
+    (1, 10, 10, 128, 64, "32", None),
+    # several 64-key sub-chunks per block (online softmax across them): the 8-page shape picks 2 itself
+    (8, 10, 10, 128, 1218, "64", None), (3, 10, 10, 128, 1218, "64", "2"), (2, 10, 10, 128, 300, "64", "4"),
+    (1, 10, 10, 128, 130, "64", "4")])
+def test_decode_attention(gpu, B, heads, kvh, hd, max_len, chunk, nsub, monkeypatch):
     """Fused decode attention (block.rs:608-789 at seq_len 1): RoPE on q / new k (block.rs:1403-1471),
     K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the f32 cache (64- and
-    32-key chunks per block)."""
+    32-key chunks, 1, 2 or 4 chunks per block)."""
     from types import SimpleNamespace
     monkeypatch.setenv("DSOCR_ATT_CH", chunk)
+    if nsub is None:
+        monkeypatch.delenv("DSOCR_ATT_NSUB", raising=False)
+    else:
+        monkeypatch.setenv("DSOCR_ATT_NSUB", nsub)
     from oracle.decoder import apply_rope, rope_tables
     rng = np.random.default_rng(B * hd + max_len)
     qkvw = (heads + 2 * kvh) * hd
