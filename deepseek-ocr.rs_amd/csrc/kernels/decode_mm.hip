@@ -560,7 +560,6 @@ __global__ __launch_bounds__(512, 4) void moe_down_mm_kernel(MoeDec2Args a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
     __shared__ int last_s;
-    __shared__ unsigned char mem_s[72][MM_MT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 15, g = lane >> 4;
     const int n_act = a.grp[0];
@@ -665,29 +664,27 @@ __global__ __launch_bounds__(512, 4) void moe_down_mm_kernel(MoeDec2Args a) {
     __syncthreads();
     if (!last_s) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
-    // the last arriver: which segments carry token t, then the ordered sum over segments
-    for (int i = tid; i < n_seg * MM_MT; i += NWV * 64) {
-        const int sg = i / MM_MT, t = i % MM_MT;
-        unsigned char m = 0;
-        if (t < a.T) {
-            if (sg >= n_act) {
-                m = 1;
-            } else {
-                const int* rr = a.grp + MOE_GRP_REC * (1 + sg);
-                const int cnt = rr[1];
-                for (int q = 0; q < cnt; ++q) m |= (rr[2 + q] / a.topk == t) ? 1 : 0;
-            }
-        }
-        mem_s[sg][t] = m;
-    }
-    __syncthreads();
+    // the last arriver: the ordered sum over segments.  A token's column of a segment it does not
+    // belong to was computed from a zero B column, so it holds exact zeros and adding it leaves every
+    // partial sum unchanged; all segments are therefore summed unconditionally, with the loads of a
+    // batch of 24 in flight together (a per-segment membership test made every load its own L2 round
+    // trip: 17 in a row at 8 pages)
+    constexpr int SB = 24;
     for (int i = tid; i < RT * MM_MT; i += NWV * 64) {
         const int t = i / RT, j = tile * RT + i % RT;
         if (t >= a.T) continue;
+        const float* src = a.dn_part + (long)t * a.Hout + j;
+        const long sstride = (long)MM_MT * a.Hout;
         float v = 0.f;
-        for (int sg = 0; sg < n_seg; ++sg)
-            if (mem_s[sg][t])
-                v += __hip_atomic_load(a.dn_part + ((long)sg * MM_MT + t) * a.Hout + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int s0 = 0; s0 < n_seg; s0 += SB) {
+            float pv[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q)
+                pv[q] = __hip_atomic_load(src + min(s0 + q, n_seg - 1) * sstride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int q = 0; q < SB; ++q)
+                if (s0 + q < n_seg) v += pv[q];
+        }
         float* op = a.out + (long)t * a.Hout + j;
         *op = *op + v;
     }
@@ -1011,8 +1008,17 @@ __global__ __launch_bounds__(256) void dec_mm_splitk_kernel(DecGemvArgs a, float
         const int m = i / RW, n = tile * RW + i % RW;
         if (m >= a.M || n >= a.N) continue;
         float v = 0.f;
-        for (int pc = 0; pc < n_pieces; ++pc)
-            v += __hip_atomic_load(part + ((long)pc * MM_MT + m) * a.N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        constexpr int SB = 16;  // pieces in flight together (one L2 round trip per batch, in order)
+        for (int p0 = 0; p0 < n_pieces; p0 += SB) {
+            float pv[SB];
+#pragma unroll
+            for (int q = 0; q < SB; ++q)
+                pv[q] = __hip_atomic_load(part + ((long)min(p0 + q, n_pieces - 1) * MM_MT + m) * a.N + n,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int q = 0; q < SB; ++q)
+                if (p0 + q < n_pieces) v += pv[q];
+        }
         v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
         float* yp = a.y + (long)m * a.ldy + n;
         if (a.accumulate) v = *yp + v;
