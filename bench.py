@@ -358,7 +358,7 @@ def main():
     elapsed = time.perf_counter() - t0
     iterative_s = sum(t["decode_iterative_ms"] for t in timings) / 1e3
     stage = {k: sum(t[k] for t in timings) / len(timings)
-             for k in ("vision_compute_ms", "decode_prefill_ms", "decode_iterative_ms")}
+             for k in ("vision_compute_ms", "decode_prefill_ms", "decode_iterative_ms", "vision_flops", "prefill_flops")}
     tokens_rank = args.steps * ppg * args.max_new_tokens
     tok_s_rank = tokens_rank / iterative_s if iterative_s > 0 else 0.0
     elapsed, tok_s = reduce_over_ranks(dist, elapsed, tok_s_rank)
@@ -417,7 +417,20 @@ def main():
                                     "512 greedy tokens" if ppg == 1 else f"deepseek-ocr, {ppg} pages/GPU batch"),
                        "pages_per_gpu": ppg, "global_batch": ppg * world, "prefill_tokens": len(batches[0][1][0][0]),
                        "max_new_tokens": args.max_new_tokens, "parallelism": f"dp{world}"},
-            "stage_ms": {k: round(v, 2) for k, v in stage.items()},
+            "stage_ms": {k: round(stage[k], 2) for k in ("vision_compute_ms", "decode_prefill_ms", "decode_iterative_ms")},
+            # MFMA roofline of the compute-bound stages: algorithmic f32 FLOPs (engine-counted: linears 2MNK,
+            # attention 4 Lq Lk d per head, causal prefill the lower triangle) / stage time, against the
+            # dense bf16 MFMA peak the split-plane GEMMs run on; the exact-f32 contract issues each linear
+            # as 3 (vision, bf16 weights) or 5 (prefill, f16 weights) bf16 planes, so `issued_frac` = plane
+            # count x frac for the linears (the attention runs on the f32 MFMA / 3 bf16 planes of P)
+            "roofline_mfma": {
+                stg: {"bound": "mfma", "achieved": round(fl / (ms * 1e-3) / 1e12, 1), "peak": 2500.0,
+                      "unit": "TFLOP/s", "frac": round(fl / (ms * 1e-3) / 1e12 / 2500.0, 4),
+                      "issued_frac": round(planes * fl / (ms * 1e-3) / 1e12 / 2500.0, 4),
+                      "tflop_per_page": round(fl / ppg / 1e12, 3), "ms_per_batch": round(ms, 2)}
+                for stg, fl, ms, planes in (("vision", stage["vision_flops"], stage["vision_compute_ms"], 3),
+                                            ("prefill", stage["prefill_flops"], stage["decode_prefill_ms"], 5))
+                if fl > 0 and ms > 0},
             "snapshot": snap,
             "host_prepare_ms_per_page": round(prep_ms, 2),
             "gpu_prepare_ms_per_page": round(gpu_prep_ms, 2),

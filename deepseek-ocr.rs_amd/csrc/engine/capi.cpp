@@ -297,6 +297,8 @@ dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t) {
         t->decode_generate_ms = x.generate_ms;
         t->decode_steps = x.steps;
         t->pages = x.pages;
+        t->vision_flops = x.vision_flops;
+        t->prefill_flops = x.prefill_flops;
     });
 }
 

@@ -619,6 +619,7 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
 // ============================================================================ compute helpers
 void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int ldy, int act, int accumulate,
                     const int* c_rows) {
+    flops_acc_ += 2.0 * M * (double)l.N * l.K;
     if (M <= 16 && !c_rows) {
         DecGemvArgs a;
         a.M = M; a.N = l.N; a.K = l.K; a.x = x; a.ldx = ldx; a.W = l.W; a.ldw = l.K; a.wdtype = l.wdt;
@@ -792,6 +793,7 @@ float* Engine::vision_pass(const float* imgs, int n, int Spx, const std::string&
             a.rel_h = gg;
             a.rel_w = gg;
         }
+        flops_acc_ += 4.0 * nseq * (double)L * L * hd * heads;
         launch_attention(a, st);
         // proj + residual (window_unpartition via row scatter)
         linear(ctx, (int)arows, C, blk.proj, x, C, 0, 1, win ? d_win2tok : nullptr);
@@ -846,6 +848,7 @@ float* Engine::vision_pass(const float* imgs, int n, int Spx, const std::string&
         a.kv_heads = CC.heads;
         a.hd = chd;
         a.scale = (float)(1.0 / std::sqrt((double)chd));
+        flops_acc_ += 4.0 * n * (double)T * T * chd * CC.heads;
         launch_attention(a, st);
         linear(cctx, (int)crow, CH, cl.out, cx, CH, 0, 1);
         launch_layernorm(cx, CH, cxn, CH, nullptr, (int)crow, CH, cl.ln2.w, cl.ln2.b, 1e-5f, st);
@@ -935,6 +938,8 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     a.heads = L.heads; a.kv_heads = L.kv_heads; a.hd = hd;
     a.scale = (float)(1.0 / std::sqrt((double)hd));
     a.causal = 1;
+    for (int q = 0; q < B && q < (int)prefill_lens_.size(); ++q)
+        flops_acc_ += 2.0 * (double)prefill_lens_[q] * (prefill_lens_[q] + 1) * hd * L.heads;
     launch_attention(a, st);
     (void)Lmax;
     (void)KVH;
@@ -968,6 +973,7 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     g1.wdtype = d.e_wdt; g1.w_group_stride = (long)2 * I * H; g1.C = G; g1.ldc = 2 * I;
     g1.group_off = EOFF; g1.groups = E; g1.max_group_rows = T;
     launch_gemm(g1, st);
+    flops_acc_ += 2.0 * TK * (2.0 * I) * H + 2.0 * TK * (double)H * I;  // routed gate/up + down (next launch)
     launch_silu_mul(G, 2 * I, I, TK, HH, I, st);
     GemmArgs g2;
     g2.M = TK; g2.N = H; g2.K = I; g2.A = HH; g2.lda = I; g2.W = d.e_d; g2.ldw = I; g2.wdtype = d.e_wdt;
@@ -1279,6 +1285,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
     auto t0 = clock::now();
     HIP_CHECK(hipEventRecord(ev[0], st));
+    flops_acc_ = 0;
 
     // ---------------- 1. vision (compute_image_embeddings, batched over pages)
     std::vector<int> prompt_len(B);
@@ -1350,6 +1357,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         }
     }
     HIP_CHECK(hipEventRecord(ev[1], st));
+    timings_.vision_flops = flops_acc_;
 
     // ---------------- 2. image rows for the injection (model/mod.rs:1208-1239)
     // host image rows of all pages concatenated (kind 1), device vision rows via per-row pointers:
@@ -1445,6 +1453,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         long Tn = 0;
         int maxl = 0;
         for (int b = 0; b < B; ++b) { Tn += lens[b]; maxl = std::max(maxl, lens[b]); }
+        prefill_lens_ = lens;
         std::vector<int> kind(Tn), index(Tn), row_page(Tn), row_pos(Tn);
         std::vector<long> q_off(B), kv_off(B), o_off(B);
         long r0 = 0;
@@ -1492,6 +1501,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         linear(SXN, B, H, lm_head_, LOGITS, L.vocab);
     };
     HIP_CHECK(hipEventRecord(ev[2], st));
+    flops_acc_ = 0;
     std::vector<std::vector<int>> extra(B);
     forward_rows(prompt_len, extra);
 
@@ -1574,6 +1584,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         HIP_CHECK(hipStreamSynchronize(st));
     }
     HIP_CHECK(hipEventRecord(ev[3], st));
+    timings_.prefill_flops = flops_acc_;
     std::vector<int> h_done(B), h_outlen(B);
     std::vector<int> h_out;
     size_t steps = 0;

@@ -103,6 +103,9 @@ struct PagePixels {
 struct Timings {
     double vision_prepare_ms = 0, vision_compute_ms = 0, prefill_ms = 0, iterative_ms = 0, generate_ms = 0;
     size_t steps = 0, pages = 0;
+    // algorithmic f32 FLOPs of the stage (linears 2 M N K, attention 4 L_q L_k d per head; causal
+    // prefill counts the lower triangle): the MFMA roofline's numerator
+    double vision_flops = 0, prefill_flops = 0;
 };
 
 struct GenRequest {
@@ -238,6 +241,8 @@ class Engine {
     size_t kv_bytes_ = 0;
     long page_stride_ = 0, head_stride_ = 0;
     Timings timings_;
+    double flops_acc_ = 0;  // FLOPs issued by linear() / attention since the last stage mark
+    std::vector<int> prefill_lens_;  // rows per page of the prefill being issued
     int last_B_ = 0;
     std::map<std::string, std::pair<void*, size_t>> pinned_;
     std::map<std::pair<int, int>, std::pair<int*, int*>> winmaps_;  // (n, grid) -> tok2win, win2tok

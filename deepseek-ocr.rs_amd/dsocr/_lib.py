@@ -51,7 +51,8 @@ class ResultC(C.Structure):
 class TimingsC(C.Structure):
     _fields_ = [("vision_prepare_ms", C.c_double), ("vision_compute_ms", C.c_double),
                 ("decode_prefill_ms", C.c_double), ("decode_iterative_ms", C.c_double),
-                ("decode_generate_ms", C.c_double), ("decode_steps", C.c_size_t), ("pages", C.c_size_t)]
+                ("decode_generate_ms", C.c_double), ("decode_steps", C.c_size_t), ("pages", C.c_size_t),
+                ("vision_flops", C.c_double), ("prefill_flops", C.c_double)]
 
 
 class KernelProfileC(C.Structure):

@@ -108,6 +108,8 @@ typedef struct {
     double decode_generate_ms;    /* decode.generate */
     size_t decode_steps;          /* decode forwards executed */
     size_t pages;
+    double vision_flops;          /* algorithmic f32 FLOPs of vision.compute_embeddings (linears 2MNK, */
+    double prefill_flops;         /* attention 4 Lq Lk d per head, causal: lower triangle) and of decode.prefill */
 } dsocr_timings;
 
 /* ---- engine lifecycle (load_model, model/mod.rs:90-115; DeepseekOcrModel::load 946-1105) */
