@@ -375,6 +375,26 @@ dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, in
         check_hip(hipDeviceSynchronize(), "gemm");
     });
 }
+dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W_bf16, const float* bias, float* C,
+                               int act, int accumulate, int splits) {
+    return guarded([&] {
+        dsocr::GemmBf16Args g;
+        g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.W = W_bf16; g.ldw = K; g.bias = bias;
+        g.C = C; g.ldc = N; g.act = act; g.accumulate = accumulate;
+        if (!dsocr::gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
+        g.splits = splits > 0 ? splits : dsocr::gemm_f32a_splits(M, N, K);
+        float* part = nullptr;
+        if (g.splits > 1) {
+            check_hip(hipMalloc(&part, sizeof(float) * (size_t)g.splits * M * N), "hipMalloc");
+            g.part = part;
+        }
+        dsocr::launch_gemm_f32a(g, nullptr);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (part) (void)hipFree(part);
+        check_hip(e, "gemm_f32a");
+    });
+}
 dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm_w, float eps, const void* W,
                           int wdtype, const float* bias, float* y, int act, int accumulate) {
     return guarded([&] {

@@ -635,6 +635,16 @@ void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int 
         g.splits = gemm_bf16_splits(M, l.N, 5 * l.K);
         if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
         launch_gemm_bf16(g, stream_);
+    } else if (l.W3 && l.wdt == WDT_BF16 && l.K % 32 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+               !(getenv("DSOCR_GEMM_FUSED") && atoi(getenv("DSOCR_GEMM_FUSED")) == 0) &&
+               !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
+        // bf16 weights, f32 rows split into 3 bf16 planes inside the GEMM's fragment loads
+        GemmBf16Args g;
+        g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K;
+        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
+        g.splits = gemm_f32a_splits(M, l.N, l.K);
+        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
+        launch_gemm_f32a(g, stream_);
     } else if (l.W3 && ldx % 4 == 0 && !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
         // f32 rows -> [lo | mid | hi] bf16 planes, then one bf16 NT GEMM over K3 = 3K
         void* planes = ws("g_planes", (size_t)M * 3 * l.K * 2);

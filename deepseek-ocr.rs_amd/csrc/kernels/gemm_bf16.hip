@@ -12,6 +12,7 @@
 // chunks via the SOURCE address so the fragment ds_read_b128s are conflict-free), counted vmcnt +
 // raw s_barrier (cdna_hip_programming.md §5, "Pipelining across barriers"), XCD-aware tile order.
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "dev_common.hpp"
@@ -26,14 +27,17 @@ constexpr int TB_M = 128, TB_N = 128, TB_K = 64;
 constexpr int TB_STAGE = (TB_M + TB_N) * TB_K;  // bf16 elements per stage
 
 // 128 rows x 64 bf16 (128-byte rows): wave w, instruction i fills rows (4w + i) * 8 .. + 7; lane L
-// writes LDS row R + L / 8, slot L % 8, which holds global chunk (L % 8) ^ (row & 7).
+// writes LDS row R + L / 8, slot L % 8, which holds global chunk (L % 8) ^ ((row >> 1) & 7).  Two rows
+// share a 256-B bank row, so row r's 16-B chunk c sits in slot (r & 1) * 8 + (c ^ ((r >> 1) & 7)): the 16
+// rows of each ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, + 32) land on 16
+// distinct slots (MI355X_MICROARCH.md §LDS; the former c ^ (r & 7) put rows 12 and 20 on one slot).
 __device__ __forceinline__ void stage_tile(const uint16_t* g, long ld, int r0, int rmax, int k0, uint16_t* lds,
                                            int wave, int lane) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int R = (wave * 4 + i) * 8;
         const int r = R + (lane >> 3);
-        const int j = (lane & 7) ^ (r & 7);
+        const int j = (lane & 7) ^ ((r >> 1) & 7);
         const long row = min(r0 + r, rmax);
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + row * ld + k0 + j * 8),
                                          (lds_void*)(lds + R * TB_K), 16, 0, 0);
@@ -42,7 +46,7 @@ __device__ __forceinline__ void stage_tile(const uint16_t* g, long ld, int r0, i
 
 // fragment of rows r .. r + 31 (lane & 31), k chunk kc + (lane >> 5), from a swizzled tile
 __device__ __forceinline__ bf16x8_v frag(const uint16_t* lds, int r, int kc) {
-    const int c = kc ^ (r & 7);
+    const int c = kc ^ ((r >> 1) & 7);
     return *reinterpret_cast<const bf16x8_v*>(lds + r * TB_K + c * 8);
 }
 
@@ -199,6 +203,190 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);
     hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    if (g.splits > 1) {
+        const long n = (long)g.M * g.N;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// The same exact-f32 linear with the plane split fused into the fragment loads: A stays f32 in HBM
+// and LDS, W is the plain bf16 [N][K] weight (not tripled).  Per 16-k step a wave reads its two f32 A
+// fragments (8 values per lane), splits each value exactly into hi + mid + lo bf16 (split3_rows'
+// RNE steps) in registers, and issues lo.W, mid.W, hi.W on v_mfma_f32_32x32x16_bf16 against the
+// same B fragment: the weight bytes per product fall to 1/3, the separate split pass (6 bytes per
+// activation written and re-read) disappears, and every product stays exact in the f32 accumulator.
+// Tiles 128 x 128 x 32, 4 waves as 2 x 2 of 64 x 64, two LDS stages of A 16 KB f32 + W 8 KB (three
+// blocks per CU) filled by 16-byte global_load_lds, one raw s_barrier per k-step (stage k + 1 is issued
+// after it, into the buffer every wave finished reading before it), counted vmcnt.  XOR-swizzled
+// 16-byte chunks (A rows 128 B: chunk ^ ((r >> 1) & 7); W rows 64 B: chunk ^ ((r >> 2) & 3)) put every
+// ds_read_b128 lane group on 16 distinct slots of the 256-B bank row (SQ_LDS_BANK_CONFLICT 0).  The
+// bijective XCD-aware tile order and deterministic split-K of gemm_bf16_nt_kernel.  Measured and not
+// kept: a third / fourth stage (fewer blocks per CU, slower or equal), register-staged loads with
+// ds_write_b128 (1.7x slower).
+constexpr int FX_M = 128, FX_N = 128, FX_K = 32;
+constexpr int FX_AS = FX_M * FX_K;      // f32 elements of an A stage
+constexpr int FX_WS = FX_N * FX_K;      // bf16 elements of a W stage
+
+__device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
+    bf16x8_v r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    return r;
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
+    __shared__ __attribute__((aligned(16))) float a_lds[2 * FX_AS];
+    __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * FX_WS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntn = (g.N + FX_N - 1) / FX_N;
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int split = wgid % g.splits, tile = wgid / g.splits;
+    const int bm = tile / ntn, bn = tile % ntn;
+    const int m0 = bm * FX_M, n0 = bn * FX_N;
+    const float* A = reinterpret_cast<const float*>(g.A);
+    const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nk_all = g.K / FX_K;
+    const int kbeg = (int)((long)nk_all * split / g.splits), kend = (int)((long)nk_all * (split + 1) / g.splits);
+    const int nk = kend - kbeg;
+    // A: 128 rows x 32 f32 (8 chunks of 16 B per row); instruction i of wave w fills rows (4w + i) * 8 .. + 7
+    // W: 128 rows x 32 bf16 (4 chunks per row);     instruction i of wave w fills rows (2w + i) * 16 .. + 15
+    // (LDS-DMA writes lane-linearly: lane L's 16 B land in row R + L / 8 (W: L / 4), slot L % 8 (L % 4),
+    // so the lane fetches the global chunk that the swizzle puts in that slot)
+    auto issue = [&](int kt) {
+        const int k0 = (kbeg + kt) * FX_K;
+        float* as = a_lds + (kt & 1) * FX_AS;
+        uint16_t* ws_ = w_lds + (kt & 1) * FX_WS;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int R = (wave * 4 + i) * 8;
+            const int r = R + (lane >> 3);
+            const int j = (lane & 7) ^ ((r >> 1) & 7);
+            const long row = min(m0 + r, g.M - 1);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(A + row * g.lda + k0 + j * 4),
+                                             (lds_void*)(as + R * FX_K), 16, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int R = (wave * 2 + i) * 16;
+            const int r = R + (lane >> 2);
+            const int j = (lane & 3) ^ ((r >> 2) & 3);
+            const long row = min(n0 + r, g.N - 1);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(W + row * g.ldw + k0 + j * 8),
+                                             (lds_void*)(ws_ + R * FX_K), 16, 0, 0);
+        }
+    };
+    if (nk > 0) issue(0);
+    for (int kt = 0; kt < nk; ++kt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage kt landed
+        __builtin_amdgcn_s_barrier();  // every wave's stage kt landed; every wave is done with stage kt - 1
+        asm volatile("" ::: "memory");
+        if (kt + 1 < nk) issue(kt + 1);  // into stage (kt - 1) & 1
+        const float* As = a_lds + (kt & 1) * FX_AS;
+        const uint16_t* Ws = w_lds + (kt & 1) * FX_WS;
+#pragma unroll
+        for (int ks = 0; ks < FX_K / 16; ++ks) {
+            const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of 4)
+            bf16x8_v bfv[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = wn * 64 + j * 32 + (lane & 31);
+                bfv[j] = *reinterpret_cast<const bf16x8_v*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = wm * 64 + i * 32 + (lane & 31);
+                const int sw = (r >> 1) & 7;
+                const float4 lo4 = *reinterpret_cast<const float4*>(As + r * FX_K + (((2 * kc) ^ sw) * 4));
+                const float4 hi4 = *reinterpret_cast<const float4*>(As + r * FX_K + (((2 * kc + 1) ^ sw) * 4));
+                const float av[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                float h[8], m[8], l[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    h[e] = (float)(__bf16)av[e];
+                    const float r1 = av[e] - h[e];
+                    m[e] = (float)(__bf16)r1;
+                    l[e] = r1 - m[e];
+                }
+                const bf16x8_v ph = fx_pack(h), pm = fx_pack(m), pl = fx_pack(l);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's reads done before the next barrier
+    }
+    const int half = lane >> 5, l32 = lane & 31;
+    if (g.splits > 1) {
+        float* P = g.part + (long)split * g.M * g.N;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = n0 + wn * 64 + j * 32 + l32;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    if (row < g.M && col < g.N) P[(long)row * g.N + col] = acc[i][j][r];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + l32;
+            if (col >= g.N) continue;
+            const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (row >= g.M) continue;
+                const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;
+                if (orow < 0) continue;
+                float v = apply_act(acc[i][j][r] + bv, g.act);
+                float* cp = g.C + orow * (long)g.ldc + col;
+                if (g.accumulate) v += *cp;
+                *cp = v;
+            }
+        }
+    }
+}
+
+int gemm_f32a_splits(int M, int N, int K) {
+    const int tiles = ((M + FX_M - 1) / FX_M) * ((N + FX_N - 1) / FX_N);
+    const int nk = K / FX_K;
+    int sp = 1;
+    while (tiles * sp < 256 && nk / (sp * 2) >= 16) sp *= 2;
+    return sp;
+}
+
+bool gemm_f32a_ok(const GemmBf16Args& g) {
+    return g.K % FX_K == 0 && g.lda % 4 == 0 && g.ldw % 8 == 0 && (reinterpret_cast<uintptr_t>(g.A) & 15) == 0 &&
+           (reinterpret_cast<uintptr_t>(g.W) & 15) == 0 && !g.out_bf16;
+}
+
+void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
+    GemmBf16Args g = g0;
+    if (g.M <= 0 || g.N <= 0) return;
+    if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
+    if (g.splits < 1 || !g.part) g.splits = 1;
+    const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
+    hipLaunchKernelGGL(gemm_f32a_nt_kernel, dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) {
         const long n = (long)g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);

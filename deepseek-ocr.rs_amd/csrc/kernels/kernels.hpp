@@ -37,6 +37,10 @@ struct GemmBf16Args {
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
 int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)
+// f32 A x bf16 W^T with the exact 3-plane split fused into the fragment loads (K % 32 == 0, f32 out)
+bool gemm_f32a_ok(const GemmBf16Args& g);
+int gemm_f32a_splits(int M, int N, int K);
+void launch_gemm_f32a(const GemmBf16Args& g, hipStream_t s);
 // f16-weight form: A5 = [lo | mid | mid | hi | hi] planes, W5 = [w_hi | w_lo | w_hi | w_lo | w_hi]
 void launch_split5_rows(const float* x, long ldx, int M, int K, void* out, long ldo, hipStream_t s);
 void launch_make_w5(const void* w, int N, int K, void* out, hipStream_t s);

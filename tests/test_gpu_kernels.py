@@ -52,6 +52,26 @@ def test_gemm(gpu, M, N, K, wdt, act, acc):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
+@pytest.mark.parametrize("M,N,K,act,acc,splits", [(256, 256, 256, 0, 0, 1), (1000, 770, 768, 1, 0, 0),
+                                                  (6400, 768, 3072, 0, 1, 0), (257, 3072, 1024, 2, 0, 0),
+                                                  (77, 130, 96, 0, 1, 3), (4096, 2304, 768, 0, 0, 1),
+                                                  (693, 1280, 2048, 0, 0, 0)])
+def test_gemm_f32a(gpu, M, N, K, act, acc, splits):
+    """Vision linear on the fused-split kernel (bf16 weights, f32 activations split into 3 exact bf16
+    planes in the fragment loads) vs an f64 matmul, incl. split-K and the accumulate epilogue."""
+    rng = np.random.default_rng(M * 7 + N + K)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    bits, w = _weights(rng, N, K, 0)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
+    dA, dW, dB, dC = Dev(a), Dev(bits), Dev(bias), Dev(c0)
+    check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, dB.ptr, dC.ptr, act, acc, splits))
+    ref = ACTS[act]((a.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias) + (c0 if acc else 0)
+    got = dC.get()
+    bound = _bound(a, w) * (2.0 if act else 1.0)
+    assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
+
+
 @pytest.mark.parametrize("M,N,K,wdt,norm", [(1, 1280, 1280, 1, True), (1, 129280, 1280, 0, True),
                                             (2, 3840, 1280, 1, True), (3, 3840, 1280, 1, False),
                                             (8, 896, 1792, 1, False), (16, 100, 64, 0, False),
