@@ -567,8 +567,8 @@ dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const flo
             }
             if (T >= 3 && T <= 8) {
                 a.dn_part = (float*)alloc(sizeof(float) * dsocr::moe_down_mm_part_floats(E, T, topk, I, a.Is, H));
-                a.dn_tick = (int*)alloc(sizeof(int) * (H / 128 + 1));
-                check_hip(hipMemset(a.dn_tick, 0, sizeof(int) * (H / 128 + 1)), "hipMemset");
+                a.dn_tick = (int*)alloc(sizeof(int) * (H / 64 + 1));
+                check_hip(hipMemset(a.dn_tick, 0, sizeof(int) * (H / 64 + 1)), "hipMemset");
             }
             if (T > 8) {
                 a.eoff = (int*)alloc(sizeof(int) * (E + 1)); a.arow = (int*)alloc(sizeof(int) * TK);

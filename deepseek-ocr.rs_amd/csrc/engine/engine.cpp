@@ -1027,7 +1027,7 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     a.route_cnt = wsi("s_route_cnt", 16);
     if (B >= 3 && B <= 8) {  // matrix-core grouped kernels: down partials + tickets
         a.dn_part = wsf("s_dnpart", moe_down_mm_part_floats(E, B, K, I, a.Is, H));
-        a.dn_tick = wsi("s_dntick", (size_t)H / 128 + 1);
+        a.dn_tick = wsi("s_dntick", (size_t)H / 64 + 1);  // one ticket per 64-row tile
     }
     if (B <= 8 && d.e_gu_swz && (!d.has_shared || d.s_gu_swz)) {  // fragment-ordered experts
         a.Wgu_swz = d.e_gu_swz; a.Wd_swz = d.e_d_swz; a.sWgu_swz = d.s_gu_swz; a.sWd_swz = d.s_d_swz;
@@ -1445,7 +1445,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // arrival tickets of the decode-attention combine: zero here, every launch leaves them zero
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
-    HIP_CHECK(hipMemsetAsync(wsi("s_dntick", (size_t)H / 128 + 1), 0, sizeof(int) * (H / 128 + 1), st));
+    HIP_CHECK(hipMemsetAsync(wsi("s_dntick", (size_t)H / 64 + 1), 0, sizeof(int) * (H / 64 + 1), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
     HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));

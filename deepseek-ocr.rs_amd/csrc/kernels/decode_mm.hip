@@ -553,10 +553,10 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
 // ticket completes the tile (every segment stored) sums the segments in order (records by expert id,
 // then the shared pieces) with sc1 loads and adds to out (split-K seam: MI355X_MICROARCH.md price list
 // 'splitk-seam'; hand-off: the sc1-load table's first row).
-template <typename WT, int PF, bool SWZ>
-__global__ __launch_bounds__(512, 4) void moe_down_mm_kernel(MoeDec2Args a) {
+template <typename WT, int PF, bool SWZ, int NWV>
+__global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a) {
     typedef typename MmT<WT>::frag frag;
-    constexpr int NWV = 8, RT = 128, U = 2;  // waves, rows per unit, chunks per lane (I <= 1024)
+    constexpr int RT = 16 * NWV, U = 2;  // rows per unit (16 per wave), chunks per lane (I <= 1024)
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
     __shared__ int last_s;
@@ -599,31 +599,40 @@ __global__ __launch_bounds__(512, 4) void moe_down_mm_kernel(MoeDec2Args a) {
             __builtin_memcpy(&f[i], &q, 16);
         }
     };
-    // wave w stages token column w: the h~ row of its pick of this expert (shared: hs[w] piece)
-    const float* srcrow = nullptr;
-    if (wave < a.T) {
-        if (shared) {
-            srcrow = a.hs + (long)wave * a.Is + (long)hpiece * a.I;
-        } else {
-            const int cnt = rec[1];
-            for (int q = 0; q < cnt; ++q) {
-                const int r = rec[2 + q];
-                if (r / a.topk == wave) srcrow = a.h + (long)r * a.I;
-            }
+    // wave w stages token columns w (and w + NWV when NWV < 8): the h~ row of the token's pick of this
+    // expert (shared: hs[t] piece), zero when the token did not pick it
+    auto src_of = [&](int t) -> const float* {
+        if (t >= a.T) return nullptr;
+        if (shared) return a.hs + (long)t * a.Is + (long)hpiece * a.I;
+        const float* p = nullptr;
+        const int cnt = rec[1];
+        for (int q = 0; q < cnt; ++q) {
+            const int r = rec[2 + q];
+            if (r / a.topk == t) p = a.h + (long)r * a.I;
         }
+        return p;
+    };
+    constexpr int SPW = MM_MT / NWV;  // token columns staged per wave
+    const float* srcrow[SPW];
+    MmRowU<U> xr[SPW];
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) {
+        srcrow[q] = src_of(wave + q * NWV);
+        if (srcrow[q]) mm_row_load<false, U>(xr[q], srcrow[q], a.I, nullptr);
     }
-    MmRowU<U> xr;
-    if (srcrow) mm_row_load<false, U>(xr, srcrow, a.I, nullptr);
     load(fa, 0);
     if (nch > 1) load(fb, 1);
     const int KP = mm_pitch(a.I);
-    if (!srcrow) {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+    for (int q = 0; q < SPW; ++q) {
+        if (!srcrow[q]) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xr.v[u][j] = 0.f;
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xr[q].v[u][j] = 0.f;
+        }
+        mm_row_store<WT, false, U>(xr[q], a.I, 0.f, xp, KP, scl, wave + q * NWV);
     }
-    mm_row_store<WT, false, U>(xr, a.I, 0.f, xp, KP, scl, wave);
     __syncthreads();
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -701,12 +710,23 @@ size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H) {
     return (size_t)(std::min(E, T * topk) + (I > 0 && Is > 0 ? Is / I : 0)) * MM_MT * H;
 }
 
+// Units of 64 output rows (4 waves) by default: 17 segments x 20 row tiles = 340 blocks at 8 pages,
+// where 128-row units (8 waves) left a third of the CUs idle (170 blocks); DSOCR_DOWN_RT=128 restores them.
 void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s) {
     if (!moe_down_mm_ok(a)) throw std::runtime_error("EINVAL: grouped decode down (matrix cores) outside its range");
     const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.I);
     const int max_seg = std::min(a.E, a.T * a.topk) + (a.sWd ? a.Is / a.I : 0);
-    dim3 grid(max_seg * (a.Hout / 128));
-#define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW>), grid, dim3(512), lds, s, a)
+    static const bool rt128 = getenv("DSOCR_DOWN_RT") && atoi(getenv("DSOCR_DOWN_RT")) == 128;
+    if (rt128) {
+        dim3 grid(max_seg * (a.Hout / 128));
+#define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 8>), grid, dim3(512), lds, s, a)
+        if (a.wdtype == WDT_BF16) { if (a.Wd_swz) DSOCR_DM(bf16_t, true); else DSOCR_DM(bf16_t, false); }
+        else { if (a.Wd_swz) DSOCR_DM(f16_t, true); else DSOCR_DM(f16_t, false); }
+#undef DSOCR_DM
+        return;
+    }
+    dim3 grid(max_seg * (a.Hout / 64));
+#define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 4>), grid, dim3(256), lds, s, a)
     if (a.wdtype == WDT_BF16) { if (a.Wd_swz) DSOCR_DM(bf16_t, true); else DSOCR_DM(bf16_t, false); }
     else { if (a.Wd_swz) DSOCR_DM(f16_t, true); else DSOCR_DM(f16_t, false); }
 #undef DSOCR_DM

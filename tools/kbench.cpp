@@ -173,7 +173,7 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     a.route_cnt = (int*)dalloc(64);
     if (T >= 3 && T <= 8) {
         a.dn_part = (float*)dalloc(moe_down_mm_part_floats(E, T, TOPK, I, IS, H) * 4);
-        a.dn_tick = (int*)dalloc(64);
+        a.dn_tick = (int*)dalloc(256);
     }
     auto set = [&](int l) {
         const MoeLayerW& w = g_moe[l % NL];
