@@ -45,6 +45,14 @@ def blas_threads():
     return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
+def visible_gpus():
+    import ctypes as C
+
+    from dsocr._lib import lib
+    n = C.c_int(0)
+    return n.value if lib().dsocr_device_count(C.byref(n)) == 0 else 1
+
+
 def page_indices(step, world, rank, ppg):
     """Pages of one bench step on one rank: rank r of W takes pages [(step*W + r)*ppg, +ppg) —
     disjoint across ranks and steps (data parallel, no collective on the data path)."""
@@ -276,6 +284,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local = local % max(1, visible_gpus())  # one GPU per rank on a node; ranks share a GPU only when there are fewer
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -55,3 +55,26 @@ def test_two_rank_gloo_sharding_and_reduction():
     for _, _, elapsed, tok_s in res:
         assert elapsed == 2.0          # max over ranks
         assert tok_s == 300.0          # sum over ranks
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_two_rank_bench_process_run(gpu):
+    """The N>1 bench as the driver launches it (torch.distributed.run, one process per rank, gloo barrier
+    and max-over-ranks timing), two engines here sharing the box's one GPU (rank r uses GPU r % count):
+    one JSON line from rank 0 whose value counts both ranks' pages."""
+    import json
+    import subprocess
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--max-new-tokens", "8", "--no-cpu-baseline",
+           "--roofline-iters", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 2 and res["value"] > 0
+    assert abs(res["value"] - 2 / (res["ms_per_step"] / 1e3)) < 1e-3 * res["value"] + 1e-3
