@@ -183,13 +183,16 @@ typedef struct dsocr_decode_profile {
                                          the dispatch picks at this batch size, named in moe_gateup_kernel */
     dsocr_kernel_profile moe_down;    /* routed + shared down + combine + residual (moe_down_kernel) */
     dsocr_kernel_profile attention;   /* dec_attn_kernel (RoPE / KV append / flash-decoding / combine): one layer */
-    dsocr_kernel_profile lm_head;     /* exact lm_head: dec_gemv over the 129280 x 1280 rows */
+    dsocr_kernel_profile lm_head;     /* exact lm_head over the 129280 x 1280 rows: dec_gemv_stream (1-2 pages) or
+                                         the matrix-core dec_mm on the fragment-ordered copy (3-8 pages) */
     int experts_touched;              /* routed experts active in the replayed step (per layer, summed / layers) */
     int tokens;                       /* pages in the batch */
     int kv_len;                       /* keys attended by page 0 */
-    dsocr_kernel_profile qkv;         /* dec_gemv: RMSNorm + fused q/k/v projection, one layer */
-    dsocr_kernel_profile o_proj;      /* dec_gemv: o_proj + residual, one layer */
-    dsocr_kernel_profile router;      /* MoE router logits (+ top-k when routed by the router kernel) */
+    dsocr_kernel_profile qkv;         /* RMSNorm + fused q/k/v projection, one layer (dec_qkv_rope with RoPE in the
+                                         epilogue at 1 page, dec_gemv at 2, dec_mm at 3-8) */
+    dsocr_kernel_profile o_proj;      /* o_proj + residual, one layer (dec_gemv at 1-2 pages, dec_mm at 3-8) */
+    dsocr_kernel_profile router;      /* MoE router: dec_gemv logits at 1-2 pages (the mix kernels rank-select),
+                                         dec_route_grp (RMSNorm + logits + top-k + expert records) at 3-8 */
     dsocr_kernel_profile layers_step; /* every decoder layer of one decode step, replayed as one hipGraph */
     dsocr_kernel_profile lm_head_screened; /* int8 screened lm_head + exact rescoring selection (B <= 2, no penalty) */
     const char* moe_gateup_kernel;    /* static strings: kernel names of the two MoE entries above */
