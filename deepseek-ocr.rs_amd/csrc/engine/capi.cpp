@@ -375,11 +375,13 @@ dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, in
         check_hip(hipDeviceSynchronize(), "gemm");
     });
 }
-dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W_bf16, const float* bias, float* C,
-                               int act, int accumulate, int splits) {
+dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias,
+                               float* C, int act, int accumulate, int splits) {
     return guarded([&] {
+        if (wdtype != dsocr::WDT_BF16 && wdtype != dsocr::WDT_F16) throw std::runtime_error("EINVAL: weights must be bf16 or f16");
         dsocr::GemmBf16Args g;
-        g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.W = W_bf16; g.ldw = K; g.bias = bias;
+        g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.W = W; g.ldw = K; g.bias = bias;
+        g.w_f16 = wdtype == dsocr::WDT_F16;
         g.C = C; g.ldc = N; g.act = act; g.accumulate = accumulate;
         if (!dsocr::gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
         g.splits = splits > 0 ? splits : dsocr::gemm_f32a_splits(M, N, K);

@@ -625,6 +625,15 @@ void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int 
         a.M = M; a.N = l.N; a.K = l.K; a.x = x; a.ldx = ldx; a.W = l.W; a.ldw = l.K; a.wdtype = l.wdt;
         a.bias = l.b; a.y = y; a.ldy = ldy; a.act = act; a.accumulate = accumulate;
         launch_dec_gemv(a, stream_);
+    } else if (l.W5 && l.wdt == WDT_F16 && l.K % 32 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+               !(getenv("DSOCR_GEMM_FUSED16") && atoi(getenv("DSOCR_GEMM_FUSED16")) == 0)) {
+        // f16 weights: f32 rows split into 3 bf16 planes and the weight into hi / lo inside the GEMM
+        GemmBf16Args g;
+        g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.w_f16 = 1;
+        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
+        g.splits = gemm_f32a_splits(M, l.N, l.K);
+        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
+        launch_gemm_f32a(g, stream_);
     } else if (l.W5 && ldx % 4 == 0 && !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
         // f16 weights: [lo | mid | mid | hi | hi] planes against W5, one bf16 NT GEMM over K5 = 5K
         void* planes = ws("g_planes", (size_t)M * 5 * l.K * 2);

@@ -235,6 +235,11 @@ __device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
     return r;
 }
 
+// F16W: f16 weights (the decoder's prefill linears): each weight splits exactly into w_hi + w_lo bf16
+// in registers (f16 has 11 significant bits) and the products lo.hi, mid.lo, mid.hi, hi.lo, hi.hi are
+// issued (lo.lo is below f32 rounding: the W5 formulation's set) — 5 MFMAs per fragment pair, A and W
+// read once instead of as 5 bf16 planes each.
+template <bool F16W>
 __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     __shared__ __attribute__((aligned(16))) float a_lds[2 * FX_AS];
     __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * FX_WS];
@@ -297,11 +302,24 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
 #pragma unroll
         for (int ks = 0; ks < FX_K / 16; ++ks) {
             const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of 4)
-            bf16x8_v bfv[2];
+            bf16x8_v bfv[2], blo[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int r = wn * 64 + j * 32 + (lane & 31);
-                bfv[j] = *reinterpret_cast<const bf16x8_v*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+                if constexpr (F16W) {
+                    const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+                    float wv[8], wh[8], wl[8];
+                    unpack8<f16_t>(raw, wv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        wh[e] = (float)(__bf16)wv[e];
+                        wl[e] = wv[e] - wh[e];
+                    }
+                    bfv[j] = fx_pack(wh);
+                    blo[j] = fx_pack(wl);
+                } else {
+                    bfv[j] = *reinterpret_cast<const bf16x8_v*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+                }
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -321,9 +339,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
                 const bf16x8_v ph = fx_pack(h), pm = fx_pack(m), pl = fx_pack(l);
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv[j], acc[i][j], 0, 0, 0);
+                    if constexpr (F16W) {  // small terms first
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, blo[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, blo[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv[j], acc[i][j], 0, 0, 0);
+                    } else {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv[j], acc[i][j], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -386,7 +412,8 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
-    hipLaunchKernelGGL(gemm_f32a_nt_kernel, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    if (g.w_f16) hipLaunchKernelGGL(gemm_f32a_nt_kernel<true>, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL(gemm_f32a_nt_kernel<false>, dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) {
         const long n = (long)g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);

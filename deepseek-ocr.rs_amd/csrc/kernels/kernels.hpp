@@ -34,6 +34,7 @@ struct GemmBf16Args {
     // epilogue rounds to bf16 as the reference's separate bf16 ops do (quant.rs:141-150):
     // v = rnd(acc); bias: v = rnd(v + b); act: v = rnd(act(v)); accumulate: v = rnd(C + v)
     int out_bf16 = 0;
+    int w_f16 = 0;  // gemm_f32a only: W holds f16 values (split into hi / lo bf16 in registers)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
 int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)

@@ -138,7 +138,7 @@ def lib():
     L.dsocr_synth_bf16.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, vp]
     L.dsocr_resize_bicubic.argtypes = [vp, u32, u32, vp, u32, u32]
     L.dsocr_k_gemm.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32]
-    L.dsocr_k_gemm_f32a.argtypes = [i32, i32, i32, vp, vp, vp, vp, i32, i32, i32]
+    L.dsocr_k_gemm_f32a.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32]
     L.dsocr_k_gemv.argtypes = [i32, i32, i32, vp, vp, f32, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_gemv_splitk.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32]
     L.dsocr_k_layernorm.argtypes = [i32, i32, vp, vp, vp, f32, vp]

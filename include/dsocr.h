@@ -217,11 +217,11 @@ dsocr_status dsocr_resize_bicubic(const uint8_t* src, uint32_t sw, uint32_t sh, 
 /* C[M][N] = act(A[M][K] . W[N][K]^T + bias) (+ C if accumulate); wdtype 0 = bf16, 1 = f16 */
 dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias, float* C,
                           int act, int accumulate);
-/* Vision linear (sam.rs:656-701, clip.rs:418-447) on the fused split kernel: f32 A [M][K], bf16 W [N][K],
- * C = act(A W^T + bias) (+ C), exact f32 products (3 bf16 planes of A split in the fragment loads);
- * splits <= 0 picks the engine's split-K count. */
-dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W_bf16, const float* bias, float* C,
-                               int act, int accumulate, int splits);
+/* Vision / prefill linear (sam.rs:656-701, clip.rs:418-447; block.rs linears) on the fused split kernel:
+ * f32 A [M][K], 16-bit W [N][K] (wdtype 0 bf16: 3 bf16 planes of A; 1 f16: W split into hi / lo bf16 too,
+ * 5 products), C = act(A W^T + bias) (+ C), exact f32 products; splits <= 0 picks the engine's split-K. */
+dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias,
+                               float* C, int act, int accumulate, int splits);
 /* Decode linear (transformer/block.rs attention / MLP projections at seq_len 1): y[M][N] =
  * act(xn . W^T + bias) (+ y), xn = rmsnorm(x; norm_w, eps) when norm_w != NULL (block.rs:24-29), else x. */
 dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm_w, float eps, const void* W,

@@ -52,20 +52,23 @@ def test_gemm(gpu, M, N, K, wdt, act, acc):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
-@pytest.mark.parametrize("M,N,K,act,acc,splits", [(256, 256, 256, 0, 0, 1), (1000, 770, 768, 1, 0, 0),
-                                                  (6400, 768, 3072, 0, 1, 0), (257, 3072, 1024, 2, 0, 0),
-                                                  (77, 130, 96, 0, 1, 3), (4096, 2304, 768, 0, 0, 1),
-                                                  (693, 1280, 2048, 0, 0, 0)])
-def test_gemm_f32a(gpu, M, N, K, act, acc, splits):
-    """Vision linear on the fused-split kernel (bf16 weights, f32 activations split into 3 exact bf16
-    planes in the fragment loads) vs an f64 matmul, incl. split-K and the accumulate epilogue."""
+@pytest.mark.parametrize("M,N,K,wdt,act,acc,splits", [(256, 256, 256, 0, 0, 0, 1), (1000, 770, 768, 0, 1, 0, 0),
+                                                      (6400, 768, 3072, 0, 0, 1, 0), (257, 3072, 1024, 0, 2, 0, 0),
+                                                      (77, 130, 96, 0, 0, 1, 3), (4096, 2304, 768, 0, 0, 0, 1),
+                                                      (693, 1280, 2048, 0, 0, 0, 0), (706, 3840, 1280, 1, 0, 0, 0),
+                                                      (706, 1280, 1280, 1, 0, 1, 0), (1412, 13696, 1280, 1, 3, 0, 0),
+                                                      (100, 64, 1280, 1, 0, 0, 2)])
+def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
+    """Vision (bf16 weights: 3 exact bf16 planes of the f32 activations) and prefill (f16 weights, split into
+    hi / lo bf16 as well: 5 products) linears on the fused-split kernel vs an f64 matmul, incl. split-K and
+    the accumulate epilogue."""
     rng = np.random.default_rng(M * 7 + N + K)
     a = rng.standard_normal((M, K)).astype(np.float32)
-    bits, w = _weights(rng, N, K, 0)
+    bits, w = _weights(rng, N, K, wdt)
     bias = rng.standard_normal(N).astype(np.float32) * 0.1
     c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
     dA, dW, dB, dC = Dev(a), Dev(bits), Dev(bias), Dev(c0)
-    check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, dB.ptr, dC.ptr, act, acc, splits))
+    check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, wdt, dB.ptr, dC.ptr, act, acc, splits))
     ref = ACTS[act]((a.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias) + (c0 if acc else 0)
     got = dC.get()
     bound = _bound(a, w) * (2.0 if act else 1.0)
