@@ -38,6 +38,10 @@ __device__ __forceinline__ uint16_t bf_bits(float v) {
     return u;
 }
 
+#ifndef AB_EXP
+#define AB_EXP(x) __expf(x)
+#endif
+
 template <int HD>
 __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) {
     constexpr int KP = HD + 8, VP = AB_KT + 8;   // LDS row pitches (bf16 elements)
@@ -123,13 +127,15 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
             }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float m_new = fmaxf(m_run, tmax);
-        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        // exp on the hardware exp2 with the log2(e) scale folded into one multiply (__expf: a few ulp
+        // from libm's expf; the tower's tolerance is set by its bf16 roundings)
+        const float alpha = (m_new == -INFINITY) ? 1.f : AB_EXP(m_run - m_new);
         float psum = 0.f;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = (m_new == -INFINITY) ? 0.f : expf(sc[u][r] - m_new);
+                const float p = (m_new == -INFINITY) ? 0.f : AB_EXP(sc[u][r] - m_new);
                 sc[u][r] = p;
                 psum += p;
             }
