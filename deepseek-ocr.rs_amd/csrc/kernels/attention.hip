@@ -101,11 +101,11 @@ __global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
         }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float m_new = fmaxf(m_run, tmax);
-        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
         float psum = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            float p = (m_new == -INFINITY) ? 0.f : expf(sc[r] - m_new);
+            float p = (m_new == -INFINITY) ? 0.f : __expf(sc[r] - m_new);
             sc[r] = p;
             psum += p;
         }
@@ -269,11 +269,11 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
         }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float m_new = fmaxf(m_run, tmax);
-        const float alpha = (m_new == -INFINITY) ? 1.f : expf(m_run - m_new);
+        const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
         float psum = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const float p = (m_new == -INFINITY) ? 0.f : expf(sc[r] - m_new);
+            const float p = (m_new == -INFINITY) ? 0.f : __expf(sc[r] - m_new);
             sc[r] = p;
             psum += p;
         }
