@@ -504,20 +504,25 @@ dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, in
             throw std::runtime_error("EINVAL: bad head / rope configuration");
         float* part = nullptr;
         int* cnt = nullptr;
-        check_hip(hipMalloc(&part, dsocr::dec_attn_workspace(B, heads, hd, max_len)), "hipMalloc");
-        check_hip(hipMalloc(&cnt, sizeof(int) * B * heads), "hipMalloc");
-        check_hip(hipMemset(cnt, 0, sizeof(int) * B * heads), "hipMemset");
+        const size_t pb = dsocr::dec_attn_workspace(B, heads, hd, max_len);
+        check_hip(hipMalloc(&part, pb), "hipMalloc");
+        check_hip(hipMalloc(&cnt, sizeof(int) * (B * heads + 1)), "hipMalloc");
+        check_hip(hipMemset(cnt, 0, sizeof(int) * (B * heads + 1)), "hipMemset");
+        dsocr::dec_attn_part_init(part, pb, nullptr);
         dsocr::DecAttn2Args a;
         a.qkv = qkv; a.ld = (long)(heads + 2 * kv_heads) * hd; a.kv_pos = kv_pos; a.B = B; a.heads = heads;
         a.kv_heads = kv_heads; a.hd = hd; a.rope_dim = rope_dim; a.use_mla = 0; a.max_len = max_len;
         a.cos = cos; a.sin = sin; a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd;
         a.page_stride = (long)kv_heads * max_len * hd; a.scale = scale; a.part = part; a.o = o;
-        a.o_ld = (long)heads * hd; a.counters = cnt;
+        a.o_ld = (long)heads * hd; a.counters = cnt; a.err = cnt + B * heads;
         dsocr::launch_dec_attn(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
+        int herr = 0;
+        if (e == hipSuccess) e = hipMemcpy(&herr, a.err, sizeof(int), hipMemcpyDeviceToHost);
         (void)hipFree(part);
         (void)hipFree(cnt);
         check_hip(e, "decode attention");
+        if (herr) throw std::runtime_error("EINTERNAL: decode attention merge timed out");
     });
 }
 dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const float* norm_w,

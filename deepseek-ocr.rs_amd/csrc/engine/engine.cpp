@@ -1455,6 +1455,10 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipMemsetAsync(wsi("s_attn_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_route_cnt", 16), 0, sizeof(int) * 16, st));
     HIP_CHECK(hipMemsetAsync(wsi("s_dntick", (size_t)H / 64 + 1), 0, sizeof(int) * (H / 64 + 1), st));
+    {  // decode attention records: sentinel-filled before the first launch (the polling merge refills them)
+        const size_t pf = dec_attn_workspace(B, L.heads, L.head_dim, Lmax) / 4 + 16;
+        dec_attn_part_init(wsf("s_part", pf), pf * 4, st);
+    }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
     HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
@@ -1848,6 +1852,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             da.kc = kc_ + (long)l * B * page_stride_; da.vc = vc_ + (long)l * B * page_stride_;
             da.page_stride = page_stride_; da.head_stride = head_stride_;
             da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
+            da.err = wsi("s_err", 4);
             da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
             launch_dec_attn(da, st);
         });

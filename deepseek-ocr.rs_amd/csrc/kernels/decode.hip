@@ -1326,6 +1326,7 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 // with one agent-scope release / acquire (cdna_hip_programming.md §5 split-K recipe).
 // CH keys per block (64 or 32: env DSOCR_ATT_CH); LPK = 256 / CH lanes score one key.
 constexpr int DA2_CH_MIN = 32;
+constexpr uint32_t DA_SENT = 0x7FBADBADu;  // "record word not written yet" (a NaN payload no arithmetic produces)
 
 // an empty asm that takes N float4 registers as operands (4 at a time): the loads that produced them
 // stay above this point
@@ -1440,7 +1441,7 @@ __device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, 
 // loads), then run the attention chunk exactly as the unfused kernel.
 // PREROT: the q / k rows arrive already rotated (dec_qkv_rope applied RoPE in its epilogue), so
 // q, k_new and v_new are loaded before the position and no RoPE table is read here.
-template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false, int NSUB = 1>
+template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false, int NSUB = 1, bool POLL = false>
 __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
@@ -1739,13 +1740,27 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         __builtin_memcpy(&bits, ml, 16);
         __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
     }
-    // 6. arrival ticket (every storing wave drains, then one relaxed agent add); the last
+    // 6. POLL: no ticket.  Chunk 0's block merges: it polls the records of the other chunks until
+    //    none of the words it needs still holds the sentinel (the record buffer enters every launch
+    //    filled with it: dec_attn_part_init, then each merge refills what it read), so a writer
+    //    neither waits for its stores' acknowledgement nor takes an atomic round trip.  A word is
+    //    written once per launch and read with sc1 loads; a value is never the sentinel's NaN
+    //    payload (arithmetic produces the canonical NaN).  Bounded spin: a give-up sets *err.
+    //    Otherwise: arrival ticket (every storing wave drains, then one relaxed agent add); the last
     //    chunk block of (b, h) merges every partial.  Every partial byte was stored sc1 and
     //    every load of it below is an sc1 buffer load, so no acquire fence is needed
     //    (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row).
+    if constexpr (POLL) {
+        if (c != 0) {
+            AT_STAMP(3);
+            return;
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
+    if (POLL) {
+        last_s = 1;
+    } else if (tid == 0) {
         int* cnt = a.counters + (long)b * a.heads + h;
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == nc - 1;
@@ -1776,10 +1791,35 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         // ONE round trip: (m, l) of chunk tid and this thread's o partials (clamped indices,
         // weight 0 past nc by a select) are all in flight together
         float ov[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) ov[j] = ld1(min(grp + KS * j, nc - 1) * PR + 4 + dim);
         const int tc = min(tid, nc - 1);
-        const float mt = ld1(tc * PR), lt0 = ld1(tc * PR + 1);
+        float mt, lt0;
+        for (unsigned it = 0;; ++it) {
+            asm volatile("" ::: "memory");  // the records change under us: re-load them every pass
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) ov[j] = ld1(min(grp + KS * j, nc - 1) * PR + 4 + dim);
+            mt = ld1(tc * PR);
+            lt0 = ld1(tc * PR + 1);
+            if (!POLL) break;
+            bool pend = __float_as_uint(mt) == DA_SENT || __float_as_uint(lt0) == DA_SENT;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) pend = pend || __float_as_uint(ov[j]) == DA_SENT;
+            if (!__syncthreads_or(pend)) break;
+            if (it > (1u << 20)) {
+                if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (POLL) {  // refill what was read (each word by exactly one thread) for the next launch
+            const uint32_t sent = DA_SENT;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (grp + KS * j < nc) __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, ((grp + KS * j) * PR + 4 + dim) * 4, 0, 16);
+            if (tid < nc) {
+                __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR) * 4, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR + 1) * 4, 0, 16);
+            }
+        }
         if (tid < nc) { ms[tid] = mt; ls[tid] = lt0; }
         __syncthreads();
         float mm = -INFINITY;
@@ -1821,9 +1861,9 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
 #undef AT_STAMP
 }
 
-template <int HD, int CH, bool PREROT, bool EARLY>
+template <int HD, int CH, bool PREROT, bool EARLY, bool POLL = false>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
-    attn_body<HD, CH, PREROT, false, EARLY>(a, nullptr);
+    attn_body<HD, CH, PREROT, false, EARLY, 1, POLL>(a, nullptr);
 }
 
 // NSUB sub-chunks per block: at most 128 VGPRs (4 blocks per CU), so the grid of >= 600 blocks is
@@ -1856,6 +1896,11 @@ void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s) {
 static int dec_attn_ch() {
     const char* e = getenv("DSOCR_ATT_CH");
     return (e && atoi(e) == 32) ? 32 : 64;
+}
+
+void dec_attn_part_init(float* part, size_t bytes, hipStream_t s) {
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(part), (int)DA_SENT, bytes / 4, s) != hipSuccess)
+        throw std::runtime_error("EINTERNAL: hipMemsetD32Async (attention records)");
 }
 
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
@@ -1899,6 +1944,14 @@ void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
         return;
     }
     dim3 g1(chunks, a.heads, a.B);
+    // polling merge (no ticket): 64-key chunks of 128-dim heads, <= 24 chunks (one load round trip in
+    // the merge), a give-up flag, a sentinel-filled record buffer (DSOCR_ATT_POLL=0: the ticket)
+    static const bool poll_env = !(getenv("DSOCR_ATT_POLL") && atoi(getenv("DSOCR_ATT_POLL")) == 0);
+    if (poll_env && a.err && ch == 64 && a.hd == 128 && chunks <= 24 && !a.split && !early) {
+        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<128, 64, true, false, true>), g1, dim3(256), 0, s, a);
+        else DSOCR_LAUNCH((dec_attn_kernel<128, 64, false, false, true>), g1, dim3(256), 0, s, a);
+        return;
+    }
 #define DSOCR_DA(HDV, CHV)                                                                          \
     do {                                                                                             \
         if (prerot && early) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true, true>), g1, dim3(256), 0, s, a);  \

@@ -261,6 +261,8 @@ void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t 
 bool dec_qkv_attn_ok(const DecAttn2Args& a);
 void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
+// the record buffer enters every dec_attn launch sentinel-filled (the polling merge refills what it reads)
+void dec_attn_part_init(float* part, size_t bytes, hipStream_t s);
 // Router top-k + grouping by expert in one block (T <= 64, E <= 256, top_k <= 8).
 struct MoeRouteArgs {
     const float* logits = nullptr;

@@ -298,12 +298,14 @@ static void case_attn(int B, int pos, hipStream_t s) {
     float* cs = rand_f32((size_t)max_len * HD, 1.f);
     float* sn = rand_f32((size_t)max_len * HD, 1.f);
     float* part = (float*)dalloc(dec_attn_workspace(B, HEADS, HD, max_len) + 64);
-    int* cnt = (int*)dalloc((size_t)B * HEADS * 4);
+    dec_attn_part_init(part, dec_attn_workspace(B, HEADS, HD, max_len), nullptr);
+    int* cnt = (int*)dalloc((size_t)B * HEADS * 4 + 16);
     float* o = (float*)dalloc((size_t)B * HEADS * HD * 4);
     DecAttn2Args a;
     a.qkv = qkv; a.ld = 3 * HEADS * HD; a.kv_pos = kv_pos; a.B = B; a.heads = HEADS; a.kv_heads = HEADS; a.hd = HD;
     a.rope_dim = HD; a.max_len = max_len; a.cos = cs; a.sin = sn; a.page_stride = page_stride; a.head_stride = head_stride;
     a.scale = 1.f / sqrtf((float)HD); a.part = part; a.counters = cnt; a.o = o; a.o_ld = HEADS * HD; a.prerot = B == 1;
+    a.err = cnt + B * HEADS;
     char nm[96];
     snprintf(nm, sizeof nm, "attn B=%d L=%d", B, pos + 1);
     const double bytes = 2.0 * B * (pos + 1) * HEADS * HD * 4;
