@@ -11,6 +11,7 @@
 // two LDS stages filled by 16-byte global_load_lds (lane-linear LDS image, XOR-swizzled 16-byte
 // chunks via the SOURCE address so the fragment ds_read_b128s are conflict-free), counted vmcnt +
 // raw s_barrier (cdna_hip_programming.md §5, "Pipelining across barriers"), XCD-aware tile order.
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -239,12 +240,17 @@ __device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
 // in registers (f16 has 11 significant bits) and the products lo.hi, mid.lo, mid.hi, hi.lo, hi.hi are
 // issued (lo.lo is below f32 rounding: the W5 formulation's set) — 5 MFMAs per fragment pair, A and W
 // read once instead of as 5 bf16 planes each.
+// Wave layout: bf16 weights use 4 x 1 waves of 32 x 128 (each A row is split by exactly one wave; a
+// 2 x 2 layout splits every A fragment in two waves and the split VALU work, not the MFMAs, bounds
+// the k-step); f16 weights keep 2 x 2 of 64 x 64 (their W split would double instead).
 template <bool F16W>
 __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
+    constexpr int WN = F16W ? 2 : 1, WM = 4 / WN;     // waves along N / M
+    constexpr int TI = FX_M / WM / 32, TJ = FX_N / WN / 32;
     __shared__ __attribute__((aligned(16))) float a_lds[2 * FX_AS];
     __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * FX_WS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     const int ntn = (g.N + FX_N - 1) / FX_N;
     const int nwg = gridDim.x;
     const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
@@ -254,11 +260,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     const int m0 = bm * FX_M, n0 = bn * FX_N;
     const float* A = reinterpret_cast<const float*>(g.A);
     const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
-    f32x16 acc[2][2];
+    f32x16 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     const int nk_all = g.K / FX_K;
@@ -302,10 +308,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
 #pragma unroll
         for (int ks = 0; ks < FX_K / 16; ++ks) {
             const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of 4)
-            bf16x8_v bfv[2], blo[2];
+            bf16x8_v bfv[TJ], blo[TJ];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int r = wn * 64 + j * 32 + (lane & 31);
+            for (int j = 0; j < TJ; ++j) {
+                const int r = wn * (FX_N / WN) + j * 32 + (lane & 31);
                 if constexpr (F16W) {
                     const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
                     float wv[8], wh[8], wl[8];
@@ -322,8 +328,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
                 }
             }
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int r = wm * 64 + i * 32 + (lane & 31);
+            for (int i = 0; i < TI; ++i) {
+                const int r = wm * (FX_M / WM) + i * 32 + (lane & 31);
                 const int sw = (r >> 1) & 7;
                 const float4 lo4 = *reinterpret_cast<const float4*>(As + r * FX_K + (((2 * kc) ^ sw) * 4));
                 const float4 hi4 = *reinterpret_cast<const float4*>(As + r * FX_K + (((2 * kc + 1) ^ sw) * 4));
@@ -338,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
                 }
                 const bf16x8_v ph = fx_pack(h), pm = fx_pack(m), pl = fx_pack(l);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+                for (int j = 0; j < TJ; ++j) {
                     if constexpr (F16W) {  // small terms first
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, blo[j], acc[i][j], 0, 0, 0);
@@ -359,28 +365,28 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     if (g.splits > 1) {
         float* P = g.part + (long)split * g.M * g.N;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int col = n0 + wn * 64 + j * 32 + l32;
+            for (int j = 0; j < TJ; ++j) {
+                const int col = n0 + wn * (FX_N / WN) + j * 32 + l32;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                    const int row = m0 + wm * (FX_M / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
                     if (row < g.M && col < g.N) P[(long)row * g.N + col] = acc[i][j][r];
                 }
             }
         return;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < TI; ++i) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + l32;
+        for (int j = 0; j < TJ; ++j) {
+            const int col = n0 + wn * (FX_N / WN) + j * 32 + l32;
             if (col >= g.N) continue;
             const float bv = g.bias ? g.bias[col] : 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int row = m0 + wm * (FX_M / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
                 if (row >= g.M) continue;
                 const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;
                 if (orow < 0) continue;
@@ -418,6 +424,161 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
         const long n = (long)g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Grouped (MoE prefill) exact-f32 GEMM: the routed experts' gate/up and down over the token rows
+// sorted by expert (block.rs:1215-1395 applies each expert to the tokens that picked it).  A prompt
+// of T tokens gives each of the 64 experts ~T·topk/64 rows (28 at one 1024 px page), so the 128-row
+// tiles of gemm_x3 issued >= 4x the needed MFMAs and staged every plane through register stores.
+// Here tiles are 32 rows x 128 columns x 32 k: a block's tile index is mapped to (expert, row tile)
+// by a 64-lane prefix sum over the per-expert tile counts (the launch covers the bound
+// sum ceil(rows_e / 32) <= M / 32 + groups; surplus blocks leave), 4 waves own 32 columns each,
+// the A rows are gathered by the LDS DMA itself (per-lane addresses), W rows of the expert's slab,
+// and the planes are split in registers as in gemm_f32a_nt_kernel (same products, same order).
+constexpr int GX_M = 32, GX_N = 128, GX_K = 32;
+
+template <bool F16W>
+__global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) float a_lds[2 * GX_M * GX_K];
+    __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * GX_N * GX_K];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // tile -> (group, row tile): inclusive prefix of ceil(rows / 32) over the groups (lane = group)
+    const int t = blockIdx.y;
+    int cnt = 0;
+    if (lane < g.groups) cnt = g.group_off[lane + 1] - g.group_off[lane];
+    const int nt = (cnt + GX_M - 1) / GX_M;
+    int pre = nt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(pre, d);
+        if (lane >= d) pre += o;
+    }
+    const unsigned long long hit = __ballot(lane < g.groups && pre > t);
+    if (!hit) return;  // whole block: surplus tile
+    const int grp = __builtin_ctzll(hit);
+    const int m_begin = __shfl(g.group_off[min(lane, g.groups - 1)], grp);
+    const int rows = __shfl(cnt, grp);
+    const int mt = t - (__shfl(pre, grp) - __shfl(nt, grp));
+    const int m0 = mt * GX_M, n0 = blockIdx.x * GX_N;
+    const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W) + (long)grp * g.w_group_stride;
+    const float* bias = g.bias ? g.bias + (long)grp * g.bias_group_stride : nullptr;
+    // DMA sources: A row (wave * 8 + lane / 8) of the tile, W rows (2 * wave + i) * 16 + lane / 4
+    const int ar = wave * 8 + (lane >> 3);
+    const int aj = (lane & 7) ^ ((ar >> 1) & 7);
+    const int arr = m_begin + min(m0 + ar, rows - 1);
+    const float* a_src = g.A + (long)(g.a_rows ? g.a_rows[arr] : arr) * g.lda + aj * 4;
+    const uint16_t* w_src[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = (wave * 2 + i) * 16 + (lane >> 2);
+        const int j = (lane & 3) ^ ((r >> 2) & 3);
+        w_src[i] = W + (long)min(n0 + r, g.N - 1) * g.ldw + j * 8;
+    }
+    auto issue = [&](int kt) {
+        const int k0 = kt * GX_K;
+        float* as = a_lds + (kt & 1) * GX_M * GX_K;
+        uint16_t* ws_ = w_lds + (kt & 1) * GX_N * GX_K;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a_src + k0), (lds_void*)(as + wave * 8 * GX_K), 16, 0,
+                                         0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(w_src[i] + k0),
+                                             (lds_void*)(ws_ + (wave * 2 + i) * 16 * GX_K), 16, 0, 0);
+    };
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int nk = g.K / GX_K;
+    issue(0);
+    for (int kt = 0; kt < nk; ++kt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 1 < nk) issue(kt + 1);
+        const float* As = a_lds + (kt & 1) * GX_M * GX_K;
+        const uint16_t* Ws = w_lds + (kt & 1) * GX_N * GX_K;
+#pragma unroll
+        for (int ks = 0; ks < GX_K / 16; ++ks) {
+            const int kc = ks * 2 + (lane >> 5);
+            bf16x8_v bfv, blo;
+            {
+                const int r = wave * 32 + (lane & 31);
+                if constexpr (F16W) {
+                    const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * GX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+                    float wv[8], wh[8], wl[8];
+                    unpack8<f16_t>(raw, wv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        wh[e] = (float)(__bf16)wv[e];
+                        wl[e] = wv[e] - wh[e];
+                    }
+                    bfv = fx_pack(wh);
+                    blo = fx_pack(wl);
+                } else {
+                    bfv = *reinterpret_cast<const bf16x8_v*>(Ws + r * GX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+                }
+            }
+            const int r = lane & 31;
+            const int sw = (r >> 1) & 7;
+            const float4 lo4 = *reinterpret_cast<const float4*>(As + r * GX_K + (((2 * kc) ^ sw) * 4));
+            const float4 hi4 = *reinterpret_cast<const float4*>(As + r * GX_K + (((2 * kc + 1) ^ sw) * 4));
+            const float av[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+            float h[8], m[8], l[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                h[e] = (float)(__bf16)av[e];
+                const float r1 = av[e] - h[e];
+                m[e] = (float)(__bf16)r1;
+                l[e] = r1 - m[e];
+            }
+            const bf16x8_v ph = fx_pack(h), pm = fx_pack(m), pl = fx_pack(l);
+            if constexpr (F16W) {  // small terms first
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, blo, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, blo, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv, acc, 0, 0, 0);
+            } else {
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv, acc, 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    const int half = lane >> 5, l32 = lane & 31;
+    const int col = n0 + wave * 32 + l32;
+    if (col >= g.N) return;
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (row >= rows) continue;
+        const long orow = g.c_rows ? (long)g.c_rows[m_begin + row] : (long)(m_begin + row);
+        if (orow < 0) continue;
+        float v = apply_act(acc[r] + bv, g.act);
+        float* cp = g.C + orow * (long)g.ldc + col;
+        if (g.accumulate) v += *cp;
+        *cp = v;
+    }
+}
+
+bool gemm_f32a_grouped_ok(const GemmArgs& g) {
+    return g.group_off && g.groups >= 1 && g.groups <= 64 && g.K % GX_K == 0 && g.lda % 4 == 0 && g.ldw % 8 == 0 &&
+           g.w_group_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(g.A) & 15) == 0 &&
+           (reinterpret_cast<uintptr_t>(g.W) & 15) == 0;
+}
+
+void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s) {
+    if (!gemm_f32a_grouped_ok(g)) throw std::runtime_error("EINVAL: grouped gemm_f32a outside its range");
+    if (g.M <= 0 || g.N <= 0) return;
+    // tiles: sum over groups of ceil(rows / 32) <= M / 32 + groups (and no group holds more than max_group_rows)
+    const long bound = std::min<long>((long)(g.M + GX_M - 1) / GX_M + g.groups,
+                                      (long)g.groups * ((std::max(g.max_group_rows, 1) + GX_M - 1) / GX_M));
+    dim3 grid((g.N + GX_N - 1) / GX_N, (unsigned)bound);
+    if (g.wdtype == WDT_F16) hipLaunchKernelGGL(gemm_f32a_grp_kernel<true>, grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL(gemm_f32a_grp_kernel<false>, grid, dim3(256), 0, s, g);
 }
 
 // ---------------------------------------------------------------------------------------

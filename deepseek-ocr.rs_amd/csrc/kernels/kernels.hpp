@@ -69,6 +69,10 @@ struct GemmArgs {
     int max_group_rows = 0;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t s);
+// Grouped routed-expert GEMM (gemm_bf16.hip): 32-row tiles mapped to (group, row tile) on the device,
+// A rows gathered by the LDS DMA, exact-f32 planes split in registers.  launch_gemm routes here.
+bool gemm_f32a_grouped_ok(const GemmArgs& g);
+void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s);
 
 // ------------------------------------------------------------------ MoE prefill helpers (moe.hip)
 // Router: scores = softmax(logits) (or sigmoid), greedy top-k (descending, stable),
