@@ -375,6 +375,24 @@ dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, in
         check_hip(hipDeviceSynchronize(), "gemm");
     });
 }
+dsocr_status dsocr_k_gemm_grouped(int M, int N, int K, const float* A, int lda, const int* a_rows, const void* W,
+                                  int wdtype, long long w_group_stride, const float* bias, long long bias_group_stride,
+                                  float* C, int ldc, const int* c_rows, int act, int accumulate, const int* group_off,
+                                  int groups, int max_group_rows, int kernel) {
+    return guarded([&] {
+        if (!A || !W || !C || !group_off || groups < 1 || M < 0 || N < 1 || K < 1)
+            throw std::runtime_error("EINVAL: grouped gemm arguments");
+        dsocr::GemmArgs g;
+        g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.a_rows = a_rows; g.W = W; g.ldw = K; g.wdtype = wdtype;
+        g.w_group_stride = (long)w_group_stride; g.bias = bias; g.bias_group_stride = (long)bias_group_stride;
+        g.C = C; g.ldc = ldc; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
+        g.group_off = group_off; g.groups = groups; g.max_group_rows = max_group_rows;
+        if (kernel == 1) dsocr::launch_gemm_f32a_grouped(g, nullptr);
+        else dsocr::launch_gemm(g, nullptr);
+        check_hip(hipGetLastError(), "grouped gemm launch");
+        check_hip(hipDeviceSynchronize(), "grouped gemm");
+    });
+}
 dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias,
                                float* C, int act, int accumulate, int splits) {
     return guarded([&] {

@@ -81,7 +81,7 @@ EXPORTS = [
     "dsocr_page_free", "dsocr_page_to_device", "dsocr_page_info", "dsocr_page_pixels_view", "dsocr_image_embeddings", "dsocr_generate",
     "dsocr_generate_batch", "dsocr_last_timings", "dsocr_profile_decode", "dsocr_device_count", "dsocr_dev_alloc", "dsocr_dev_free",
     "dsocr_memcpy_h2d", "dsocr_memcpy_d2h", "dsocr_dev_sync", "dsocr_synth_bf16", "dsocr_resize_bicubic",
-    "dsocr_k_gemm", "dsocr_k_gemm_f32a", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
+    "dsocr_k_gemm", "dsocr_k_gemm_f32a", "dsocr_k_gemm_grouped", "dsocr_k_gemv", "dsocr_k_layernorm", "dsocr_k_rmsnorm", "dsocr_k_attention", "dsocr_k_decode_attention", "dsocr_k_moe",
     "dsocr_k_sample_greedy", "dsocr_k_sample_stoch", "dsocr_k_dsq_dequant", "dsocr_prepare_page_device", "dsocr_page_read_device",
     "dsocr_generate_trace", "dsocr_k_moe_kernels", "dsocr_k_lmhead_screened",
     "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
@@ -139,6 +139,8 @@ def lib():
     L.dsocr_resize_bicubic.argtypes = [vp, u32, u32, vp, u32, u32]
     L.dsocr_k_gemm.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_gemm_f32a.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32]
+    L.dsocr_k_gemm_grouped.argtypes = [i32, i32, i32, vp, i32, vp, vp, i32, C.c_longlong, vp, C.c_longlong, vp, i32, vp, i32,
+                                       i32, vp, i32, i32, i32]
     L.dsocr_k_gemv.argtypes = [i32, i32, i32, vp, vp, f32, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_gemv_splitk.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32]
     L.dsocr_k_layernorm.argtypes = [i32, i32, vp, vp, vp, f32, vp]

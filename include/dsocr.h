@@ -222,6 +222,15 @@ dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, in
  * 5 products), C = act(A W^T + bias) (+ C), exact f32 products; splits <= 0 picks the engine's split-K. */
 dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias,
                                float* C, int act, int accumulate, int splits);
+/* Routed-expert linear of the prefill (block.rs:1215-1395 applies expert e to the rows that picked it):
+ * group g owns gathered rows group_off[g] .. group_off[g+1] (device array), row r reads A row
+ * a_rows ? a_rows[r] : r and writes C row c_rows ? c_rows[r] : r (-1 drops it), weights W + g * w_group_stride
+ * ([N][K] 16-bit), bias + g * bias_group_stride.  kernel 0: the engine's dispatch (launch_gemm); 1: the
+ * 32-row-tile grouped kernel whatever the rows per group. */
+dsocr_status dsocr_k_gemm_grouped(int M, int N, int K, const float* A, int lda, const int* a_rows, const void* W,
+                                  int wdtype, long long w_group_stride, const float* bias, long long bias_group_stride,
+                                  float* C, int ldc, const int* c_rows, int act, int accumulate, const int* group_off,
+                                  int groups, int max_group_rows, int kernel);
 /* Decode linear (transformer/block.rs attention / MLP projections at seq_len 1): y[M][N] =
  * act(xn . W^T + bias) (+ y), xn = rmsnorm(x; norm_w, eps) when norm_w != NULL (block.rs:24-29), else x. */
 dsocr_status dsocr_k_gemv(int M, int N, int K, const float* x, const float* norm_w, float eps, const void* W,

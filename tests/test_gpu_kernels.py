@@ -75,6 +75,47 @@ def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
+@pytest.mark.parametrize("T,E,topk,N,K,wdt,act,acc,kernel", [
+    (300, 64, 6, 1792, 1280, 1, 0, 0, 1),   # one page's routed gate/up (~28 rows per expert)
+    (300, 64, 6, 1280, 896, 1, 0, 1, 1),    # ... down, accumulate epilogue
+    (37, 16, 3, 200, 96, 0, 3, 0, 1),       # bf16 weights, ragged N, empty experts, SiLU epilogue
+    (3000, 64, 6, 1792, 1280, 1, 0, 0, 0),  # many rows per expert: the engine dispatch keeps the 128-row tiles
+    (3000, 64, 6, 1792, 1280, 1, 0, 0, 1)])  # ... and the 32-row kernel at the same size
+def test_gemm_grouped(gpu, T, E, topk, N, K, wdt, act, acc, kernel):
+    """Prefill routed experts (block.rs:1215-1395: expert e on the rows that picked it) through the grouped
+    exact-f32 GEMM: rows gathered by a sorted row list, weights of each expert's slab, rows scattered back,
+    vs an f64 matmul per expert (same per-element bound as test_gemm)."""
+    rng = np.random.default_rng(T + E + N)
+    a = rng.standard_normal((T, K)).astype(np.float32)
+    picks = np.stack([rng.choice(E // 2 if E > 16 else E - 4, topk, replace=False) for _ in range(T)])  # some experts empty
+    flat = picks.reshape(-1)
+    order = np.argsort(flat, kind="stable")
+    arow = (order // topk).astype(np.int32)                 # sorted position -> token
+    counts = np.bincount(flat, minlength=E)
+    eoff = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    M = T * topk
+    crow = np.arange(M, dtype=np.int32)[::-1].copy()        # scatter to reversed rows
+    ws, wf = zip(*[_weights(rng, N, K, wdt) for _ in range(E)])
+    bits = np.stack(ws)
+    bias = (rng.standard_normal((E, N)) * 0.1).astype(np.float32)
+    c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
+    dA, dW, dB, dC, dR, dO, dCr = Dev(a), Dev(bits), Dev(bias), Dev(c0), Dev(arow), Dev(eoff), Dev(crow)
+    check(lib().dsocr_k_gemm_grouped(M, N, K, dA.ptr, K, dR.ptr, dW.ptr, wdt, N * K, dB.ptr, N, dC.ptr, N, dCr.ptr, act,
+                                     acc, dO.ptr, E, int(counts.max()), kernel))
+    got = dC.get()
+    ref = c0.copy()
+    for e in range(E):
+        rows = np.arange(eoff[e], eoff[e + 1])
+        if rows.size == 0:
+            continue
+        x = a[arow[rows]]
+        y = ACTS[act]((x.astype(np.float64) @ wf[e].T.astype(np.float64)).astype(np.float32) + bias[e])
+        bound = _bound(x, wf[e]) * (2.0 if act else 1.0)
+        r = crow[rows]
+        exp = y + (c0[r] if acc else 0)
+        assert np.all(np.abs(got[r] - exp) <= bound + 1e-5 * np.abs(exp)), (e, np.max(np.abs(got[r] - exp)))
+
+
 @pytest.mark.parametrize("M,N,K,wdt,norm", [(1, 1280, 1280, 1, True), (1, 129280, 1280, 0, True),
                                             (2, 3840, 1280, 1, True), (3, 3840, 1280, 1, False),
                                             (8, 896, 1792, 1, False), (16, 100, 64, 0, False),
