@@ -243,9 +243,9 @@ __device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
 // Wave layout: bf16 weights use 4 x 1 waves of 32 x 128 (each A row is split by exactly one wave; a
 // 2 x 2 layout splits every A fragment in two waves and the split VALU work, not the MFMAs, bounds
 // the k-step); f16 weights keep 2 x 2 of 64 x 64 (their W split would double instead).
-template <bool F16W>
+template <bool F16W, bool W22 = F16W>
 __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
-    constexpr int WN = F16W ? 2 : 1, WM = 4 / WN;     // waves along N / M
+    constexpr int WN = W22 ? 2 : 1, WM = 4 / WN;     // waves along N / M
     constexpr int TI = FX_M / WM / 32, TJ = FX_N / WN / 32;
     __shared__ __attribute__((aligned(16))) float a_lds[2 * FX_AS];
     __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * FX_WS];
@@ -418,8 +418,10 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
-    if (g.w_f16) hipLaunchKernelGGL(gemm_f32a_nt_kernel<true>, dim3(tiles * g.splits), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL(gemm_f32a_nt_kernel<false>, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    static const bool w22 = getenv("DSOCR_GEMM_W22") && atoi(getenv("DSOCR_GEMM_W22")) != 0;  // A/B: 2 x 2 for bf16
+    if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else if (w22) hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) {
         const long n = (long)g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
