@@ -387,7 +387,7 @@ dsocr_status dsocr_k_gemm_grouped(int M, int N, int K, const float* A, int lda, 
         g.w_group_stride = (long)w_group_stride; g.bias = bias; g.bias_group_stride = (long)bias_group_stride;
         g.C = C; g.ldc = ldc; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
         g.group_off = group_off; g.groups = groups; g.max_group_rows = max_group_rows;
-        if (kernel == 1) dsocr::launch_gemm_f32a_grouped(g, nullptr);
+        if (kernel == 1 || kernel == 2) dsocr::launch_gemm_f32a_grouped(g, nullptr, kernel == 2 ? 128 : 32);
         else dsocr::launch_gemm(g, nullptr);
         check_hip(hipGetLastError(), "grouped gemm launch");
         check_hip(hipDeviceSynchronize(), "grouped gemm");

@@ -329,15 +329,11 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
     int mtiles = (g.group_off ? g.max_group_rows : g.M);
     dim3 grid((g.N + GB_N - 1) / GB_N, (mtiles + GB_M - 1) / GB_M, g.group_off ? g.groups : 1);
     if (grid.y == 0 || grid.x == 0) return;
-    // grouped (MoE prefill) with few rows per group (one 1024 px page: ~85 per expert): the 32-row-tile
-    // exact-f32 kernel (1 page: 10.1 -> 9.4 ms prefill, 2 pages: 13.4 -> 13.1).  Many rows per group (4
-    // pages: ~340, 18.5 vs 19.5 ms; 8 pages: ~670) re-read
-    // every expert's weights once per 32-row tile there, so the 128-row gemm_x3 tiles stay (36.7 vs
-    // 33.1 ms prefill at 8 pages); DSOCR_GEMM_GRP=0 / DSOCR_GEMM_GRP_ROWS=<mean rows per group> move
-    // the switch (A/B comparisons)
-    static const bool grp_off = getenv("DSOCR_GEMM_GRP") && atoi(getenv("DSOCR_GEMM_GRP")) == 0;
-    static const int grp_rows = getenv("DSOCR_GEMM_GRP_ROWS") ? atoi(getenv("DSOCR_GEMM_GRP_ROWS")) : 256;
-    if (g.group_off && !grp_off && (long)g.M <= (long)grp_rows * g.groups && gemm_f32a_grouped_ok(g)) {
+    // grouped (MoE prefill): the exact-f32 grouped kernel (gemm_bf16.hip) — 32-row tiles up to 256 mean
+    // rows per expert (1 page: prefill 10.1 -> 9.4 ms, 2 pages 13.4 -> 13.1), 128-row tiles above.
+    // DSOCR_GEMM_GRP=0: gemm_x3 always; =2: gemm_x3 above 256 rows (A/B comparisons)
+    static const int grp_mode = getenv("DSOCR_GEMM_GRP") ? atoi(getenv("DSOCR_GEMM_GRP")) : 1;
+    if (g.group_off && grp_mode != 0 && !(grp_mode == 2 && (long)g.M > 256L * g.groups) && gemm_f32a_grouped_ok(g)) {
         launch_gemm_f32a_grouped(g, s);
         return;
     }

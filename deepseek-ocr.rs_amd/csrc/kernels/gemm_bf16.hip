@@ -438,10 +438,13 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
 // sum ceil(rows_e / 32) <= M / 32 + groups; surplus blocks leave), 4 waves own 32 columns each,
 // the A rows are gathered by the LDS DMA itself (per-lane addresses), W rows of the expert's slab,
 // and the planes are split in registers as in gemm_f32a_nt_kernel (same products, same order).
-constexpr int GX_M = 32, GX_N = 128, GX_K = 32;
+constexpr int GX_N = 128, GX_K = 32;
 
-template <bool F16W>
+// GM = 32: 4 x 1 waves of 32 x 32; GM = 128 (many rows per expert): 2 x 2 waves of 64 x 64
+template <bool F16W, int GM>
 __global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
+    constexpr int GX_M = GM, WM = GM == 32 ? 1 : 2, WN = 4 / WM, TI = GM / WM / 32, TJ = GX_N / WN / 32;
+    constexpr int AI = GM / 32;  // A DMA instructions per thread
     __shared__ __attribute__((aligned(16))) float a_lds[2 * GX_M * GX_K];
     __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * GX_N * GX_K];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -465,11 +468,15 @@ __global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
     const int m0 = mt * GX_M, n0 = blockIdx.x * GX_N;
     const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W) + (long)grp * g.w_group_stride;
     const float* bias = g.bias ? g.bias + (long)grp * g.bias_group_stride : nullptr;
-    // DMA sources: A row (wave * 8 + lane / 8) of the tile, W rows (2 * wave + i) * 16 + lane / 4
-    const int ar = wave * 8 + (lane >> 3);
-    const int aj = (lane & 7) ^ ((ar >> 1) & 7);
-    const int arr = m_begin + min(m0 + ar, rows - 1);
-    const float* a_src = g.A + (long)(g.a_rows ? g.a_rows[arr] : arr) * g.lda + aj * 4;
+    // DMA sources: A rows (wave * AI + i) * 8 + lane / 8 of the tile, W rows (2 * wave + i) * 16 + lane / 4
+    const float* a_src[AI];
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+        const int ar = (wave * AI + i) * 8 + (lane >> 3);
+        const int aj = (lane & 7) ^ ((ar >> 1) & 7);
+        const int arr = m_begin + min(m0 + ar, rows - 1);
+        a_src[i] = g.A + (long)(g.a_rows ? g.a_rows[arr] : arr) * g.lda + aj * 4;
+    }
     const uint16_t* w_src[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -481,16 +488,23 @@ __global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
         const int k0 = kt * GX_K;
         float* as = a_lds + (kt & 1) * GX_M * GX_K;
         uint16_t* ws_ = w_lds + (kt & 1) * GX_N * GX_K;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a_src + k0), (lds_void*)(as + wave * 8 * GX_K), 16, 0,
-                                         0);
+#pragma unroll
+        for (int i = 0; i < AI; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a_src[i] + k0),
+                                             (lds_void*)(as + (wave * AI + i) * 8 * GX_K), 16, 0, 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(w_src[i] + k0),
                                              (lds_void*)(ws_ + (wave * 2 + i) * 16 * GX_K), 16, 0, 0);
     };
-    f32x16 acc;
+    const int wm = wave / WN, wn = wave % WN;
+    f32x16 acc[TI][TJ];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     const int nk = g.K / GX_K;
     issue(0);
     for (int kt = 0; kt < nk; ++kt) {
@@ -503,9 +517,10 @@ __global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
 #pragma unroll
         for (int ks = 0; ks < GX_K / 16; ++ks) {
             const int kc = ks * 2 + (lane >> 5);
-            bf16x8_v bfv, blo;
-            {
-                const int r = wave * 32 + (lane & 31);
+            bf16x8_v bfv[TJ], blo[TJ];
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                const int r = wn * (GX_N / WN) + j * 32 + (lane & 31);
                 if constexpr (F16W) {
                     const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * GX_K + ((kc ^ ((r >> 2) & 3)) * 8));
                     float wv[8], wh[8], wl[8];
@@ -515,13 +530,15 @@ __global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
                         wh[e] = (float)(__bf16)wv[e];
                         wl[e] = wv[e] - wh[e];
                     }
-                    bfv = fx_pack(wh);
-                    blo = fx_pack(wl);
+                    bfv[j] = fx_pack(wh);
+                    blo[j] = fx_pack(wl);
                 } else {
-                    bfv = *reinterpret_cast<const bf16x8_v*>(Ws + r * GX_K + ((kc ^ ((r >> 2) & 3)) * 8));
+                    bfv[j] = *reinterpret_cast<const bf16x8_v*>(Ws + r * GX_K + ((kc ^ ((r >> 2) & 3)) * 8));
                 }
             }
-            const int r = lane & 31;
+#pragma unroll
+            for (int i = 0; i < TI; ++i) {
+            const int r = wm * (GX_M / WM) + i * 32 + (lane & 31);
             const int sw = (r >> 1) & 7;
             const float4 lo4 = *reinterpret_cast<const float4*>(As + r * GX_K + (((2 * kc) ^ sw) * 4));
             const float4 hi4 = *reinterpret_cast<const float4*>(As + r * GX_K + (((2 * kc + 1) ^ sw) * 4));
@@ -535,34 +552,44 @@ __global__ __launch_bounds__(256) void gemm_f32a_grp_kernel(GemmArgs g) {
                 l[e] = r1 - m[e];
             }
             const bf16x8_v ph = fx_pack(h), pm = fx_pack(m), pl = fx_pack(l);
-            if constexpr (F16W) {  // small terms first
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, blo, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, blo, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv, acc, 0, 0, 0);
-            } else {
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv, acc, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                if constexpr (F16W) {  // small terms first
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, blo[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, blo[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv[j], acc[i][j], 0, 0, 0);
+                } else {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl, bfv[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm, bfv[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph, bfv[j], acc[i][j], 0, 0, 0);
+                }
+            }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     const int half = lane >> 5, l32 = lane & 31;
-    const int col = n0 + wave * 32 + l32;
-    if (col >= g.N) return;
-    const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (row >= rows) continue;
-        const long orow = g.c_rows ? (long)g.c_rows[m_begin + row] : (long)(m_begin + row);
-        if (orow < 0) continue;
-        float v = apply_act(acc[r] + bv, g.act);
-        float* cp = g.C + orow * (long)g.ldc + col;
-        if (g.accumulate) v += *cp;
-        *cp = v;
+    for (int j = 0; j < TJ; ++j) {
+        const int col = n0 + wn * (GX_N / WN) + j * 32 + l32;
+        if (col >= g.N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * (GX_M / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (row >= rows) continue;
+                const long orow = g.c_rows ? (long)g.c_rows[m_begin + row] : (long)(m_begin + row);
+                if (orow < 0) continue;
+                float v = apply_act(acc[i][j][r] + bv, g.act);
+                float* cp = g.C + orow * (long)g.ldc + col;
+                if (g.accumulate) v += *cp;
+                *cp = v;
+            }
+        }
     }
 }
 
@@ -572,15 +599,22 @@ bool gemm_f32a_grouped_ok(const GemmArgs& g) {
            (reinterpret_cast<uintptr_t>(g.W) & 15) == 0;
 }
 
-void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s) {
+void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s, int tile_rows) {
     if (!gemm_f32a_grouped_ok(g)) throw std::runtime_error("EINVAL: grouped gemm_f32a outside its range");
     if (g.M <= 0 || g.N <= 0) return;
-    // tiles: sum over groups of ceil(rows / 32) <= M / 32 + groups (and no group holds more than max_group_rows)
-    const long bound = std::min<long>((long)(g.M + GX_M - 1) / GX_M + g.groups,
-                                      (long)g.groups * ((std::max(g.max_group_rows, 1) + GX_M - 1) / GX_M));
+    // 32-row tiles up to 256 mean rows per group, 128-row tiles above (each expert's weights re-read
+    // once per row tile); tiles: sum over groups of ceil(rows / GM) <= M / GM + groups
+    const int gm = (tile_rows == 32 || tile_rows == 128) ? tile_rows : ((long)g.M <= 256L * g.groups ? 32 : 128);
+    const long bound = std::min<long>((long)(g.M + gm - 1) / gm + g.groups,
+                                      (long)g.groups * ((std::max(g.max_group_rows, 1) + gm - 1) / gm));
     dim3 grid((g.N + GX_N - 1) / GX_N, (unsigned)bound);
-    if (g.wdtype == WDT_F16) hipLaunchKernelGGL(gemm_f32a_grp_kernel<true>, grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL(gemm_f32a_grp_kernel<false>, grid, dim3(256), 0, s, g);
+    if (gm == 32) {
+        if (g.wdtype == WDT_F16) hipLaunchKernelGGL((gemm_f32a_grp_kernel<true, 32>), grid, dim3(256), 0, s, g);
+        else hipLaunchKernelGGL((gemm_f32a_grp_kernel<false, 32>), grid, dim3(256), 0, s, g);
+    } else {
+        if (g.wdtype == WDT_F16) hipLaunchKernelGGL((gemm_f32a_grp_kernel<true, 128>), grid, dim3(256), 0, s, g);
+        else hipLaunchKernelGGL((gemm_f32a_grp_kernel<false, 128>), grid, dim3(256), 0, s, g);
+    }
 }
 
 // ---------------------------------------------------------------------------------------

@@ -72,7 +72,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t s);
 // Grouped routed-expert GEMM (gemm_bf16.hip): 32-row tiles mapped to (group, row tile) on the device,
 // A rows gathered by the LDS DMA, exact-f32 planes split in registers.  launch_gemm routes here.
 bool gemm_f32a_grouped_ok(const GemmArgs& g);
-void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s);
+void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s, int tile_rows = 0);  // 0: by rows per group
 
 // ------------------------------------------------------------------ MoE prefill helpers (moe.hip)
 // Router: scores = softmax(logits) (or sigmoid), greedy top-k (descending, stable),

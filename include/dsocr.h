@@ -225,8 +225,8 @@ dsocr_status dsocr_k_gemm_f32a(int M, int N, int K, const float* A, const void* 
 /* Routed-expert linear of the prefill (block.rs:1215-1395 applies expert e to the rows that picked it):
  * group g owns gathered rows group_off[g] .. group_off[g+1] (device array), row r reads A row
  * a_rows ? a_rows[r] : r and writes C row c_rows ? c_rows[r] : r (-1 drops it), weights W + g * w_group_stride
- * ([N][K] 16-bit), bias + g * bias_group_stride.  kernel 0: the engine's dispatch (launch_gemm); 1: the
- * 32-row-tile grouped kernel whatever the rows per group. */
+ * ([N][K] 16-bit), bias + g * bias_group_stride.  kernel 0: the engine's dispatch (launch_gemm); 1 / 2: the
+ * grouped kernel with 32- / 128-row tiles whatever the rows per group. */
 dsocr_status dsocr_k_gemm_grouped(int M, int N, int K, const float* A, int lda, const int* a_rows, const void* W,
                                   int wdtype, long long w_group_stride, const float* bias, long long bias_group_stride,
                                   float* C, int ldc, const int* c_rows, int act, int accumulate, const int* group_off,

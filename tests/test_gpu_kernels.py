@@ -79,8 +79,10 @@ def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
     (300, 64, 6, 1792, 1280, 1, 0, 0, 1),   # one page's routed gate/up (~28 rows per expert)
     (300, 64, 6, 1280, 896, 1, 0, 1, 1),    # ... down, accumulate epilogue
     (37, 16, 3, 200, 96, 0, 3, 0, 1),       # bf16 weights, ragged N, empty experts, SiLU epilogue
-    (3000, 64, 6, 1792, 1280, 1, 0, 0, 0),  # many rows per expert: the engine dispatch keeps the 128-row tiles
-    (3000, 64, 6, 1792, 1280, 1, 0, 0, 1)])  # ... and the 32-row kernel at the same size
+    (3000, 64, 6, 1792, 1280, 1, 0, 0, 0),  # many rows per expert: the engine dispatch (128-row tiles)
+    (3000, 64, 6, 1792, 1280, 1, 0, 0, 1),  # ... the 32-row tiles at the same size
+    (300, 64, 6, 1280, 896, 1, 0, 1, 2),    # 128-row tiles with few rows (padding rows, accumulate)
+    (37, 16, 3, 200, 96, 0, 3, 0, 2)])      # ... bf16, ragged N, empty experts
 def test_gemm_grouped(gpu, T, E, topk, N, K, wdt, act, acc, kernel):
     """Prefill routed experts (block.rs:1215-1395: expert e on the rows that picked it) through the grouped
     exact-f32 GEMM: rows gathered by a sorted row list, weights of each expert's slab, rows scattered back,
