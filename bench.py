@@ -53,6 +53,31 @@ def visible_gpus():
     return n.value if lib().dsocr_device_count(C.byref(n)) == 0 else 1
 
 
+def relaunch_under_torchrun(n):
+    """`bench.py --gpus N` with no launcher: run N ranks under torch.distributed.run as a CHILD process
+    (this process has made no HIP call yet) and return its exit code.  The ranks see WORLD_SIZE and
+    take the normal path below."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n} without a launcher: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
+
+
+def rank_devices(dist, local):
+    """Device ordinal of every rank (rank order)."""
+    if dist is None:
+        return [local]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, local)
+    return out
+
+
 def page_indices(step, world, rank, ppg):
     """Pages of one bench step on one rank: rank r of W takes pages [(step*W + r)*ppg, +ppg) —
     disjoint across ranks and steps (data parallel, no collective on the data path)."""
@@ -104,9 +129,9 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
     forwards at the prompt's KV length and `decode_steps` more at the last step's KV length
     (prompt + max_new - 1, the cache padded with copies of its own rows: attention and the cache
     append cost what they cost at that length).  Decode time is linear in the KV length, so the
-    page's (max_new - 1) decode steps are the trapezoid of the two measured step times."""
-    import numpy as np
-
+    page's (max_new - 1) decode steps are the trapezoid of the two measured step times.
+    Timed twice: with BLAS on every core this process may run on (len(sched_getaffinity)), which is
+    the reported `value`, and with the pool the environment sets (OMP_NUM_THREADS), as `at_env_threads`."""
     import dsocr
     from oracle.model import OracleModel
     from oracle.specs import tensor_names
@@ -119,7 +144,38 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
             W.get(n, shape)
     log(f"[cpu] oracle weights ready in {time.time() - t:.1f}s")
     orc = OracleModel(cfg, W)
-    img = pages[0]
+    env_threads = blas_threads()
+    try:
+        all_cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        all_cores = os.cpu_count() or 1
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:
+        threadpool_limits = None
+    runs = []
+    for threads in ([all_cores, env_threads] if all_cores != env_threads and threadpool_limits else [env_threads]):
+        if threadpool_limits:
+            with threadpool_limits(limits=threads, user_api="blas"):
+                r = _cpu_page_sample(orc, pages[0], tok_ids, mask, max_new, decode_steps)
+        else:
+            r = _cpu_page_sample(orc, pages[0], tok_ids, mask, max_new, decode_steps)
+        r["cores"] = threads
+        log(f"[cpu] {threads} BLAS threads: {r['value']:.4f} pages/s ({r['sample']})")
+        runs.append(r)
+    best = runs[0]
+    out = {"value": best["value"], "unit": "pages/s", "cores": best["cores"], "kind": "port",
+           "port": "oracle/ numpy restatement of the reference page path (f32, BLAS-threaded); "
+                   "the Rust reference cannot be built here",
+           "decode_tok_s": best["decode_tok_s"], "host_cpus": os.cpu_count(), "allowed_cpus": all_cores,
+           "cpu_model": cpu_model(), "sample": best["sample"]}
+    if len(runs) > 1:
+        out["at_env_threads"] = {k: runs[1][k] for k in ("value", "cores", "decode_tok_s", "sample")}
+    return out
+
+
+def _cpu_page_sample(orc, img, tok_ids, mask, max_new, decode_steps):
+    import numpy as np
     t0 = time.time()
     emb, _ = orc.image_embeddings(img)
     t1 = time.time()
@@ -150,17 +206,58 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
     step_last = steps()
     decode_s = (step_first + step_last) / 2 * (max_new - 1)
     page_s = (t1 - t0) + (t2 - t1) + decode_s
-    threads = blas_threads()
-    return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads,
-            "kind": "port",
-            "port": "oracle/ numpy restatement of the reference page path (f32, BLAS-threaded); "
-                    "the Rust reference cannot be built here",
-            "decode_tok_s": (max_new - 1) / decode_s,
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+    return {"value": 1.0 / page_s, "decode_tok_s": (max_new - 1) / decode_s,
             "sample": f"1 synthetic 1024x1024 page: vision {t1 - t0:.2f}s + prefill {t2 - t1:.2f}s "
                       f"({len(tok_ids)} tok) + {decode_steps} decode steps at KV {l_first} "
                       f"({step_first * 1e3:.0f} ms/step) and {decode_steps} at KV {l_last} "
                       f"({step_last * 1e3:.0f} ms/step), {max_new - 1} decode steps by the trapezoid"}
+
+
+SPAN_HZ = 100e6  # s_memrealtime
+
+
+def lang_dims(cfg):
+    """Decoder dimensions the span pricing needs (the checkpoint's language_config)."""
+    c = cfg.get("language_config", cfg)
+    heads, kvh = c["num_attention_heads"], c["num_key_value_heads"]
+    H = c["hidden_size"]
+    hd = H // heads
+    return {"H": H, "I": c["moe_intermediate_size"], "Is": c["moe_intermediate_size"] * c.get("n_shared_experts", 0),
+            "K": c["num_experts_per_tok"], "heads": heads, "kv_heads": kvh, "hd": hd, "qkvn": (heads + 2 * kvh) * hd}
+
+
+def span_bytes(kind, d, B, P, experts, step):
+    """Algorithmic HBM bytes of one decode launch: 16-bit weights streamed once + f32 activations.
+    gate/up: the distinct routed experts' gate+up rows + the shared expert's, x in, h out; down: their
+    down rows, h in, residual read + write; attention: f32 K and V of every attended key (page b at
+    step s attends P + s keys) + the q/k/v row in and the context row out."""
+    H, I, Is, K = d["H"], d["I"], d["Is"], d["K"]
+    if kind == "moe_gateup":
+        return (experts * 2 * I + 2 * Is) * H * 2 + B * H * 4 + (B * K * I + B * Is) * 4
+    if kind == "moe_down":
+        return (experts * I + Is) * H * 2 + (B * K * I + B * Is) * 4 + 2 * B * H * 4
+    return B * (P + step) * d["kv_heads"] * d["hd"] * 4 * 2 + B * (d["qkvn"] + H) * 4
+
+
+def span_roofline(spans, d, B, P):
+    """Per kind: launches, mean in-kernel duration and achieved GB/s = sum of algorithmic bytes / sum of
+    durations over every decode launch of the generate (each priced from its own expert count / step)."""
+    import numpy as np
+    out = {}
+    for kind, arr in spans.items():
+        layer, step = np.nonzero(arr[..., 0] > 0)
+        if not len(layer):
+            continue
+        rec = arr[layer, step]
+        dur = (rec[:, 1].astype(np.int64) - rec[:, 0].astype(np.int64)) / SPAN_HZ
+        ex = rec[:, 2].astype(np.int64)
+        by = np.array([span_bytes(kind, d, B, P, int(e), int(s)) for e, s in zip(ex, step)], np.float64)
+        out[kind] = {"launches": int(len(dur)), "avg_us": float(dur.mean() * 1e6),
+                     "p50_us": float(np.median(dur) * 1e6), "max_us": float(dur.max() * 1e6),
+                     "bytes_per_launch": float(by.mean()), "GB/s": float(by.sum() / dur.sum() / 1e9),
+                     "frac": float(by.sum() / dur.sum() / 1e9 / HBM_PEAK_GBS),
+                     "experts_mean": float(ex.mean()), "experts_range": [int(ex.min()), int(ex.max())]}
+    return out
 
 
 def dots_flops(cfg, N):
@@ -279,20 +376,35 @@ def main():
     ap.add_argument("--snapshot", default=None, choices=["q4k"],
                     help="q4k: configs[4], a full-size synthetic Q4_K DSQ snapshot loaded through the engine's "
                          "dequant-on-load path (written to $TMPDIR first)")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks then share devices; n_gpus reports the "
+                         "distinct devices used, `ranks` the rank count) - a test of the launch path only")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_under_torchrun(args.gpus))   # before any HIP call in this process
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    local = local % max(1, visible_gpus())  # one GPU per rank on a node; ranks share a GPU only when there are fewer
+    if world != args.gpus:
+        log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per requested GPU")
+        sys.exit(2)
+    n_vis = max(1, visible_gpus())
+    if world > n_vis and not args.oversubscribe:
+        log(f"[bench] {world} ranks but {n_vis} visible GPU(s): refusing to share devices (--oversubscribe to test)")
+        sys.exit(2)
+    local = local % n_vis   # one GPU per rank; ranks share a GPU only under --oversubscribe
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")   # host-side barrier / max only; the data path has no collective
+    devices = rank_devices(dist, local)
+    n_dev = len(set(devices))
 
     if args.workload == "dots2048":
         res = run_dots(args, rank, world, local, dist)
         if res is not None:
+            res.update(n_gpus=n_dev, ranks=world, devices=devices)
             print(json.dumps(res), flush=True)
         if dist is not None:
             dist.barrier()
@@ -376,25 +488,38 @@ def main():
 
     result = None
     if rank == 0:
+        # in context: the first timed batch decoded once more with launch spans on (every step's graph
+        # replay; each stamped launch is followed by a one-block fold launch, outside its own span)
+        eng.set_spans(True)
+        eng.generate_batch(batches[args.warmup][1], params, ignore_eos=True)
+        eng.set_spans(False)
+        ctx = span_roofline(eng.spans(), lang_dims(json.load(open(dsocr.FULL_CONFIG))), ppg,
+                            len(batches[args.warmup][1][0][0]))
         prof = eng.profile_decode(args.roofline_iters)
         gu = prof["moe_gateup"]
         kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
-        achieved = gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+        g = ctx["moe_gateup"]
+        roofline = {"bound": "hbm", "achieved": round(g["GB/s"], 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(g["GB/s"] / HBM_PEAK_GBS, 4),
                     "traffic": pmc_traffic(kernel),
-                    "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts + shared experts)",
-                    "avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
-                    # the same kernel chained in a hipGraph replay (what the decode loop sees per launch,
-                    # kernel boundary included): a second figure, not the one frac is priced on
-                    "replay_launch_us": round(gu["replay_us"], 2),
-                    "replay_frac": round(gu["bytes"] / (gu["replay_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
-                    if gu["replay_us"] > 0 else None,
-                    "experts_touched": prof["experts_touched"],
+                    "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
+                    # achieved = sum over every gate/up launch of the timed generate's decode steps of its
+                    # algorithmic bytes (priced from the experts that launch streamed) / sum of its
+                    # in-kernel duration (first wave entry -> last wave exit, s_memrealtime)
+                    "avg_launch_us": round(g["avg_us"], 3), "bytes_per_launch": round(g["bytes_per_launch"]),
+                    "launches": g["launches"], "experts_touched_mean": round(g["experts_mean"], 2),
+                    "experts_touched_range": g["experts_range"], "timing": "in-context launch spans",
+                    "in_context": ctx,
+                    # the same kernel outside the decode loop (profile_decode: HIP events on each launch's
+                    # dispatch packet, and n launches chained in one graph replay), on the last step's routing
+                    "isolated": {"avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
+                                 "frac": round(gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "replay_launch_us": round(gu["replay_us"], 2),
+                                 "experts_touched": prof["experts_touched"]},
                     "down_kernel": prof["moe_down_kernel"],
                     "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
                                    "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
-                               for k in ("moe_down", "attention", "lm_head", "lm_head_screened")
+                               for k in ("lm_head", "lm_head_screened")
                                if prof.get(k, {}).get("avg_us", 0) > 0},
                     "kv_len": prof["kv_len"]}
         cpu = None
@@ -409,7 +534,9 @@ def main():
             "value": round(value, 4),
             "unit": "pages/s",
             "decode_tok_s": round(tok_s, 1),
-            "n_gpus": world,
+            "n_gpus": n_dev,       # distinct devices the ranks ran on (== ranks unless --oversubscribe)
+            "ranks": world,
+            "devices": devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),

@@ -2,6 +2,10 @@
 // prefixed with a status tag ("EINVAL: ...") and mapped to dsocr_status.
 #include "../../../include/dsocr.h"
 
+#include <fcntl.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -50,6 +54,37 @@ dsocr_status guarded(F&& f) {
     } catch (...) {
         return status_from("EINTERNAL: unknown error");
     }
+}
+
+// Diagnostics (DSOCR_SEGV_MAPS=1): on SIGSEGV write the fault address and /proc/self/maps to stderr
+// (async-signal-safe: open/read/write only), then hand the signal back to the handler that was there
+// before (a profiler's or the default), so unsymbolised PCs in its stack dump resolve to library + offset.
+struct sigaction g_prev_segv;
+void segv_maps_handler(int sig, siginfo_t* si, void* uc) {
+    char buf[4096];
+    int n = snprintf(buf, sizeof(buf), "\n[dsocr] SIGSEGV at %p; /proc/self/maps follows\n", si ? si->si_addr : nullptr);
+    if (n > 0) (void)!write(2, buf, (size_t)n);
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        ssize_t r;
+        while ((r = read(fd, buf, sizeof(buf))) > 0) (void)!write(2, buf, (size_t)r);
+        close(fd);
+    }
+    (void)!write(2, "[dsocr] end of maps\n", 20);
+    sigaction(SIGSEGV, &g_prev_segv, nullptr);  // the faulting instruction re-runs under the previous handler
+    (void)sig;
+    (void)uc;
+}
+void install_segv_maps_once() {
+    static bool done = false;
+    if (done || !getenv("DSOCR_SEGV_MAPS")) return;
+    done = true;
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = segv_maps_handler;
+    sa.sa_flags = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
 }
 
 void check_hip(hipError_t e, const char* what) {
@@ -101,6 +136,7 @@ dsocr_status dsocr_engine_load(const dsocr_load_args* args, dsocr_engine** out) 
         if (!args || !out) throw std::runtime_error("EINVAL: NULL argument");
         if (!args->config_path) throw std::runtime_error("EINVAL: config_path is required");
         if (args->dtype < DSOCR_F32 || args->dtype > DSOCR_BF16) throw std::runtime_error("EINVAL: bad dtype");
+        install_segv_maps_once();
         auto* e = new dsocr_engine;
         try {
             e->impl.reset(new dsocr::Engine(args->config_path, args->weights_path ? args->weights_path : "",
@@ -268,9 +304,14 @@ dsocr_status dsocr_generate_batch(dsocr_engine* e, size_t n, const dsocr_request
 }
 
 dsocr_status dsocr_generate_trace(dsocr_engine* e, size_t n, const dsocr_request* reqs,
-                                  const dsocr_decode_params* params, dsocr_result* results, float* logits_out) {
+                                  const dsocr_decode_params* params, dsocr_result* results, float* logits_out,
+                                  size_t logits_cap) {
     return guarded([&] {
-        if (!e || (!reqs && n) || (!results && n) || !logits_out) throw std::runtime_error("EINVAL: NULL argument");
+        if (!e || (!reqs && n) || (!results && n) || !logits_out || !params) throw std::runtime_error("EINVAL: NULL argument");
+        const size_t need = n * (size_t)params->max_new_tokens * e->impl->cfg().lang.vocab;
+        if (need > logits_cap)
+            throw std::runtime_error("EINVAL: logits_out holds " + std::to_string(logits_cap) + " floats, the trace needs " +
+                                     std::to_string(need) + " (n * max_new_tokens * vocab)");
         std::vector<dsocr::GenRequest> rq;
         for (size_t i = 0; i < n; ++i) rq.push_back(to_request(reqs[i]));
         dsocr::GenParams g = to_params(params);
@@ -329,6 +370,31 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
 }
 
 // ---------------------------------------------------------------- device helpers
+dsocr_status dsocr_engine_set_spans(dsocr_engine* e, int enable) {
+    return guarded([&] {
+        if (!e) throw std::runtime_error("EINVAL: NULL engine");
+        e->impl->set_spans(enable != 0);
+    });
+}
+
+dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap, size_t* kinds, size_t* layers,
+                                size_t* steps) {
+    return guarded([&] {
+        if (!e) throw std::runtime_error("EINVAL: NULL engine");
+        const auto& v = e->impl->spans();
+        const size_t nl = e->impl->cfg().lang.layers;
+        const size_t ns = v.empty() ? 0 : (size_t)e->impl->span_steps();
+        if (kinds) *kinds = dsocr::Engine::SPAN_KINDS;
+        if (layers) *layers = nl;
+        if (steps) *steps = ns;
+        if (!out) return;  // size query
+        if (v.size() > cap)
+            throw std::runtime_error("EINVAL: span buffer holds " + std::to_string(cap) + " values, " +
+                                     std::to_string(v.size()) + " needed");
+        if (!v.empty()) std::memcpy(out, v.data(), v.size() * 8);
+    });
+}
+
 dsocr_status dsocr_device_count(int* n) {
     return guarded([&] { check_hip(hipGetDeviceCount(n), "hipGetDeviceCount"); });
 }

@@ -1119,7 +1119,9 @@ void Engine::decode_step(int B, int Lmax) {
             launch_dec_qkv_rope(g, re, st);
             da.prerot = 1;
             da.split = oproj_comb ? 1 : 0;
+            da.span = span_rec_ ? span_slots_ : nullptr;
             launch_dec_attn(da, st);
+            if (da.span) launch_span_reduce(span_slots_, span_rec(SPAN_ATTN, l), span_step_, span_cap_, nullptr, 0, st);
         } else {
             DecGemvArgs g;
             g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
@@ -1128,7 +1130,9 @@ void Engine::decode_step(int B, int Lmax) {
             if (fuse_norm || B <= 8) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
             else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
             launch_dec_gemv(g, st);
+            da.span = span_rec_ ? span_slots_ : nullptr;
             launch_dec_attn(da, st);
+            if (da.span) launch_span_reduce(span_slots_, span_rec(SPAN_ATTN, l), span_step_, span_cap_, nullptr, 0, st);
         }
         if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
         else launch_dec_gemv(go, st);
@@ -1164,7 +1168,17 @@ void Engine::decode_step(int B, int Lmax) {
             launch_moe_down2(m, st);
             continue;
         }
-        launch_moe_decode(moe_args(l, B, X), st);
+        if (!span_rec_) {
+            launch_moe_decode(moe_args(l, B, X), st);
+            continue;
+        }
+        MoeDecodeArgs ma = moe_args(l, B, X);
+        launch_moe_decode(ma, st, MOE_ROUTE);
+        ma.span = span_slots_;
+        launch_moe_decode(ma, st, MOE_GATEUP);
+        launch_span_reduce(span_slots_, span_rec(SPAN_GATEUP, l), span_step_, span_cap_, ma.ids, B * ma.topk, st);
+        launch_moe_decode(ma, st, MOE_DOWN);
+        launch_span_reduce(span_slots_, span_rec(SPAN_DOWN, l), span_step_, span_cap_, ma.ids, B * ma.topk, st);
     }
 }
 
@@ -1659,6 +1673,15 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         HIP_CHECK(hipEventRecord(ev[5], st));
         HIP_CHECK(hipStreamSynchronize(st));
     } else {
+    if (spans_on_) {
+        span_cap_ = (int)std::max<size_t>(p.max_new, 1);
+        const size_t rec_bytes = (size_t)SPAN_KINDS * L.layers * span_cap_ * 4 * 8;
+        span_slots_ = (unsigned long long*)ws("s_span_slots", (size_t)SPAN_SLOTS * 16);
+        span_rec_ = (unsigned long long*)ws("s_span_rec", rec_bytes);
+        span_step_ = d_outlen;
+        HIP_CHECK(hipMemsetAsync(span_slots_, 0, (size_t)SPAN_SLOTS * 16, st));
+        HIP_CHECK(hipMemsetAsync(span_rec_, 0, rec_bytes, st));
+    }
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
@@ -1702,6 +1725,13 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipStreamSynchronize(st));
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
+    if (span_rec_) {
+        spans_host_.resize((size_t)SPAN_KINDS * L.layers * span_cap_ * 4);
+        HIP_CHECK(hipMemcpy(spans_host_.data(), span_rec_, spans_host_.size() * 8, hipMemcpyDeviceToHost));
+        span_rec_ = nullptr;  // profile_decode and later generates run unstamped unless re-enabled
+        span_slots_ = nullptr;
+        span_step_ = nullptr;
+    }
     }  // cached decode loop
     HIP_CHECK(hipHostFree(pin_done));
     {

@@ -1443,6 +1443,7 @@ __device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, 
 // q, k_new and v_new are loaded before the position and no RoPE table is read here.
 template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false, int NSUB = 1, bool POLL = false>
 __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
+    WaveSpan span_(a.span);
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
     constexpr int DG = HD / 4, KG = 256 / DG, KPG = CH / KG;     // PV: float4 dim groups x key groups
@@ -2759,6 +2760,7 @@ __device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int so
 
 template <typename WT, int RB = 2>
 __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn) {
+    WaveSpan span_(a.span);
     __shared__ __attribute__((aligned(16))) float rank_lds[4][64];
     constexpr int U = 3;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2849,6 +2851,7 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
 // partials meet once in LDS and x[j] += (p0 + p1) + (p2 + p3).
 template <typename WT, int RPB, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void moe_down_mix_kernel(MoeDec2Args a) {
+    WaveSpan span_(a.span);
     __shared__ float part[NW][RPB];
     constexpr int U = 16 / NW;  // chunks per lane: (topk * I + Is) / 8 / NW waves <= 64 U
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -3357,7 +3360,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     m.topk = K; m.E = E; m.I = a.I; m.Wgu = a.Wgu; m.Wd = a.Wd; m.wdtype = a.wdtype; m.h = a.h; m.ids = a.ids;
     if (a.sWgu && a.sWd && a.Is > 0) { m.Is = a.Is; m.sWgu = a.sWgu; m.sWd = a.sWd; m.hs = a.hs; }
     m.Wgu_swz = a.Wgu_swz; m.sWgu_swz = a.sWgu_swz; m.Wd_swz = a.Wd_swz; m.sWd_swz = a.sWd_swz;
-    m.dn_part = a.dn_part; m.dn_tick = a.dn_tick;
+    m.dn_part = a.dn_part; m.dn_tick = a.dn_tick; m.span = a.span;
     DecGemvArgs& gr = p.router;
     gr.M = T; gr.N = E; gr.K = a.H; gr.x = mx; gr.ldx = a.H; gr.W = a.router; gr.ldw = a.H; gr.wdtype = a.router_wdt;
     gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps;

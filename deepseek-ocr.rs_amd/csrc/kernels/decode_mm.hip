@@ -383,6 +383,7 @@ void launch_dec_mm(const DecGemvArgs& a, hipStream_t s) {
 // same) and dropped.
 template <typename WT, int PF, bool SWZ>
 __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
+    WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
     constexpr int NWV = 8;
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
@@ -555,6 +556,7 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
 // 'splitk-seam'; hand-off: the sc1-load table's first row).
 template <typename WT, int PF, bool SWZ, int NWV>
 __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a) {
+    WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
     constexpr int RT = 16 * NWV, U = 2;  // rows per unit (16 per wave), chunks per lane (I <= 1024)
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]

@@ -138,6 +138,29 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     }
 }
 
+// In-context launch spans (Engine::set_spans, off by default): a kernel whose args carry a slot
+// array opens a WaveSpan first thing; every wave then writes (entry, exit) wall clock (s_memrealtime,
+// 100 MHz) to its own slot, exit being the destructor, i.e. after the wave's last store is issued on
+// whichever path it leaves by.  span_reduce_kernel (misc.hip), launched right after on the same
+// stream, folds the slots to the launch's (first entry, last exit) and clears them.
+struct WaveSpan {
+    unsigned long long* s;
+    unsigned long long t0 = 0;
+    __device__ __forceinline__ explicit WaveSpan(unsigned long long* slots) : s(slots) {
+        if (s) t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ ~WaveSpan() {
+        if (!s) return;
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const long gw = ((long)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
+                        (threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0 && gw < SPAN_SLOTS) {
+            s[2 * gw] = t0;
+            s[2 * gw + 1] = t1;
+        }
+    }
+};
+
 // order-preserving float <-> unsigned key (atomicMax over floats); key 0 sorts below every
 // float and decodes to -inf
 __device__ __forceinline__ unsigned fkey(float f) {

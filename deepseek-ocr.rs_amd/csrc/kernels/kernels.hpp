@@ -11,6 +11,12 @@ enum WDType : int { WDT_BF16 = 0, WDT_F16 = 1 };
 // DSOCR_LAUNCH (decode.hip, lmhead.hip) records its own dispatch begin / end into the two events
 // (hipExtLaunchKernelGGL: the dispatch-packet timestamps rocprofv3's kernel trace reports) and the
 // pair is cleared.  Host-side, per thread; never set while a stream is being captured.
+// In-context launch spans (dev_common.hpp WaveSpan): per-wave (entry, exit) slots of one launch,
+// folded by launch_span_reduce into rec[min(*step, cap - 1)] = {first entry, last exit, distinct ids
+// among ids[0..n_ids) (0 if none), waves seen} (100 MHz wall clock) and cleared for the next launch.
+constexpr long SPAN_SLOTS = 16384;
+void launch_span_reduce(unsigned long long* slots, unsigned long long* rec, const int* step, int cap, const int* ids,
+                        int n_ids, hipStream_t s);
 struct ProfEvents {
     hipEvent_t start = nullptr, stop = nullptr;
 };
@@ -240,6 +246,7 @@ struct DecAttn2Args {
     const void* Wqkv = nullptr; int wdtype = WDT_F16; const float* qkv_bias = nullptr;
     int* qkv_cnt = nullptr; int* err = nullptr;
     unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
+    unsigned long long* span = nullptr;    // launch-span slots (SPAN_SLOTS pairs) or null
     int prerot = 0;                        // q / k rows already rotated (dec_qkv_rope)
     int split = 0;                         // no in-kernel combine: dim-major records for dec_oproj_comb
 };
@@ -301,6 +308,7 @@ struct MoeDec2Args {
     int* ids_out = nullptr; float* w_out = nullptr;
     int dbg = 0;  // experiment knobs (DSOCR_DBG_GU): 1 skip routing, 2 skip weight stream
     unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
+    unsigned long long* span = nullptr;    // launch-span slots (SPAN_SLOTS pairs) or null
     // fused launch (moe_fused_slot_kernel): arrival counters (SYNC_SHARDS lines, zeroed before
     // the launch), arrivals to wait for (set by the launcher), give-up flag
     int* sync = nullptr; int sync_target = 0; int* err = nullptr;
@@ -374,6 +382,7 @@ struct MoeDecodeArgs {
     int* dn_tick = nullptr;     // [H / 128], zero between launches
     int* eoff = nullptr; int* arow = nullptr; int* apos = nullptr; int* active = nullptr;  // T > 8:
     int* n_active = nullptr; float* aw = nullptr;                                          // [E+1],[TK],[TK],[E],[1],[TK]
+    unsigned long long* span = nullptr;  // launch-span slots for the gate/up and down launches (or null)
 };
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments

@@ -202,4 +202,60 @@ void launch_rep_penalty(const SampleArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(rep_penalty_kernel, dim3(8, a.B), dim3(256), 0, s, a);
 }
 
+// ------------------------------------------------------------------ launch spans (diagnostics)
+// One block folds the per-wave (entry, exit) slots of the launch just made (dev_common.hpp WaveSpan):
+// first entry, last exit, slots seen; clears them; counts the distinct ids of the launch (e.g. the
+// experts its routing picked) and stores the record at the step the device is on (out_len of page 0).
+__global__ __launch_bounds__(1024) void span_reduce_kernel(unsigned long long* slots, unsigned long long* rec,
+                                                            const int* step, int cap, const int* ids, int n_ids) {
+    __shared__ unsigned long long lo_s[16], hi_s[16];
+    __shared__ int cnt_s[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long lo = ~0ull, hi = 0;
+    int cnt = 0;
+    for (long i = tid; i < SPAN_SLOTS; i += 1024) {
+        const unsigned long long a = slots[2 * i], b = slots[2 * i + 1];
+        if (a != 0) {
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+            ++cnt;
+            slots[2 * i] = 0;
+            slots[2 * i + 1] = 0;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long l2 = __shfl_xor(lo, o), h2 = __shfl_xor(hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+        cnt += __shfl_xor(cnt, o);
+    }
+    if (lane == 0) { lo_s[wave] = lo; hi_s[wave] = hi; cnt_s[wave] = cnt; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 16; ++w) {
+            lo = lo_s[w] < lo ? lo_s[w] : lo;
+            hi = hi_s[w] > hi ? hi_s[w] : hi;
+            cnt += cnt_s[w];
+        }
+        int distinct = 0;
+        for (int i = 0; i < n_ids; ++i) {
+            bool seen = false;
+            for (int j = 0; j < i; ++j) seen = seen || ids[j] == ids[i];
+            distinct += (!seen && ids[i] >= 0) ? 1 : 0;
+        }
+        int k = step ? *step : 0;
+        k = k < 0 ? 0 : (k >= cap ? cap - 1 : k);
+        unsigned long long* r = rec + 4L * k;
+        r[0] = cnt ? lo : 0;
+        r[1] = hi;
+        r[2] = (unsigned long long)distinct;
+        r[3] = (unsigned long long)cnt;
+    }
+}
+
+void launch_span_reduce(unsigned long long* slots, unsigned long long* rec, const int* step, int cap, const int* ids,
+                        int n_ids, hipStream_t s) {
+    hipLaunchKernelGGL(span_reduce_kernel, dim3(1), dim3(1024), 0, s, slots, rec, step, cap, ids, n_ids);
+}
+
 }  // namespace dsocr

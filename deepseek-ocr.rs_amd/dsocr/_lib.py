@@ -86,6 +86,7 @@ EXPORTS = [
     "dsocr_generate_trace", "dsocr_k_moe_kernels", "dsocr_k_lmhead_screened",
     "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
     "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16", "dsocr_k_gemv_splitk",
+    "dsocr_engine_set_spans", "dsocr_engine_spans",
 ]
 
 _lib = None
@@ -116,7 +117,8 @@ def lib():
     L.dsocr_generate.argtypes = [vp, C.POINTER(RequestC), C.POINTER(DecodeParamsC), STREAM_CB, vp, vp, sz,
                                  C.POINTER(sz)]
     L.dsocr_generate_batch.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC)]
-    L.dsocr_generate_trace.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC), vp]
+    L.dsocr_generate_trace.argtypes = [vp, sz, C.POINTER(RequestC), C.POINTER(DecodeParamsC), C.POINTER(ResultC), vp,
+                                       sz]
     L.dsocr_k_attention_bf16.argtypes = [i32, i32, i32, i32, f32, vp, C.c_long, vp, C.c_long, i32]
     L.dsocr_dots_load.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64, i32, C.POINTER(vp)]
     L.dsocr_dots_free.argtypes = [vp]
@@ -130,6 +132,8 @@ def lib():
     L.dsocr_k_moe_kernels.argtypes = [i32, i32, i32, i32, i32, i32, i32, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
     L.dsocr_last_timings.argtypes = [vp, C.POINTER(TimingsC)]
     L.dsocr_profile_decode.argtypes = [vp, i32, C.POINTER(DecodeProfileC)]
+    L.dsocr_engine_set_spans.argtypes = [vp, i32]
+    L.dsocr_engine_spans.argtypes = [vp, vp, sz, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
     L.dsocr_device_count.argtypes = [C.POINTER(i32)]
     L.dsocr_dev_alloc.argtypes = [sz, C.POINTER(vp)]
     L.dsocr_dev_free.argtypes = [vp]

@@ -271,13 +271,31 @@ class DeepseekOcrEngine:
         logits = np.zeros((len(requests), max(params.max_new_tokens, 1), self.vocab), np.float32)
         pc = _params_c(params, self.eos_token_id, ignore_eos)
         check(lib().dsocr_generate_trace(self._h, len(requests), reqs, C.byref(pc), res,
-                                         logits.ctypes.data_as(C.c_void_p)))
+                                         logits.ctypes.data_as(C.c_void_p), logits.size))
         return [outs[i][:res[i].n_out].tolist() for i in range(len(requests))], logits
 
     def last_timings(self) -> dict:
         t = TimingsC()
         check(lib().dsocr_last_timings(self._h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in TimingsC._fields_}
+
+    SPAN_KINDS = ("moe_gateup", "moe_down", "attention")
+
+    def set_spans(self, on: bool = True):
+        """In-context launch spans for the following generates (dsocr_engine_set_spans)."""
+        check(lib().dsocr_engine_set_spans(self._h, 1 if on else 0))
+
+    def spans(self) -> dict:
+        """Launch spans of the last generate run with spans on: {kind: array [layers][steps][4] uint64
+        (entry, exit, distinct experts, waves), 100 MHz wall clock}; only the decode steps
+        (index 1 .. steps - 1) of the layers that have the launch are non-zero."""
+        k, l, st = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        check(lib().dsocr_engine_spans(self._h, None, 0, C.byref(k), C.byref(l), C.byref(st)))
+        if st.value == 0:
+            return {}
+        buf = np.zeros((k.value, l.value, st.value, 4), np.uint64)
+        check(lib().dsocr_engine_spans(self._h, buf.ctypes.data_as(C.c_void_p), buf.size, None, None, None))
+        return {name: buf[i] for i, name in enumerate(self.SPAN_KINDS[:k.value])}
 
     def profile_decode(self, iters: int = 3) -> dict:
         """HIP-event timings + algorithmic bytes of the dominant decode kernels (see dsocr.h)."""

@@ -163,9 +163,11 @@ dsocr_status dsocr_last_timings(const dsocr_engine* e, dsocr_timings* t);
  * counterparts: the cli-debug top-2 logits dump (crates/infer-deepseek/src/debug.rs:17-21,
  * model/mod.rs:1937-1949) and the teacher-forcing logits its baseline tests compare
  * (tests/baseline.rs:1108).  Selection runs on the exact lm_head while tracing (the screened head
- * never forms the full logits; its ids equal the exact head's). */
+ * never forms the full logits; its ids equal the exact head's).  logits_cap = capacity of logits_out in
+ * floats; DSOCR_EINVAL (nothing written) when n * max_new_tokens * vocab exceeds it. */
 dsocr_status dsocr_generate_trace(dsocr_engine* e, size_t n, const dsocr_request* reqs,
-                                  const dsocr_decode_params* params, dsocr_result* results, float* logits_out);
+                                  const dsocr_decode_params* params, dsocr_result* results, float* logits_out,
+                                  size_t logits_cap);
 
 /* Decode-kernel profile (bench roofline): replays the dominant decode kernels of the
  * last generate() call on its final routing / KV state, each timed with HIP events on
@@ -199,6 +201,18 @@ typedef struct dsocr_decode_profile {
     const char* moe_down_kernel;
 } dsocr_decode_profile;
 dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out);
+
+/* In-context launch spans (diagnostics for the roofline line; no reference counterpart): while enabled,
+ * the decode steps of every following generate record, per decoder layer, the first-wave entry and
+ * last-wave exit (s_memrealtime, 100 MHz) of the MoE gate/up (kind 0), MoE down (1) and attention (2)
+ * launches inside the replayed step graph, plus the distinct experts the MoE launches streamed.
+ * dsocr_engine_spans copies the last such generate's records, [kinds][layers][steps][4] uint64
+ * {entry, exit, distinct experts, waves}, into out (cap = capacity in uint64; DSOCR_EINVAL if short;
+ * out NULL: only the dimensions are returned);
+ * step s = tokens emitted before the step, decode steps are 1 .. steps - 1, unused entries are 0. */
+dsocr_status dsocr_engine_set_spans(dsocr_engine* e, int enable);
+dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap, size_t* kinds, size_t* layers,
+                                size_t* steps);
 
 /* ---- device helpers for tests / tooling (plain pointers; no torch) */
 dsocr_status dsocr_device_count(int* n);

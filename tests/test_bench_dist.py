@@ -57,24 +57,73 @@ def test_two_rank_gloo_sharding_and_reduction():
         assert tok_s == 300.0          # sum over ranks
 
 
+def test_world_size_must_match_gpus():
+    """A launcher's WORLD_SIZE that disagrees with --gpus is refused before any device work."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2 and "WORLD_SIZE=2 but --gpus 1" in out.stderr
+
+
+@pytest.mark.timeout(300)
+def test_gpus_flag_launches_ranks_and_refuses_shared_devices():
+    """`bench.py --gpus 2` with no launcher starts two ranks under torch.distributed.run; with fewer
+    visible GPUs than ranks (none here) every rank refuses to share a device, so the run exits non-zero
+    and prints no JSON line instead of reporting shared-device throughput as 2 GPUs."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"], cwd=ROOT,
+                         env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode != 0
+    assert "without a launcher" in out.stderr and "refusing to share devices" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_two_rank_bench_process_run(gpu):
-    """The N>1 bench as the driver launches it (torch.distributed.run, one process per rank, gloo barrier
-    and max-over-ranks timing), two engines here sharing the box's one GPU (rank r uses GPU r % count):
-    one JSON line from rank 0 whose value counts both ranks' pages."""
+    """`python bench.py --gpus 2` exactly as a user types it (no launcher): the bench re-launches itself under
+    torch.distributed.run (one process per rank, gloo barrier and max-over-ranks timing).  The box has one
+    GPU, so --oversubscribe lets both engines share it: one JSON line from rank 0 whose value counts both
+    ranks' pages, ranks == 2, and n_gpus == the distinct devices actually used."""
     import json
     import subprocess
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "1", "--warmup", "0", "--max-new-tokens", "8", "--no-cpu-baseline",
-           "--roofline-iters", "1"]
-    env = dict(os.environ, OMP_NUM_THREADS="4")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--oversubscribe", "--steps", "1",
+           "--warmup", "0", "--max-new-tokens", "8", "--no-cpu-baseline", "--roofline-iters", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "4"
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 2 and res["value"] > 0
+    assert res["ranks"] == 2 and len(res["devices"]) == 2 and res["n_gpus"] == len(set(res["devices"]))
+    assert res["config"]["global_batch"] == 2 and res["value"] > 0
     assert abs(res["value"] - 2 / (res["ms_per_step"] / 1e3)) < 1e-3 * res["value"] + 1e-3
+
+
+def test_span_roofline_prices_each_launch():
+    """bench.span_roofline: every recorded launch priced from its own expert count (gate/up, down) or
+    step (attention), achieved = sum(bytes) / sum(durations); empty slots ignored."""
+    import numpy as np
+    d = bench.lang_dims({"hidden_size": 1280, "moe_intermediate_size": 896, "n_shared_experts": 2,
+                         "num_experts_per_tok": 6, "num_attention_heads": 10, "num_key_value_heads": 10})
+    arr = np.zeros((3, 12, 8, 4), np.uint64)
+    # gate/up, layer 1: steps 1 and 2, 9 us and 11 us (900 / 1100 ticks of 10 ns), 6 and 30 experts
+    arr[0, 1, 1] = [1000, 1900, 6, 7168]
+    arr[0, 1, 2] = [5000, 6100, 30, 7168]
+    # attention, layer 0, step 3: 8 us
+    arr[2, 0, 3] = [100, 900, 0, 800]
+    got = bench.span_roofline({"moe_gateup": arr[0], "moe_down": arr[1], "attention": arr[2]}, d, 8, 706)
+    assert set(got) == {"moe_gateup", "attention"}
+    g = got["moe_gateup"]
+    b6 = bench.span_bytes("moe_gateup", d, 8, 706, 6, 1)
+    b30 = bench.span_bytes("moe_gateup", d, 8, 706, 30, 2)
+    assert b30 - b6 == 24 * 2 * 896 * 1280 * 2
+    assert g["launches"] == 2 and abs(g["avg_us"] - 10.0) < 1e-9
+    assert abs(g["GB/s"] - (b6 + b30) / 20e-6 / 1e9) < 1e-6 and g["experts_range"] == [6, 30]
+    a = got["attention"]
+    assert abs(a["GB/s"] - bench.span_bytes("attention", d, 8, 706, 0, 3) / 8e-6 / 1e9) < 1e-6
+    assert bench.span_bytes("attention", d, 1, 706, 0, 3) == 709 * 10 * 128 * 8 + (3840 + 1280) * 4

@@ -33,6 +33,13 @@ for step in "$@"; do
     pmc_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_write.log 2>&1 ;;
     pmc_calib) run 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_calib -o mb --output-format csv -- ./tools/mb_stream > gpurun_out/pmc_calib.log 2>&1 ;;
     mbprof) run 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mbprof -o mb --output-format csv -- ./tools/mb_stream > gpurun_out/mbprof.log 2>&1 ;;
+    spans1) run 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/spans1.log 2>&1 ;;
+    spans8) run 600 python bench.py --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/spans8.log 2>&1 ;;
+    # graph-mode kernel trace with the HIP runtime's graph packet capture off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0)
+    gprof_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_nopc -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_nopc.log 2>&1 ;;
+    gprof8_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8_nopc.log 2>&1 ;;
+    # the round-2 crash reproduced with the maps dump (expected SIGSEGV: run it last)
+    gprof_maps) DSOCR_SEGV_MAPS=1 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_maps.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
