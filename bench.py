@@ -240,23 +240,36 @@ def span_bytes(kind, d, B, P, experts, step):
 
 
 def span_roofline(spans, d, B, P):
-    """Per kind: launches, mean in-kernel duration and achieved GB/s = sum of algorithmic bytes / sum of
-    durations over every decode launch of the generate (each priced from its own expert count / step)."""
+    """Per kind, over every decode launch of the generate (each priced from its own expert count / step):
+    launches; `avg_us` = mean dispatch duration (HIP events recorded around the launch inside the replayed
+    step graph, what rocprofv3's kernel trace reports; the in-kernel wave span when no events were taken)
+    and `GB/s` = sum of algorithmic bytes / sum of those durations; `wave_avg_us` / `wave_GB/s` the same
+    over the in-kernel span (first wave entry -> last wave exit, s_memrealtime) where recorded."""
     import numpy as np
     out = {}
     for kind, arr in spans.items():
-        layer, step = np.nonzero(arr[..., 0] > 0)
+        valid = (arr[..., 4] > 0) | (arr[..., 0] > 0)
+        layer, step = np.nonzero(valid)
         if not len(layer):
             continue
         rec = arr[layer, step]
-        dur = (rec[:, 1].astype(np.int64) - rec[:, 0].astype(np.int64)) / SPAN_HZ
+        ev = rec[:, 4].astype(np.float64) * 1e-9
+        has_wave = rec[:, 0] > 0
+        wave = (rec[:, 1].astype(np.int64) - rec[:, 0].astype(np.int64)) / SPAN_HZ
+        events = bool(np.all(ev > 0))
+        dur = ev if events else wave
         ex = rec[:, 2].astype(np.int64)
         by = np.array([span_bytes(kind, d, B, P, int(e), int(s)) for e, s in zip(ex, step)], np.float64)
-        out[kind] = {"launches": int(len(dur)), "avg_us": float(dur.mean() * 1e6),
-                     "p50_us": float(np.median(dur) * 1e6), "max_us": float(dur.max() * 1e6),
-                     "bytes_per_launch": float(by.mean()), "GB/s": float(by.sum() / dur.sum() / 1e9),
-                     "frac": float(by.sum() / dur.sum() / 1e9 / HBM_PEAK_GBS),
-                     "experts_mean": float(ex.mean()), "experts_range": [int(ex.min()), int(ex.max())]}
+        o = {"launches": int(len(dur)), "avg_us": float(dur.mean() * 1e6),
+             "p50_us": float(np.median(dur) * 1e6), "max_us": float(dur.max() * 1e6),
+             "bytes_per_launch": float(by.mean()), "GB/s": float(by.sum() / dur.sum() / 1e9),
+             "frac": float(by.sum() / dur.sum() / 1e9 / HBM_PEAK_GBS),
+             "timing": "hip events in graph" if events else "in-kernel wave span",
+             "experts_mean": float(ex.mean()), "experts_range": [int(ex.min()), int(ex.max())]}
+        if np.all(has_wave):
+            o["wave_avg_us"] = float(wave.mean() * 1e6)
+            o["wave_GB/s"] = float(by.sum() / wave.sum() / 1e9)
+        out[kind] = o
     return out
 
 
@@ -490,11 +503,17 @@ def main():
     if rank == 0:
         # in context: the first timed batch decoded once more with launch spans on (every step's graph
         # replay; each stamped launch is followed by a one-block fold launch, outside its own span)
-        eng.set_spans(True)
+        dims = lang_dims(json.load(open(dsocr.FULL_CONFIG)))
+        P = len(batches[args.warmup][1][0][0])
+        eng.set_spans(eng.SPAN_EVENTS)
         eng.generate_batch(batches[args.warmup][1], params, ignore_eos=True)
-        eng.set_spans(False)
-        ctx = span_roofline(eng.spans(), lang_dims(json.load(open(dsocr.FULL_CONFIG))), ppg,
-                            len(batches[args.warmup][1][0][0]))
+        ctx = span_roofline(eng.spans(), dims, ppg, P)
+        eng.set_spans(eng.SPAN_WAVES)   # a second pass for the in-kernel wave spans
+        eng.generate_batch(batches[args.warmup][1], params, ignore_eos=True)
+        eng.set_spans(0)
+        for k, v in span_roofline(eng.spans(), dims, ppg, P).items():
+            if k in ctx:
+                ctx[k]["wave_avg_us"], ctx[k]["wave_GB/s"] = v["wave_avg_us"], v["wave_GB/s"]
         prof = eng.profile_decode(args.roofline_iters)
         gu = prof["moe_gateup"]
         kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
@@ -503,12 +522,13 @@ def main():
                     "unit": "GB/s", "frac": round(g["GB/s"] / HBM_PEAK_GBS, 4),
                     "traffic": pmc_traffic(kernel),
                     "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
-                    # achieved = sum over every gate/up launch of the timed generate's decode steps of its
-                    # algorithmic bytes (priced from the experts that launch streamed) / sum of its
-                    # in-kernel duration (first wave entry -> last wave exit, s_memrealtime)
+                    # achieved = sum over every gate/up launch of a whole generate's decode steps (the first
+                    # timed batch decoded again) of its algorithmic bytes (priced from the experts that launch
+                    # streamed) / sum of its dispatch durations, HIP events recorded around it inside the
+                    # replayed step graph
                     "avg_launch_us": round(g["avg_us"], 3), "bytes_per_launch": round(g["bytes_per_launch"]),
                     "launches": g["launches"], "experts_touched_mean": round(g["experts_mean"], 2),
-                    "experts_touched_range": g["experts_range"], "timing": "in-context launch spans",
+                    "experts_touched_range": g["experts_range"], "timing": g["timing"],
                     "in_context": ctx,
                     # the same kernel outside the decode loop (profile_decode: HIP events on each launch's
                     # dispatch packet, and n launches chained in one graph replay), on the last step's routing

@@ -373,7 +373,7 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
 dsocr_status dsocr_engine_set_spans(dsocr_engine* e, int enable) {
     return guarded([&] {
         if (!e) throw std::runtime_error("EINVAL: NULL engine");
-        e->impl->set_spans(enable != 0);
+        e->impl->set_spans(enable);
     });
 }
 
@@ -394,6 +394,7 @@ dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap
         if (!v.empty()) std::memcpy(out, v.data(), v.size() * 8);
     });
 }
+static_assert(dsocr::Engine::SPAN_FIELDS == 5, "dsocr.h documents 5 fields per span record");
 
 dsocr_status dsocr_device_count(int* n) {
     return guarded([&] { check_hip(hipGetDeviceCount(n), "hipGetDeviceCount"); });

@@ -318,6 +318,7 @@ void Engine::prepare_page_device(const uint8_t* rgb, int w, int h, PagePixels& p
 
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& e : span_ev_) (void)hipEventDestroy(e);
     for (auto& kv : pinned_) (void)hipHostFree(kv.second.first);
     for (auto& kv : winmaps_) { (void)hipFree(kv.second.first); (void)hipFree(kv.second.second); }
     for (auto& kv : ws_) (void)hipFree(kv.second.first);
@@ -1073,6 +1074,23 @@ void Engine::decode_step(int B, int Lmax) {
     float* part = wsf("s_part", dec_attn_workspace(B, L.heads, hd, Lmax) / 4 + 16);
     if (L.heads % L.kv_heads) throw std::runtime_error("EINVAL: num_attention_heads must be a multiple of num_key_value_heads");
     int* err = wsi("s_err", 4);
+    // launch spans (set_spans): HIP events on the stream around the launch (dispatch-level duration,
+    // what rocprofv3's kernel trace reports) + the in-kernel wave span folded right after it
+    auto stamped = [&](int kind, int l, const std::function<void()>& launch, const int* ids, int n_ids) {
+        if (!span_rec_) {
+            launch();
+            return;
+        }
+        hipEvent_t* ev = &span_ev_[((size_t)kind * L.layers + l) * 2];
+        const bool events = (span_mode_ & SPAN_EVENTS) != 0, waves = (span_mode_ & SPAN_WAVES) != 0;
+        if (events) HIP_CHECK(hipEventRecord(ev[0], st));
+        launch();
+        if (events) HIP_CHECK(hipEventRecord(ev[1], st));
+        // the fold: after every launch with wave spans; events only: once per MoE layer, after the
+        // down launch (its record carries the layer's distinct experts for both MoE launches)
+        if (waves || (kind == SPAN_DOWN && ids))
+            launch_span_reduce(span_slots_, span_rec(kind, l), span_step_, span_cap_, ids, n_ids, st);
+    };
     for (int l = 0; l < L.layers; ++l) {
         DecLayer& d = layers_[l];
         const int QKVN = d.qkv.N;
@@ -1119,9 +1137,8 @@ void Engine::decode_step(int B, int Lmax) {
             launch_dec_qkv_rope(g, re, st);
             da.prerot = 1;
             da.split = oproj_comb ? 1 : 0;
-            da.span = span_rec_ ? span_slots_ : nullptr;
-            launch_dec_attn(da, st);
-            if (da.span) launch_span_reduce(span_slots_, span_rec(SPAN_ATTN, l), span_step_, span_cap_, nullptr, 0, st);
+            da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
+            stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
         } else {
             DecGemvArgs g;
             g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
@@ -1130,9 +1147,8 @@ void Engine::decode_step(int B, int Lmax) {
             if (fuse_norm || B <= 8) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
             else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
             launch_dec_gemv(g, st);
-            da.span = span_rec_ ? span_slots_ : nullptr;
-            launch_dec_attn(da, st);
-            if (da.span) launch_span_reduce(span_slots_, span_rec(SPAN_ATTN, l), span_step_, span_cap_, nullptr, 0, st);
+            da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
+            stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
         }
         if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
         else launch_dec_gemv(go, st);
@@ -1174,11 +1190,9 @@ void Engine::decode_step(int B, int Lmax) {
         }
         MoeDecodeArgs ma = moe_args(l, B, X);
         launch_moe_decode(ma, st, MOE_ROUTE);
-        ma.span = span_slots_;
-        launch_moe_decode(ma, st, MOE_GATEUP);
-        launch_span_reduce(span_slots_, span_rec(SPAN_GATEUP, l), span_step_, span_cap_, ma.ids, B * ma.topk, st);
-        launch_moe_decode(ma, st, MOE_DOWN);
-        launch_span_reduce(span_slots_, span_rec(SPAN_DOWN, l), span_step_, span_cap_, ma.ids, B * ma.topk, st);
+        ma.span = (span_mode_ & SPAN_WAVES) ? span_slots_ : nullptr;
+        stamped(SPAN_GATEUP, l, [&] { launch_moe_decode(ma, st, MOE_GATEUP); }, ma.ids, B * ma.topk);
+        stamped(SPAN_DOWN, l, [&] { launch_moe_decode(ma, st, MOE_DOWN); }, ma.ids, B * ma.topk);
     }
 }
 
@@ -1673,7 +1687,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         HIP_CHECK(hipEventRecord(ev[5], st));
         HIP_CHECK(hipStreamSynchronize(st));
     } else {
-    if (spans_on_) {
+    if (span_mode_) {
         span_cap_ = (int)std::max<size_t>(p.max_new, 1);
         const size_t rec_bytes = (size_t)SPAN_KINDS * L.layers * span_cap_ * 4 * 8;
         span_slots_ = (unsigned long long*)ws("s_span_slots", (size_t)SPAN_SLOTS * 16);
@@ -1681,7 +1695,24 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         span_step_ = d_outlen;
         HIP_CHECK(hipMemsetAsync(span_slots_, 0, (size_t)SPAN_SLOTS * 16, st));
         HIP_CHECK(hipMemsetAsync(span_rec_, 0, rec_bytes, st));
+        if (span_ev_.empty()) {
+            span_ev_.resize((size_t)SPAN_KINDS * L.layers * 2);
+            for (auto& e : span_ev_) HIP_CHECK(hipEventCreate(&e));
+        }
+        span_ev_ns_.assign((size_t)SPAN_KINDS * L.layers * span_cap_, 0.0);
     }
+    // after a stamped step: the dispatch-level duration of every bracketed launch, at the step's index
+    auto read_span_events = [&](size_t step) {
+        HIP_CHECK(hipEventSynchronize(span_ev_.back()));
+        const size_t k = std::min(step, (size_t)span_cap_ - 1);
+        for (size_t i = 0; i < (size_t)SPAN_KINDS * L.layers; ++i) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, span_ev_[2 * i], span_ev_[2 * i + 1]) == hipSuccess)
+                span_ev_ns_[i * span_cap_ + k] = ms * 1e6;
+            else
+                (void)hipGetLastError();  // pair not recorded this step (e.g. the dense layer)
+        }
+    };
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
@@ -1713,6 +1744,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     for (size_t i = 1; i < p.max_new; ++i) {
         if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
         else step_body();
+        if (span_rec_ && (span_mode_ & SPAN_EVENTS)) read_span_events(i);
         ++steps;
         const bool check = cb != nullptr || (!p.ignore_eos && (i % 8 == 0 || i + 1 == p.max_new));
         if (check) {
@@ -1726,8 +1758,17 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
     if (span_rec_) {
-        spans_host_.resize((size_t)SPAN_KINDS * L.layers * span_cap_ * 4);
-        HIP_CHECK(hipMemcpy(spans_host_.data(), span_rec_, spans_host_.size() * 8, hipMemcpyDeviceToHost));
+        const size_t nrec = (size_t)SPAN_KINDS * L.layers * span_cap_;
+        std::vector<unsigned long long> dev(nrec * 4);
+        HIP_CHECK(hipMemcpy(dev.data(), span_rec_, dev.size() * 8, hipMemcpyDeviceToHost));
+        spans_host_.assign(nrec * SPAN_FIELDS, 0);
+        const size_t per_kind = (size_t)L.layers * span_cap_;
+        for (size_t r = 0; r < nrec; ++r) {
+            for (int f = 0; f < 4; ++f) spans_host_[r * SPAN_FIELDS + f] = dev[r * 4 + f];
+            if (span_mode_ & SPAN_EVENTS) spans_host_[r * SPAN_FIELDS + 4] = (unsigned long long)llround(span_ev_ns_[r]);
+            // events only: the gate/up record takes its layer's expert count from the down record
+            if (!(span_mode_ & SPAN_WAVES) && r < per_kind) spans_host_[r * SPAN_FIELDS + 2] = dev[(per_kind + r) * 4 + 2];
+        }
         span_rec_ = nullptr;  // profile_decode and later generates run unstamped unless re-enabled
         span_slots_ = nullptr;
         span_step_ = nullptr;

@@ -166,9 +166,12 @@ class Engine {
     // attention launches, with the distinct experts the MoE launches streamed (WaveSpan +
     // span_reduce_kernel; one extra fold launch after each stamped launch, inside the replayed graph).
     enum SpanKind : int { SPAN_GATEUP = 0, SPAN_DOWN = 1, SPAN_ATTN = 2, SPAN_KINDS = 3 };
-    void set_spans(bool on) { spans_on_ = on; }
-    // [kind][layer][step][4] u64 {entry, exit, distinct experts, waves} (100 MHz wall clock) of the last
-    // generate with spans on; step = tokens emitted before the step (1 .. steps - 1 are decode steps)
+    static constexpr int SPAN_FIELDS = 5;
+    enum SpanMode : int { SPAN_WAVES = 1, SPAN_EVENTS = 2 };  // bit mask; 0 = off
+    void set_spans(int mode) { span_mode_ = mode & (SPAN_WAVES | SPAN_EVENTS); }
+    // [kind][layer][step][SPAN_FIELDS] u64 {entry, exit (100 MHz wall clock), distinct experts, waves,
+    // dispatch duration in ns (HIP events recorded around the launch inside the replayed graph)} of the
+    // last generate with spans on; step = tokens emitted before the step (1 .. steps - 1 are decode steps)
     const std::vector<unsigned long long>& spans() const { return spans_host_; }
     int span_steps() const { return span_cap_; }
     hipStream_t stream() const { return stream_; }
@@ -258,12 +261,14 @@ class Engine {
     std::map<std::pair<int, int>, std::pair<int*, int*>> winmaps_;  // (n, grid) -> tok2win, win2tok
     int last_Lmax_ = 0;
     float* trace_ = nullptr;  // device logits trace of the running generate (parity hook)
-    bool spans_on_ = false;
+    int span_mode_ = 0;
     unsigned long long* span_slots_ = nullptr;  // device [SPAN_SLOTS][2]
     unsigned long long* span_rec_ = nullptr;    // device [SPAN_KINDS][layers][span_cap_][4]
     const int* span_step_ = nullptr;            // device step counter (out_len of page 0)
     int span_cap_ = 0;
     std::vector<unsigned long long> spans_host_;
+    std::vector<hipEvent_t> span_ev_;           // [SPAN_KINDS][layers][2]
+    std::vector<double> span_ev_ns_;            // [SPAN_KINDS][layers][span_cap_]
     unsigned long long* span_rec(int kind, int layer) const {
         return span_rec_ + ((size_t)kind * cfg_.lang.layers + layer) * span_cap_ * 4;
     }

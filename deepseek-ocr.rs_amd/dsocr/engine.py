@@ -281,19 +281,22 @@ class DeepseekOcrEngine:
 
     SPAN_KINDS = ("moe_gateup", "moe_down", "attention")
 
-    def set_spans(self, on: bool = True):
-        """In-context launch spans for the following generates (dsocr_engine_set_spans)."""
-        check(lib().dsocr_engine_set_spans(self._h, 1 if on else 0))
+    SPAN_WAVES, SPAN_EVENTS = 1, 2
+
+    def set_spans(self, mode: int):
+        """In-context launch spans for the following generates (dsocr_engine_set_spans): 0 off, bit 1 wave
+        spans, bit 2 HIP events around the launches inside the replayed step graph."""
+        check(lib().dsocr_engine_set_spans(self._h, int(mode)))
 
     def spans(self) -> dict:
-        """Launch spans of the last generate run with spans on: {kind: array [layers][steps][4] uint64
-        (entry, exit, distinct experts, waves), 100 MHz wall clock}; only the decode steps
-        (index 1 .. steps - 1) of the layers that have the launch are non-zero."""
+        """Launch spans of the last generate run with spans on: {kind: array [layers][steps][5] uint64
+        (entry, exit (100 MHz wall clock), distinct experts, waves, HIP-event dispatch duration ns)};
+        only the decode steps (index 1 .. steps - 1) of the layers that have the launch are non-zero."""
         k, l, st = C.c_size_t(), C.c_size_t(), C.c_size_t()
         check(lib().dsocr_engine_spans(self._h, None, 0, C.byref(k), C.byref(l), C.byref(st)))
         if st.value == 0:
             return {}
-        buf = np.zeros((k.value, l.value, st.value, 4), np.uint64)
+        buf = np.zeros((k.value, l.value, st.value, 5), np.uint64)
         check(lib().dsocr_engine_spans(self._h, buf.ctypes.data_as(C.c_void_p), buf.size, None, None, None))
         return {name: buf[i] for i, name in enumerate(self.SPAN_KINDS[:k.value])}
 

@@ -202,15 +202,17 @@ typedef struct dsocr_decode_profile {
 } dsocr_decode_profile;
 dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profile* out);
 
-/* In-context launch spans (diagnostics for the roofline line; no reference counterpart): while enabled,
- * the decode steps of every following generate record, per decoder layer, the first-wave entry and
- * last-wave exit (s_memrealtime, 100 MHz) of the MoE gate/up (kind 0), MoE down (1) and attention (2)
- * launches inside the replayed step graph, plus the distinct experts the MoE launches streamed.
- * dsocr_engine_spans copies the last such generate's records, [kinds][layers][steps][4] uint64
- * {entry, exit, distinct experts, waves}, into out (cap = capacity in uint64; DSOCR_EINVAL if short;
- * out NULL: only the dimensions are returned);
+/* In-context launch spans (diagnostics for the roofline line; no reference counterpart).  mode is a bit
+ * mask, 0 = off: 1 = wave spans (every wave of the MoE gate/up (kind 0), MoE down (1) and attention (2)
+ * launches writes its entry / exit s_memrealtime (100 MHz) to a slot, a one-block fold launch after each
+ * keeps the first entry / last exit), 2 = HIP events recorded on the stream around those launches inside
+ * the replayed step graph (the dispatch-level duration rocprofv3's kernel trace reports; read back after
+ * every step).  Either mode also records the distinct experts each MoE layer streamed.  The decode steps
+ * of every following generate are recorded; dsocr_engine_spans copies the last such generate's records,
+ * [kinds][layers][steps][5] uint64 {entry, exit, distinct experts, waves, event duration ns}, into out
+ * (cap = capacity in uint64; DSOCR_EINVAL if short; out NULL: only the dimensions are returned);
  * step s = tokens emitted before the step, decode steps are 1 .. steps - 1, unused entries are 0. */
-dsocr_status dsocr_engine_set_spans(dsocr_engine* e, int enable);
+dsocr_status dsocr_engine_set_spans(dsocr_engine* e, int mode);
 dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap, size_t* kinds, size_t* layers,
                                 size_t* steps);
 

@@ -110,19 +110,20 @@ def test_span_roofline_prices_each_launch():
     import numpy as np
     d = bench.lang_dims({"hidden_size": 1280, "moe_intermediate_size": 896, "n_shared_experts": 2,
                          "num_experts_per_tok": 6, "num_attention_heads": 10, "num_key_value_heads": 10})
-    arr = np.zeros((3, 12, 8, 4), np.uint64)
+    arr = np.zeros((3, 12, 8, 5), np.uint64)
     # gate/up, layer 1: steps 1 and 2, 9 us and 11 us (900 / 1100 ticks of 10 ns), 6 and 30 experts
-    arr[0, 1, 1] = [1000, 1900, 6, 7168]
-    arr[0, 1, 2] = [5000, 6100, 30, 7168]
+    arr[0, 1, 1] = [1000, 1900, 6, 7168, 9000]
+    arr[0, 1, 2] = [5000, 6100, 30, 7168, 11000]
     # attention, layer 0, step 3: 8 us
-    arr[2, 0, 3] = [100, 900, 0, 800]
+    arr[2, 0, 3] = [100, 900, 0, 800, 8000]
     got = bench.span_roofline({"moe_gateup": arr[0], "moe_down": arr[1], "attention": arr[2]}, d, 8, 706)
     assert set(got) == {"moe_gateup", "attention"}
     g = got["moe_gateup"]
     b6 = bench.span_bytes("moe_gateup", d, 8, 706, 6, 1)
     b30 = bench.span_bytes("moe_gateup", d, 8, 706, 30, 2)
     assert b30 - b6 == 24 * 2 * 896 * 1280 * 2
-    assert g["launches"] == 2 and abs(g["avg_us"] - 10.0) < 1e-9
+    assert g["launches"] == 2 and abs(g["avg_us"] - 10.0) < 1e-9 and abs(g["wave_avg_us"] - 10.0) < 1e-9
+    assert g["timing"] == "hip events in graph"
     assert abs(g["GB/s"] - (b6 + b30) / 20e-6 / 1e9) < 1e-6 and g["experts_range"] == [6, 30]
     a = got["attention"]
     assert abs(a["GB/s"] - bench.span_bytes("attention", d, 8, 706, 0, 3) / 8e-6 / 1e9) < 1e-6
