@@ -503,44 +503,43 @@ def main():
     if rank == 0:
         # in context: the first timed batch decoded once more with launch spans on (every step's graph
         # replay; each stamped launch is followed by a one-block fold launch, outside its own span)
+        # in-kernel wave spans over a whole generate (the first timed batch decoded again with every
+        # MoE / attention launch's first-wave entry and last-wave exit recorded, expert counts per launch)
         dims = lang_dims(json.load(open(dsocr.FULL_CONFIG)))
         P = len(batches[args.warmup][1][0][0])
-        eng.set_spans(eng.SPAN_EVENTS)
-        eng.generate_batch(batches[args.warmup][1], params, ignore_eos=True)
-        ctx = span_roofline(eng.spans(), dims, ppg, P)
-        eng.set_spans(eng.SPAN_WAVES)   # a second pass for the in-kernel wave spans
+        eng.set_spans(eng.SPAN_WAVES)
         eng.generate_batch(batches[args.warmup][1], params, ignore_eos=True)
         eng.set_spans(0)
-        for k, v in span_roofline(eng.spans(), dims, ppg, P).items():
-            if k in ctx:
-                ctx[k]["wave_avg_us"], ctx[k]["wave_GB/s"] = v["wave_avg_us"], v["wave_GB/s"]
+        waves = span_roofline(eng.spans(), dims, ppg, P)
         prof = eng.profile_decode(args.roofline_iters)
-        gu = prof["moe_gateup"]
         kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
-        g = ctx["moe_gateup"]
-        roofline = {"bound": "hbm", "achieved": round(g["GB/s"], 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(g["GB/s"] / HBM_PEAK_GBS, 4),
+
+        def ctx_line(k):
+            p = prof[k]
+            return {"ctx_us": round(p["ctx_us"], 3), "bytes": p["bytes"],
+                    "GB/s": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9, 1) if p["ctx_us"] > 0 else None,
+                    "frac": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if p["ctx_us"] > 0 else None,
+                    "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
+        gu = ctx_line("moe_gateup")
+        roofline = {"bound": "hbm", "achieved": gu["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gu["frac"],
                     "traffic": pmc_traffic(kernel),
                     "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
-                    # achieved = sum over every gate/up launch of a whole generate's decode steps (the first
-                    # timed batch decoded again) of its algorithmic bytes (priced from the experts that launch
-                    # streamed) / sum of its dispatch durations, HIP events recorded around it inside the
-                    # replayed step graph
-                    "avg_launch_us": round(g["avg_us"], 3), "bytes_per_launch": round(g["bytes_per_launch"]),
-                    "launches": g["launches"], "experts_touched_mean": round(g["experts_mean"], 2),
-                    "experts_touched_range": g["experts_range"], "timing": g["timing"],
-                    "in_context": ctx,
-                    # the same kernel outside the decode loop (profile_decode: HIP events on each launch's
-                    # dispatch packet, and n launches chained in one graph replay), on the last step's routing
-                    "isolated": {"avg_launch_us": round(gu["avg_us"], 2), "bytes_per_launch": gu["bytes"],
-                                 "frac": round(gu["bytes"] / (gu["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                                 "replay_launch_us": round(gu["replay_us"], 2),
-                                 "experts_touched": prof["experts_touched"]},
+                    # avg_launch_us = in-context duration: (one decode step's layers replayed as a hipGraph - the
+                    # same graph without the gate/up launches) / MoE layers, HIP events around the replays on the
+                    # engine stream: the kernel with its own dispatch inside the real dependent chain (what
+                    # rocprofv3's kernel trace reports as its duration there); bytes priced at the routing the
+                    # replayed step takes (experts_touched distinct experts)
+                    "avg_launch_us": gu["ctx_us"], "bytes_per_launch": gu["bytes"],
+                    "experts_touched": prof["experts_touched"], "timing": "in-context step-graph difference",
                     "down_kernel": prof["moe_down_kernel"],
+                    "in_context": {k: ctx_line(k) for k in ("moe_gateup", "moe_down", "attention")},
+                    # the same launches' waves alone, over every decode step of a generate (no dispatch)
+                    "in_kernel_waves": waves,
                     "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
                                    "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
-                               for k in ("lm_head", "lm_head_screened")
+                               for k in ("lm_head", "lm_head_screened", "qkv", "o_proj", "router")
                                if prof.get(k, {}).get("avg_us", 0) > 0},
+                    "layers_step_us": round(prof["layers_step"]["avg_us"], 1),
                     "kv_len": prof["kv_len"]}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not snap:

@@ -350,6 +350,7 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
         auto cp = [](const dsocr::Engine::KernelProfile& k) {
             dsocr_kernel_profile r;
             r.avg_us = k.avg_us; r.bytes = k.bytes; r.flops = k.flops; r.launches = k.launches; r.replay_us = k.replay_us;
+            r.ctx_us = k.ctx_us;
             return r;
         };
         out->moe_gateup = cp(p.moe_gateup);

@@ -1138,7 +1138,7 @@ void Engine::decode_step(int B, int Lmax) {
             da.prerot = 1;
             da.split = oproj_comb ? 1 : 0;
             da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
-            stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
+            if (!(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
         } else {
             DecGemvArgs g;
             g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
@@ -1148,7 +1148,7 @@ void Engine::decode_step(int B, int Lmax) {
             else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
             launch_dec_gemv(g, st);
             da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
-            stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
+            if (!(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
         }
         if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
         else launch_dec_gemv(go, st);
@@ -1185,7 +1185,8 @@ void Engine::decode_step(int B, int Lmax) {
             continue;
         }
         if (!span_rec_) {
-            launch_moe_decode(moe_args(l, B, X), st);
+            const int parts = MOE_ROUTE | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) | ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
+            launch_moe_decode(moe_args(l, B, X), st, parts);
             continue;
         }
         MoeDecodeArgs ma = moe_args(l, B, X);
@@ -2045,34 +2046,52 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         float* X0 = wsf("p_x0", (size_t)B * H);
         HIP_CHECK(hipMemcpyAsync(X0, X, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
         decode_step(B, Lmax);  // every workspace exists before capture
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t gexec = nullptr;
-        capturing_ = true;
-        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
-        decode_step(B, Lmax);
-        HIP_CHECK(hipStreamEndCapture(st, &graph));
-        capturing_ = false;
-        HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
-        {
+        // the step graph, and the same graph without one kernel's launches: the difference per launch is
+        // that kernel's in-context cost (its dispatch and its place in the dependent chain included)
+        auto step_us = [&](int skip) {
+            hipGraph_t g = nullptr;
+            hipGraphExec_t ge = nullptr;
+            step_skip_ = skip;
+            capturing_ = true;
+            HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
+            decode_step(B, Lmax);
+            HIP_CHECK(hipStreamEndCapture(st, &g));
+            capturing_ = false;
+            step_skip_ = 0;
+            HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
             const int n = std::max(8, iters * 4);
             hipEvent_t e0, e1;
             HIP_CHECK(hipEventCreate(&e0));
             HIP_CHECK(hipEventCreate(&e1));
-            HIP_CHECK(hipGraphLaunch(gexec, st));
+            HIP_CHECK(hipGraphLaunch(ge, st));
             HIP_CHECK(hipEventRecord(e0, st));
-            for (int i = 0; i < n; ++i) HIP_CHECK(hipGraphLaunch(gexec, st));
+            for (int i = 0; i < n; ++i) HIP_CHECK(hipGraphLaunch(ge, st));
             HIP_CHECK(hipEventRecord(e1, st));
             HIP_CHECK(hipEventSynchronize(e1));
-            prof.layers_step.avg_us = 1000.0 * ms_between(e0, e1) / n;
-            prof.layers_step.launches = n;
+            const double us = 1000.0 * ms_between(e0, e1) / n;
             (void)hipEventDestroy(e0);
             (void)hipEventDestroy(e1);
+            (void)hipGraphExecDestroy(ge);
+            (void)hipGraphDestroy(g);
+            return us;
+        };
+        int n_moe = 0;
+        for (const DecLayer& d : layers_) n_moe += d.moe ? 1 : 0;
+        double full = step_us(0);
+        const double no_gu = n_moe ? step_us(SKIP_GATEUP) : full;
+        const double no_dn = n_moe ? step_us(SKIP_DOWN) : full;
+        const double no_at = step_us(SKIP_ATTN);
+        full = 0.5 * (full + step_us(0));  // bracket the variants: replay-to-replay drift averages out
+        prof.layers_step.avg_us = full;
+        prof.layers_step.launches = std::max(8, iters * 4);
+        if (n_moe) {
+            prof.moe_gateup.ctx_us = (full - no_gu) / n_moe;
+            prof.moe_down.ctx_us = (full - no_dn) / n_moe;
         }
+        prof.attention.ctx_us = (full - no_at) / L.layers;
         HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
         HIP_CHECK(hipStreamSynchronize(st));
-        (void)hipGraphExecDestroy(gexec);
-        (void)hipGraphDestroy(graph);
     }
     return prof;
 }

@@ -153,6 +153,7 @@ class Engine {
         double avg_us = 0, bytes = 0, flops = 0;
         int launches = 0;
         double replay_us = 0;
+        double ctx_us = 0;  // in-context marginal cost per launch (step graph with / without it)
     };
     struct DecodeProfile {
         KernelProfile moe_gateup, moe_down, attention, lm_head, qkv, o_proj, router, layers_step, lm_head_screened;
@@ -262,6 +263,9 @@ class Engine {
     int last_Lmax_ = 0;
     float* trace_ = nullptr;  // device logits trace of the running generate (parity hook)
     int span_mode_ = 0;
+    // profile_decode: launches decode_step leaves out (the with / without step-graph differences)
+    enum StepSkip : int { SKIP_GATEUP = 1, SKIP_DOWN = 2, SKIP_ATTN = 4 };
+    int step_skip_ = 0;
     unsigned long long* span_slots_ = nullptr;  // device [SPAN_SLOTS][2]
     unsigned long long* span_rec_ = nullptr;    // device [SPAN_KINDS][layers][span_cap_][4]
     const int* span_step_ = nullptr;            // device step counter (out_len of page 0)

@@ -57,7 +57,7 @@ class TimingsC(C.Structure):
 
 class KernelProfileC(C.Structure):
     _fields_ = [("avg_us", C.c_double), ("bytes", C.c_double), ("flops", C.c_double), ("launches", C.c_int),
-                ("replay_us", C.c_double)]
+                ("replay_us", C.c_double), ("ctx_us", C.c_double)]
 
 
 class DecodeProfileC(C.Structure):

@@ -310,7 +310,7 @@ class DeepseekOcrEngine:
                   "lm_head_screened"):
             kp = getattr(p, k)
             out[k] = {"avg_us": kp.avg_us, "bytes": kp.bytes, "flops": kp.flops, "launches": kp.launches,
-                      "replay_us": kp.replay_us}
+                      "replay_us": kp.replay_us, "ctx_us": kp.ctx_us}
         out.update(experts_touched=p.experts_touched, tokens=p.tokens, kv_len=p.kv_len,
                    moe_gateup_kernel=(p.moe_gateup_kernel or b"").decode(),
                    moe_down_kernel=(p.moe_down_kernel or b"").decode())

@@ -179,6 +179,9 @@ typedef struct dsocr_kernel_profile {
     double flops;
     int launches;
     double replay_us;  /* per launch in a back-to-back hipGraph replay (incl. the kernel boundary) */
+    double ctx_us;     /* in context: (one decode step's layers replayed as a hipGraph - the same graph without this
+                          launch in any layer) / its launches per step, i.e. what it costs inside the real step
+                          chain, its own dispatch included (MoE gate/up, MoE down, attention; else 0) */
 } dsocr_kernel_profile;
 typedef struct dsocr_decode_profile {
     dsocr_kernel_profile moe_gateup;  /* decode MoE gate/up launch(es) of one layer (routed + shared): the kernel
