@@ -389,6 +389,10 @@ def main():
     ap.add_argument("--snapshot", default=None, choices=["q4k"],
                     help="q4k: configs[4], a full-size synthetic Q4_K DSQ snapshot loaded through the engine's "
                          "dequant-on-load path (written to $TMPDIR first)")
+    ap.add_argument("--text-pages", action="store_true",
+                    help="each page is a 706-token text prompt (dsocr.synth.text_page_prompt) instead of an image: "
+                         "prefill + decode only; the pages decode distinct streams, so a batch routes its MoE layers "
+                         "like distinct real pages (~35 experts per layer at 8 pages)")
     ap.add_argument("--oversubscribe", action="store_true",
                     help="allow more ranks than visible GPUs (ranks then share devices; n_gpus reports the "
                          "distinct devices used, `ranks` the rank count) - a test of the launch path only")
@@ -429,7 +433,7 @@ def main():
     import dsocr
     from dsocr import DecodeParameters, ModelLoadArgs, Page, VisionSettings, build_prompt_tokens, load_model
     from dsocr._lib import check, lib
-    from dsocr.synth import BENCH_PROMPT, SyntheticTokenizer, synthetic_page
+    from dsocr.synth import BENCH_PROMPT, SyntheticTokenizer, synthetic_page, text_page_prompt
 
     def barrier():
         check(lib().dsocr_dev_sync())
@@ -463,6 +467,10 @@ def main():
     def make_batch(step):
         imgs, reqs = [], []
         for idx in page_indices(step, world, rank, ppg):
+            if args.text_pages:
+                imgs.append(None)
+                reqs.append((text_page_prompt(idx, vocab=eng.vocab), None, None, None))
+                continue
             img = synthetic_page(idx)
             t0 = time.time()
             page = Page(img, vs, eng)   # a1-a3 on the GPU: pixels HBM-resident before the timed region
@@ -476,7 +484,8 @@ def main():
     batches = [make_batch(s) for s in range(args.warmup + args.steps)]
     gpu_prep_ms = prep_gpu_s[0] * 1e3 / max(1, len(batches) * ppg)
     t = time.time()
-    Page(synthetic_page(0), vs)  # the host C++ path on the same page, for the report
+    if not args.text_pages:
+        Page(synthetic_page(0), vs)  # the host C++ path on the same page, for the report
     prep_ms = (time.time() - t) * 1e3
     for s in range(args.warmup):
         eng.generate_batch(batches[s][1], params, ignore_eos=True)
@@ -542,7 +551,7 @@ def main():
                     "layers_step_us": round(prof["layers_step"]["avg_us"], 1),
                     "kv_len": prof["kv_len"]}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not snap:
+        if world == 1 and not args.no_cpu_baseline and not snap and not args.text_pages:
             b = batches[args.warmup]
             try:
                 cpu = cpu_baseline(b[0], b[1][0][0], b[1][0][1], args.max_new_tokens, args.cpu_decode_steps)
@@ -568,7 +577,9 @@ def main():
                     + ("; snapshot linears: random valid Q4_K / Q8_0 blocks" if snap else ""),
             "config": {"workload": ("configs[4]: deepseek-ocr-q4k DSQ snapshot, dequant-on-load -> fp16 kernels, "
                                     f"{ppg} pages/GPU batch") if snap else
-                                   ("configs[1]: deepseek-ocr, 1024x1024 page, crop (2,2), 706-token prefill, "
+                                   (f"deepseek-ocr, {ppg} text pages/GPU: 706-token text prompts (no vision), 512 "
+                                    "greedy tokens, distinct decode streams per page" if args.text_pages else
+                                    "configs[1]: deepseek-ocr, 1024x1024 page, crop (2,2), 706-token prefill, "
                                     "512 greedy tokens" if ppg == 1 else f"deepseek-ocr, {ppg} pages/GPU batch"),
                        "pages_per_gpu": ppg, "global_batch": ppg * world, "prefill_tokens": len(batches[0][1][0][0]),
                        "max_new_tokens": args.max_new_tokens, "parallelism": f"dp{world}"},

@@ -2,6 +2,7 @@
 // Reference call stacks followed here: SURVEY §3.2-3.4; per-stage citations inline.
 #include "engine.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <random>
 #include <cstdlib>
@@ -1105,6 +1106,7 @@ void Engine::decode_step(int B, int Lmax) {
         da.page_stride = page_stride_; da.head_stride = head_stride_;
         da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
         da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
+        da.kv_bound = kv_bound_;
         // q/k/v projection: fused into the attention launch (each head's chunk blocks compute
         // that head's rows, dec_qkv_attn) when in range, else its own GEMV launch
         // (off by default: measured +7 us / layer on MI355X at B = 1 — 160 blocks carry both the
@@ -1716,6 +1718,12 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     };
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
+    // attention key bound per 64-step band: step i decodes position P_b + i - 1, so every page's length
+    // is <= max P + 64 (band + 1); the attention kernel issues its K / V loads before it knows the position
+    const int pmax = *std::max_element(kvpos.begin(), kvpos.end());
+    auto band_of = [](size_t i) { return (int)((i - 1) / 64); };
+    auto band_bound = [&](int band) { return std::min(Lmax, pmax + 64 * (band + 1)); };
+    kv_bound_ = std::min(Lmax, pmax + 1);
     decode_step(B, Lmax);
     HIP_CHECK(hipMemcpyAsync(d_kvpos, kvpos.data(), B * 4, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_kvlen, kvlen.data(), B * 4, hipMemcpyHostToDevice, st));
@@ -1730,20 +1738,31 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         decode_step(B, Lmax);
         decode_head(B, sa, pen);
     };
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t gexec = nullptr;
-    if (use_graph) {
-        capturing_ = true;
-        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        step_body();
-        HIP_CHECK(hipStreamEndCapture(st, &graph));
-        capturing_ = false;
-        HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
-    }
+    // one step graph per band (captured when the loop enters it; every graph is kept until the loop's
+    // final synchronisation, so none is destroyed while queued)
+    std::vector<hipGraph_t> graphs;
+    std::vector<hipGraphExec_t> gexecs;
+    int band = -1;
 
     HIP_CHECK(hipEventRecord(ev[4], st));
     for (size_t i = 1; i < p.max_new; ++i) {
-        if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
+        if (band_of(i) != band) {
+            band = band_of(i);
+            kv_bound_ = band_bound(band);
+            if (use_graph) {
+                hipGraph_t g = nullptr;
+                hipGraphExec_t ge = nullptr;
+                capturing_ = true;
+                HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+                step_body();
+                HIP_CHECK(hipStreamEndCapture(st, &g));
+                capturing_ = false;
+                HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+                graphs.push_back(g);
+                gexecs.push_back(ge);
+            }
+        }
+        if (use_graph) HIP_CHECK(hipGraphLaunch(gexecs.back(), st));
         else step_body();
         if (span_rec_ && (span_mode_ & SPAN_EVENTS)) read_span_events(i);
         ++steps;
@@ -1756,8 +1775,9 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipEventRecord(ev[5], st));
     HIP_CHECK(hipStreamSynchronize(st));
-    if (gexec) (void)hipGraphExecDestroy(gexec);
-    if (graph) (void)hipGraphDestroy(graph);
+    for (auto& ge : gexecs) (void)hipGraphExecDestroy(ge);
+    for (auto& g : graphs) (void)hipGraphDestroy(g);
+    kv_bound_ = 0;
     if (span_rec_) {
         const size_t nrec = (size_t)SPAN_KINDS * L.layers * span_cap_;
         std::vector<unsigned long long> dev(nrec * 4);
@@ -1824,6 +1844,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     for (int b = 0; b < B; ++b) { pm1[b] = std::max(0, kvpos[b] - 1); keys += pm1[b] + 1; }
     int* d_pos = wsi("p_kvpos", B);
     HIP_CHECK(hipMemcpy(d_pos, pm1.data(), B * 4, hipMemcpyHostToDevice));
+    const int pm1max = *std::max_element(pm1.begin(), pm1.end());
     prof.tokens = B;
     prof.kv_len = pm1[0] + 1;
     // n back-to-back launches captured in one hipGraph, replayed between two events on the
@@ -1926,6 +1947,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
             da.err = wsi("s_err", 4);
             da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
+            da.kv_bound = std::min(Lmax, pm1max + 1);
             launch_dec_attn(da, st);
         });
         if (const char* path = getenv("DSOCR_ATT_STAMPS_OUT")) {
@@ -2045,6 +2067,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         float* X = wsf("s_x", (size_t)B * H);
         float* X0 = wsf("p_x0", (size_t)B * H);
         HIP_CHECK(hipMemcpyAsync(X0, X, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
+        kv_bound_ = std::min(Lmax, *std::max_element(kvpos.begin(), kvpos.end()) + 1);  // the replays' position
         decode_step(B, Lmax);  // every workspace exists before capture
         // the step graph, and the same graph without one kernel's launches: the difference per launch is
         // that kernel's in-context cost (its dispatch and its place in the dependent chain included)
@@ -2090,6 +2113,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             prof.moe_down.ctx_us = (full - no_dn) / n_moe;
         }
         prof.attention.ctx_us = (full - no_at) / L.layers;
+        kv_bound_ = 0;
         HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
         HIP_CHECK(hipStreamSynchronize(st));
     }

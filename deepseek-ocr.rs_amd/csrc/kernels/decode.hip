@@ -1922,6 +1922,8 @@ static int dec_attn_nsub(const DecAttn2Args& a, int chunks) {
 }
 
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
+    static const bool old_kernel = getenv("DSOCR_ATTN_OLD") && atoi(getenv("DSOCR_ATTN_OLD")) != 0;
+    if (!old_kernel && !a.split) return launch_dec_attn3(a, s);
     if (!a.counters) throw std::runtime_error("EINTERNAL: dec_attn needs a zeroed counter array");
     const int ch = dec_attn_ch();
     if (a.max_len > 512 * ch) throw std::runtime_error("EINVAL: decode context too long for the attention combine");

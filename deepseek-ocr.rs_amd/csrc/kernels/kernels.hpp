@@ -248,6 +248,7 @@ struct DecAttn2Args {
     unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
     unsigned long long* span = nullptr;    // launch-span slots (SPAN_SLOTS pairs) or null
     int prerot = 0;                        // q / k rows already rotated (dec_qkv_rope)
+    int kv_bound = 0;                      // > 0: every page's length <= kv_bound (K / V loads issued before the position)
     int split = 0;                         // no in-kernel combine: dim-major records for dec_oproj_comb
 };
 // Attention combine (split-mode records of dec_attn, one token) fused into the o_proj GEMV.
@@ -260,6 +261,7 @@ struct DecCombArgs {
 bool dec_oproj_comb_ok(const DecGemvArgs& a, const DecCombArgs& cb);
 void launch_dec_oproj_comb(const DecGemvArgs& a, const DecCombArgs& cb, hipStream_t s);
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
+void launch_dec_attn3(const DecAttn2Args& a, hipStream_t s);  // decode_attn.hip
 // q/k/v projection of one token with RoPE applied in the epilogue (rows < rot_rows rotated at
 // position kv_pos[0]; table layout [pos][hd], rope on the full head dim, rotate_half pairing).
 struct DecRopeEpi {

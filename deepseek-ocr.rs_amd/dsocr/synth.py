@@ -3,6 +3,10 @@
 * ``synthetic_page``: 1024x1024 RGB8 "document" pages: white
   background, dark glyph boxes in text rows (8-24 px high), Gaussian noise sigma 8,
   seeded by the page index (numpy PCG64).
+* ``text_page_prompt``: a page's worth of text tokens (BOS + random ids, 706 by default: the prompt
+  length of an image page) seeded by the page index; the decode streams of such prompts differ from
+  page to page, so a batch of them routes its MoE layers like distinct real pages (the synthetic
+  checkpoint decodes every synthetic image page into nearly the same stream).
 * ``SyntheticTokenizer``: a deterministic stand-in exposing the two calls
   build_prompt_tokens needs (`encode`, `token_to_id("<image>")`); a real
   `tokenizers.Tokenizer` works the same way.
@@ -28,6 +32,12 @@ def synthetic_page(index: int, width: int = 1024, height: int = 1024) -> np.ndar
         y += line_h + int(rng.integers(6, 20))
     noise = rng.normal(0.0, 8.0, img.shape)
     return np.clip(img.astype(np.float32) + noise, 0, 255).astype(np.uint8)
+
+
+def text_page_prompt(index: int, length: int = 706, vocab: int = 129280) -> list:
+    """BOS (0) + length - 1 token ids uniform in [16, vocab - 280), numpy PCG64 seeded by 500 + index."""
+    rng = np.random.default_rng(500 + index)
+    return [0] + rng.integers(16, vocab - 280, length - 1).astype(np.int64).tolist()
 
 
 class _Enc:

@@ -9,6 +9,10 @@ BASELINE configs[1] workload through the oracle (numpy restatement of the refere
 * ``synthetic0``: the bench's synthetic 1024x1024 document page 0 (crop grid (2,2), 693 image rows);
   ``synthetic1`` .. ``synthetic7`` (64 tokens each, `--max-new 64`) complete the 8-page batch of the
   configs[2] shape (8 pages per GPU);
+* ``text0`` .. ``text7`` (64 tokens): text-only prompts of an image page's length (706 tokens,
+  ``dsocr.synth.text_page_prompt``): their decode streams differ from page to page, so the 8-page batch
+  routes ~35 distinct experts per MoE layer and step (the image pages of the synthetic checkpoint
+  decode into nearly the same stream and route 10-20);
 * ``sample_1``: the reference's own asset ``assets/sample_1.png`` (2852x1756 RGBA; the reference
   drops alpha with ``to_rgb8``, model/mod.rs:2323 / preprocess.rs:115), committed here as
   tests/golden/sample_1.png (crop grid (3,2)).
@@ -22,6 +26,7 @@ reference's own bars this is read against: teacher-forcing logits <= 0.6
 
     python tests/golden/make_full_golden.py [--pages synthetic0,sample_1] [--max-new 512]
     python tests/golden/make_full_golden.py --pages synthetic1,...,synthetic7 --max-new 64
+    python tests/golden/make_full_golden.py --pages text0,...,text7 --max-new 64
 """
 import argparse
 import json
@@ -63,13 +68,19 @@ def banned(ctx, n):
 
 def make(name, orc, tok, max_new):
     from oracle.model import build_prompt_tokens
-    img = page_image(name)
     t0 = time.time()
-    emb, crop = orc.image_embeddings(img)
+    if name.startswith("text"):
+        from dsocr.synth import text_page_prompt
+        ids = text_page_prompt(int(name[len("text"):]), vocab=tok.vocab_size)
+        mask = [0] * len(ids)
+        emb, crop = np.zeros((0, 1280), np.float32), (0, 0)
+    else:
+        img = page_image(name)
+        emb, crop = orc.image_embeddings(img)
+        segs = [tok.encode(s).ids for s in PROMPT.split("<image>")]
+        ids, mask = build_prompt_tokens(segs, tok.token_to_id("<image>"), [emb.shape[0]])
     t1 = time.time()
-    segs = [tok.encode(s).ids for s in PROMPT.split("<image>")]
-    ids, mask = build_prompt_tokens(segs, tok.token_to_id("<image>"), [emb.shape[0]])
-    gen, logs = orc.generate(ids, mask, emb, max_new, eos_token_id=None, no_repeat_ngram_size=20, record_logits=True)
+    gen, logs = orc.generate(ids, mask, emb if len(emb) else None, max_new, eos_token_id=None, no_repeat_ngram_size=20, record_logits=True)
     t2 = time.time()
     V = logs[0].shape[0]
     probe = probe_indices(V)
@@ -96,7 +107,8 @@ def make(name, orc, tok, max_new):
         prompt_ids=np.asarray(ids, np.int64), image_mask=np.asarray(mask, np.uint8),
         crop=np.asarray(crop, np.int64), n_image_rows=np.int64(emb.shape[0]),
         emb_sum=np.float64(emb.astype(np.float64).sum()), emb_abs_sum=np.float64(np.abs(emb).astype(np.float64).sum()),
-        emb_row0=emb[0, :16].astype(np.float32), emb_rowlast=emb[-1, :16].astype(np.float32),
+        emb_row0=emb[0, :16].astype(np.float32) if len(emb) else np.zeros(16, np.float32),
+        emb_rowlast=emb[-1, :16].astype(np.float32) if len(emb) else np.zeros(16, np.float32),
         ids=np.asarray(gen, np.int64), top_idx=top_idx, top_val=top_val, probe_idx=probe, probe_val=probe_val,
         margin=margin, weights_seed=np.int64(SEED), max_new=np.int64(max_new))
 

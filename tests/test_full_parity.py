@@ -125,6 +125,31 @@ def test_full_batch8_equals_oracle(engine):
         assert s is None, f"{name}: first divergent step {s}: engine {g[s]} oracle {ref[s]} margin {fx['margin'][s]:.3g}"
 
 
+def test_full_text_batch8_equals_oracle(engine):
+    """The realistic-routing 8-page batch (bench --text-pages): 706-token text prompts whose decode streams
+    differ page to page (~35 distinct experts per MoE layer and step, the grouped matrix-core MoE at its
+    widest) -> every page's 64 oracle ids, and the traced logits at the oracle's top-8 indices."""
+    from dsocr.synth import text_page_prompt
+    names = [f"text{i}" for i in range(8)]
+    fxs = [fixture(n) for n in names]
+    n = min(int(f["max_new"]) for f in fxs)
+    reqs = []
+    for i, fx in enumerate(fxs):
+        ids = text_page_prompt(i, vocab=engine.vocab)
+        assert ids == fx["prompt_ids"].tolist()
+        reqs.append((ids, None, None, None))
+    got, logits = engine.generate_trace(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
+    worst = 0.0
+    for name, fx, g, lg in zip(names, fxs, got, logits):
+        ref = fx["ids"][:n].tolist()
+        s = first_divergence(g, ref)
+        assert s is None, f"{name}: first divergent step {s}: engine {g[s]} oracle {ref[s]} margin {fx['margin'][s]:.3g}"
+        top = fx["top_idx"][:n]
+        worst = max(worst, float(np.max(np.abs(np.take_along_axis(lg[:n], top, 1) - fx["top_val"][:n]))))
+    assert worst <= LOGIT_TOL, worst
+    assert len({t for g in got for t in g}) > 64  # distinct streams, not one repeated token
+
+
 def test_full_screened_head_equals_traced_ids(engine):
     """The bench path (screened lm_head + hipGraph loop) gives the traced (exact head) ids on page 0."""
     fx = fixture("synthetic0")

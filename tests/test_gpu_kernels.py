@@ -236,49 +236,55 @@ def test_attention_sam_relpos(gpu, g, rel_len):
         assert np.max(np.abs(got[:, hl] - ref)) < 5e-5
 
 
-@pytest.mark.parametrize("B,heads,kvh,hd,max_len,chunk,nsub", [
-    (1, 10, 10, 128, 1218, "64", None), (3, 4, 4, 32, 300, "64", None), (5, 12, 4, 64, 700, "64", None),
-    (2, 10, 10, 128, 257, "64", None), (1, 10, 10, 128, 64, "64", None), (1, 10, 10, 128, 1218, "32", None),
-    (3, 4, 4, 32, 300, "32", None), (5, 12, 4, 64, 700, "32", None), (2, 10, 10, 128, 257, "32", None),
-    (1, 10, 10, 128, 64, "32", None),
-    # several 64-key sub-chunks per block (online softmax across them): the 8-page shape picks 2 itself
-    (8, 10, 10, 128, 1218, "64", None), (3, 10, 10, 128, 1218, "64", "2"), (2, 10, 10, 128, 300, "64", "4"),
-    (1, 10, 10, 128, 130, "64", "4")])
-def test_decode_attention(gpu, B, heads, kvh, hd, max_len, chunk, nsub, monkeypatch):
-    """Fused decode attention (block.rs:608-789 at seq_len 1): RoPE on q / new k (block.rs:1403-1471),
-    K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the f32 cache (64- and
-    32-key chunks, 1, 2 or 4 chunks per block)."""
+@pytest.mark.parametrize("B,heads,kvh,hd,max_len,prerot,bound", [
+    (1, 10, 10, 128, 1218, 0, "none"), (3, 4, 4, 32, 300, 0, "none"), (5, 12, 4, 64, 700, 0, "none"),
+    (2, 10, 10, 128, 257, 0, "none"), (1, 10, 10, 128, 64, 0, "none"), (8, 10, 10, 128, 1218, 0, "none"),
+    # the decode loop's forms: q / k pre-rotated by the projection (one page), K / V loads issued before the
+    # position against a per-band key bound (tight, or up to 63 keys past the longest page)
+    (1, 10, 10, 128, 1218, 1, "none"), (1, 10, 10, 128, 1218, 1, "tight"), (1, 10, 10, 128, 1218, 1, "band"),
+    (8, 10, 10, 128, 1218, 0, "band"), (3, 4, 4, 32, 300, 0, "band"), (5, 12, 4, 64, 700, 1, "band"),
+    (2, 10, 10, 128, 2000, 0, "band"), (1, 10, 10, 128, 130, 1, "tight")])
+def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot, bound):
+    """Fused decode attention (block.rs:608-789 at seq_len 1): RoPE on q / new k (block.rs:1403-1471) in the
+    kernel or already applied (prerot), K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the
+    f32 cache (64-key chunks; polled merge up to 24 chunks, ticket beyond), with the K / V loads bounded by
+    the position or issued early against a key bound.  The cache past the position holds NaN: keys past the
+    position must contribute nothing."""
     from types import SimpleNamespace
-    monkeypatch.setenv("DSOCR_ATT_CH", chunk)
-    if nsub is None:
-        monkeypatch.delenv("DSOCR_ATT_NSUB", raising=False)
-    else:
-        monkeypatch.setenv("DSOCR_ATT_NSUB", nsub)
     from oracle.decoder import apply_rope, rope_tables
-    rng = np.random.default_rng(B * hd + max_len)
+    rng = np.random.default_rng(B * hd + max_len + prerot)
     qkvw = (heads + 2 * kvh) * hd
     qkv = rng.standard_normal((B, qkvw)).astype(np.float32)
     kc = rng.standard_normal((B, kvh, max_len, hd)).astype(np.float32)
     vc = rng.standard_normal((B, kvh, max_len, hd)).astype(np.float32)
     pos = rng.integers(0, max_len, B).astype(np.int32)
-    pos[0] = max_len - 1
+    pos[0] = max_len - 1 if bound == "none" else max_len - 70
     if B > 1:
         pos[1] = 0
     if B > 2:
         pos[2] = 63
+    for b in range(B):
+        kc[b, :, pos[b] + 1:] = np.nan
+        vc[b, :, pos[b] + 1:] = np.nan
+    kv_bound = {"none": 0, "tight": int(pos.max()) + 1, "band": min(max_len, int(pos.max()) + 64)}[bound]
     lang = SimpleNamespace(rope_theta=10000.0)
     cos, sin = rope_tables(lang, max_len, hd)
-    dqkv, dk, dv, dp, do = Dev(qkv), Dev(kc), Dev(vc), Dev(pos), Dev.zeros((B, heads * hd))
+    rot = qkv.copy()
+    for b in range(B):
+        cs, sn = cos[pos[b]][None], sin[pos[b]][None]
+        rot[b, :heads * hd] = apply_rope(qkv[b, :heads * hd].reshape(heads, hd), cs, sn, False).reshape(-1)
+        rot[b, heads * hd:(heads + kvh) * hd] = apply_rope(qkv[b, heads * hd:(heads + kvh) * hd].reshape(kvh, hd),
+                                                           cs, sn, False).reshape(-1)
+    dqkv, dk, dv, dp, do = Dev(rot if prerot else qkv), Dev(kc), Dev(vc), Dev(pos), Dev.zeros((B, heads * hd))
     dcos, dsin = Dev(cos), Dev(sin)
     scale = 1.0 / math.sqrt(hd)
     check(lib().dsocr_k_decode_attention(B, heads, kvh, hd, hd, max_len, scale, dqkv.ptr, dcos.ptr, dsin.ptr,
-                                         dk.ptr, dv.ptr, dp.ptr, do.ptr))
+                                         dk.ptr, dv.ptr, dp.ptr, do.ptr, prerot, kv_bound))
     got, gk, gv = do.get(), dk.get(), dv.get()
     for b in range(B):
         p = pos[b]
-        cs, sn = cos[p][None], sin[p][None]
-        q = apply_rope(qkv[b, :heads * hd].reshape(heads, hd), cs, sn, False)
-        kn = apply_rope(qkv[b, heads * hd:(heads + kvh) * hd].reshape(kvh, hd), cs, sn, False)
+        q = rot[b, :heads * hd].reshape(heads, hd)
+        kn = rot[b, heads * hd:(heads + kvh) * hd].reshape(kvh, hd)
         vn = qkv[b, (heads + kvh) * hd:].reshape(kvh, hd)
         assert np.max(np.abs(gk[b, :, p] - kn)) < 1e-5 and np.array_equal(gv[b, :, p], vn)
         K = kc[b].copy(); V = vc[b].copy()

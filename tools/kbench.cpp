@@ -310,6 +310,13 @@ static void case_attn(int B, int pos, hipStream_t s) {
     snprintf(nm, sizeof nm, "attn B=%d L=%d", B, pos + 1);
     const double bytes = 2.0 * B * (pos + 1) * HEADS * HD * 4;
     report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
+    a.kv_bound = pos + 1;  // the decode loop's per-band key bound (tightest case): loads before the position
+    snprintf(nm, sizeof nm, "attn B=%d L=%d bound", B, pos + 1);
+    report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
+    a.kv_bound = std::min(max_len, pos + 64);
+    snprintf(nm, sizeof nm, "attn B=%d L=%d bound+63", B, pos + 1);
+    report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
+    a.kv_bound = 0;
     if (getenv("KB_STAMPS")) {  // per-block phase clocks: [0] wall entry, [1..] shader clock at the phase points
         const int nb = 4096;
         auto* st = (unsigned long long*)dalloc((size_t)nb * 8 * 8);
