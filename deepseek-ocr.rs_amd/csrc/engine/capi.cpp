@@ -583,10 +583,9 @@ dsocr_status dsocr_k_attention_bf16(int n_seq, int L, int heads, int hd, float s
 }
 dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, int rope_dim, int max_len, float scale,
                                       const float* qkv, const float* cos, const float* sin, float* kc, float* vc,
-                                      const int* kv_pos, float* o, int prerot, int kv_bound) {
+                                      const int* kv_pos, float* o, int prerot) {
     return guarded([&] {
         if (hd != 32 && hd != 64 && hd != 128) throw std::runtime_error("EINVAL: head_dim must be 32, 64 or 128");
-        if (kv_bound < 0 || kv_bound > max_len) throw std::runtime_error("EINVAL: kv_bound outside [0, max_len]");
         if (prerot && rope_dim != hd) throw std::runtime_error("EINVAL: pre-rotated rows need rope_dim == head_dim");
         if (kv_heads <= 0 || heads % kv_heads || rope_dim > hd || rope_dim % 2)
             throw std::runtime_error("EINVAL: bad head / rope configuration");
@@ -603,7 +602,7 @@ dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, in
         a.cos = cos; a.sin = sin; a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd;
         a.page_stride = (long)kv_heads * max_len * hd; a.scale = scale; a.part = part; a.o = o;
         a.o_ld = (long)heads * hd; a.counters = cnt; a.err = cnt + B * heads;
-        a.prerot = prerot != 0; a.kv_bound = kv_bound;
+        a.prerot = prerot != 0;
         dsocr::launch_dec_attn(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
         int herr = 0;

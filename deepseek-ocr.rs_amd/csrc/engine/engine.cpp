@@ -525,20 +525,6 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
                                                : upf(std::vector<float>(cfg_.proj_out, 0.f));
     separator_ = vecf("model.view_seperator", cfg_.proj_out);
 
-    // the split-plane GEMM's tripled weights [W | W | W] (bf16 vision linears; ~1.2 GB of HBM)
-    auto triple = [&](Lin& l) {
-        if (l.wdt != WDT_BF16 || l.K % 64) return;
-        l.W3 = dev_alloc((size_t)l.N * 3 * l.K * 2);
-        for (int p = 0; p < 3; ++p)
-            HIP_CHECK(hipMemcpy2D((char*)l.W3 + (size_t)p * l.K * 2, (size_t)3 * l.K * 2, l.W, (size_t)l.K * 2,
-                                  (size_t)l.K * 2, l.N, hipMemcpyDeviceToDevice));
-    };
-    triple(sam_.patch);
-    for (auto& blk : sam_.blocks) { triple(blk.qkv); triple(blk.proj); triple(blk.fc1); triple(blk.fc2); }
-    triple(sam_.neck0); triple(sam_.neck2); triple(sam_.net2); triple(sam_.net3);
-    for (auto& cl : clip_.layers) { triple(cl.qkv); triple(cl.out); triple(cl.fc1); triple(cl.fc2); }
-    triple(proj_);
-
     // ---------------- language model (transformer/weights.rs:444-606)
     const LangConfig& L = cfg_.lang;
     {
@@ -593,16 +579,6 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
                 d.s_d = lin(lp + "mlp.shared_experts.down_proj", H, Is, true);
             }
         }
-        // prefill GEMM forms of the decoder linears (the decode path keeps reading W)
-        for (Lin* l : {&d.qkv, &d.o, &d.gu, &d.down, &d.router, &d.s_gu, &d.s_d}) {
-            if (!l->W || l->K % 64) continue;
-            if (l->wdt == WDT_F16) {
-                l->W5 = dev_alloc((size_t)l->N * 5 * l->K * 2);
-                launch_make_w5(l->W, l->N, l->K, l->W5, nullptr);
-            } else {
-                triple(*l);
-            }
-        }
         layers_.push_back(d);
     }
     HIP_CHECK(hipDeviceSynchronize());
@@ -627,45 +603,16 @@ void Engine::linear(const float* x, int M, int ldx, const Lin& l, float* y, int 
         a.M = M; a.N = l.N; a.K = l.K; a.x = x; a.ldx = ldx; a.W = l.W; a.ldw = l.K; a.wdtype = l.wdt;
         a.bias = l.b; a.y = y; a.ldy = ldy; a.act = act; a.accumulate = accumulate;
         launch_dec_gemv(a, stream_);
-    } else if (l.W5 && l.wdt == WDT_F16 && l.K % 32 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-               !(getenv("DSOCR_GEMM_FUSED16") && atoi(getenv("DSOCR_GEMM_FUSED16")) == 0)) {
-        // f16 weights: f32 rows split into 3 bf16 planes and the weight into hi / lo inside the GEMM
+    } else if ((l.wdt == WDT_F16 || l.wdt == WDT_BF16) && l.K % 32 == 0 && ldx % 4 == 0 &&
+               (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        // the exact-f32 linear on the bf16 matrix cores: the f32 rows split into 3 bf16 planes (and f16
+        // weights into hi / lo bf16) inside the GEMM's fragment loads (gemm_bf16.hip, gemm_f32a)
         GemmBf16Args g;
-        g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.w_f16 = 1;
+        g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.w_f16 = l.wdt == WDT_F16;
         g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
         g.splits = gemm_f32a_splits(M, l.N, l.K);
         if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
         launch_gemm_f32a(g, stream_);
-    } else if (l.W5 && ldx % 4 == 0 && !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
-        // f16 weights: [lo | mid | mid | hi | hi] planes against W5, one bf16 NT GEMM over K5 = 5K
-        void* planes = ws("g_planes", (size_t)M * 5 * l.K * 2);
-        launch_split5_rows(x, ldx, M, l.K, planes, 5L * l.K, stream_);
-        GemmBf16Args g;
-        g.M = M; g.N = l.N; g.K = 5 * l.K; g.A = planes; g.lda = 5L * l.K; g.W = l.W5; g.ldw = 5L * l.K;
-        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
-        g.splits = gemm_bf16_splits(M, l.N, 5 * l.K);
-        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
-        launch_gemm_bf16(g, stream_);
-    } else if (l.W3 && l.wdt == WDT_BF16 && l.K % 32 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-               !(getenv("DSOCR_GEMM_FUSED") && atoi(getenv("DSOCR_GEMM_FUSED")) == 0) &&
-               !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
-        // bf16 weights, f32 rows split into 3 bf16 planes inside the GEMM's fragment loads
-        GemmBf16Args g;
-        g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K;
-        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
-        g.splits = gemm_f32a_splits(M, l.N, l.K);
-        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
-        launch_gemm_f32a(g, stream_);
-    } else if (l.W3 && ldx % 4 == 0 && !(getenv("DSOCR_GEMM_BF16") && atoi(getenv("DSOCR_GEMM_BF16")) == 0)) {
-        // f32 rows -> [lo | mid | hi] bf16 planes, then one bf16 NT GEMM over K3 = 3K
-        void* planes = ws("g_planes", (size_t)M * 3 * l.K * 2);
-        launch_split3_rows(x, ldx, nullptr, M, l.K, planes, 3L * l.K, stream_);
-        GemmBf16Args g;
-        g.M = M; g.N = l.N; g.K = 3 * l.K; g.A = planes; g.lda = 3L * l.K; g.W = l.W3; g.ldw = 3L * l.K;
-        g.bias = l.b; g.C = y; g.ldc = ldy; g.c_rows = c_rows; g.act = act; g.accumulate = accumulate;
-        g.splits = gemm_bf16_splits(M, l.N, 3 * l.K);
-        if (g.splits > 1) g.part = wsf("g_splitk", (size_t)g.splits * M * l.N);
-        launch_gemm_bf16(g, stream_);
     } else {
         GemmArgs g;
         g.M = M; g.N = l.N; g.K = l.K; g.A = x; g.lda = ldx; g.W = l.W; g.ldw = l.K; g.wdtype = l.wdt;
@@ -1052,7 +999,6 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
 
 // the dense MLP's matrix-core form at 3..8 pages (decode_mm.hip): q/k/v-sized K for gate|up, K % 64 for down
 bool Engine::dense_mm_ok(const DecLayer& d, int B) const {
-    if (getenv("DSOCR_DENSE_MM") && atoi(getenv("DSOCR_DENSE_MM")) == 0) return false;
     const LangConfig& L = cfg_.lang;
     DecGemvArgs g1;
     g1.M = B; g1.N = 2 * L.inter; g1.K = L.hidden; g1.ldw = L.hidden;
@@ -1106,54 +1052,32 @@ void Engine::decode_step(int B, int Lmax) {
         da.page_stride = page_stride_; da.head_stride = head_stride_;
         da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
         da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
-        da.kv_bound = kv_bound_;
-        // q/k/v projection: fused into the attention launch (each head's chunk blocks compute
-        // that head's rows, dec_qkv_attn) when in range, else its own GEMV launch
-        // (off by default: measured +7 us / layer on MI355X at B = 1 — 160 blocks carry both the
-        // projection and the KV stream; DSOCR_FUSED_QKV=1 enables it)
-        static const bool fused_qkv = getenv("DSOCR_FUSED_QKV") && atoi(getenv("DSOCR_FUSED_QKV")) != 0;
-        da.x = X; da.ldx = H; da.norm_w = d.in_norm.w; da.eps = L.rms_eps; da.K = H;
-        da.Wqkv = d.qkv.W; da.wdtype = d.qkv.wdt; da.qkv_bias = d.qkv.b;
-        da.qkv_cnt = wsi("s_qkv_cnt", (size_t)B * L.heads); da.err = err;
-        static const bool qkv_rope = !(getenv("DSOCR_QKV_ROPE") && atoi(getenv("DSOCR_QKV_ROPE")) == 0);
-        // attention combine fused into the o_proj launch (B = 1; experiment, off: every o_proj
-        // block re-reads every partial, measured +4 us / layer on MI355X)
-        static const bool oc_env = getenv("DSOCR_OPROJ_COMB") && atoi(getenv("DSOCR_OPROJ_COMB")) != 0;
+        da.err = err;
+        da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
+        // q/k/v projection with the input RMSNorm fused; one page: RoPE in the projection's epilogue, so the
+        // attention reads q / k already rotated (B <= 2: the row block-staged; 3..8: dec_gemv_lds / dec_mm)
+        DecGemvArgs g;
+        g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
+        g.y = QKV; g.ldy = QKVN; g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps;
+        if (B == 1 && !L.use_mla && L.rope_dim == hd) {
+            DecRopeEpi re;
+            re.kv_pos = kv_pos; re.cos = rope_cos_; re.sin = rope_sin_; re.hd = hd;
+            re.rot_rows = (L.heads + L.kv_heads) * hd;
+            launch_dec_qkv_rope(g, re, st);
+            da.prerot = 1;
+        } else if (B <= 8) {
+            launch_dec_gemv(g, st);
+        } else {
+            launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st);
+            g.x = XN; g.norm_w = nullptr;
+            launch_dec_gemv(g, st);
+        }
+        if (!(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
+        // o_proj + residual
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
         go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
-        DecCombArgs cb;
-        cb.part = part; cb.kv_pos = kv_pos; cb.heads = L.heads; cb.hd = hd; cb.cm = (Lmax + 63) / 64; cb.ch = 64;
-        const bool oproj_comb = oc_env && B == 1 && qkv_rope && !L.use_mla && L.rope_dim == hd && fuse_norm &&
-                                dec_oproj_comb_ok(go, cb) && !(getenv("DSOCR_ATT_CH") && atoi(getenv("DSOCR_ATT_CH")) == 32);
-        DecRopeEpi re;
-        re.kv_pos = kv_pos; re.cos = rope_cos_; re.sin = rope_sin_; re.hd = hd;
-        re.rot_rows = (L.heads + L.kv_heads) * hd;
-        if (fused_qkv && fuse_norm && dec_qkv_attn_ok(da)) {
-            launch_dec_qkv_attn(da, st);
-        } else if (qkv_rope && B == 1 && !L.use_mla && L.rope_dim == hd && fuse_norm) {
-            // RoPE in the projection epilogue: the attention reads q / k already rotated
-            DecGemvArgs g;
-            g.M = 1; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
-            g.y = QKV; g.ldy = QKVN; g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps;
-            launch_dec_qkv_rope(g, re, st);
-            da.prerot = 1;
-            da.split = oproj_comb ? 1 : 0;
-            da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
-            if (!(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
-        } else {
-            DecGemvArgs g;
-            g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
-            g.y = QKV; g.ldy = QKVN;
-            // the input RMSNorm rides in the projection (B <= 2: block-staged; 3..8: dec_gemv_lds)
-            if (fuse_norm || B <= 8) { g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps; }
-            else { launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st); g.x = XN; g.ldx = H; }
-            launch_dec_gemv(g, st);
-            da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
-            if (!(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
-        }
-        if (oproj_comb) launch_dec_oproj_comb(go, cb, st);
-        else launch_dec_gemv(go, st);
+        launch_dec_gemv(go, st);
         // MLP / MoE
         if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
             // dense MLP (layer 0) on the matrix cores: gate|up with the post-attention RMSNorm fused,
@@ -1219,7 +1143,6 @@ void Engine::reserve_head_ws(int B) {
 // + the expert weights again, ~5.3 GB of the 288)
 void Engine::ensure_mm_weights(int B) {
     if (B > 8 || capturing_) return;
-    if (getenv("DSOCR_MM_SWZ") && atoi(getenv("DSOCR_MM_SWZ")) == 0) return;
     const LangConfig& L = cfg_.lang;
     if (B >= 3 && !lm_swz_) {
         DecGemvArgs g;
@@ -1230,9 +1153,9 @@ void Engine::ensure_mm_weights(int B) {
         }
     }
     // the experts of every MoE layer (routed [E * 2I][H], [E * H][I]; shared [2Is][H], [H][Is]): the
-    // grouped matrix-core kernels stream them (one page: only with DSOCR_MIX_MM=1)
+    // grouped matrix-core kernels stream them (3..8 pages)
     const int H = L.hidden, E = L.n_routed, I = L.moe_inter;
-    if (B < 3 && !(getenv("DSOCR_MIX_MM") && atoi(getenv("DSOCR_MIX_MM")) != 0)) return;
+    if (B < 3) return;
     for (DecLayer& d : layers_) {
         if (!d.moe || d.e_gu_swz || d.e_wdt != WDT_F16 || H % 32 || I % 32) continue;
         d.e_gu_swz = dev_alloc(mm_swizzle_elems(E * 2 * I, H) * 2);
@@ -1276,7 +1199,6 @@ void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
         q.blk_cnt = wsi("s_blkcnt", (size_t)B * q.nblk); q.blk_t = wsf("s_blkt", (size_t)B * q.nblk);
         q.cand = wsi("s_cand", (size_t)B * q.nblk * q.slot); q.cand_hi = wsf("s_candhi", (size_t)B * q.nblk * q.slot);
         q.xn_out = wsf("s_lmxn", (size_t)B * H);
-        if (getenv("DSOCR_LQ_MODE")) q.mode = atoi(getenv("DSOCR_LQ_MODE"));  // diagnostics only
         launch_lmhead_q8(q, st);
         DecSampleArgs ss = sa;
         ss.blk_cnt = q.blk_cnt; ss.blk_t = q.blk_t; ss.cand = q.cand; ss.cand_hi = q.cand_hi; ss.nblk = q.nblk; ss.slot = q.slot;
@@ -1492,7 +1414,6 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
-    HIP_CHECK(hipMemsetAsync(wsi("s_qkv_cnt", (size_t)B * L.heads), 0, sizeof(int) * B * L.heads, st));
     const int QKVN = layers_[0].qkv.N;
     float* SX = wsf("s_x", (size_t)B * H);
     float* SXN = wsf("s_xn", (size_t)B * H);
@@ -1718,12 +1639,6 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     };
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
-    // attention key bound per 64-step band: step i decodes position P_b + i - 1, so every page's length
-    // is <= max P + 64 (band + 1); the attention kernel issues its K / V loads before it knows the position
-    const int pmax = *std::max_element(kvpos.begin(), kvpos.end());
-    auto band_of = [](size_t i) { return (int)((i - 1) / 64); };
-    auto band_bound = [&](int band) { return std::min(Lmax, pmax + 64 * (band + 1)); };
-    kv_bound_ = std::min(Lmax, pmax + 1);
     decode_step(B, Lmax);
     HIP_CHECK(hipMemcpyAsync(d_kvpos, kvpos.data(), B * 4, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_kvlen, kvlen.data(), B * 4, hipMemcpyHostToDevice, st));
@@ -1738,31 +1653,20 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         decode_step(B, Lmax);
         decode_head(B, sa, pen);
     };
-    // one step graph per band (captured when the loop enters it; every graph is kept until the loop's
-    // final synchronisation, so none is destroyed while queued)
-    std::vector<hipGraph_t> graphs;
-    std::vector<hipGraphExec_t> gexecs;
-    int band = -1;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    if (use_graph) {
+        capturing_ = true;
+        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        step_body();
+        HIP_CHECK(hipStreamEndCapture(st, &graph));
+        capturing_ = false;
+        HIP_CHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+    }
 
     HIP_CHECK(hipEventRecord(ev[4], st));
     for (size_t i = 1; i < p.max_new; ++i) {
-        if (band_of(i) != band) {
-            band = band_of(i);
-            kv_bound_ = band_bound(band);
-            if (use_graph) {
-                hipGraph_t g = nullptr;
-                hipGraphExec_t ge = nullptr;
-                capturing_ = true;
-                HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-                step_body();
-                HIP_CHECK(hipStreamEndCapture(st, &g));
-                capturing_ = false;
-                HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-                graphs.push_back(g);
-                gexecs.push_back(ge);
-            }
-        }
-        if (use_graph) HIP_CHECK(hipGraphLaunch(gexecs.back(), st));
+        if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
         else step_body();
         if (span_rec_ && (span_mode_ & SPAN_EVENTS)) read_span_events(i);
         ++steps;
@@ -1775,9 +1679,8 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipEventRecord(ev[5], st));
     HIP_CHECK(hipStreamSynchronize(st));
-    for (auto& ge : gexecs) (void)hipGraphExecDestroy(ge);
-    for (auto& g : graphs) (void)hipGraphDestroy(g);
-    kv_bound_ = 0;
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
     if (span_rec_) {
         const size_t nrec = (size_t)SPAN_KINDS * L.layers * span_cap_;
         std::vector<unsigned long long> dev(nrec * 4);
@@ -1844,7 +1747,6 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     for (int b = 0; b < B; ++b) { pm1[b] = std::max(0, kvpos[b] - 1); keys += pm1[b] + 1; }
     int* d_pos = wsi("p_kvpos", B);
     HIP_CHECK(hipMemcpy(d_pos, pm1.data(), B * 4, hipMemcpyHostToDevice));
-    const int pm1max = *std::max_element(pm1.begin(), pm1.end());
     prof.tokens = B;
     prof.kv_len = pm1[0] + 1;
     // n back-to-back launches captured in one hipGraph, replayed between two events on the
@@ -1947,31 +1849,8 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
             da.err = wsi("s_err", 4);
             da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
-            da.kv_bound = std::min(Lmax, pm1max + 1);
             launch_dec_attn(da, st);
         });
-        if (const char* path = getenv("DSOCR_ATT_STAMPS_OUT")) {
-            const size_t nstamp = 4096 * 8;
-            auto* d_st = (unsigned long long*)ws("p_stamps", nstamp * 8);
-            HIP_CHECK(hipMemsetAsync(d_st, 0, nstamp * 8, st));
-            DecAttn2Args da;
-            da.qkv = wsf("s_qkv", (size_t)B * QKVN); da.ld = QKVN; da.kv_pos = d_pos; da.B = B; da.heads = L.heads;
-            da.kv_heads = L.kv_heads; da.hd = hd; da.rope_dim = L.rope_dim; da.use_mla = L.use_mla; da.max_len = Lmax;
-            da.cos = rope_cos_; da.sin = rope_sin_;
-            da.kc = kc_; da.vc = vc_;
-            da.page_stride = page_stride_; da.head_stride = head_stride_;
-            da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
-            da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
-            da.stamps = d_st;
-            launch_dec_attn(da, st);
-            std::vector<unsigned long long> h(nstamp);
-            HIP_CHECK(hipMemcpyAsync(h.data(), d_st, nstamp * 8, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            if (FILE* f = fopen(path, "wb")) {
-                fwrite(h.data(), 8, nstamp, f);
-                fclose(f);
-            }
-        }
         // K and V of every attended key (f32 cache) + q/k/v row + context out
         prof.attention.bytes = (double)keys * L.kv_heads * hd * 4.0 * 2.0 + (double)B * (QKVN + H) * 4.0;
         prof.attention.flops = 4.0 * keys * L.heads * hd;
@@ -2067,7 +1946,6 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         float* X = wsf("s_x", (size_t)B * H);
         float* X0 = wsf("p_x0", (size_t)B * H);
         HIP_CHECK(hipMemcpyAsync(X0, X, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
-        kv_bound_ = std::min(Lmax, *std::max_element(kvpos.begin(), kvpos.end()) + 1);  // the replays' position
         decode_step(B, Lmax);  // every workspace exists before capture
         // the step graph, and the same graph without one kernel's launches: the difference per launch is
         // that kernel's in-context cost (its dispatch and its place in the dependent chain included)
@@ -2113,7 +1991,6 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             prof.moe_down.ctx_us = (full - no_dn) / n_moe;
         }
         prof.attention.ctx_us = (full - no_at) / L.layers;
-        kv_bound_ = 0;
         HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
         HIP_CHECK(hipStreamSynchronize(st));
     }

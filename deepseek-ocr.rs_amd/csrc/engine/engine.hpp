@@ -26,8 +26,6 @@ namespace dsocr {
 
 struct Lin {
     void* W = nullptr;
-    void* W3 = nullptr;  // vision (bf16) linears: [W | W | W] along K for the split-plane GEMM
-    void* W5 = nullptr;  // decoder (f16) prefill linears: [w_hi | w_lo | w_hi | w_lo | w_hi] bf16
     int wdt = WDT_BF16;
     int N = 0, K = 0;
     float* b = nullptr;
@@ -266,7 +264,6 @@ class Engine {
     // profile_decode: launches decode_step leaves out (the with / without step-graph differences)
     enum StepSkip : int { SKIP_GATEUP = 1, SKIP_DOWN = 2, SKIP_ATTN = 4 };
     int step_skip_ = 0;
-    int kv_bound_ = 0;  // decode attention key bound of the steps being issued (0: none, loads after the position)
     unsigned long long* span_slots_ = nullptr;  // device [SPAN_SLOTS][2]
     unsigned long long* span_rec_ = nullptr;    // device [SPAN_KINDS][layers][span_cap_][4]
     const int* span_step_ = nullptr;            // device step counter (out_len of page 0)

@@ -318,8 +318,7 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     if (grid.x == 0 || a.n_seq == 0) return;
     AttnArgs b = a;
     if (b.kv_heads == 0) b.kv_heads = b.heads;
-    static const bool v1 = getenv("DSOCR_ATTN_V1") && atoi(getenv("DSOCR_ATTN_V1")) != 0;
-    if (!v1 && (a.hd == 64 || a.hd == 128)) {
+    if (a.hd == 64 || a.hd == 128) {  // exact-f32 MFMA flash attention; other head dims: attention_fwd_kernel
         const bool rel = b.relbias != nullptr;
         const size_t lds = rel ? (size_t)4 * AT_Q * (b.rel_h + b.rel_w + 1) * 4 : 0;
         static bool attr = false;
@@ -428,7 +427,7 @@ void launch_sam_relbias(const float* q, long q_row_stride, int n_seq, int gh, in
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr = true;
     }
-    if (hd == 64 && lds <= 96 * 1024 && !(getenv("DSOCR_RELBIAS_V1") && atoi(getenv("DSOCR_RELBIAS_V1")))) {
+    if (hd == 64 && lds <= 96 * 1024) {  // tables staged in LDS; otherwise the direct kernel below
         dim3 grid((gh * gw + 255) / 256, n_seq * heads);
         hipLaunchKernelGGL(sam_relbias2_kernel<64>, grid, dim3(256), lds, s, q, q_row_stride, n_seq, gh, gw, heads, Rh,
                            Rw, out);

@@ -156,25 +156,6 @@ __device__ __forceinline__ void xstage(const XRegs<MT, XR>& r, int M, int K, boo
     __syncthreads();
 }
 
-// In-launch hand-off counters: SYNC_SHARDS arrival counters per hand-off, one per 128-byte line
-// (arrivals spread over shards so no single word serialises every producer's atomic).
-// One lane polls every shard with relaxed agent-scope (sc1) loads, s_sleep between polls; a
-// bounded spin that gives up sets *err (checked by the host after the step) instead of hanging.
-__device__ __noinline__ void wait_arrivals(const int* sync, int target, int* err) {
-    for (unsigned it = 0;; ++it) {
-        int n = 0;
-#pragma unroll
-        for (int i = 0; i < SYNC_SHARDS; ++i)
-            n += __hip_atomic_load(sync + i * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n >= target) return;
-        if (it > (1u << 21) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
 // 8 consecutive f32 (LDS or global) into registers
 __device__ __forceinline__ void ld_x8(const float* xs, float* o) {
     const float4 a = *reinterpret_cast<const float4*>(xs);
@@ -254,70 +235,6 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
             for (int r = 0; r < RB; ++r) {
                 const int n = min(n0 + r, a.N - 1);
                 wq[u][r] = ldg_nt16(W + (long)n * a.ldw + (min(c, chunks - 1) << 3));
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-            float v = wave_sum(acc[r][m]);
-            const int n = n0 + r;
-            if (lane == 0 && m < a.M && n < a.N) {
-                v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
-                float* yp = a.y + (long)m * a.ldy + n;
-                if (a.accumulate) v = *yp + v;
-                *yp = v;
-            }
-        }
-}
-
-// Several tokens (M = 3..8, x already normalised): the x rows are read straight from L2 per chunk
-// instead of being staged through LDS, so a block needs no LDS (the 8-row staging window capped
-// residency at 3 blocks per CU and made the launch two rounds deep).  Same per-row arithmetic as
-// dec_gemv_kernel (chunk u-major, then j), so the results are bit-identical.
-template <typename WT, int MT, int RB>
-__global__ __launch_bounds__(256) void dec_gemv_direct_kernel(DecGemvArgs a) {
-    constexpr int U = 3;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = (blockIdx.x * 4 + wave) * RB;
-    if (n0 >= a.N) return;  // whole wave: nothing below synchronises the block
-    const WT* W = reinterpret_cast<const WT*>(a.W);
-    const int chunks = a.K >> 3;
-    uint4 wq[U][RB];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int c = u * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            const int n = min(n0 + r, a.N - 1);
-            wq[u][r] = ldg_nt16(W + (long)n * a.ldw + (min(c, chunks - 1) << 3));
-        }
-    }
-    float acc[RB][MT];
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int c = u * 64 + lane;
-        const int cc = min(c, chunks - 1);
-        float xv[MT][8];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) ld_x8(a.x + (long)min(m, a.M - 1) * a.ldx + (cc << 3), xv[m]);
-        if (c < chunks) {
-            float w8[RB][8];
-#pragma unroll
-            for (int r = 0; r < RB; ++r) unpack8<WT>(wq[u][r], w8[r]);
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                if (m < a.M) {
-#pragma unroll
-                    for (int r = 0; r < RB; ++r)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) acc[r][m] = fmaf(xv[m][j], w8[r][j], acc[r][m]);
-                }
             }
         }
     }
@@ -524,17 +441,14 @@ static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
     const size_t lds = stage_bytes(a.M, a.K);
     if constexpr (MT >= 4 && MT <= 8) {  // several tokens: no LDS staging
         // matrix-core form (decode_mm.hip): weights straight into MFMA, activations as 16-bit planes
-        static const bool use_mm = !(getenv("DSOCR_GEMV_MM") && atoi(getenv("DSOCR_GEMV_MM")) == 0);
-        if (use_mm && dec_mm_ok(a)) {
+        if (dec_mm_ok(a)) {
             launch_dec_mm(a, s);
             return;
         }
-        // rows per wave of dec_gemv_lds (DSOCR_GEMV_RB: 1 / 2 / 4; 0 = the direct kernel); measured on
-        // MI355X at M = 8, K = 1280 (tools/kbench gemv8): RB 2 for N = 3840 (8.4 us vs 10.6 direct,
-        // 11.1 with the norm fused vs 5 + 10.6), RB 1 for N = 1280 (5.9 vs 6.8)
-        static const int env_rb = getenv("DSOCR_GEMV_RB") ? atoi(getenv("DSOCR_GEMV_RB")) : -1;
-        const int rows_rb = env_rb >= 0 ? env_rb : (a.N >= 2560 ? 2 : 1);
-        if (rows_rb > 0 && a.N <= 16384 && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
+        // rows per wave of dec_gemv_lds, measured on MI355X at M = 8, K = 1280 (tools/kbench gemv8): 2 for
+        // N = 3840 (8.4 us, 11.1 with the norm fused vs 5 + 10.6 for a separate RMSNorm), 1 for N = 1280 (5.9)
+        const int rows_rb = a.N >= 2560 ? 2 : 1;
+        if (a.N <= 16384 && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
             const size_t xl = sizeof(float) * MT * (size_t)a.K;
 #define DSOCR_GR(R)                                                                                                   \
     do {                                                                                                              \
@@ -542,25 +456,13 @@ static void dec_gemv_rb(const DecGemvArgs& a, hipStream_t s) {
         if (a.norm_w) DSOCR_LAUNCH((dec_gemv_lds_kernel<WT, MT, R, true>), g, dim3(256), xl, s, a);                   \
         else DSOCR_LAUNCH((dec_gemv_lds_kernel<WT, MT, R, false>), g, dim3(256), xl, s, a);                           \
     } while (0)
-            if (rows_rb == 1) DSOCR_GR(1); else if (rows_rb == 2) DSOCR_GR(2); else DSOCR_GR(4);
+            if (rows_rb == 1) DSOCR_GR(1); else DSOCR_GR(2);
 #undef DSOCR_GR
-            return;
-        }
-        static const bool direct = !(getenv("DSOCR_GEMV_DIRECT") && atoi(getenv("DSOCR_GEMV_DIRECT")) == 0);
-        if (direct && a.N <= 16384 && !a.norm_w && !a.xn_out && a.K <= 64 * 3 * 8 && a.K % 8 == 0) {
-            DSOCR_LAUNCH((dec_gemv_direct_kernel<WT, MT, 1>), dim3((a.N + 3) / 4), dim3(256), 0, s, a);
             return;
         }
     }
     // small N: one row per wave so the whole matrix is in flight at once; large N: RB rows per wave
-    // (DSOCR_GEMV_STREAM=G: small N on the streaming kernel with at most G blocks, experiment)
-    static const int stream_blocks = getenv("DSOCR_GEMV_STREAM") ? atoi(getenv("DSOCR_GEMV_STREAM")) : 0;
-    if (stream_blocks > 0 && a.N <= 16384 && a.K <= 64 * 3 * 8 && MT <= 2) {
-        constexpr int RB = 2;
-        const int groups = (a.N + RB - 1) / RB;
-        const int blocks = std::max(1, std::min((groups + 3) / 4, stream_blocks));
-        DSOCR_LAUNCH((dec_gemv_stream_kernel<WT, MT, RB>), dim3(blocks), dim3(256), lds, s, a);
-    } else if (a.N <= 16384) {
+    if (a.N <= 16384) {
         constexpr int RB = 1;
         DSOCR_LAUNCH((dec_gemv_kernel<WT, MT, RB, 3>), dim3((a.N + 4 * RB - 1) / (4 * RB)), dim3(256), lds, s, a);
     } else if (a.K <= 64 * 3 * 8 && MT <= 2) {
@@ -611,77 +513,12 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
 // the rotation meet in one lane; q and k segments are rotated at the decode position, v rows pass
 // through.  The per-row arithmetic is dec_gemv's (chunk u-major, then j), the rotation is the
 // attention kernel's formula x*cos + sign*partner*sin.  One token (M = 1).
-// WAVENORM: every wave normalises the row itself (its lanes hold exactly the 24 elements their
-// dot-product chunks use, the sum of squares is one wave reduction): no LDS and no block barrier.
-template <typename WT, bool WAVENORM>
+// (Every wave normalising the row itself, without LDS or a block barrier, measured +0.75 us per layer:
+// the block-staged row is read from LDS, not re-read from L2 by each wave.)
+template <typename WT>
 __global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRopeEpi r) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int U = 3, XR = 2;
-    if (WAVENORM) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const int half = r.hd / 2;
-        const int p = blockIdx.x * 4 + wave;
-        const int npairs = a.N / 2;
-        if (p >= npairs) return;  // whole wave: nothing below synchronises the block
-        const int n0 = (p / half) * r.hd + p % half, n1 = n0 + half;
-        const WT* W = reinterpret_cast<const WT*>(a.W);
-        const int chunks = a.K >> 3;
-        float xv[U][8], nw[U][8];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int cc = min(u * 64 + lane, chunks - 1);
-            ld_x8(a.x + (cc << 3), xv[u]);
-            ld_x8(a.norm_w + (cc << 3), nw[u]);
-        }
-        const int pos = r.kv_pos[0];
-        uint4 w0[U], w1[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int cc = min(u * 64 + lane, chunks - 1);
-            w0[u] = ldg_nt16(W + (long)n0 * a.ldw + (cc << 3));
-            w1[u] = ldg_nt16(W + (long)n1 * a.ldw + (cc << 3));
-        }
-        const int d = n0 % r.hd;
-        const bool rot = n0 < r.rot_rows;
-        const float c0 = rot ? r.cos[(long)pos * r.hd + d] : 1.f, s0 = rot ? r.sin[(long)pos * r.hd + d] : 0.f;
-        const float c1 = rot ? r.cos[(long)pos * r.hd + d + half] : 1.f, s1 = rot ? r.sin[(long)pos * r.hd + d + half] : 0.f;
-        float q = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (u * 64 + lane < chunks)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) q += xv[u][j] * xv[u][j];
-        const float den = sqrtf(wave_sum(q) / (float)a.K + a.eps);
-        float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (u * 64 + lane < chunks) {
-                float f0[8], f1[8];
-                unpack8<WT>(w0[u], f0);
-                unpack8<WT>(w1[u], f1);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float xn = (xv[u][j] / den) * nw[u][j];
-                    acc0 = fmaf(xn, f0[j], acc0);
-                    acc1 = fmaf(xn, f1[j], acc1);
-                }
-            }
-        }
-        float y0 = wave_sum(acc0), y1 = wave_sum(acc1);
-        if (lane == 0) {
-            y0 = y0 + (a.bias ? a.bias[n0] : 0.f);
-            y1 = y1 + (a.bias ? a.bias[n1] : 0.f);
-            if (rot) {
-                const float o0 = y0 * c0 + (-1.f * y1) * s0;
-                const float o1 = y1 * c1 + (1.f * y0) * s1;
-                y0 = o0;
-                y1 = o1;
-            }
-            a.y[n0] = y0;
-            a.y[n1] = y1;
-        }
-        return;
-    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int half = r.hd / 2;
     const int p = blockIdx.x * 4 + wave;                 // pair index
@@ -748,134 +585,8 @@ void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t 
     if (!dec_qkv_rope_ok(a, r)) throw std::runtime_error("EINVAL: dec_qkv_rope outside its range");
     const size_t lds = stage_bytes(1, a.K);
     dim3 grid((a.N / 2 + 3) / 4);
-    // (off by default: every wave re-reading x and the norm weight from L2 measured +0.75 us/layer)
-    static const bool wn = getenv("DSOCR_WAVENORM") && atoi(getenv("DSOCR_WAVENORM")) != 0;
-    if (wn && a.norm_w) {
-        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_rope_kernel<bf16_t, true>), grid, dim3(256), 0, s, a, r);
-        else DSOCR_LAUNCH((dec_qkv_rope_kernel<f16_t, true>), grid, dim3(256), 0, s, a, r);
-        return;
-    }
-    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_rope_kernel<bf16_t, false>), grid, dim3(256), lds, s, a, r);
-    else DSOCR_LAUNCH((dec_qkv_rope_kernel<f16_t, false>), grid, dim3(256), lds, s, a, r);
-}
-
-// ------------------------------------------------------------------ attention combine + o_proj
-// One token: the flash-decoding combine of every head (the split-mode records of dec_attn) runs
-// in each block's prologue — the same arithmetic as the in-kernel combine (per head: global max,
-// even / odd chunk partial sums in chunk order, (a0 + a1) / (l0 + l1)) — while the block's o_proj
-// weight rows stream; then y[j] (+)= W_o[j] . ctx (dec_gemv's per-row order).  Records: per head
-// [m[CM] | l[CM] | o[HD][CM]].  Writes ctx to ctx_out (block 0) for the tests / fallbacks.
-template <typename WT, int RW, int NCM, int EPT>
-__global__ __launch_bounds__(256) void dec_oproj_comb_kernel(DecGemvArgs a, DecCombArgs cb) {
-    constexpr int U = 3;  // K <= 1536; NCM >= chunks per head (even), EPT * 256 >= heads * hd
-    __shared__ __attribute__((aligned(16))) float xs[1536];
-    __shared__ float wts[16][NCM];  // expf(m - max) per (head, chunk)
-    __shared__ float lsum[16][NCM];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    const int n0 = (blockIdx.x * 4 + wave) * RW;
-    const WT* W = reinterpret_cast<const WT*>(a.W);
-    const int chunks = a.K >> 3;
-    // 1. this wave's weight rows first (independent of everything in this step)
-    uint4 wq[RW][U];
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-        const int n = min(n0 + r, a.N - 1);
-#pragma unroll
-        for (int u = 0; u < U; ++u) wq[r][u] = ldg_nt16(W + (long)n * a.ldw + (min(u * 64 + lane, chunks - 1) << 3));
-    }
-    const int pos = cb.kv_pos[0];
-    const int nc = (pos + cb.ch) / cb.ch;  // chunks holding keys 0..pos
-    const int CM = cb.cm, HD = cb.hd, heads = cb.heads;
-    // 2. every o partial this thread folds: elements e = tid + 256 i, chunks 0..NCM-1 (clamped
-    //    to the capacity; chunks >= nc get weight 0 by a select)
-    float ov[EPT][NCM];
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const int e = min(tid + 256 * i, heads * HD - 1);
-        const float* src = cb.part + (long)(e / HD) * (2 + HD) * CM + 2 * CM + e % HD;
-#pragma unroll
-        for (int q = 0; q < NCM; ++q) ov[i][q] = src[(long)min(q, CM - 1) * HD];
-    }
-    // 3. chunk maxima / sums -> per-head weights in LDS
-    for (int t = tid; t < heads * NCM; t += 256) {
-        const int hh = t / NCM, q = t % NCM;
-        const float* Q = cb.part + (long)hh * (2 + HD) * CM;
-        wts[hh][q] = Q[min(q, CM - 1)];
-        lsum[hh][q] = Q[CM + min(q, CM - 1)];
-    }
-    __syncthreads();
-    if (tid < heads) {
-        float mm = -INFINITY;
-        for (int q = 0; q < nc; ++q) mm = fmaxf(mm, wts[tid][q]);
-        for (int q = 0; q < NCM; ++q) wts[tid][q] = q < nc ? expf(wts[tid][q] - mm) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-        const int e = tid + 256 * i;
-        if (e < heads * HD) {
-            const int hh = e / HD;
-            float a0 = 0.f, a1 = 0.f, l0 = 0.f, l1 = 0.f;
-#pragma unroll
-            for (int q = 0; q < NCM; q += 2) {
-                const float w0 = wts[hh][q], w1 = wts[hh][q + 1];
-                if (q < nc) { l0 += lsum[hh][q] * w0; a0 += ov[i][q] * w0; }
-                if (q + 1 < nc) { l1 += lsum[hh][q + 1] * w1; a1 += ov[i][q + 1] * w1; }
-            }
-            float at = 0.f, lt = 0.f;
-            at += a0; at += a1;
-            lt += l0; lt += l1;
-            xs[e] = at / lt;
-        }
-    }
-    __syncthreads();
-    if (cb.ctx_out && blockIdx.x == 0)
-        for (int e = tid; e < heads * HD; e += 256) cb.ctx_out[e] = xs[e];
-    // 4. the rows
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-        float acc = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int cc = u * 64 + lane;
-            if (cc < chunks) {
-                float w8[8], xv[8];
-                unpack8<WT>(wq[r][u], w8);
-                ld_x8(xs + (cc << 3), xv);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], w8[j], acc);
-            }
-        }
-        float v = wave_sum(acc);
-        const int n = n0 + r;
-        if (lane == 0 && n < a.N) {
-            v = v + (a.bias ? a.bias[n] : 0.f);
-            float* yp = a.y + n;
-            if (a.accumulate) v = *yp + v;
-            *yp = v;
-        }
-    }
-}
-
-bool dec_oproj_comb_ok(const DecGemvArgs& a, const DecCombArgs& cb) {
-    return a.M == 1 && a.K == cb.heads * cb.hd && a.K <= 1536 && a.K % 8 == 0 && cb.heads <= 16 && cb.cm <= 24 &&
-           cb.part && cb.kv_pos && cb.ch > 0;
-}
-
-void launch_dec_oproj_comb(const DecGemvArgs& a, const DecCombArgs& cb, hipStream_t s) {
-    if (!dec_oproj_comb_ok(a, cb)) throw std::runtime_error("EINVAL: dec_oproj_comb outside its range");
-    static const int rw = getenv("DSOCR_OC_RW") ? atoi(getenv("DSOCR_OC_RW")) : 1;
-#define DSOCR_OC(WTY, R, NC, E) \
-    DSOCR_LAUNCH((dec_oproj_comb_kernel<WTY, R, NC, E>), dim3((a.N + 4 * R - 1) / (4 * R)), dim3(256), 0, s, a, cb)
-#define DSOCR_OC2(WTY, NC, E) do { if (rw == 2) DSOCR_OC(WTY, 2, NC, E); else DSOCR_OC(WTY, 1, NC, E); } while (0)
-#define DSOCR_OC3(WTY) do { \
-        if (cb.cm <= 20 && a.K <= 1280) DSOCR_OC2(WTY, 20, 5); else if (cb.cm <= 20) DSOCR_OC2(WTY, 20, 6); \
-        else if (a.K <= 1280) DSOCR_OC2(WTY, 24, 5); else DSOCR_OC2(WTY, 24, 6); } while (0)
-    if (a.wdtype == WDT_BF16) DSOCR_OC3(bf16_t);
-    else DSOCR_OC3(f16_t);
-#undef DSOCR_OC3
-#undef DSOCR_OC2
-#undef DSOCR_OC
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_rope_kernel<bf16_t>), grid, dim3(256), lds, s, a, r);
+    else DSOCR_LAUNCH((dec_qkv_rope_kernel<f16_t>), grid, dim3(256), lds, s, a, r);
 }
 
 // ------------------------------------------------------------------ router + top-k
@@ -1318,32 +1029,15 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 }
 
 // ------------------------------------------------------------------ decode attention
-// grid (chunks of 64 keys, heads, B).  The token being decoded sits at pos = kv_pos[b]:
-// q and k are rotated here (rotate_half RoPE, block.rs:1403-1471), the block owning
-// chunk pos/64 appends k,v to the f32 cache (block.rs:776-789) and uses them directly.
-// Each block issues its K and V cache loads first, then builds q; the block that
-// arrives last for a (page, head) merges the chunk partials (flash-decoding combine)
-// with one agent-scope release / acquire (cdna_hip_programming.md §5 split-K recipe).
-// CH keys per block (64 or 32: env DSOCR_ATT_CH); LPK = 256 / CH lanes score one key.
-constexpr int DA2_CH_MIN = 32;
+// grid (chunks of 64 keys, heads, B).  The token being decoded sits at pos = kv_pos[b]: q and the new
+// k are rotated here (rotate_half RoPE, block.rs:1403-1471) unless the projection's epilogue already
+// did (PREROT, one page: dec_qkv_rope); the block owning chunk pos/64 appends k, v to the f32 cache
+// (block.rs:776-789) and uses them directly.  Each block issues its K and V cache loads first, then
+// builds q; the chunk partials of a (page, head) are merged by chunk 0's block polling them (POLL, <= 24
+// chunks of 128-dim heads) or by the last arriver of a ticket (flash-decoding combine).
+constexpr int DA_CH = 64;       // keys per block
+constexpr int DA2_CH_MIN = DA_CH;
 constexpr uint32_t DA_SENT = 0x7FBADBADu;  // "record word not written yet" (a NaN payload no arithmetic produces)
-
-// an empty asm that takes N float4 registers as operands (4 at a time): the loads that produced them
-// stay above this point
-template <int N>
-__device__ __forceinline__ void keep_f4(const float4* r) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int i = 0; i < N; i += 4) {
-        f4v t[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float4 u = r[min(i + j, N - 1)];
-            t[j] = f4v{u.x, u.y, u.z, u.w};
-        }
-        asm volatile("" ::"v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]));
-    }
-}
 
 // sum over aligned groups of N lanes (N = 4 or 8), result in every lane of the group
 template <int N>
@@ -1354,103 +1048,14 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
-// q / k / v rows of head h for page b, computed by chunk block c of the nc active blocks:
-// flattened rows f in [c*R, (c+1)*R) of the head's 3*HD rows (q, then k, then v), R = ceil(3HD/nc),
-// wave w owning f = c*R + w + 4j.  x = rmsnorm(x_b) staged once (xload / xstage, the dec_gemv
-// arithmetic), every row a wave dot product in dec_gemv's order (chunk u-major, then j),
-// stored write-through; then the per-head arrival counter and the wait for all nc blocks.
-template <int HD>
-__device__ __forceinline__ void qkv_rows_for_head(const DecAttn2Args& a, int b, int h, int c, int nc, float* smem) {
-    constexpr int U = 3, XR = 2, RBM = 8;  // K <= 1536; up to 8 rows per wave per batch
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int R = (3 * HD + nc - 1) / nc;
-    const int f0 = c * R, f1 = min(3 * HD, f0 + R);
-    const int chunks = a.K >> 3;
-    auto row_of = [&](int f) {
-        const int seg = f / HD, i = f % HD;
-        return seg == 0 ? h * HD + i : (seg == 1 ? a.heads * HD + h * HD + i : (2 * a.heads) * HD + h * HD + i);
-    };
-    XRegs<1, XR> xr;
-    xload<1, XR>(xr, a.x + (long)b * a.ldx, a.ldx, nullptr, 1, a.K, a.norm_w);
-    bool staged = false;
-    float* yrow = const_cast<float*>(a.qkv) + (long)b * a.ld;
-    const int nbat = (R + 4 * RBM - 1) / (4 * RBM);  // uniform over the block's waves
-    for (int bt = 0; bt < nbat; ++bt) {
-        // batch: rows fb, fb + 4, ..., fb + 4 * (RBM - 1) of this wave (clamped loads past f1)
-        const int fb = f0 + wave + bt * 4 * RBM;
-        uint4 wq[RBM][U];
-        const bool any = fb < f1;
-#pragma unroll
-        for (int r = 0; r < RBM; ++r) {
-            const int f = min(fb + 4 * r, f1 - 1);
-            const uint16_t* W = reinterpret_cast<const uint16_t*>(a.Wqkv) + (long)row_of(f) * a.K;
-#pragma unroll
-            for (int u = 0; u < U; ++u) wq[r][u] = ldg_nt16(W + (min(u * 64 + lane, chunks - 1) << 3));
-        }
-        if (!staged) {
-            xstage<1, XR>(xr, 1, a.K, a.norm_w != nullptr, a.eps, smem);
-            staged = true;
-        }
-        const float* xs = smem + XS_RED;
-        if (any) {
-#pragma unroll
-            for (int r = 0; r < RBM; ++r) {
-                float acc = 0.f;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int cc = u * 64 + lane;
-                    if (cc < chunks) {
-                        float w8[8], xv[8];
-                        if (a.wdtype == WDT_BF16) unpack8<bf16_t>(wq[r][u], w8);
-                        else unpack8<f16_t>(wq[r][u], w8);
-                        ld_x8(xs + (cc << 3), xv);
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], w8[j], acc);
-                    }
-                }
-                float v = wave_sum(acc);
-                const int f = fb + 4 * r;
-                if (lane == 0 && f < f1) {
-                    const int n = row_of(f);
-                    v = v + (a.qkv_bias ? a.qkv_bias[n] : 0.f);
-                    __hip_atomic_store(yrow + n, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-        }
-    }
-    // R1 publish: every storing wave drains its sc1 stores, one lane counts the block, then
-    // one lane waits for all nc blocks of the head
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int* cnt = a.qkv_cnt + (long)b * a.heads + h;
-        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (unsigned it = 0;; ++it) {
-            if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nc) break;
-            if (it > (1u << 21)) { __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
-}
-
-// FUSED (dec_qkv_attn): the blocks of one (page, head) first compute that head's q / k / v
-// rows of the fused projection themselves (RMSNorm + GEMV, the same per-row arithmetic as
-// dec_gemv), hand them over through a per-head arrival counter (write-through stores, sc1
-// loads), then run the attention chunk exactly as the unfused kernel.
-// PREROT: the q / k rows arrive already rotated (dec_qkv_rope applied RoPE in its epilogue), so
-// q, k_new and v_new are loaded before the position and no RoPE table is read here.
-template <int HD, int CH, bool PREROT, bool FUSED, bool EARLY = false, int NSUB = 1, bool POLL = false>
-__device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
+template <int HD, bool PREROT, bool POLL>
+__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     WaveSpan span_(a.span);
+    constexpr int CH = DA_CH;
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
     constexpr int DG = HD / 4, KG = 256 / DG, KPG = CH / KG;     // PV: float4 dim groups x key groups
-    constexpr int KB = CH * NSUB;                                // keys per block (NSUB sub-chunks of CH)
-    static_assert(LPK == 4 || LPK == 8, "CH must be 64 or 32");
-    static_assert(KPG >= 1 && DPL % 4 == 0, "unsupported head_dim / chunk");
-    static_assert(NSUB == 1 || !FUSED, "the fused q/k/v path runs one chunk per block");
+    static_assert(KPG >= 1 && DPL % 4 == 0, "unsupported head_dim");
     __shared__ float qs[HD];
     __shared__ float knew[HD];
     __shared__ float vnew[HD];
@@ -1459,32 +1064,22 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     __shared__ int last_s;
     __shared__ float4 o_s[384];  // P.V partials; reused by the combine (m, l per chunk + per-group sums)
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const long sbid = ((long)b * gridDim.y + h) * gridDim.x + c;
-#define AT_STAMP(i)                                                                          \
-    if (a.stamps && threadIdx.x == 0) {                                                      \
-        if ((i) == 0) a.stamps[sbid * 8] = __builtin_amdgcn_s_memrealtime();                 \
-        a.stamps[sbid * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();                         \
-    }
-    AT_STAMP(0);
-    const int k0 = c * KB;
+    const int k0 = c * CH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvh = h / (a.heads / a.kv_heads);
     float* Kc = a.kc + (long)b * a.page_stride + (long)kvh * a.head_stride;
     float* Vc = a.vc + (long)b * a.page_stride + (long)kvh * a.head_stride;
-    // 1. the chunk's K / V cache loads go out first and depend on nothing computed this step
-    //    (keys clamped to the cache capacity, not to the position: keys past pos are masked
-    //    at use), so the HBM stream overlaps the position / RoPE-table round trips below
+    // 1. the chunk's K / V cache loads (keys clamped to the position: keys past it are masked at use)
     const int key = tid / LPK, sub = tid % LPK;
-    const int kcap = a.max_len - 1;
     const int dg = tid % DG, kg = tid / DG;
     float4 kreg[DPL / 4];
     float4 vreg[KPG];
-    // TK (64-key chunks of 128-dim heads): K is loaded like V, instruction i of wave w reading keys
-    // w*16 + 2i and w*16 + 2i + 1 whole (1 KiB contiguous per instruction: 8 L2 lines, where one
-    // key per 4 lanes touched 64 lines per instruction); lane l holds dims 4 (l & 31) .. + 3 of key
-    // tk_key(i) = w*16 + 2i + (l >> 5), and the q.k dot products are finished by a transposing
-    // butterfly over the 32 lanes of a key (9 swizzle / DPP adds for 8 keys).
-    constexpr bool TK = CH == 64 && HD == 128;
+    // TK (128-dim heads): K is loaded like V, instruction i of wave w reading keys w*16 + 2i and
+    // w*16 + 2i + 1 whole (1 KiB contiguous per instruction: 8 L2 lines, where one key per 4 lanes touched
+    // 64 lines per instruction); lane l holds dims 4 (l & 31) .. + 3 of key tk_key(i) = w*16 + 2i + (l >> 5),
+    // and the q.k dot products are finished by a transposing butterfly over the 32 lanes of a key
+    // (9 swizzle / DPP adds for 8 keys).
+    constexpr bool TK = HD == 128;
     const int tk_half = lane >> 5, tk_d4 = (lane & 31) * 4;
     auto tk_key = [&](int i) { return wave * 16 + 2 * i + tk_half; };
     auto issue_k = [&](int kb, int klim) {
@@ -1513,30 +1108,16 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         k_pre = row[a.heads * HD + kvh * HD + td];
         v_pre = row[(a.heads + a.kv_heads) * HD + kvh * HD + td];
     }
-    // EARLY (one page: latency-bound): the chunk's K / V loads go out before the position is known,
-    // clamped to the cache capacity (keys past pos are masked at use), overlapping the pos round trip
     const int pos = a.kv_pos[b];
-    if (EARLY) {
-        issue_k(k0, kcap);
-        issue_v(k0, kcap);
-        // every loaded register is an operand here, so the compiler cannot sink a cache load below
-        // the position test (it did: two round trips instead of one); the test then waits for the
-        // loads, which left with the position load
-        keep_f4<DPL / 4>(kreg);
-        keep_f4<KPG>(vreg);
-    }
     const int len = pos + 1;
     if (k0 >= len) return;
-    if (!EARLY) { issue_k(k0, min(k0 + CH, len) - 1); issue_v(k0, min(k0 + CH, len) - 1); }
-    const bool own = pos >= k0 && pos < k0 + KB;
-    const int nc = (len + KB - 1) / KB;
-    if (FUSED) qkv_rows_for_head<HD>(a, b, h, c, nc, smem);
+    issue_k(k0, min(k0 + CH, len) - 1);
+    issue_v(k0, min(k0 + CH, len) - 1);
+    const bool own = pos >= k0 && pos < k0 + CH;
+    const int nc = (len + CH - 1) / CH;
     // 2. RoPE inputs
     const float* krow = row + a.heads * HD + kvh * HD;
     const float* vrow = row + (a.heads + a.kv_heads) * HD + kvh * HD;
-    auto ldv = [&](const float* p) {
-        return FUSED ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
-    };
     float qx = 0.f, qr = 0.f, kx = 0.f, kr = 0.f, vx = 0.f, cs = 1.f, sn = 0.f, sg = 0.f;
     if (PREROT) {
         if (tid < HD) {
@@ -1561,12 +1142,12 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
             cs = a.cos[(long)pos * a.rope_dim + tid];
             sn = a.sin[(long)pos * a.rope_dim + tid];
         }
-        qx = ldv(row + h * HD + ix);
-        qr = ldv(row + h * HD + ir);
+        qx = row[h * HD + ix];
+        qr = row[h * HD + ir];
         if (own) {
-            kx = ldv(krow + ix);
-            kr = ldv(krow + ir);
-            vx = ldv(vrow + tid);
+            kx = krow[ix];
+            kr = krow[ir];
+            vx = vrow[tid];
         }
     }
     // 3. rotated q (and the new k, v in the owning chunk): x*cos + sign*partner*sin
@@ -1583,146 +1164,97 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         }
     }
     __syncthreads();
-    AT_STAMP(1);
-    // NSUB sub-chunks of CH keys, merged in registers by the online softmax (running max m, sum l,
-    // and this thread's P.V partial o, each rescaled by exp(m_old - m_new)); the next sub-chunk's K
-    // loads go out once the scores consumed kreg, its V loads once P.V consumed vreg.  NSUB = 1 is
-    // the one-chunk arithmetic exactly (the first sub-chunk assigns, it does not rescale).
-    float m = -INFINITY, l_run = 0.f;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int kn = min(CH, len - k0);
+    // 4. scores: LPK lanes per key, wave w owns keys w*CH/4 .. (w+1)*CH/4 - 1
+    if constexpr (TK) {
+        const float4 q4 = *reinterpret_cast<const float4*>(qs + tk_d4);
+        const float4 kn4 = *reinterpret_cast<const float4*>(knew + tk_d4);
+        float v[8];
 #pragma unroll
-    for (int s = 0; s < NSUB; ++s) {
-        const int ks = k0 + s * CH;
-        if (s > 0 && ks >= len) break;  // block-uniform
-        const int kn = min(CH, len - ks);
-        const bool more = s + 1 < NSUB && ks + CH < len;
-        // 4. scores: LPK lanes per key, wave w owns keys w*CH/4 .. (w+1)*CH/4 - 1
-        if constexpr (TK) {
-            const float4 q4 = *reinterpret_cast<const float4*>(qs + tk_d4);
-            const float4 kn4 = *reinterpret_cast<const float4*>(knew + tk_d4);
-            float v[8];
+        for (int i = 0; i < 8; ++i) {
+            const float4 k4 = k0 + tk_key(i) == pos ? kn4 : kreg[i];
+            v[i] = fmaf(q4.w, k4.w, fmaf(q4.z, k4.z, fmaf(q4.y, k4.y, q4.x * k4.x)));
+        }
+        // butterfly: after the xor-16 / 8 / 4 steps lane l holds key i = b2 + 2 b3 + 4 b4 (bits of l)
+        // summed over its 8 lanes of that bit pattern; the quad sum finishes the 32 lanes
+        const int b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1;
+        float u[4];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float4 k4 = ks + tk_key(i) == pos ? kn4 : kreg[i];
-                v[i] = fmaf(q4.w, k4.w, fmaf(q4.z, k4.z, fmaf(q4.y, k4.y, q4.x * k4.x)));
-            }
-            if (more) issue_k(ks + CH, len - 1);
-            // butterfly: after the xor-16 / 8 / 4 steps lane l holds key i = b2 + 2 b3 + 4 b4 (bits of l)
-            // summed over its 8 lanes of that bit pattern; the quad sum finishes the 32 lanes
-            const int b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1;
-            float u[4];
+        for (int j = 0; j < 4; ++j) {
+            const float keep = b4 ? v[j + 4] : v[j], send = b4 ? v[j] : v[j + 4];
+            u[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (16 << 10)));
+        }
+        float t[2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float keep = b4 ? v[j + 4] : v[j], send = b4 ? v[j] : v[j + 4];
-                u[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (16 << 10)));
-            }
-            float t[2];
+        for (int j = 0; j < 2; ++j) {
+            const float keep = b3 ? u[j + 2] : u[j], send = b3 ? u[j] : u[j + 2];
+            t[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (8 << 10)));
+        }
+        float r;
+        {
+            const float keep = b2 ? t[1] : t[0], send = b2 ? t[0] : t[1];
+            r = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (4 << 10)));
+        }
+        r = group_sum<4>(r);
+        const int kk = tk_key(b2 + 2 * b3 + 4 * b4);
+        const float sc = kk < kn ? r * a.scale : -INFINITY;
+        if ((lane & 3) == 0) p_s[kk] = sc;
+        const float mw = wave_max(sc);
+        if (lane == 0) red[wave] = mw;
+    } else {
+        float acc = 0.f;
+        if (key < kn) {
+            if (k0 + key == pos) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const float keep = b3 ? u[j + 2] : u[j], send = b3 ? u[j] : u[j + 2];
-                t[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (8 << 10)));
-            }
-            float r;
-            {
-                const float keep = b2 ? t[1] : t[0], send = b2 ? t[0] : t[1];
-                r = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x1f | (4 << 10)));
-            }
-            r = group_sum<4>(r);
-            const int kk = tk_key(b2 + 2 * b3 + 4 * b4);
-            const float sc = kk < kn ? r * a.scale : -INFINITY;
-            if ((lane & 3) == 0) p_s[kk] = sc;
-            const float mw = wave_max(sc);
-            if (lane == 0) red[wave] = mw;
-        } else {
-            float acc = 0.f;
-            if (key < kn) {
-                if (ks + key == pos) {
+                for (int i = 0; i < DPL; ++i) acc = fmaf(qs[sub * DPL + i], knew[sub * DPL + i], acc);
+            } else {
 #pragma unroll
-                    for (int i = 0; i < DPL; ++i) acc = fmaf(qs[sub * DPL + i], knew[sub * DPL + i], acc);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < DPL / 4; ++i) {
-                        acc = fmaf(qs[sub * DPL + 4 * i + 0], kreg[i].x, acc);
-                        acc = fmaf(qs[sub * DPL + 4 * i + 1], kreg[i].y, acc);
-                        acc = fmaf(qs[sub * DPL + 4 * i + 2], kreg[i].z, acc);
-                        acc = fmaf(qs[sub * DPL + 4 * i + 3], kreg[i].w, acc);
-                    }
+                for (int i = 0; i < DPL / 4; ++i) {
+                    acc = fmaf(qs[sub * DPL + 4 * i + 0], kreg[i].x, acc);
+                    acc = fmaf(qs[sub * DPL + 4 * i + 1], kreg[i].y, acc);
+                    acc = fmaf(qs[sub * DPL + 4 * i + 2], kreg[i].z, acc);
+                    acc = fmaf(qs[sub * DPL + 4 * i + 3], kreg[i].w, acc);
                 }
             }
-            if (more) issue_k(ks + CH, len - 1);
-            acc = group_sum<LPK>(acc);
-            const float sc = key < kn ? acc * a.scale : -INFINITY;
-            if (sub == 0) p_s[key] = sc;
-            const float mw = wave_max(sc);
-            if (lane == 0) red[wave] = mw;
         }
-        __syncthreads();
-        const float mc = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-        const float mn = s == 0 ? mc : fmaxf(m, mc);
-        if (wave == 0) {  // whole wave active for the DPP reduction
-            const float p = (tid < CH && tid < kn) ? expf(p_s[tid] - mn) : 0.f;
-            if (tid < CH) p_s[tid] = p;
-            const float l = wave_sum(p);
-            if (tid == 0) red[4] = l;
-        }
-        __syncthreads();
-        if (s == 0) AT_STAMP(2);
-        // 5. P.V over this thread's KPG keys
-        float4 oc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int j = 0; j < KPG; ++j) {
-            const int key2 = TK ? tk_key(j) : kg * KPG + j;
-            if (key2 >= kn) vreg[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // never 0 * (stale cache bits)
-            else if (ks + key2 == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
-        }
-#pragma unroll
-        for (int j = 0; j < KPG; ++j) {
-            const float p = p_s[TK ? tk_key(j) : kg * KPG + j];
-            oc.x = fmaf(p, vreg[j].x, oc.x);
-            oc.y = fmaf(p, vreg[j].y, oc.y);
-            oc.z = fmaf(p, vreg[j].z, oc.z);
-            oc.w = fmaf(p, vreg[j].w, oc.w);
-        }
-        if (more) issue_v(ks + CH, len - 1);
-        if (s == 0) {
-            o = oc;
-            l_run = red[4];
-        } else {
-            const float al = expf(m - mn);
-            o.x = fmaf(o.x, al, oc.x);
-            o.y = fmaf(o.y, al, oc.y);
-            o.z = fmaf(o.z, al, oc.z);
-            o.w = fmaf(o.w, al, oc.w);
-            l_run = fmaf(l_run, al, red[4]);
-        }
-        m = mn;
-        if (more) __syncthreads();  // p_s / red are rewritten by the next sub-chunk
+        acc = group_sum<LPK>(acc);
+        const float sc = key < kn ? acc * a.scale : -INFINITY;
+        if (sub == 0) p_s[key] = sc;
+        const float mw = wave_max(sc);
+        if (lane == 0) red[wave] = mw;
     }
+    __syncthreads();
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (wave == 0) {  // whole wave active for the DPP reduction
+        const float p = (tid < CH && tid < kn) ? expf(p_s[tid] - m) : 0.f;
+        if (tid < CH) p_s[tid] = p;
+        const float l = wave_sum(p);
+        if (tid == 0) red[4] = l;
+    }
+    __syncthreads();
+    // 5. P.V over this thread's KPG keys
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < KPG; ++j) {
+        const int key2 = TK ? tk_key(j) : kg * KPG + j;
+        if (key2 >= kn) vreg[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // never 0 * (stale cache bits)
+        else if (k0 + key2 == pos) vreg[j] = *reinterpret_cast<const float4*>(vnew + dg * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < KPG; ++j) {
+        const float p = p_s[TK ? tk_key(j) : kg * KPG + j];
+        o.x = fmaf(p, vreg[j].x, o.x);
+        o.y = fmaf(p, vreg[j].y, o.y);
+        o.z = fmaf(p, vreg[j].z, o.z);
+        o.w = fmaf(p, vreg[j].w, o.w);
+    }
+    const float l_run = red[4];
     o_s[tid] = o;
     __syncthreads();
-    if (a.split) {
-        // split mode: no in-kernel combine; per (page, head) [m[CM] | l[CM] | o[CM][HD]] for the o_proj
-        // kernel's combine prologue (next launch: plain stores; o rows coalesce along d)
-        const int CM = (a.max_len + KB - 1) / KB;
-        float* Q = a.part + ((long)b * a.heads + h) * (2 + HD) * CM;
-        if (tid < DG) {
-            float4 t = o_s[tid];
-            for (int g = 1; g < KG; ++g) {
-                const float4 u = o_s[g * DG + tid];
-                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-            }
-            *reinterpret_cast<float4*>(Q + 2 * CM + (long)c * HD + tid * 4) = t;
-        }
-        if (tid == 0) {
-            Q[c] = m;
-            Q[CM + c] = l_run;
-        }
-        return;
-    }
     // partial record of chunk c: [m, l, -, -, o[HD]] (16-byte aligned), stored WRITE-THROUGH (sc1)
     // so the hand-off needs no L2-writeback release fence (cdna_hip_programming.md Guideline 16 R1)
     constexpr int PR = HD + 4;
-    const int chunks = (a.max_len + KB - 1) / KB;
+    const int chunks = (a.max_len + CH - 1) / CH;
     float* part0 = a.part + ((long)b * a.heads + h) * chunks * PR;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part0, (short)0, chunks * PR * 4, 0x00020000);
     if (tid < DG) {
@@ -1752,10 +1284,7 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
     //    every load of it below is an sc1 buffer load, so no acquire fence is needed
     //    (MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire, first row).
     if constexpr (POLL) {
-        if (c != 0) {
-            AT_STAMP(3);
-            return;
-        }
+        if (c != 0) return;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1765,15 +1294,10 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         int* cnt = a.counters + (long)b * a.heads + h;
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == nc - 1;
-        if (last) {
-            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // every block of (b, h) has passed its q/k/v wait before adding its ticket
-            if (FUSED) __hip_atomic_store(a.qkv_cnt + (long)b * a.heads + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_s = last;
     }
     __syncthreads();
-    AT_STAMP(3);
     if (!last_s) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
     auto ld1 = [&](int idx) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, idx * 4, 0, 16)); };
@@ -1858,45 +1382,6 @@ __device__ __forceinline__ void attn_body(const DecAttn2Args& a, float* smem) {
         for (int g = 0; g < KS; ++g) { at += accp[g * HD + tid]; lt += lp[g * HD + tid]; }
         a.o[(long)b * a.o_ld + (long)h * HD + tid] = at / lt;
     }
-    AT_STAMP(4);
-#undef AT_STAMP
-}
-
-template <int HD, int CH, bool PREROT, bool EARLY, bool POLL = false>
-__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
-    attn_body<HD, CH, PREROT, false, EARLY, 1, POLL>(a, nullptr);
-}
-
-// NSUB sub-chunks per block: at most 128 VGPRs (4 blocks per CU), so the grid of >= 600 blocks is
-// resident at once (without the cap the compiler hoists the next sub-chunk's loads to 132 VGPRs)
-template <int HD, int CH, bool PREROT, int NSUB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void dec_attn_sub_kernel(DecAttn2Args a) {
-    attn_body<HD, CH, PREROT, false, false, NSUB>(a, nullptr);
-}
-
-template <int HD, int CH>
-__global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecAttn2Args a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    attn_body<HD, CH, false, true>(a, smem);
-}
-
-bool dec_qkv_attn_ok(const DecAttn2Args& a) {
-    return a.heads == a.kv_heads && a.hd == 128 && a.x && a.Wqkv && a.qkv_cnt && a.err && a.K % 8 == 0 &&
-           a.K <= 64 * 3 * 8 && a.max_len <= 512 * 64;
-}
-
-void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s) {
-    if (!dec_qkv_attn_ok(a) || !a.counters) throw std::runtime_error("EINVAL: fused q/k/v + attention outside its range");
-    const int chunks = (a.max_len + 63) / 64;
-    dim3 g1(chunks, a.heads, a.B);
-    const size_t lds = stage_bytes(1, a.K);
-    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
-    else DSOCR_LAUNCH((dec_qkv_attn_kernel<128, 64>), g1, dim3(256), lds, s, a);
-}
-
-static int dec_attn_ch() {
-    const char* e = getenv("DSOCR_ATT_CH");
-    return (e && atoi(e) == 32) ? 32 : 64;
 }
 
 void dec_attn_part_init(float* part, size_t bytes, hipStream_t s) {
@@ -1908,65 +1393,26 @@ size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
     return (size_t)B * heads * ((max_len + DA2_CH_MIN - 1) / DA2_CH_MIN) * (hd + 4) * sizeof(float);
 }
 
-// Keys per block: NSUB sub-chunks of ch (env DSOCR_ATT_NSUB).  A block holds its chunk's K / V in
-// registers (90 VGPRs: 5 blocks per CU), so 8 pages at L 1217 (1600 blocks) run 1.25 rounds; NSUB 2
-// keeps the grid within one round but each block's second sub-chunk then waits behind the first.
-static int dec_attn_nsub(const DecAttn2Args& a, int chunks) {
-    const char* e = getenv("DSOCR_ATT_NSUB");
-    if (e) {
-        const int v = atoi(e);
-        return v >= 4 ? 4 : v >= 2 ? 2 : 1;
-    }
-    (void)a; (void)chunks;  // 2 / 4 measured slower at 8 pages (27.5 / 37.2 vs 26.0 us at L 1217)
-    return 1;
-}
-
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
-    static const bool old_kernel = getenv("DSOCR_ATTN_OLD") && atoi(getenv("DSOCR_ATTN_OLD")) != 0;
-    if (!old_kernel && !a.split) return launch_dec_attn3(a, s);
     if (!a.counters) throw std::runtime_error("EINTERNAL: dec_attn needs a zeroed counter array");
-    const int ch = dec_attn_ch();
-    if (a.max_len > 512 * ch) throw std::runtime_error("EINVAL: decode context too long for the attention combine");
+    if (a.max_len > 512 * DA_CH) throw std::runtime_error("EINVAL: decode context too long for the attention combine");
     if (a.hd != 128 && a.hd != 64 && a.hd != 32) throw std::runtime_error("EINVAL: decode attention supports head_dim 32 / 64 / 128");
-    const int chunks = (a.max_len + ch - 1) / ch;
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
     const bool prerot = a.prerot != 0;
-    // EARLY (K / V loads before the position, one page): measured slower once the loads really go
-    // out first (7.9 vs 8.7 us at L 707: the test then waits for the whole chunk), so opt-in
-    static const bool early_env = getenv("DSOCR_ATT_EARLY") && atoi(getenv("DSOCR_ATT_EARLY")) != 0;
-    const bool early = early_env && a.B == 1;
-    const int nsub = (ch == 64 && a.hd == 128 && !a.split) ? dec_attn_nsub(a, chunks) : 1;
-    if (nsub > 1) {
-        dim3 g((chunks + nsub - 1) / nsub, a.heads, a.B);
-#define DSOCR_DAN(NS)                                                                                   \
-        do {                                                                                            \
-            if (prerot) DSOCR_LAUNCH((dec_attn_sub_kernel<128, 64, true, NS>), g, dim3(256), 0, s, a);      \
-            else DSOCR_LAUNCH((dec_attn_sub_kernel<128, 64, false, NS>), g, dim3(256), 0, s, a);            \
-        } while (0)
-        if (nsub == 2) DSOCR_DAN(2); else DSOCR_DAN(4);
-#undef DSOCR_DAN
-        return;
-    }
     dim3 g1(chunks, a.heads, a.B);
-    // polling merge (no ticket): 64-key chunks of 128-dim heads, <= 24 chunks (one load round trip in
-    // the merge), a give-up flag, a sentinel-filled record buffer (DSOCR_ATT_POLL=0: the ticket)
-    static const bool poll_env = !(getenv("DSOCR_ATT_POLL") && atoi(getenv("DSOCR_ATT_POLL")) == 0);
-    if (poll_env && a.err && ch == 64 && a.hd == 128 && chunks <= 24 && !a.split && !early) {
-        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<128, 64, true, false, true>), g1, dim3(256), 0, s, a);
-        else DSOCR_LAUNCH((dec_attn_kernel<128, 64, false, false, true>), g1, dim3(256), 0, s, a);
+    // polling merge (no ticket): 128-dim heads, <= 24 chunks (one load round trip in the merge), a
+    // give-up flag, a sentinel-filled record buffer; otherwise the arrival ticket
+    if (a.err && a.hd == 128 && chunks <= 24) {
+        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<128, true, true>), g1, dim3(256), 0, s, a);
+        else DSOCR_LAUNCH((dec_attn_kernel<128, false, true>), g1, dim3(256), 0, s, a);
         return;
     }
-#define DSOCR_DA(HDV, CHV)                                                                          \
-    do {                                                                                             \
-        if (prerot && early) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true, true>), g1, dim3(256), 0, s, a);  \
-        else if (prerot) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, true, false>), g1, dim3(256), 0, s, a);     \
-        else if (early) DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, false, true>), g1, dim3(256), 0, s, a);      \
-        else DSOCR_LAUNCH((dec_attn_kernel<HDV, CHV, false, false>), g1, dim3(256), 0, s, a);                \
+#define DSOCR_DA(HDV)                                                                                         \
+    do {                                                                                                       \
+        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<HDV, true, false>), g1, dim3(256), 0, s, a);                \
+        else DSOCR_LAUNCH((dec_attn_kernel<HDV, false, false>), g1, dim3(256), 0, s, a);                      \
     } while (0)
-    if (ch == 64) {
-        if (a.hd == 128) DSOCR_DA(128, 64); else if (a.hd == 64) DSOCR_DA(64, 64); else DSOCR_DA(32, 64);
-    } else {
-        if (a.hd == 128) DSOCR_DA(128, 32); else if (a.hd == 64) DSOCR_DA(64, 32); else DSOCR_DA(32, 32);
-    }
+    if (a.hd == 128) DSOCR_DA(128); else if (a.hd == 64) DSOCR_DA(64); else DSOCR_DA(32);
 #undef DSOCR_DA
 }
 
@@ -2318,42 +1764,22 @@ __global__ __launch_bounds__(256) void moe_gateup2_kernel(MoeDec2Args a) {
 // in-order vmcnt accounting stays exact (activation loads -> [routing] -> weight stream ->
 // stage -> FMA).  Blocks [0, T*topk*units_r) are (token, pick) slots that route themselves;
 // the rest are the shared experts over all T tokens (MT >= T).
-// FUSED: the block is a producer inside moe_fused_slot_kernel: every store of h (and of the
-// picks) is write-through (sc1) so the down blocks of the same launch can read it (Guideline 16 R1).
-template <typename WT, int MT, bool FUSED, int RB = 2>
+template <typename WT, int MT, int RB = 2>
 __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int bid, float* smem) {
     __shared__ int sel_e;
     __shared__ float sel_w;
     constexpr int U = 3, XR = 2;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
-    // dev stamps: [0] wall clock (100 MHz) at entry, [1..7] shader clock at phase points
-#define GU_STAMP(i)                                                                          \
-    if (a.stamps && threadIdx.x == 0) {                                                      \
-        if ((i) == 0) a.stamps[(long)bid * 8] = __builtin_amdgcn_s_memrealtime();            \
-        a.stamps[(long)bid * 8 + 1 + (i)] = __builtin_amdgcn_s_memtime();                    \
-    }
-    GU_STAMP(0);
     const bool routed = bid < a.slots * units_r;
     if (!routed && !a.sWgu) return;
     const int sl = routed ? bid / units_r : 0;
     const int t = sl / max(1, a.topk), k = sl % max(1, a.topk);
     const int u = routed ? bid % units_r : bid - a.slots * units_r;
     const int M = routed ? 1 : a.T;
-    int e_pre = 0;
-    float w_pre = 1.f;
-    const bool pre = routed && !a.logits;  // routed by dec_router: ids / aw already in memory
-    if (pre) {  // first in the vmcnt queue: the weight stream waits only for this load
-        e_pre = a.ids[sl];
-        w_pre = a.aw[sl];
-    }
     XRegs<MT, XR> xr;
     xload<MT, XR>(xr, a.x + (routed ? (long)t * a.K : 0L), a.K, nullptr, M, a.K, a.norm_w);
-    if (pre) {
-    } else if (routed && (a.dbg & 1)) {
-        if (threadIdx.x == 0) { sel_e = sl % a.E; sel_w = 1.f; }
-        __syncthreads();
-    } else if (routed) {
+    if (routed) {
         if (wave == 0) {
             int e;
             float v, wsum;
@@ -2364,21 +1790,15 @@ __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int
                 sel_e = e;
                 sel_w = v;
                 if (u == 0) {
-                    if (FUSED) {
-                        __hip_atomic_store(a.ids_out + sl, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(a.w_out + sl, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } else {
-                        a.ids_out[sl] = e;
-                        a.w_out[sl] = v;
-                    }
+                    a.ids_out[sl] = e;
+                    a.w_out[sl] = v;
                 }
             }
         }
         __syncthreads();
     }
-    GU_STAMP(1);
     const int rows_I = routed ? a.I : a.Is;
-    const int e_sel = pre ? e_pre : sel_e;
+    const int e_sel = sel_e;
     const WT* Wg = routed ? reinterpret_cast<const WT*>(a.Wgu) + (long)e_sel * 2 * a.I * a.K
                           : reinterpret_cast<const WT*>(a.sWgu);
     const WT* Wu = Wg + (long)rows_I * a.K;
@@ -2393,18 +1813,11 @@ __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int
         for (int r = 0; r < RB; ++r) {
             const int i = min(i0 + r, rows_I - 1);
             const int cc = min(c, chunks - 1);
-            if (a.dbg & 2) {
-                qg[uu][r] = make_uint4(cc, i, 0u, 0u);
-                qu[uu][r] = make_uint4(i, cc, 0u, 0u);
-            } else {
-                qg[uu][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
-                qu[uu][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
-            }
+            qg[uu][r] = ldg_nt16(Wg + (long)i * a.K + (cc << 3));
+            qu[uu][r] = ldg_nt16(Wu + (long)i * a.K + (cc << 3));
         }
     }
-    GU_STAMP(2);
-    xstage<MT, XR>(xr, M, a.K, a.norm_w != nullptr && !(a.dbg & 4), a.eps, smem);
-    GU_STAMP(3);
+    xstage<MT, XR>(xr, M, a.K, a.norm_w != nullptr, a.eps, smem);
     if (!active) return;
     const float* xs = smem + XS_RED;
     float ag[RB][MT], au[RB][MT];
@@ -2415,7 +1828,7 @@ __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int
 #pragma unroll
     for (int uu = 0; uu < U; ++uu) {
         const int c = uu * 64 + lane;
-        if (c >= chunks || (a.dbg & 8)) continue;
+        if (c >= chunks) continue;
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             float wg[8], wu[8];
@@ -2435,8 +1848,7 @@ __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int
             }
         }
     }
-    GU_STAMP(4);
-    const float scale = routed ? (pre ? w_pre : sel_w) : 1.f;
+    const float scale = routed ? sel_w : 1.f;
     float* hout = routed ? a.h + (long)sl * a.I : a.hs;
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -2448,25 +1860,22 @@ __device__ __forceinline__ void gateup_slot_body(const MoeDec2Args& a, const int
             if (lane == 0 && m < M && i < rows_I) {
                 float hv = (gs / (1.0f + expf(-gs))) * us;  // silu (candle: x / (1 + exp(-x)))
                 if (routed) hv = hv * scale;
-                if (FUSED) __hip_atomic_store(hout + (long)m * rows_I + i, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else hout[(long)m * rows_I + i] = hv;
+                hout[(long)m * rows_I + i] = hv;
             }
         }
-    GU_STAMP(5);
-#undef GU_STAMP
 }
 
 template <typename WT, int MT>
 __global__ __launch_bounds__(256) void moe_gateup_slot_kernel(MoeDec2Args a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    gateup_slot_body<WT, MT, false>(a, blockIdx.x, smem);
+    gateup_slot_body<WT, MT>(a, blockIdx.x, smem);
 }
 // the shared-expert blocks of the slot grid on their own (bid offset past the routed slots), so the
 // routed launch carries single-token registers and LDS (B > 1: MT = T only where it is needed)
 template <typename WT, int MT, int RB>
 __global__ __launch_bounds__(256) void moe_gateup_shared_kernel(MoeDec2Args a, int bid0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    gateup_slot_body<WT, MT, false, RB>(a, bid0 + blockIdx.x, smem);
+    gateup_slot_body<WT, MT, RB>(a, bid0 + blockIdx.x, smem);
 }
 
 // ------------------------------------------------------------------ MoE down + combine + residual
@@ -2580,13 +1989,8 @@ __global__ __launch_bounds__(256) void moe_down2_kernel(MoeDec2Args a) {
 // Slot-mode down (T <= 8, topk = KT at compile time, I <= 1024, Is <= 2048): per token,
 // activations -> registers, every routed + shared weight load, then LDS staging and FMAs;
 // straight-line so each consumer waits only for the loads it needs.
-// FUSED: the block is a consumer inside moe_fused_slot_kernel: it routes itself (the same
-// greedy top-k as the gate/up blocks) so its weight loads go out before h exists, then waits
-// for every gate/up block's arrival and reads h with sc1 loads only (no acquire needed:
-// MI355X_MICROARCH.md, hand-offs with sc1 loads in place of the acquire).
-template <typename WT, int KT, bool FUSED>
+template <typename WT, int KT>
 __device__ __forceinline__ void down_slot_body(const MoeDec2Args& a, const int bid, float* hsm) {
-    __shared__ int ids_s[8 * KT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = bid * 4 + wave;
     const bool active = j < a.Hout;
@@ -2596,54 +2000,27 @@ __device__ __forceinline__ void down_slot_body(const MoeDec2Args& a, const int b
     const WT* Ws = a.sWd ? reinterpret_cast<const WT*>(a.sWd) + (long)jj * a.Is
                          : reinterpret_cast<const WT*>(a.Wd) + (long)jj * a.I;
     const int cs_max = a.sWd ? ch_s - 1 : ch_r - 1;
-    if (FUSED) {
-        // picks of every token (wave t routes token t), then every weight load, then the wait
-        __shared__ float w_s[8 * KT];
-        if (wave < a.T)
-            topk_write(a.logits + (long)wave * a.E, a.E, KT, a.softmax_scoring, a.norm_topk, a.scaling,
-                       ids_s + wave * KT, w_s + wave * KT);
-        __syncthreads();
-    }
-    // h of the fused launch is read with sc1 buffer loads (bypass the non-coherent L1)
-    const auto hr_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.h, (short)0, a.T * KT * a.I * 4, 0x00020000);
-    const auto hs_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.sWd ? a.hs : a.h, (short)0,
-                                                           a.sWd ? a.T * a.Is * 4 : a.T * KT * a.I * 4, 0x00020000);
     for (int t = 0; t < a.T; ++t) {
         // slot rows t*KT .. t*KT+KT-1 of h are contiguous: [KT*I routed | Is shared] as one vector
         const float* hr = a.h + (long)t * KT * a.I;
         const float* hsh = a.sWd ? a.hs + (long)t * a.Is : hr;
         f32x4 hreg[DN_HREG];  // native vector type: a float4 struct array stays in scratch here
-        if (!FUSED) {
 #pragma unroll
-            for (int r = 0; r < DN_HREG; ++r) {
-                const int f = min(tid + r * 256, n4 - 1);
-                const float* src = f < nr4 ? hr + f * 4 : hsh + (f - nr4) * 4;
-                hreg[r] = *reinterpret_cast<const f32x4*>(src);
-            }
+        for (int r = 0; r < DN_HREG; ++r) {
+            const int f = min(tid + r * 256, n4 - 1);
+            const float* src = f < nr4 ? hr + f * 4 : hsh + (f - nr4) * 4;
+            hreg[r] = *reinterpret_cast<const f32x4*>(src);
         }
         uint4 qr[KT][2], qs[4];
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-            const int e = FUSED ? ids_s[t * KT + k] : a.ids[t * KT + k];
+            const int e = a.ids[t * KT + k];
             const WT* Wd = reinterpret_cast<const WT*>(a.Wd) + ((long)e * a.Hout + jj) * a.I;
 #pragma unroll
             for (int uu = 0; uu < 2; ++uu) qr[k][uu] = ldg_nt16(Wd + (min(uu * 64 + lane, ch_r - 1) << 3));
         }
 #pragma unroll
         for (int uu = 0; uu < 4; ++uu) qs[uu] = ldg_nt16(Ws + (min(uu * 64 + lane, cs_max) << 3));
-        if (FUSED) {
-            if (t == 0) {  // every gate/up block of this launch has stored its h rows
-                if (tid == 0) wait_arrivals(a.sync, a.sync_target, a.err);
-                __syncthreads();
-            }
-#pragma unroll
-            for (int r = 0; r < DN_HREG; ++r) {
-                const int f = min(tid + r * 256, n4 - 1);
-                const u32x4 bits = f < nr4 ? __builtin_amdgcn_raw_buffer_load_b128(hr_rsrc, (t * nr4 + f) * 16, 0, 16)
-                                           : __builtin_amdgcn_raw_buffer_load_b128(hs_rsrc, (t * ns4 + f - nr4) * 16, 0, 16);
-                __builtin_memcpy(&hreg[r], &bits, 16);
-            }
-        }
         __syncthreads();  // previous token's rows consumed (unconditional: keeps hreg in VGPRs)
 #pragma unroll
         for (int r = 0; r < DN_HREG; ++r)  // LDS holds 256*DN_HREG float4: no bounds branch
@@ -2686,27 +2063,7 @@ __device__ __forceinline__ void down_slot_body(const MoeDec2Args& a, const int b
 template <typename WT, int KT>
 __global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
-    down_slot_body<WT, KT, false>(a, blockIdx.x, hsm);
-}
-
-// One launch for the whole decode MoE of a layer (slot mode): blocks [0, NG) are the gate/up
-// blocks (producers of h), blocks [NG, NG + ND) the down blocks.  Producers have the lower
-// block ids, so a resident down block only ever waits for blocks dispatched before it.
-template <typename WT, int MT, int KT>
-__global__ __launch_bounds__(256) void moe_fused_slot_kernel(MoeDec2Args a, int NG) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int bid = blockIdx.x;
-    if (bid < NG) {
-        gateup_slot_body<WT, MT, true>(a, bid, smem);
-        // R1 publish: every storing wave drains its sc1 stores, then ONE lane counts the block
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(a.sync + (bid % SYNC_SHARDS) * SYNC_STRIDE, 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        down_slot_body<WT, KT, true>(a, bid - NG, smem);
-    }
+    down_slot_body<WT, KT>(a, blockIdx.x, hsm);
 }
 
 // ------------------------------------------------------------------ decode gate/up, T = 1 (mix)
@@ -2760,8 +2117,9 @@ __device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int so
     w_out = v;
 }
 
-template <typename WT, int RB = 2>
+template <typename WT>
 __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn) {
+    constexpr int RB = 1;  // one gate + up row pair per wave (66 VGPRs: the 1792-block grid is resident at once)
     WaveSpan span_(a.span);
     __shared__ __attribute__((aligned(16))) float rank_lds[4][64];
     constexpr int U = 3;  // K <= 1536
@@ -2846,16 +2204,17 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
     }
 }
 
-// Decode down + combine + residual for one token (T = 1), split-K over the block's 4 waves:
+// Decode down + combine + residual for one token (T = 1), split-K over the block's NW = 8 waves:
 // the K axis [topk routed h rows (I each, slot order, w_k already folded) | shared h (Is)] is
-// cut in 4 contiguous chunk ranges, wave w owns one for the block's RPB output rows, its h
-// values come straight from L2 into registers (no block barrier before the FMAs); the 4 wave
-// partials meet once in LDS and x[j] += (p0 + p1) + (p2 + p3).
-template <typename WT, int RPB, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void moe_down_mix_kernel(MoeDec2Args a) {
+// cut in 8 contiguous chunk ranges, wave w owns one for the block's RPB = 2 output rows, its h
+// values come straight from L2 into registers (no block barrier before the FMAs); the 8 wave
+// partials meet once in LDS and x[j] += ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)).
+template <typename WT>
+__global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
+    constexpr int RPB = 2, NW = 8;
     WaveSpan span_(a.span);
     __shared__ float part[NW][RPB];
-    constexpr int U = 16 / NW;  // chunks per lane: (topk * I + Is) / 8 / NW waves <= 64 U
+    constexpr int U = 16 / NW;  // chunks per lane: (topk * I + Is) / 8 / NW waves <= 64 U (= 2)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int j0 = blockIdx.x * RPB;
     const int cpi = a.I >> 3, cps = a.sWd ? (a.Is >> 3) : 0;
@@ -2913,9 +2272,7 @@ __global__ __launch_bounds__(64 * NW) void moe_down_mix_kernel(MoeDec2Args a) {
     __syncthreads();
     if (threadIdx.x < RPB && j0 + threadIdx.x < a.Hout) {
         const int r = threadIdx.x;
-        float v;
-        if constexpr (NW == 4) v = (part[0][r] + part[1][r]) + (part[2][r] + part[3][r]);
-        else v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) + ((part[4][r] + part[5][r]) + (part[6][r] + part[7][r]));
+        const float v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) + ((part[4][r] + part[5][r]) + (part[6][r] + part[7][r]));
         float* xp = a.out + j0 + r;
         *xp = *xp + v;
     }
@@ -2923,28 +2280,17 @@ __global__ __launch_bounds__(64 * NW) void moe_down_mix_kernel(MoeDec2Args a) {
 
 bool moe_down_mix_ok(const MoeDec2Args& a) {
     const int nch = a.topk * (a.I >> 3) + (a.sWd ? (a.Is >> 3) : 0);
-    return a.slot_mode && a.T == 1 && !a.apos && a.I % 8 == 0 && (!a.sWd || a.Is % 8 == 0) && (nch + 3) / 4 <= 256 &&
+    return a.slot_mode && a.T == 1 && !a.apos && a.I % 8 == 0 && (!a.sWd || a.Is % 8 == 0) && (nch + 7) / 8 <= 128 &&
            a.ids;
 }
 
 void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s) {
     if (!moe_down_mix_ok(a)) throw std::runtime_error("EINVAL: moe_down_mix outside its range");
-    static const int rpb = getenv("DSOCR_DN_RPB") ? atoi(getenv("DSOCR_DN_RPB")) : 2;  // 2: measured best
-    // 8 waves of 2 chunks per lane (50 VGPRs, 8 waves per SIMD) instead of 4 of 4 (84 VGPRs): shorter
-    // per-wave load chains, 6.49 -> 6.01 us; DSOCR_DN_NW8=0 for the 4-wave kernel (A/B)
-    static const bool nw8 = !(getenv("DSOCR_DN_NW8") && atoi(getenv("DSOCR_DN_NW8")) == 0) && rpb == 2;
-    if (nw8) {
-        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_down_mix_kernel<bf16_t, 2, 8>), dim3((a.Hout + 1) / 2), dim3(512), 0, s, a);
-        else DSOCR_LAUNCH((moe_down_mix_kernel<f16_t, 2, 8>), dim3((a.Hout + 1) / 2), dim3(512), 0, s, a);
-        return;
-    }
-#define DSOCR_DM(WTY, R) DSOCR_LAUNCH((moe_down_mix_kernel<WTY, R>), dim3((a.Hout + R - 1) / R), dim3(256), 0, s, a)
-    if (a.wdtype == WDT_BF16) {
-        if (rpb == 4) DSOCR_DM(bf16_t, 4); else if (rpb == 1) DSOCR_DM(bf16_t, 1); else DSOCR_DM(bf16_t, 2);
-    } else {
-        if (rpb == 4) DSOCR_DM(f16_t, 4); else if (rpb == 1) DSOCR_DM(f16_t, 1); else DSOCR_DM(f16_t, 2);
-    }
-#undef DSOCR_DM
+    // 8 waves of 2 chunks per lane (50 VGPRs, 8 waves per SIMD) beat 4 of 4 (84 VGPRs): shorter per-wave
+    // load chains, 6.49 -> 6.01 us; 2 output rows per block
+    const dim3 grid((a.Hout + 1) / 2);
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_down_mix_kernel<bf16_t>), grid, dim3(512), 0, s, a);
+    else DSOCR_LAUNCH((moe_down_mix_kernel<f16_t>), grid, dim3(512), 0, s, a);
 }
 
 bool moe_gateup_mix_ok(const MoeDec2Args& a) {
@@ -2954,46 +2300,12 @@ bool moe_gateup_mix_ok(const MoeDec2Args& a) {
 
 void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s) {
     if (!moe_gateup_mix_ok(a) || !xn) throw std::runtime_error("EINVAL: moe_gateup_mix outside its range");
-    // rows per wave: 1 (66 VGPRs, 7 waves per SIMD: the 1792-block grid is resident at once) — gate/up
-    // 9.46 -> 8.73 us, 3.47 -> 3.55 pages/s against 2 rows (98 / 90 VGPRs); DSOCR_GU_RB=2 for A/B
-    static const int RB = getenv("DSOCR_GU_RB") && atoi(getenv("DSOCR_GU_RB")) == 2 ? 2 : 1;
-    const int n_sh = a.sWgu ? (a.Is + RB - 1) / RB : 0;
-    const int n_rt = a.topk * ((a.I + RB - 1) / RB);
+    // one gate + up row pair per wave: 9.46 -> 8.73 us against two (98 / 90 VGPRs), 3.47 -> 3.55 pages/s
+    const int n_sh = a.sWgu ? a.Is : 0;
+    const int n_rt = a.topk * a.I;
     dim3 grid(std::max(n_sh, (n_rt + 2) / 3));
-    if (RB == 1) {
-        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t, 1>), grid, dim3(256), 0, s, a, xn);
-        else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t, 1>), grid, dim3(256), 0, s, a, xn);
-    } else {
-        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t, 2>), grid, dim3(256), 0, s, a, xn);
-        else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t, 2>), grid, dim3(256), 0, s, a, xn);
-    }
-}
-
-bool moe_fused_ok(const MoeDec2Args& a) {
-    const long n4 = (long)a.topk * (a.I / 4) + (a.sWd ? a.Is / 4 : 0);
-    return a.slot_mode && a.logits && a.T <= 2 && a.K <= 64 * 3 * 8 && (a.topk == 6 || a.topk == 3) &&
-           a.I <= 1024 && (!a.sWd || a.Is <= 2048) && n4 <= 256L * DN_HREG && a.sync && a.err;
-}
-
-void launch_moe_fused(const MoeDec2Args& a, hipStream_t s) {
-    if (!moe_fused_ok(a)) throw std::runtime_error("EINVAL: fused decode MoE outside its slot-mode range");
-    constexpr int RB = 2;
-    const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
-    const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
-    const int NG = a.slots * units_r + units_s;
-    const int ND = (a.Hout + 3) / 4;
-    MoeDec2Args b = a;
-    b.sync_target = NG;
-    const size_t lds = std::max(stage_bytes(a.T == 1 ? 1 : 2, a.K), (size_t)256 * DN_HREG * 16);
-#define DSOCR_FU(WTY, MTV, KTV) DSOCR_LAUNCH((moe_fused_slot_kernel<WTY, MTV, KTV>), dim3(NG + ND), dim3(256), lds, s, b, NG)
-    if (a.wdtype == WDT_BF16) {
-        if (a.T == 1) { if (a.topk == 6) DSOCR_FU(bf16_t, 1, 6); else DSOCR_FU(bf16_t, 1, 3); }
-        else { if (a.topk == 6) DSOCR_FU(bf16_t, 2, 6); else DSOCR_FU(bf16_t, 2, 3); }
-    } else {
-        if (a.T == 1) { if (a.topk == 6) DSOCR_FU(f16_t, 1, 6); else DSOCR_FU(f16_t, 1, 3); }
-        else { if (a.topk == 6) DSOCR_FU(f16_t, 2, 6); else DSOCR_FU(f16_t, 2, 3); }
-    }
-#undef DSOCR_FU
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t>), grid, dim3(256), 0, s, a, xn);
+    else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t>), grid, dim3(256), 0, s, a, xn);
 }
 
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
@@ -3001,7 +2313,7 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
     const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
     dim3 grid(a.slots * units_r + units_s);
-    if (a.slot_mode && a.K <= 64 * 3 * 8 && a.T > 2 && a.T <= 8 && !(getenv("DSOCR_SLOT_ONE") && atoi(getenv("DSOCR_SLOT_ONE")))) {
+    if (a.slot_mode && a.K <= 64 * 3 * 8 && a.T > 2 && a.T <= 8) {
         // routed slots (one token each) with MT = 1, then the shared expert over the T tokens
         MoeDec2Args r = a;
         r.sWgu = nullptr;
@@ -3014,11 +2326,8 @@ void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
             const size_t lds = stage_bytes(mt, a.K);
             MoeDec2Args sh = a;
             sh.slots = 0;
-            static const int srb = getenv("DSOCR_SHARED_RB") ? atoi(getenv("DSOCR_SHARED_RB")) : 1;
-            const int ns = srb == 1 ? (a.Is + 3) / 4 : units_s;
-#define DSOCR_SH(WTY, MTV) \
-    if (srb == 1) DSOCR_LAUNCH((moe_gateup_shared_kernel<WTY, MTV, 1>), dim3(ns), dim3(256), lds, s, sh, 0); \
-    else DSOCR_LAUNCH((moe_gateup_shared_kernel<WTY, MTV, 2>), dim3(ns), dim3(256), lds, s, sh, 0);
+            const int ns = (a.Is + 3) / 4;
+#define DSOCR_SH(WTY, MTV) DSOCR_LAUNCH((moe_gateup_shared_kernel<WTY, MTV, 1>), dim3(ns), dim3(256), lds, s, sh, 0);
             if (a.wdtype == WDT_BF16) {
                 if (mt == 4) { DSOCR_SH(bf16_t, 4) } else { DSOCR_SH(bf16_t, 8) }
             } else {
@@ -3326,21 +2635,17 @@ void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ decode MoE layer dispatch
-static bool env_flag(const char* name, bool dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) != 0 : dflt;
-}
 
 namespace {
 struct MoePlan {
     MoeDec2Args m;
     DecGemvArgs router;
     int mode = 0;  // 0 mix (T = 1), 1 slot (T <= 2), 2 grouped (3..8), 3 sorted (T > 8)
-    bool epi = false, mix_dn = false;
-    bool route1 = false;  // grouped mode: dec_route_grp (norm + router + top-k + records, one block)
+    bool mix_dn = false;  // one token: the split-K down (moe_down_mix)
+    bool route1 = false;  // grouped mode: dec_route_grp (norm + router + top-k + records, one launch);
+                          // else dec_router's last-block epilogue writes the records
     bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
     bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
-    bool gu_mix_mm = false;  // one token: gate/up on the matrix cores (moe_gateup_mix_mm)
 };
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
@@ -3348,13 +2653,8 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     if (T <= 0 || TK > 512 || E > 256 || K > 8 || K > E)
         throw std::runtime_error("EINVAL: decode MoE supports batch*top_k <= 512, <= 256 experts, top_k <= min(8, E)");
     if (a.H % 8 || a.I % 8 || (a.Is && a.Is % 8)) throw std::runtime_error("EINVAL: MoE dims must be multiples of 8");
-    // experiment switches, read per plan (host-side, once per layer when a step is captured)
-    const bool router_epi = env_flag("DSOCR_ROUTER_EPI", false);
-    const bool gu_mix = env_flag("DSOCR_GU_MIX", true);
-    const bool dn_mix = env_flag("DSOCR_DN_MIX", true);
-    const bool grouped = env_flag("DSOCR_MOE_GRP", true);
     MoePlan p;
-    const bool fuse_norm = T <= 2;  // T > 2: the rows are normalised once (launch_rmsnorm into xn)
+    const bool fuse_norm = T <= 2;  // T > 2: the rows are normalised once (by the router launch, into xn)
     const float* mx = (fuse_norm || !a.norm_w) ? a.x : a.xn;
     const float* mnorm = fuse_norm ? a.norm_w : nullptr;
     MoeDec2Args& m = p.m;
@@ -3366,35 +2666,24 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     DecGemvArgs& gr = p.router;
     gr.M = T; gr.N = E; gr.K = a.H; gr.x = mx; gr.ldx = a.H; gr.W = a.router; gr.ldw = a.H; gr.wdtype = a.router_wdt;
     gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps;
-    const bool rt_ok = dec_router_ok(T, E, a.H, K) && a.route_cnt;
-    if (T >= 3 && T <= 8 && grouped && rt_ok && a.grp) {
+    if (T >= 3 && T <= 8 && dec_router_ok(T, E, a.H, K) && a.route_cnt && a.grp) {
         p.mode = 2;
         m.slot_mode = 1; m.slots = TK; m.grp = a.grp; m.aw = a.wts;
         if (!moe_grp_ok(m)) p.mode = 1;
     }
     if (p.mode == 2) {
-        p.epi = true;
-        p.route1 = env_flag("DSOCR_ROUTE1", true) && a.route_cnt && dec_route_grp_ok(T, E, a.H, K);
-        p.gu_mm = env_flag("DSOCR_MOE_MM", true) && moe_gateup_mm_ok(m);
-        p.dn_mm = env_flag("DSOCR_MOE_MM", true) && env_flag("DSOCR_DN_MM", true) && moe_down_mm_ok(m);
+        p.route1 = dec_route_grp_ok(T, E, a.H, K);
+        p.gu_mm = moe_gateup_mm_ok(m);
+        p.dn_mm = moe_down_mm_ok(m);
     } else if (T <= 8) {
+        // every gate/up block routes itself from the router logits (rank / serial greedy top-k)
         m.grp = nullptr;
         m.slot_mode = 1; m.slots = TK;
-        if (router_epi && rt_ok) {
-            // routed by dec_router's last-block epilogue (measured +1.6 us / layer on MI355X at T = 1
-            // vs self-routing: the write-through + ticket hand-off costs more than it saves)
-            p.epi = true; m.logits = nullptr; m.aw = a.wts;
-        } else {
-            // every gate/up block routes itself from the router logits
-            m.logits = a.logits; m.softmax_scoring = a.softmax_scoring; m.norm_topk = a.norm_topk;
-            m.scaling = a.scaling; m.ids_out = a.ids; m.w_out = a.wts;
-        }
-        p.mode = (gu_mix && fuse_norm && moe_gateup_mix_ok(m) && a.xn_router) ? 0 : 1;
+        m.logits = a.logits; m.softmax_scoring = a.softmax_scoring; m.norm_topk = a.norm_topk;
+        m.scaling = a.scaling; m.ids_out = a.ids; m.w_out = a.wts;
+        p.mode = (fuse_norm && moe_gateup_mix_ok(m) && a.xn_router) ? 0 : 1;
         if (p.mode == 0) gr.xn_out = a.xn_router;  // the router hands its normalised row to gate/up
-        // one-token gate/up on the matrix cores: equal to moe_gateup_mix on MI355X (9.7 us both, tools/kbench
-        // moe1: the routing round trip and the staging barrier eat the coalescing gain) -> off by default
-        p.gu_mix_mm = p.mode == 0 && env_flag("DSOCR_MIX_MM", false) && moe_gateup_mix_mm_ok(m);
-        p.mix_dn = dn_mix && moe_down_mix_ok(m);
+        p.mix_dn = moe_down_mix_ok(m);
     } else {
         p.mode = 3;
         if (!(a.eoff && a.arow && a.apos && a.active && a.n_active && a.aw))
@@ -3410,7 +2699,7 @@ void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const 
     const MoePlan p = moe_plan(a);
     const char* gu = "moe_gateup2_kernel";
     const char* dn = "moe_down2_kernel";
-    if (p.mode == 0) gu = p.gu_mix_mm ? "moe_gateup_mix_mm_kernel" : "moe_gateup_mix_kernel";
+    if (p.mode == 0) gu = "moe_gateup_mix_kernel";
     else if (p.mode == 1) gu = (a.T > 2 && a.Is) ? "moe_gateup_slot_kernel+moe_gateup_shared_kernel" : "moe_gateup_slot_kernel";
     else if (p.mode == 2) gu = p.gu_mm ? "moe_gateup_mm_kernel" : "moe_gateup_grp_kernel";
     if (p.mode == 2) dn = p.dn_mm ? "moe_down_mm_kernel" : "moe_down_grp_kernel";
@@ -3432,11 +2721,10 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
         launch_dec_route_grp(g, re, s);
     } else if (parts & MOE_ROUTE) {
         if (a.T > 2 && a.norm_w) launch_rmsnorm(a.x, a.H, a.xn, a.H, a.T, a.H, a.norm_w, a.eps, s);
-        if (p.epi) {
+        if (p.mode == 2) {
             DecRouteEpi re;
             re.topk = a.topk; re.softmax_scoring = a.softmax_scoring; re.norm_topk = a.norm_topk;
-            re.scaling = a.scaling; re.ids = a.ids; re.w = a.wts; re.counter = a.route_cnt;
-            if (p.mode == 2) re.grp = a.grp;
+            re.scaling = a.scaling; re.ids = a.ids; re.w = a.wts; re.counter = a.route_cnt; re.grp = a.grp;
             launch_dec_router(p.router, re, s);
         } else {
             launch_dec_gemv(p.router, s);
@@ -3450,10 +2738,7 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
         }
     }
     if (parts & MOE_GATEUP) {
-        if (const char* sp = getenv("DSOCR_MOE_STAMPS"))  // dev: per-block phase clocks (profile only)
-            const_cast<MoeDec2Args&>(m).stamps = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(sp, nullptr, 10));
-        if (p.mode == 0 && p.gu_mix_mm) launch_moe_gateup_mix_mm(m, a.xn_router, s);
-        else if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
+        if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
         else if (p.mode == 2 && p.gu_mm) launch_moe_gateup_mm(m, s);
         else if (p.mode == 2) launch_moe_gateup_grp(m, s);
         else launch_moe_gateup2(m, s);

@@ -315,26 +315,19 @@ static void mm_launch(const DecGemvArgs& a, hipStream_t s) {
     DSOCR_LAUNCH((dec_mm_kernel<WT, WR, WK, PF, Q, NORM, SWZ>), dim3(blocks), dim3(64 * WR * WK), lds, s, a);
 }
 
-// block shapes (K steps of 32 a multiple of 40: per-wave batches divide evenly); DSOCR_MM_CFG
-// (experiments) forces one: 0 = WR 8 persistent, 1 = WK 8, 2 = WK 4, 3 = WR 4 persistent,
-// 4 = WR 8 persistent with Q 5 (k-permuted A: measured 2x slower — keep Q 1)
+// block shapes (K steps of 32 a multiple of 40: per-wave batches divide evenly): WR 8 persistent for the
+// large-N head, WK 8 (K split over 8 waves) otherwise (measured: WK 4, WR 4 persistent and a k-permuted A
+// fragment order were slower)
 template <typename WT, bool NORM>
 static void mm_dispatch(const DecGemvArgs& a, hipStream_t s) {
-    static const int cfg_env = getenv("DSOCR_MM_CFG") ? atoi(getenv("DSOCR_MM_CFG")) : -1;
     if (a.w_swz) {  // fragment-ordered weights (the lm_head's B > 2 copy)
         DecGemvArgs b = a;
         b.W = a.w_swz;
         mm_launch<WT, 8, 1, 10, 1, NORM, true>(b, s);
         return;
     }
-    const int cfg = cfg_env >= 0 ? cfg_env : (a.N >= 16384 ? 0 : 1);
-    switch (cfg) {
-        case 0: mm_launch<WT, 8, 1, 10, 1, NORM>(a, s); break;
-        case 2: mm_launch<WT, 1, 4, 10, 1, NORM>(a, s); break;
-        case 3: mm_launch<WT, 4, 1, 10, 1, NORM>(a, s); break;
-        case 4: mm_launch<WT, 8, 1, 10, 5, NORM>(a, s); break;
-        default: mm_launch<WT, 1, 8, 5, 1, NORM>(a, s); break;
-    }
+    if (a.N >= 16384) mm_launch<WT, 8, 1, 10, 1, NORM>(a, s);
+    else mm_launch<WT, 1, 8, 5, 1, NORM>(a, s);
 }
 
 // W [N][K] row-major -> fragment order [N/16 tiles][K/32 steps][64 lanes][8]: lane l of step t of tile
@@ -390,9 +383,6 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     __shared__ float scl[MM_MT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 15, g = lane >> 4;
-#define GM_STAMP(i) \
-    if (a.stamps && lane == 0) a.stamps[((long)blockIdx.x * NWV + wave) * 4 + (i)] = __builtin_amdgcn_s_memrealtime();
-    GM_STAMP(0);
     const int tiles_r = a.I >> 4, tiles_s = a.sWgu ? a.Is >> 4 : 0;
     const int n_units = tiles_s + a.grp[0] * tiles_r;
     const int steps = a.K >> 5, nch = steps / PF;
@@ -453,7 +443,6 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     const int KP = mm_pitch(a.K);
     if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
     __syncthreads();
-    GM_STAMP(1);
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
     f32x4 accg = {0.f, 0.f, 0.f, 0.f}, accu = {0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const frag(&fg)[PF], const frag(&fu)[PF], int c) {
@@ -514,11 +503,8 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
 #pragma unroll
             for (int i = 0; i < PF; ++i) { ga[i] = gb[i]; ua[i] = ub[i]; }
         }
-        if (unit == blockIdx.x + gridDim.x * wave) GM_STAMP(2);  // first unit done
         first = false;
     }
-    GM_STAMP(3);
-#undef GM_STAMP
 }
 
 bool moe_gateup_mm_ok(const MoeDec2Args& a) {
@@ -712,21 +698,12 @@ size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H) {
     return (size_t)(std::min(E, T * topk) + (I > 0 && Is > 0 ? Is / I : 0)) * MM_MT * H;
 }
 
-// Units of 64 output rows (4 waves) by default: 17 segments x 20 row tiles = 340 blocks at 8 pages,
-// where 128-row units (8 waves) left a third of the CUs idle (170 blocks); DSOCR_DOWN_RT=128 restores them.
+// Units of 64 output rows (4 waves): 17 segments x 20 row tiles = 340 blocks at 8 pages, where 128-row
+// units (8 waves) left a third of the CUs idle (170 blocks).
 void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s) {
     if (!moe_down_mm_ok(a)) throw std::runtime_error("EINVAL: grouped decode down (matrix cores) outside its range");
     const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.I);
     const int max_seg = std::min(a.E, a.T * a.topk) + (a.sWd ? a.Is / a.I : 0);
-    static const bool rt128 = getenv("DSOCR_DOWN_RT") && atoi(getenv("DSOCR_DOWN_RT")) == 128;
-    if (rt128) {
-        dim3 grid(max_seg * (a.Hout / 128));
-#define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 8>), grid, dim3(512), lds, s, a)
-        if (a.wdtype == WDT_BF16) { if (a.Wd_swz) DSOCR_DM(bf16_t, true); else DSOCR_DM(bf16_t, false); }
-        else { if (a.Wd_swz) DSOCR_DM(f16_t, true); else DSOCR_DM(f16_t, false); }
-#undef DSOCR_DM
-        return;
-    }
     dim3 grid(max_seg * (a.Hout / 64));
 #define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 4>), grid, dim3(256), lds, s, a)
     if (a.wdtype == WDT_BF16) { if (a.Wd_swz) DSOCR_DM(bf16_t, true); else DSOCR_DM(bf16_t, false); }
@@ -734,215 +711,6 @@ void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s) {
 #undef DSOCR_DM
 }
 
-
-// Rank form of the greedy top-k for one token (the mix kernel's topk_rank_pick, decode.hip): lane e
-// holds expert e's logit; returns pick `want`'s (expert, weight).  lds: 64 floats per block, used by
-// one wave at a time (a wave barrier orders its writes and reads; every wave computes the same
-// values, so concurrent waves write identical data).
-__device__ __forceinline__ void topk_rank_pick_mm(float logit, int E, int K, int softmax_scoring, int norm_topk,
-                                                  float scaling, int want, float* lds, int wave, int& e_out,
-                                                  float& w_out) {
-    const int lane = threadIdx.x & 63;
-    float sc;
-    if (softmax_scoring) {
-        const float v = lane < E ? logit : -INFINITY;
-        const float mx = wave_max(v);
-        const float ex = lane < E ? expf(v - mx) : 0.f;
-        const float sum = wave_sum(ex);
-        sc = lane < E ? ex / sum : -INFINITY;
-    } else {
-        sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
-    }
-    int rank = 0;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        const float o = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), j));
-        rank += (o > sc || (o == sc && j < lane)) ? 1 : 0;
-    }
-    (void)lds;
-    (void)wave;
-    if (lane >= E) rank = 1 << 20;
-    float wsum = 0.f;
-    if (K > 1 && norm_topk) {
-        for (int k = 0; k < K; ++k) {
-            const unsigned long long bm = __ballot(rank == k);
-            const int ek = __builtin_ctzll(bm);
-            wsum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), ek));
-        }
-    }
-    const unsigned long long bm = __ballot(rank == want);
-    const int ew = __builtin_ctzll(bm);
-    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), ew));
-    if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
-    if (scaling != 1.0f) v = v * scaling;
-    e_out = ew;
-    w_out = v;
-}
-
-// ------------------------------------------------------------------ decode MoE gate/up, one token
-// The single-page form of moe_gateup_mm (BASELINE configs[1]).  Units of 16 intermediate rows (gate
-// and up): the shared expert's Is/16 first, then pick k's expert, I/16 units each; a unit is one
-// 4-wave block, wave w streaming K-steps [w S/4, (w+1) S/4) of both matrices as MFMA A fragments from
-// the fragment-ordered copies, all in flight at once (20 x 1 KiB per wave).  Routed blocks select
-// their expert from the router logits first (rank form of the greedy top-k, topk_rank of the mix
-// kernel: identical picks / weights); shared blocks stream from their first instruction.  The token
-// row (the router's normalised x̂) is the B operand's column 0 as three f16 planes (power-of-two
-// scaled; other columns read a zero line); the 4 K-quarter partial tiles meet in LDS (summed in
-// order), then h = silu(g) * u (* w_k) for the unit's 16 rows.
-template <typename WT>
-__global__ __launch_bounds__(256) void moe_gateup_mix_mm_kernel(MoeDec2Args a, const float* xn) {
-    typedef typename MmT<WT>::frag frag;
-    constexpr int PQ = 10;  // K-steps per wave (K = 4 PQ * 32 = 1280)
-    __shared__ __attribute__((aligned(16))) uint16_t xp[3][1280 + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t zero16[8];
-    __shared__ f32x4 red[3][2][64];
-    __shared__ float sc_rank[64];
-    __shared__ float xmax_s[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int col = lane & 15, g = lane >> 4;
-#define MX_STAMP(i) \
-    if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();
-    MX_STAMP(0);
-    const int units_s = a.sWgu ? a.Is >> 4 : 0, units_r = a.I >> 4;
-    const int unit = blockIdx.x;
-    const bool shared = unit < units_s;
-    const int k_pick = shared ? 0 : (unit - units_s) / units_r;
-    const int t = shared ? unit : (unit - units_s) % units_r;
-    const int steps = a.K >> 5;
-    const int t0 = wave * PQ;
-    // the token row first (its loads must not queue behind the weight stream: vmcnt retires in order):
-    // the lane's three chunks for the row maximum and its chunk of this wave's K quarter
-    const int chunks = a.K >> 3;
-    float4 xr[3][2], xq[2];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-        const int c = min(u * 64 + lane, chunks - 1);
-        xr[u][0] = *reinterpret_cast<const float4*>(xn + (c << 3));
-        xr[u][1] = *reinterpret_cast<const float4*>(xn + (c << 3) + 4);
-    }
-    const int cq = wave * (chunks / 4) + min(lane, chunks / 4 - 1);  // this wave's quarter: chunks/4 = 40 chunks
-    xq[0] = *reinterpret_cast<const float4*>(xn + (cq << 3));
-    xq[1] = *reinterpret_cast<const float4*>(xn + (cq << 3) + 4);
-    // routing (routed blocks): every wave ranks the logits itself (no barrier before its loads)
-    int e = 0;
-    float wk = 1.f;
-    if (!shared) {
-        const int ln = min(lane, a.E - 1);
-        const float lg = a.logits[ln];
-        float wsel;
-        int esel;
-        topk_rank_pick_mm(lg, a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, k_pick, sc_rank, wave, esel, wsel);
-        e = esel;
-        wk = wsel;
-    }
-    const long tg = shared ? (long)t : (long)e * (2 * a.I / 16) + t;
-    const long tu = tg + (shared ? a.Is : a.I) / 16;
-    const WT* base = shared ? reinterpret_cast<const WT*>(a.sWgu_swz) : reinterpret_cast<const WT*>(a.Wgu_swz);
-    const WT* pg = base + (tg * steps + t0) * 512 + lane * 8;
-    const WT* pu = base + (tu * steps + t0) * 512 + lane * 8;
-    MX_STAMP(1);
-    frag fg[PQ], fu[PQ];
-#pragma unroll
-    for (int i = 0; i < PQ; ++i) {
-        const uint4 q0 = ldg_nt16(pg + (long)i * 512);
-        const uint4 q1 = ldg_nt16(pu + (long)i * 512);
-        __builtin_memcpy(&fg[i], &q0, 16);
-        __builtin_memcpy(&fu[i], &q1, 16);
-    }
-    float mx = 0.f;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-        if (u * 64 + lane < chunks) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float4 q = xr[u][h];
-                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
-            }
-        }
-    }
-    mx = wave_max(mx);
-    int sx = 0;
-    if (mx > 0.f) {
-        int ex;
-        (void)frexpf(mx, &ex);
-        sx = 15 - ex;
-    }
-    if (lane < chunks / 4) {
-        float v[8];
-        v[0] = xq[0].x; v[1] = xq[0].y; v[2] = xq[0].z; v[3] = xq[0].w; v[4] = xq[1].x; v[5] = xq[1].y; v[6] = xq[1].z; v[7] = xq[1].w;
-        uint16_t pb[3][8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float b0, b1, b2;
-            const float y = ldexpf(v[j], sx);
-            pb[0][j] = MmT<WT>::to_bits(y, b0);
-            const float r1 = y - b0;
-            pb[1][j] = MmT<WT>::to_bits(r1, b1);
-            const float r2 = r1 - b1;
-            pb[2][j] = MmT<WT>::to_bits(r2, b2);
-        }
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            uint4 q;
-            q.x = pb[p][0] | ((uint32_t)pb[p][1] << 16);
-            q.y = pb[p][2] | ((uint32_t)pb[p][3] << 16);
-            q.z = pb[p][4] | ((uint32_t)pb[p][5] << 16);
-            q.w = pb[p][6] | ((uint32_t)pb[p][7] << 16);
-            *reinterpret_cast<uint4*>(&xp[p][cq << 3]) = q;
-        }
-    }
-    if (tid < 8) zero16[tid] = 0;
-    __syncthreads();
-    MX_STAMP(2);
-    f32x4 accg = {0.f, 0.f, 0.f, 0.f}, accu = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < PQ; ++i) {
-        const int k = 32 * (t0 + i) + 8 * g;
-#pragma unroll
-        for (int p = 2; p >= 0; --p) {
-            const uint16_t* src = col == 0 ? &xp[p][k] : zero16;
-            const frag b = *reinterpret_cast<const frag*>(src);
-            accg = MmT<WT>::mfma(fg[i], b, accg);
-            accu = MmT<WT>::mfma(fu[i], b, accu);
-        }
-    }
-    if (wave > 0) { red[wave - 1][0][lane] = accg; red[wave - 1][1][lane] = accu; }
-    __syncthreads();
-    if (wave == 0 && col == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const f32x4 og = red[q][0][lane], ou = red[q][1][lane];
-            accg[0] += og[0]; accg[1] += og[1]; accg[2] += og[2]; accg[3] += og[3];
-            accu[0] += ou[0]; accu[1] += ou[1]; accu[2] += ou[2]; accu[3] += ou[3];
-        }
-        const float sc = ldexpf(1.f, -sx);
-        float hv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float gs = accg[i] * sc, us = accu[i] * sc;
-            const float h = (gs / (1.0f + expf(-gs))) * us;
-            hv[i] = shared ? h : h * wk;
-        }
-        float* dst = shared ? a.hs : a.h + (long)k_pick * a.I;
-        *reinterpret_cast<float4*>(dst + t * 16 + 4 * g) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-        if (!shared && t == 0 && g == 0) { a.ids_out[k_pick] = e; a.w_out[k_pick] = wk; }
-    }
-    (void)xmax_s;
-    MX_STAMP(3);
-#undef MX_STAMP
-}
-
-bool moe_gateup_mix_mm_ok(const MoeDec2Args& a) {
-    return a.T == 1 && a.slot_mode && a.logits && a.Wgu_swz && (!a.sWgu || a.sWgu_swz) && a.K == 1280 && a.E <= 64 &&
-           a.topk <= 8 && a.I % 16 == 0 && (!a.sWgu || a.Is % 16 == 0) && a.ids_out && a.w_out;
-}
-
-void launch_moe_gateup_mix_mm(const MoeDec2Args& a, const float* xn, hipStream_t s) {
-    if (!moe_gateup_mix_mm_ok(a) || !xn) throw std::runtime_error("EINVAL: single-token gate/up (matrix cores) outside its range");
-    const int units = (a.sWgu ? a.Is / 16 : 0) + a.topk * (a.I / 16);
-    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_mm_kernel<bf16_t>), dim3(units), dim3(256), 0, s, a, xn);
-    else DSOCR_LAUNCH((moe_gateup_mix_mm_kernel<f16_t>), dim3(units), dim3(256), 0, s, a, xn);
-}
 
 // ------------------------------------------------------------------ long-K projection, 3..8 tokens
 // Y[m][n] (+)= X[m] . W[n]^T (+ bias) for K too long to stage whole (the dense layer-0 down

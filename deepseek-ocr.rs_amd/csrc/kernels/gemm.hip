@@ -330,17 +330,14 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
     dim3 grid((g.N + GB_N - 1) / GB_N, (mtiles + GB_M - 1) / GB_M, g.group_off ? g.groups : 1);
     if (grid.y == 0 || grid.x == 0) return;
     // grouped (MoE prefill): the exact-f32 grouped kernel (gemm_bf16.hip) — 32-row tiles up to 256 mean
-    // rows per expert (1 page: prefill 10.1 -> 9.4 ms, 2 pages 13.4 -> 13.1), 128-row tiles above.
-    // DSOCR_GEMM_GRP=0: gemm_x3 always; =2: gemm_x3 above 256 rows (A/B comparisons)
-    static const int grp_mode = getenv("DSOCR_GEMM_GRP") ? atoi(getenv("DSOCR_GEMM_GRP")) : 1;
-    if (g.group_off && grp_mode != 0 && !(grp_mode == 2 && (long)g.M > 256L * g.groups) && gemm_f32a_grouped_ok(g)) {
+    // rows per expert (1 page: prefill 10.1 -> 9.4 ms, 2 pages 13.4 -> 13.1), 128-row tiles above
+    if (g.group_off && gemm_f32a_grouped_ok(g)) {
         launch_gemm_f32a_grouped(g, s);
         return;
     }
-    // split-bf16 MFMA path when the tiles are whole along K and the rows 16-byte aligned;
-    // DSOCR_GEMM_F32=1 forces the f32-input MFMA kernel (A/B comparisons)
-    static const bool force_f32 = getenv("DSOCR_GEMM_F32") && atoi(getenv("DSOCR_GEMM_F32"));
-    const bool x3 = !force_f32 && g.K % XB_K == 0 && g.lda % 4 == 0 && g.ldw % 8 == 0 &&
+    // split-bf16 MFMA path when the tiles are whole along K and the rows 16-byte aligned; else the
+    // f32-input kernel
+    const bool x3 = g.K % XB_K == 0 && g.lda % 4 == 0 && g.ldw % 8 == 0 &&
                     (reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.W) & 15) == 0;
     if (x3) {
         dim3 gx((g.N + XB_N - 1) / XB_N, (mtiles + XB_M - 1) / XB_M, g.group_off ? g.groups : 1);

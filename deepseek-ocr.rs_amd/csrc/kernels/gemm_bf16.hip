@@ -418,9 +418,9 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
-    static const bool w22 = getenv("DSOCR_GEMM_W22") && atoi(getenv("DSOCR_GEMM_W22")) != 0;  // A/B: 2 x 2 for bf16
+    // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once); f16 weights: 2 x 2 (their W split
+    // would double under 4 x 1)
     if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
-    else if (w22) hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) {
         const long n = (long)g.M * g.N;
@@ -615,109 +615,6 @@ void launch_gemm_f32a_grouped(const GemmArgs& g, hipStream_t s, int tile_rows) {
         if (g.wdtype == WDT_F16) hipLaunchKernelGGL((gemm_f32a_grp_kernel<true, 128>), grid, dim3(256), 0, s, g);
         else hipLaunchKernelGGL((gemm_f32a_grp_kernel<false, 128>), grid, dim3(256), 0, s, g);
     }
-}
-
-// ---------------------------------------------------------------------------------------
-// f32 rows -> [lo | mid | hi] bf16 planes (row r of the output = input row rows ? rows[r] : r).
-// a = hi + mid + lo exactly: hi = RNE(a), mid = RNE(a - hi), lo = RNE(a - hi - mid) (the two
-// residuals are exact in f32).  One thread per 4 consecutive elements.
-__global__ __launch_bounds__(256) void split3_rows_kernel(const float* __restrict__ x, long ldx, const int* rows, int M,
-                                                          int K, uint16_t* __restrict__ out, long ldo) {
-    const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
-    const int per = K >> 2;
-    if (i4 >= (long)M * per) return;
-    const int r = (int)(i4 / per), k = (int)(i4 % per) * 4;
-    const long src = rows ? (long)rows[r] : (long)r;
-    const float4 v = *reinterpret_cast<const float4*>(x + src * ldx + k);
-    const float a[4] = {v.x, v.y, v.z, v.w};
-    __bf16 h[4], m[4], l[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        h[j] = (__bf16)a[j];
-        const float r1 = a[j] - (float)h[j];
-        m[j] = (__bf16)r1;
-        l[j] = (__bf16)(r1 - (float)m[j]);
-    }
-    uint16_t* o = out + (long)r * ldo + k;
-    uint2 ul, um, uh;
-    __builtin_memcpy(&ul, l, 8);
-    __builtin_memcpy(&um, m, 8);
-    __builtin_memcpy(&uh, h, 8);
-    *reinterpret_cast<uint2*>(o) = ul;
-    *reinterpret_cast<uint2*>(o + K) = um;
-    *reinterpret_cast<uint2*>(o + 2 * K) = uh;
-}
-
-// f32 rows -> [lo | mid | mid | hi | hi] bf16 planes: the activation side of the f16-weight form,
-// paired with W5 = [w_hi | w_lo | w_hi | w_lo | w_hi] (make_w5) so that A5 . W5^T holds the five
-// products lo.hi, mid.lo, mid.hi, hi.lo, hi.hi (lo.lo is below f32 rounding), as gemm_x3 does.
-__global__ __launch_bounds__(256) void split5_rows_kernel(const float* __restrict__ x, long ldx, int M, int K,
-                                                          uint16_t* __restrict__ out, long ldo) {
-    const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
-    const int per = K >> 2;
-    if (i4 >= (long)M * per) return;
-    const int r = (int)(i4 / per), k = (int)(i4 % per) * 4;
-    const float4 v = *reinterpret_cast<const float4*>(x + (long)r * ldx + k);
-    const float a[4] = {v.x, v.y, v.z, v.w};
-    __bf16 h[4], m[4], l[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        h[j] = (__bf16)a[j];
-        const float r1 = a[j] - (float)h[j];
-        m[j] = (__bf16)r1;
-        l[j] = (__bf16)(r1 - (float)m[j]);
-    }
-    uint16_t* o = out + (long)r * ldo + k;
-    uint2 ul, um, uh;
-    __builtin_memcpy(&ul, l, 8);
-    __builtin_memcpy(&um, m, 8);
-    __builtin_memcpy(&uh, h, 8);
-    *reinterpret_cast<uint2*>(o) = ul;
-    *reinterpret_cast<uint2*>(o + K) = um;
-    *reinterpret_cast<uint2*>(o + 2 * K) = um;
-    *reinterpret_cast<uint2*>(o + 3 * K) = uh;
-    *reinterpret_cast<uint2*>(o + 4 * K) = uh;
-}
-
-void launch_split5_rows(const float* x, long ldx, int M, int K, void* out, long ldo, hipStream_t s) {
-    if (M <= 0) return;
-    if (K % 4 || ldx % 4 || ldo < 5L * K) throw std::runtime_error("EINVAL: split5_rows needs K % 4 == 0");
-    const long n4 = (long)M * (K / 4);
-    hipLaunchKernelGGL(split5_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, ldx, M, K,
-                       reinterpret_cast<uint16_t*>(out), ldo);
-}
-
-// f16 weight rows -> [w_hi | w_lo | w_hi | w_lo | w_hi] bf16 (w = w_hi + w_lo exactly: f16 has 11
-// significant bits)
-__global__ __launch_bounds__(256) void make_w5_kernel(const uint16_t* __restrict__ w, int N, int K,
-                                                      uint16_t* __restrict__ out) {
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (long)N * K) return;
-    const int r = (int)(i / K), k = (int)(i % K);
-    _Float16 hv;
-    __builtin_memcpy(&hv, &w[i], 2);
-    const float f = (float)hv;
-    const __bf16 hi = (__bf16)f;
-    const __bf16 lo = (__bf16)(f - (float)hi);
-    uint16_t uh, ul;
-    __builtin_memcpy(&uh, &hi, 2);
-    __builtin_memcpy(&ul, &lo, 2);
-    uint16_t* o = out + (long)r * 5 * K + k;
-    o[0] = uh; o[K] = ul; o[2 * K] = uh; o[3 * K] = ul; o[4 * K] = uh;
-}
-
-void launch_make_w5(const void* w, int N, int K, void* out, hipStream_t s) {
-    const long n = (long)N * K;
-    hipLaunchKernelGGL(make_w5_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<const uint16_t*>(w), N, K, reinterpret_cast<uint16_t*>(out));
-}
-
-void launch_split3_rows(const float* x, long ldx, const int* rows, int M, int K, void* out, long ldo, hipStream_t s) {
-    if (M <= 0) return;
-    if (K % 4 || ldx % 4 || ldo < 3L * K) throw std::runtime_error("EINVAL: split3_rows needs K % 4 == 0");
-    const long n4 = (long)M * (K / 4);
-    hipLaunchKernelGGL(split3_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, ldx, rows, M, K,
-                       reinterpret_cast<uint16_t*>(out), ldo);
 }
 
 }  // namespace dsocr

@@ -48,11 +48,6 @@ int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8
 bool gemm_f32a_ok(const GemmBf16Args& g);
 int gemm_f32a_splits(int M, int N, int K);
 void launch_gemm_f32a(const GemmBf16Args& g, hipStream_t s);
-// f16-weight form: A5 = [lo | mid | mid | hi | hi] planes, W5 = [w_hi | w_lo | w_hi | w_lo | w_hi]
-void launch_split5_rows(const float* x, long ldx, int M, int K, void* out, long ldo, hipStream_t s);
-void launch_make_w5(const void* w, int N, int K, void* out, hipStream_t s);
-// f32 rows (optionally gathered) -> bf16 planes [lo | mid | hi] of K each (row stride ldo >= 3K)
-void launch_split3_rows(const float* x, long ldx, const int* rows, int M, int K, void* out, long ldo, hipStream_t s);
 
 struct GemmArgs {
     int M = 0, N = 0, K = 0;
@@ -239,29 +234,11 @@ struct DecAttn2Args {
     float* part = nullptr;
     int* counters = nullptr;                            // [B][heads] arrival tickets, zero between launches
     float* o = nullptr; long o_ld = 0;
-    // fused q/k/v projection (dec_qkv_attn): residual rows x [B][ldx], RMSNorm weight, fused
-    // [(heads + 2 kv_heads) hd][K] weight, per-(page, head) arrival counters (zero between
-    // launches; the combine resets them), give-up flag; qkv above is then the OUTPUT buffer
-    const float* x = nullptr; long ldx = 0; const float* norm_w = nullptr; float eps = 0.f; int K = 0;
-    const void* Wqkv = nullptr; int wdtype = WDT_F16; const float* qkv_bias = nullptr;
-    int* qkv_cnt = nullptr; int* err = nullptr;
-    unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
-    unsigned long long* span = nullptr;    // launch-span slots (SPAN_SLOTS pairs) or null
-    int prerot = 0;                        // q / k rows already rotated (dec_qkv_rope)
-    int kv_bound = 0;                      // > 0: every page's length <= kv_bound (K / V loads issued before the position)
-    int split = 0;                         // no in-kernel combine: dim-major records for dec_oproj_comb
+    int* err = nullptr;                                 // polled merge: give-up flag (set instead of hanging)
+    unsigned long long* span = nullptr;                 // launch-span slots (SPAN_SLOTS pairs) or null
+    int prerot = 0;                                     // q / k rows already rotated (dec_qkv_rope)
 };
-// Attention combine (split-mode records of dec_attn, one token) fused into the o_proj GEMV.
-struct DecCombArgs {
-    const float* part = nullptr;   // [heads][(2 + hd) * cm] records
-    const int* kv_pos = nullptr;
-    int heads = 0, hd = 0, cm = 0, ch = 64;  // cm = chunk capacity per head, ch = keys per chunk
-    float* ctx_out = nullptr;      // optional: the combined context row (block 0 writes it)
-};
-bool dec_oproj_comb_ok(const DecGemvArgs& a, const DecCombArgs& cb);
-void launch_dec_oproj_comb(const DecGemvArgs& a, const DecCombArgs& cb, hipStream_t s);
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
-void launch_dec_attn3(const DecAttn2Args& a, hipStream_t s);  // decode_attn.hip
 // q/k/v projection of one token with RoPE applied in the epilogue (rows < rot_rows rotated at
 // position kv_pos[0]; table layout [pos][hd], rope on the full head dim, rotate_half pairing).
 struct DecRopeEpi {
@@ -271,8 +248,6 @@ struct DecRopeEpi {
 };
 bool dec_qkv_rope_ok(const DecGemvArgs& a, const DecRopeEpi& r);
 void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t s);
-bool dec_qkv_attn_ok(const DecAttn2Args& a);
-void launch_dec_qkv_attn(const DecAttn2Args& a, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
 // the record buffer enters every dec_attn launch sentinel-filled (the polling merge refills what it reads)
 void dec_attn_part_init(float* part, size_t bytes, hipStream_t s);
@@ -308,12 +283,7 @@ struct MoeDec2Args {
     int softmax_scoring = 1, norm_topk = 0;
     float scaling = 1.f;
     int* ids_out = nullptr; float* w_out = nullptr;
-    int dbg = 0;  // experiment knobs (DSOCR_DBG_GU): 1 skip routing, 2 skip weight stream
-    unsigned long long* stamps = nullptr;  // dev: per-block phase clocks [block][8] (profile only)
     unsigned long long* span = nullptr;    // launch-span slots (SPAN_SLOTS pairs) or null
-    // fused launch (moe_fused_slot_kernel): arrival counters (SYNC_SHARDS lines, zeroed before
-    // the launch), arrivals to wait for (set by the launcher), give-up flag
-    int* sync = nullptr; int sync_target = 0; int* err = nullptr;
     // grouped mode (3 <= T <= 8): expert groups written by the router epilogue (MOE_GRP_* layout);
     // h rows stay in slot order (t*topk + k)
     const int* grp = nullptr;
@@ -325,9 +295,6 @@ struct MoeDec2Args {
     // arrival tickets [Hout / 128] (zero between launches; the last arriver resets them)
     float* dn_part = nullptr; int* dn_tick = nullptr;
 };
-constexpr int SYNC_SHARDS = 8, SYNC_STRIDE = 32;  // counters per hand-off, ints between counters
-constexpr int SYNC_INTS = SYNC_SHARDS * SYNC_STRIDE;  // ints of one hand-off's counter block
-bool moe_fused_ok(const MoeDec2Args& a);
 // Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams
 // shared-expert rows from its first instruction, 3 of 4 route themselves (rank-based top-k of
 // the router logits) and stream their routed expert's rows; activations = the normalised row
@@ -337,7 +304,6 @@ void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s)
 // Decode down + combine + residual for one token: split-K over each block's waves.
 bool moe_down_mix_ok(const MoeDec2Args& a);
 void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s);
-void launch_moe_fused(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s);
 void launch_moe_down2(const MoeDec2Args& a, hipStream_t s);
 // Grouped decode MoE (3 <= T <= 8): every distinct routed expert's rows are streamed once per layer
@@ -350,8 +316,6 @@ void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s);
 // token rows as three exact f16 planes
 bool moe_gateup_mm_ok(const MoeDec2Args& a);
 void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s);
-bool moe_gateup_mix_mm_ok(const MoeDec2Args& a);
-void launch_moe_gateup_mix_mm(const MoeDec2Args& a, const float* xn, hipStream_t s);
 bool moe_down_mm_ok(const MoeDec2Args& a);
 size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H);
 void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s);
@@ -435,7 +399,6 @@ struct LmHeadQ8Args {
     int* blk_cnt = nullptr; float* blk_t = nullptr; int* cand = nullptr; float* cand_hi = nullptr;
     int nblk = 0; long slot = 0;  // from lmhead_q8_grid
     float* xn_out = nullptr;  // [B][K]
-    int mode = 0;             // diagnostics: 1 = stream only (no selection state; results invalid)
 };
 void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s);
 // grid of the screened lm_head for B pages: blocks per page and the per-block slot length

@@ -277,7 +277,6 @@ __global__ __launch_bounds__(256) void lmhead_q8_kernel(LmHeadQ8Args a) {
         const int nrow = g * LQ_RB + lane;
         const bool trig = lane < LQ_RB && nrow < a.N && (lo > Tw || hi >= Tw);
         unsigned long long m = __ballot(trig);
-        if (a.mode == 1) m = 0;  // diagnostics: stream only
         while (m) {
             const int r = __ffsll((long long)m) - 1;
             m &= m - 1;

@@ -151,7 +151,7 @@ def lib():
     L.dsocr_k_rmsnorm.argtypes = [i32, i32, vp, vp, f32, vp]
     L.dsocr_k_dsq_dequant.argtypes = [i32, vp, sz, sz, sz, vp]
     L.dsocr_k_attention.argtypes = [i32, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp, vp, i32, i32]
-    L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, vp, i32, i32]
+    L.dsocr_k_decode_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, vp, i32]
     L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]
     L.dsocr_k_sample_greedy.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, vp]
     L.dsocr_k_sample_stoch.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, C.c_double, C.c_size_t, C.c_double,

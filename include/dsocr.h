@@ -281,11 +281,10 @@ dsocr_status dsocr_k_attention_bf16(int n_seq, int L, int heads, int hd, float s
  * token at position pos = kv_pos[b] has its q / k rotated (cos/sin tables [max_len][rope_dim]; prerot != 0:
  * the q / k rows of qkv are already rotated), k and v appended to the f32 cache [B][kv_heads][max_len][hd]
  * at pos, then o[b] = softmax(scale * q.K[:pos+1]^T) . V[:pos+1].  qkv: [B][(heads + 2 kv_heads) * hd];
- * o: [B][heads*hd].  kv_bound > 0: every pos + 1 <= kv_bound <= max_len (the decode loop's per-band key
- * bound: the kernel issues its K / V loads before it reads the position). */
+ * o: [B][heads*hd]. */
 dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, int rope_dim, int max_len, float scale,
                                       const float* qkv, const float* cos, const float* sin, float* kc, float* vc,
-                                      const int* kv_pos, float* o, int prerot, int kv_bound);
+                                      const int* kv_pos, float* o, int prerot);
 /* Decode MoE layer (the north-star kernel chain, block.rs:1215-1395): [RMSNorm] + router GEMV +
  * softmax top-k + grouping + grouped SwiGLU experts + shared experts + weighted combine,
  * out[T][H] += moe(xn), xn = rmsnorm(x; norm_w, eps) if norm_w != NULL else x.  Runs exactly the

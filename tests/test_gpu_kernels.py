@@ -236,20 +236,16 @@ def test_attention_sam_relpos(gpu, g, rel_len):
         assert np.max(np.abs(got[:, hl] - ref)) < 5e-5
 
 
-@pytest.mark.parametrize("B,heads,kvh,hd,max_len,prerot,bound", [
-    (1, 10, 10, 128, 1218, 0, "none"), (3, 4, 4, 32, 300, 0, "none"), (5, 12, 4, 64, 700, 0, "none"),
-    (2, 10, 10, 128, 257, 0, "none"), (1, 10, 10, 128, 64, 0, "none"), (8, 10, 10, 128, 1218, 0, "none"),
-    # the decode loop's forms: q / k pre-rotated by the projection (one page), K / V loads issued before the
-    # position against a per-band key bound (tight, or up to 63 keys past the longest page)
-    (1, 10, 10, 128, 1218, 1, "none"), (1, 10, 10, 128, 1218, 1, "tight"), (1, 10, 10, 128, 1218, 1, "band"),
-    (8, 10, 10, 128, 1218, 0, "band"), (3, 4, 4, 32, 300, 0, "band"), (5, 12, 4, 64, 700, 1, "band"),
-    (2, 10, 10, 128, 2000, 0, "band"), (1, 10, 10, 128, 130, 1, "tight")])
-def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot, bound):
+@pytest.mark.parametrize("B,heads,kvh,hd,max_len,prerot", [
+    (1, 10, 10, 128, 1218, 0), (3, 4, 4, 32, 300, 0), (5, 12, 4, 64, 700, 0), (2, 10, 10, 128, 257, 0),
+    (1, 10, 10, 128, 64, 0), (8, 10, 10, 128, 1218, 0), (2, 10, 10, 128, 2000, 0),
+    # the one-page decode loop's form: q / k pre-rotated by the projection's epilogue
+    (1, 10, 10, 128, 1218, 1), (1, 10, 10, 128, 130, 1), (1, 10, 10, 128, 2000, 1)])
+def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot):
     """Fused decode attention (block.rs:608-789 at seq_len 1): RoPE on q / new k (block.rs:1403-1471) in the
     kernel or already applied (prerot), K/V append at pos = kv_pos[b], flash-decoding over pos + 1 keys of the
-    f32 cache (64-key chunks; polled merge up to 24 chunks, ticket beyond), with the K / V loads bounded by
-    the position or issued early against a key bound.  The cache past the position holds NaN: keys past the
-    position must contribute nothing."""
+    f32 cache (64-key chunks; polled merge up to 24 chunks, ticket beyond).  The cache past the position holds
+    NaN: keys past the position must contribute nothing."""
     from types import SimpleNamespace
     from oracle.decoder import apply_rope, rope_tables
     rng = np.random.default_rng(B * hd + max_len + prerot)
@@ -258,7 +254,7 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot, bound):
     kc = rng.standard_normal((B, kvh, max_len, hd)).astype(np.float32)
     vc = rng.standard_normal((B, kvh, max_len, hd)).astype(np.float32)
     pos = rng.integers(0, max_len, B).astype(np.int32)
-    pos[0] = max_len - 1 if bound == "none" else max_len - 70
+    pos[0] = max_len - 1
     if B > 1:
         pos[1] = 0
     if B > 2:
@@ -266,7 +262,6 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot, bound):
     for b in range(B):
         kc[b, :, pos[b] + 1:] = np.nan
         vc[b, :, pos[b] + 1:] = np.nan
-    kv_bound = {"none": 0, "tight": int(pos.max()) + 1, "band": min(max_len, int(pos.max()) + 64)}[bound]
     lang = SimpleNamespace(rope_theta=10000.0)
     cos, sin = rope_tables(lang, max_len, hd)
     rot = qkv.copy()
@@ -279,7 +274,7 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot, bound):
     dcos, dsin = Dev(cos), Dev(sin)
     scale = 1.0 / math.sqrt(hd)
     check(lib().dsocr_k_decode_attention(B, heads, kvh, hd, hd, max_len, scale, dqkv.ptr, dcos.ptr, dsin.ptr,
-                                         dk.ptr, dv.ptr, dp.ptr, do.ptr, prerot, kv_bound))
+                                         dk.ptr, dv.ptr, dp.ptr, do.ptr, prerot))
     got, gk, gv = do.get(), dk.get(), dv.get()
     for b in range(B):
         p = pos[b]
@@ -295,14 +290,13 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot, bound):
             assert np.max(np.abs(got[b, h * hd:(h + 1) * hd] - ref)) < 2e-5, (b, h)
 
 
-@pytest.mark.parametrize("T,H,E,topk,I,ns,norm,epi", [(3, 256, 16, 6, 64, 2, False, 0), (1, 256, 16, 6, 64, 2, True, 0),
-                                                      (2, 1280, 64, 6, 896, 2, True, 0), (9, 128, 8, 3, 32, 1, False, 0),
-                                                      (1, 1280, 64, 6, 896, 2, True, 1), (4, 256, 16, 6, 64, 2, False, 1)])
-def test_moe_decode_layer(gpu, monkeypatch, T, H, E, topk, I, ns, norm, epi):
+@pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(3, 256, 16, 6, 64, 2, False), (1, 256, 16, 6, 64, 2, True),
+                                                  (2, 1280, 64, 6, 896, 2, True), (9, 128, 8, 3, 32, 1, False),
+                                                  (4, 256, 16, 6, 64, 2, False)])
+def test_moe_decode_layer(gpu, T, H, E, topk, I, ns, norm):
     """Decode MoE (north-star kernel chain) vs the oracle's run_moe (block.rs:1215-1395).
-    T <= 8: slot mode (gate/up blocks route themselves; epi=1: the router kernel's epilogue routes);
-    T > 8: one block groups the assignments by expert."""
-    monkeypatch.setenv("DSOCR_ROUTER_EPI", str(epi))
+    T <= 2: slot mode (gate/up blocks route themselves); 3..8: grouped (the router launch writes the
+    expert groups); T > 8: one block groups the assignments by expert."""
     from oracle.decoder import Decoder
     rng = np.random.default_rng(5 + T)
     Is = I * ns

@@ -46,7 +46,7 @@ for step in "$@"; do
     gprof128) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof128 -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 128 --no-cpu-baseline > gpurun_out/gprof128.log 2>&1 ;;
     gprof_full_maps) DSOCR_SEGV_MAPS=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_full_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/gprof_full_maps.log 2>&1 ;;
     katt) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k decode_attention > gpurun_out/katt.log 2>&1 ;;
-    kb_attn) run 120 ./tools/kbench attn1 attn8 > gpurun_out/kb_attn_new.log 2>&1 && DSOCR_ATTN_OLD=1 run 120 ./tools/kbench attn1 attn8 > gpurun_out/kb_attn_old.log 2>&1 ;;
+    kb_attn) run 120 ./tools/kbench attn1 attn8 > gpurun_out/kb_attn.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done

@@ -223,41 +223,6 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     const double dnb = ((double)touched * I + IS) * H * 2;
     snprintf(nm, sizeof nm, "moe%d gateup", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_GATEUP); }, s), gub);
-    if (getenv("KB_STAMPS")) {  // per-block phase clocks of the gate/up launch (wall clock, 100 MHz)
-        const int nb = 8192;
-        auto* st = (unsigned long long*)dalloc((size_t)nb * 4 * 8);
-        set(5);
-        MoeDecodeArgs b = a;
-        // stamps ride in the dispatch's MoeDec2Args through a global hook: DSOCR_STAMPS_PTR
-        char buf[64];
-        snprintf(buf, sizeof buf, "%llu", (unsigned long long)(uintptr_t)st);
-        setenv("DSOCR_MOE_STAMPS", buf, 1);
-        launch_moe_decode(b, s, MOE_GATEUP);
-        CK(hipStreamSynchronize(s));
-        unsetenv("DSOCR_MOE_STAMPS");
-        std::vector<unsigned long long> h((size_t)nb * 4);
-        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-        // per record: 4 wall-clock stamps (kernel-specific phase points), relative to the first entry
-        unsigned long long t0 = ~0ull;
-        for (int i = 0; i < nb; ++i)
-            if (h[i * 4]) t0 = std::min(t0, h[i * 4]);
-        std::vector<double> ph[4];
-        for (int i = 0; i < nb; ++i) {
-            if (!h[i * 4] || !h[i * 4 + 3]) continue;
-            for (int k = 0; k < 4; ++k)
-                if (h[i * 4 + k]) ph[k].push_back(((long long)h[i * 4 + k] - (long long)t0) / 100.0);
-        }
-        auto pr = [](const char* n, std::vector<double> v) {
-            if (v.empty()) return;
-            std::sort(v.begin(), v.end());
-            printf("  %s: n %zu p10 %.2f p50 %.2f p90 %.2f max %.2f us\n", n, v.size(), v[v.size() / 10], v[v.size() / 2],
-                   v[v.size() * 9 / 10], v.back());
-        };
-        pr("stamp0", ph[0]);
-        pr("stamp1", ph[1]);
-        pr("stamp2", ph[2]);
-        pr("stamp3", ph[3]);
-    }
     snprintf(nm, sizeof nm, "moe%d down", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_DOWN); }, s), dnb);
 }
@@ -310,45 +275,6 @@ static void case_attn(int B, int pos, hipStream_t s) {
     snprintf(nm, sizeof nm, "attn B=%d L=%d", B, pos + 1);
     const double bytes = 2.0 * B * (pos + 1) * HEADS * HD * 4;
     report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
-    a.kv_bound = pos + 1;  // the decode loop's per-band key bound (tightest case): loads before the position
-    snprintf(nm, sizeof nm, "attn B=%d L=%d bound", B, pos + 1);
-    report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
-    a.kv_bound = std::min(max_len, pos + 64);
-    snprintf(nm, sizeof nm, "attn B=%d L=%d bound+63", B, pos + 1);
-    report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
-    a.kv_bound = 0;
-    if (getenv("KB_STAMPS")) {  // per-block phase clocks: [0] wall entry, [1..] shader clock at the phase points
-        const int nb = 4096;
-        auto* st = (unsigned long long*)dalloc((size_t)nb * 8 * 8);
-        a.kc = kc[2]; a.vc = vc[2];
-        launch_dec_attn(a, s);  // a warm predecessor on the stream (the decode loop never idles)
-        a.kc = kc[3]; a.vc = vc[3]; a.stamps = st;
-        launch_dec_attn(a, s);
-        CK(hipStreamSynchronize(s));
-        a.stamps = nullptr;
-        std::vector<unsigned long long> h((size_t)nb * 8);
-        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-        unsigned long long w0 = ~0ull;
-        for (int i = 0; i < nb; ++i) if (h[i * 8]) w0 = std::min(w0, h[i * 8]);
-        std::vector<double> ent, ph[4];
-        for (int i = 0; i < nb; ++i) {
-            if (!h[i * 8]) continue;
-            ent.push_back((h[i * 8] - w0) / 100.0);
-            for (int k = 0; k < 4; ++k)
-                if (h[i * 8 + 2 + k]) ph[k].push_back((h[i * 8 + 2 + k] - h[i * 8 + 1]) / 2400.0);
-        }
-        auto pr = [](const char* n, std::vector<double> v) {
-            if (v.empty()) return;
-            std::sort(v.begin(), v.end());
-            printf("  %-14s n %4zu p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us\n", n, v.size(), v[v.size() / 10], v[v.size() / 2],
-                   v[v.size() * 9 / 10], v.back());
-        };
-        pr("entry (wall)", ent);
-        pr("q ready", ph[0]);
-        pr("softmax done", ph[1]);
-        pr("ticket", ph[2]);
-        pr("combine done", ph[3]);
-    }
     for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); }
 }
 
