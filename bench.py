@@ -286,8 +286,9 @@ def dots_flops(cfg, N):
 
 
 def run_dots(args, rank, world, local, dist):
-    """BASELINE configs[3]: dots.ocr (bf16) vision tower on a 2048-px class page per GPU per step
-    (2044 x 2044: the reference's smart_resize keeps it, grid 146 x 146 = 21316 patch tokens)."""
+    """BASELINE configs[3]: dots.ocr (bf16) vision tower on a 2048 x 2048 page per GPU per step (the
+    reference's smart_resize maps it to 2044 x 2044, fast_image_resize's Catmull-Rom pass resizes it,
+    grid 146 x 146 = 21316 patch tokens; preprocessing on the host before the timed region)."""
     import ctypes as C
 
     import numpy as np
@@ -351,7 +352,8 @@ def run_dots(args, rank, world, local, dist):
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16 (reference semantics: bf16 tensors between ops; f32 attention math)",
         "data": "synthetic document pages + seeded synthetic weights (no checkpoint offline)",
-        "config": {"workload": f"configs[3]: dots.ocr vision tower, {size}x{size} page, grid {grid[1]}x{grid[2]}, "
+        "config": {"workload": f"configs[3]: dots.ocr vision tower, {size}x{size} page (resized to "
+                               f"{grid[1] * 14}x{grid[2] * 14}), grid {grid[1]}x{grid[2]}, "
                                f"{N} patch tokens, {groups} output rows", "pages_per_gpu": ppg,
                    "global_batch": ppg * world, "parallelism": f"dp{world}"},
         "stage_ms": {"page_ms": round(page_ms, 2), "blocks_ms": round(tm["blocks_ms"], 2),
@@ -385,7 +387,8 @@ def main():
     ap.add_argument("--roofline-iters", type=int, default=20)
     ap.add_argument("--workload", default="deepseek", choices=["deepseek", "dots2048"],
                     help="deepseek: configs[1]/[2] (default); dots2048: configs[3], the dots.ocr vision tower")
-    ap.add_argument("--dots-size", type=int, default=2044)
+    ap.add_argument("--dots-size", type=int, default=2048,
+                    help="page side: 2048 (configs[3]) is resized to 2044 by smart_resize + the Catmull-Rom pass")
     ap.add_argument("--snapshot", default=None, choices=["q4k"],
                     help="q4k: configs[4], a full-size synthetic Q4_K DSQ snapshot loaded through the engine's "
                          "dequant-on-load path (written to $TMPDIR first)")

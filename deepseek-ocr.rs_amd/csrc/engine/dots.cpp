@@ -99,7 +99,7 @@ DotsPatches dots_preprocess(const DotsConfig& c, const uint8_t* rgb, int w, int 
     const uint8_t* src = rgb;
     if (rh != h || rw != w) {
         resized.resize((size_t)rh * rw * 3);
-        resize_bicubic(rgb, w, h, resized.data(), (int)rw, (int)rh);
+        resize_catmull_rom_fir(rgb, w, h, resized.data(), (int)rw, (int)rh);
         src = resized.data();
     }
     const int P = c.patch, M = c.merge;

@@ -35,9 +35,9 @@ struct DotsPatches {
     int grid_t = 1, grid_h = 0, grid_w = 0;
     int resized_h = 0, resized_w = 0;
 };
-// preprocess_image (preprocess.rs:103-145): smart_resize, resize (Pillow-exact Catmull-Rom / bicubic
-// a = -0.5 — the reference's fast_image_resize CatmullRom convolution, parity unpinned), normalise,
-// patches in merge-group order
+// preprocess_image (preprocess.rs:103-145): smart_resize, resize (fast_image_resize's Catmull-Rom
+// convolution restated, host_ops.hpp resize_catmull_rom_fir; parity unpinned), normalise, patches in
+// merge-group order
 DotsPatches dots_preprocess(const DotsConfig& c, const uint8_t* rgb, int w, int h);
 
 struct DotsTimings {

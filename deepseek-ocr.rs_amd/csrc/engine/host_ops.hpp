@@ -113,6 +113,111 @@ inline void resize_bicubic(const uint8_t* src, int sw, int sh, uint8_t* dst, int
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// dots.ocr page resize (crates/infer-dots/src/vision/preprocess.rs:283-299): fast_image_resize 5.3.0
+// (Cargo.lock) ResizeAlg::Convolution(FilterType::CatmullRom) on U8x3, restated from that crate's
+// published algorithm (the crate is not in the repository: parity unpinned):
+//   * per axis: scale = in / out, filter scale = max(scale, 1), radius = 2 * filter scale; output x
+//     centres at (x + 0.5) * scale, taps floor(centre - radius) .. ceil(centre + radius) clamped to the
+//     image, weight k((i - centre + 0.5) / filter scale) with the Catmull-Rom cubic (B = 0, C = 0.5),
+//     normalised to sum 1;
+//   * the weights become i16 at the largest precision p <= 14 whose doubled maximum still fits
+//     (round half away from zero), the accumulator starts at 2^(p-1), the result is acc >> p clamped to
+//     0..255;
+//   * horizontal pass first into an 8-bit image, then the vertical pass.
+// Against Pillow's bicubic (the same cubic at 22-bit precision, resize_bicubic above) the two differ
+// only in rounding: tests/test_dots.py::test_fir_catmull_rom_vs_pillow states by how much.
+inline double catmull_rom_fir(double x) {
+    const double B = 0.0, C = 0.5;
+    x = std::fabs(x);
+    if (x < 1.0) return ((12.0 - 9.0 * B - 6.0 * C) * x * x * x + (-18.0 + 12.0 * B + 6.0 * C) * x * x + (6.0 - 2.0 * B)) / 6.0;
+    if (x < 2.0)
+        return ((-B - 6.0 * C) * x * x * x + (6.0 * B + 30.0 * C) * x * x + (-12.0 * B - 48.0 * C) * x + (8.0 * B + 24.0 * C)) /
+               6.0;
+    return 0.0;
+}
+
+struct FirCoeffs {
+    std::vector<int> start, size;
+    std::vector<std::vector<int16_t>> w;
+    int precision = 0;
+};
+
+inline FirCoeffs fir_coeffs(int in_size, int out_size) {
+    FirCoeffs fc;
+    const double scale = (double)in_size / (double)out_size;
+    const double fscale = std::max(scale, 1.0);
+    const double radius = 2.0 * fscale;
+    std::vector<std::vector<double>> wd((size_t)out_size);
+    double max_w = 0.0;
+    for (int x = 0; x < out_size; ++x) {
+        const double centre = ((double)x + 0.5) * scale;
+        const long x0 = std::max(0L, (long)std::floor(centre - radius));
+        const long x1 = std::min((long)in_size, (long)std::ceil(centre + radius));
+        double sum = 0.0;
+        for (long i = x0; i < x1; ++i) {
+            const double v = catmull_rom_fir(((double)i - centre + 0.5) / fscale);
+            wd[x].push_back(v);
+            sum += v;
+        }
+        if (sum != 0.0)
+            for (double& v : wd[x]) v /= sum;
+        for (double v : wd[x]) max_w = std::max(max_w, v);
+        fc.start.push_back((int)x0);
+        fc.size.push_back((int)(x1 - x0));
+    }
+    int precision = 0;
+    for (int cur = 0; cur < 15; ++cur) {
+        precision = cur;
+        if (std::round(max_w * (double)(1 << (cur + 1))) >= (double)(1 << 15)) break;
+    }
+    fc.precision = precision;
+    const double sc = (double)(1 << precision);
+    fc.w.resize((size_t)out_size);
+    for (int x = 0; x < out_size; ++x)
+        for (double v : wd[x]) fc.w[x].push_back((int16_t)std::round(v * sc));  // std::round: half away from zero
+    return fc;
+}
+
+inline uint8_t fir_clip(int32_t v, int precision) {
+    const int32_t s = v >> precision;
+    return (uint8_t)(s < 0 ? 0 : (s > 255 ? 255 : s));
+}
+
+// src HWC RGB8 (sw x sh) -> dst (dw x dh)
+inline void resize_catmull_rom_fir(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh) {
+    if (dw <= 0 || dh <= 0) return;
+    const FirCoeffs cx = fir_coeffs(sw, dw), cy = fir_coeffs(sh, dh);
+    std::vector<uint8_t> hz((size_t)sh * dw * 3);
+    if (dw == sw) {
+        std::copy(src, src + (size_t)sh * sw * 3, hz.begin());
+    } else {
+        const int32_t init = 1 << (cx.precision - 1);
+        for (int y = 0; y < sh; ++y)
+            for (int x = 0; x < dw; ++x) {
+                int32_t acc[3] = {init, init, init};
+                const uint8_t* row = src + ((size_t)y * sw + cx.start[x]) * 3;
+                for (int i = 0; i < cx.size[x]; ++i)
+                    for (int c = 0; c < 3; ++c) acc[c] += (int32_t)row[i * 3 + c] * (int32_t)cx.w[x][i];
+                for (int c = 0; c < 3; ++c) hz[((size_t)y * dw + x) * 3 + c] = fir_clip(acc[c], cx.precision);
+            }
+    }
+    if (dh == sh) {
+        std::copy(hz.begin(), hz.end(), dst);
+        return;
+    }
+    const int32_t init = 1 << (cy.precision - 1);
+    for (int y = 0; y < dh; ++y)
+        for (int x = 0; x < dw; ++x) {
+            int32_t acc[3] = {init, init, init};
+            for (int i = 0; i < cy.size[y]; ++i) {
+                const uint8_t* px = hz.data() + ((size_t)(cy.start[y] + i) * dw + x) * 3;
+                for (int c = 0; c < 3; ++c) acc[c] += (int32_t)px[c] * (int32_t)cy.w[y][i];
+            }
+            for (int c = 0; c < 3; ++c) dst[((size_t)y * dw + x) * 3 + c] = fir_clip(acc[c], cy.precision);
+        }
+}
+
 inline double round_ties_to_even(double v) {
     double r = std::round(v);  // half away from zero, like Rust f64::round
     if (std::fabs(v - r) != 0.5) return r;

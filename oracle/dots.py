@@ -19,9 +19,11 @@ The model dtype is bf16 (BASELINE configs[3] "dots-ocr bf16"): every op output i
 follow the reference's GPU kernels op by op (candle-kernels unary.cu silu_fwd / gelu_fwd computed
 in the bf16 type: every multiply / add rounds to bf16) — a third-party crate (candle 0.9.2) not in
 /root/reference, restated from its published kernels: parity of those two ops is unpinned.
-fast_image_resize's Catmull-Rom resampler (a third-party crate) is not restated: pages whose
-smart_resize target equals their size (multiples of 28 within the pixel budget) need no resize, and
-that is what the tests and the bench use.
+The page resize (preprocess.rs:283-299) goes through fast_image_resize 5.3.0 (Cargo.lock), a
+third-party crate not in /root/reference: `fir_resize_catmull_rom` restates its published
+Convolution(CatmullRom) algorithm for U8x3 (i16 weights at the largest precision <= 14 bits,
+horizontal pass then vertical); parity of the resize is unpinned against the crate (no Rust toolchain),
+and tests/test_dots.py states how far it lies from Pillow's bicubic on the bench's 2048 -> 2044 page.
 """
 from __future__ import annotations
 
@@ -73,6 +75,69 @@ def smart_resize(height, width, factor, min_pixels, max_pixels):
     return int(h_bar), int(w_bar)
 
 
+def _catmull_rom(x):
+    """fast_image_resize's cubic with B = 0, C = 0.5 (Mitchell-Netravali form)."""
+    B, C = 0.0, 0.5
+    x = abs(x)
+    if x < 1.0:
+        return ((12.0 - 9.0 * B - 6.0 * C) * x * x * x + (-18.0 + 12.0 * B + 6.0 * C) * x * x + (6.0 - 2.0 * B)) / 6.0
+    if x < 2.0:
+        return ((-B - 6.0 * C) * x * x * x + (6.0 * B + 30.0 * C) * x * x + (-12.0 * B - 48.0 * C) * x
+                + (8.0 * B + 24.0 * C)) / 6.0
+    return 0.0
+
+
+def _round_away(v):
+    return math.floor(v + 0.5) if v >= 0 else -math.floor(-v + 0.5)
+
+
+def fir_coeffs(in_size, out_size):
+    """Per output pixel (first tap, i16 weights) and the fixed-point precision of one axis."""
+    scale = in_size / out_size
+    fscale = max(scale, 1.0)
+    radius = 2.0 * fscale
+    rows, max_w = [], 0.0
+    for x in range(out_size):
+        centre = (x + 0.5) * scale
+        x0 = max(0, math.floor(centre - radius))
+        x1 = min(in_size, math.ceil(centre + radius))
+        ws = [_catmull_rom((i - centre + 0.5) / fscale) for i in range(x0, x1)]
+        tot = sum(ws)
+        if tot != 0.0:
+            ws = [w / tot for w in ws]
+        max_w = max([max_w] + ws)
+        rows.append((x0, ws))
+    precision = 0
+    for cur in range(15):
+        precision = cur
+        if _round_away(max_w * (1 << (cur + 1))) >= (1 << 15):
+            break
+    return [(x0, np.asarray([_round_away(w * (1 << precision)) for w in ws], np.int64)) for x0, ws in rows], precision
+
+
+def _fir_pass(img, coeffs, precision):
+    """Convolve axis 1 of img [rows][in][3] (uint8) -> [rows][out][3]."""
+    out = np.empty((img.shape[0], len(coeffs), 3), np.uint8)
+    src = img.astype(np.int64)
+    for x, (x0, w) in enumerate(coeffs):
+        acc = (1 << (precision - 1)) + np.einsum("rkc,k->rc", src[:, x0:x0 + len(w)], w)
+        out[:, x] = np.clip(acc >> precision, 0, 255)
+    return out
+
+
+def fir_resize_catmull_rom(rgb, out_w, out_h):
+    """fast_image_resize Convolution(CatmullRom), U8x3: horizontal pass, then vertical."""
+    img = np.asarray(rgb, np.uint8)
+    h, w = img.shape[:2]
+    if out_w != w:
+        cx, px = fir_coeffs(w, out_w)
+        img = _fir_pass(img, cx, px)
+    if out_h != h:
+        cy, py = fir_coeffs(h, out_h)
+        img = _fir_pass(img.transpose(1, 0, 2), cy, py).transpose(1, 0, 2)
+    return np.ascontiguousarray(img)
+
+
 def frame_positions(h, w, merge):
     """build_frame_positions dots_vit.rs:188-211: (hpos, wpos) in merge-group order."""
     pos = []
@@ -85,14 +150,15 @@ def frame_positions(h, w, merge):
 
 
 def preprocess(rgb, cfg=PREPROC):
-    """preprocess_image (preprocess.rs:103-145) for pages that need no resize: returns
-    (patches [N][3*p*p] f32 in merge-group order, grid (t, h, w))."""
+    """preprocess_image (preprocess.rs:103-145): returns (patches [N][3*p*p] f32 in merge-group order,
+    grid (t, h, w)); pages off the smart_resize grid go through the Catmull-Rom resize (283-299)."""
     rgb = np.asarray(rgb, np.uint8)
     H, W = rgb.shape[:2]
     p, m = cfg["patch_size"], cfg["merge_size"]
     rh, rw = smart_resize(H, W, p * m, cfg["min_pixels"], cfg["max_pixels"])
     if (rh, rw) != (H, W):
-        raise NotImplementedError(f"page {W}x{H} needs the fast_image_resize Catmull-Rom pass to {rw}x{rh}")
+        rgb = fir_resize_catmull_rom(rgb, rw, rh)
+        H, W = rh, rw
     rescale = F32(1.0) / F32(255.0)
     mean = np.asarray(cfg["image_mean"], F32)
     std = np.asarray(cfg["image_std"], F32)

@@ -27,6 +27,12 @@ reference's own bars this is read against: teacher-forcing logits <= 0.6
     python tests/golden/make_full_golden.py [--pages synthetic0,sample_1] [--max-new 512]
     python tests/golden/make_full_golden.py --pages synthetic1,...,synthetic7 --max-new 64
     python tests/golden/make_full_golden.py --pages text0,...,text7 --max-new 64
+    python tests/golden/make_full_golden.py --snapshot q4k --seed 0 --pages synthetic0 --max-new 64
+
+``--snapshot q4k``: BASELINE configs[4] — the full-size synthetic Q4_K / Q8_0 DSQ snapshot
+(dsocr.synth.write_synthetic_snapshot, seed 0, written to $TMPDIR) replaces every linear the reference's
+DeepSeek-OCR adapter quantises, dequantised to fp16 as the engine's dequant-on-load does; the fixtures
+are named full_q4k_<page>.npz.
 """
 import argparse
 import json
@@ -66,7 +72,7 @@ def banned(ctx, n):
     return banned_ngram_tokens(ctx, n)
 
 
-def make(name, orc, tok, max_new):
+def make(name, orc, tok, max_new, prefix="full", seed=SEED):
     from oracle.model import build_prompt_tokens
     t0 = time.time()
     if name.startswith("text"):
@@ -103,29 +109,40 @@ def make(name, orc, tok, max_new):
     print(f"[{name}] crop {crop} rows {emb.shape[0]} vision {t1 - t0:.1f}s generate {t2 - t1:.1f}s "
           f"min margin {margin.min():.3g} distinct ids {len(set(gen))}", flush=True)
     np.savez_compressed(
-        os.path.join(HERE, f"full_{name}.npz"),
+        os.path.join(HERE, f"{prefix}_{name}.npz"),
         prompt_ids=np.asarray(ids, np.int64), image_mask=np.asarray(mask, np.uint8),
         crop=np.asarray(crop, np.int64), n_image_rows=np.int64(emb.shape[0]),
         emb_sum=np.float64(emb.astype(np.float64).sum()), emb_abs_sum=np.float64(np.abs(emb).astype(np.float64).sum()),
         emb_row0=emb[0, :16].astype(np.float32) if len(emb) else np.zeros(16, np.float32),
         emb_rowlast=emb[-1, :16].astype(np.float32) if len(emb) else np.zeros(16, np.float32),
         ids=np.asarray(gen, np.int64), top_idx=top_idx, top_val=top_val, probe_idx=probe, probe_val=probe_val,
-        margin=margin, weights_seed=np.int64(SEED), max_new=np.int64(max_new))
+        margin=margin, weights_seed=np.int64(seed), max_new=np.int64(max_new))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pages", default="synthetic0,sample_1")
     ap.add_argument("--max-new", type=int, default=512)
+    ap.add_argument("--seed", type=int, default=SEED)
+    ap.add_argument("--snapshot", choices=["q4k"], default=None)
     a = ap.parse_args()
     from dsocr.synth import SyntheticTokenizer
     from oracle.model import OracleModel
     from oracle.weights import Weights
     cfg = json.load(open(FULL))
-    orc = OracleModel(cfg, Weights(seed=SEED, dtype="f16"))
+    snap, prefix = None, "full"
+    if a.snapshot == "q4k":
+        import tempfile
+
+        from dsocr.synth import write_synthetic_snapshot
+        from oracle import dsq
+        path = os.path.join(tempfile.gettempdir(), "dsocr_golden_q4k.dsq")
+        write_synthetic_snapshot(cfg, path, seed=0)
+        snap, prefix = dsq.Snapshot(path), "full_q4k"
+    orc = OracleModel(cfg, Weights(seed=a.seed, dtype="f16", snapshot=snap))
     tok = SyntheticTokenizer(cfg.get("language_config", cfg).get("vocab_size", 129280))
     for name in a.pages.split(","):
-        make(name, orc, tok, a.max_new)
+        make(name, orc, tok, a.max_new, prefix=prefix, seed=a.seed)
 
 
 if __name__ == "__main__":

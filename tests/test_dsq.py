@@ -399,3 +399,37 @@ def test_full_q4k_snapshot_engine_matches_oracle(gpu, tmp_path):
             err = max(float(np.max(np.abs(logits[0, s] - lg[s]))) for s in range(n_new))
             assert err < 2e-3, err
         assert ids8[i] == ref, (i, ids8[i], ref)
+
+
+@pytest.mark.gpu
+def test_full_q4k_snapshot_page_matches_fixture(gpu, tmp_path):
+    """configs[4] with a page: the full-size synthetic Q4_K snapshot (the projector from its Q8_0 record)
+    through vision -> projector -> 706-token prefill -> 64 greedy tokens on the bench's synthetic 1024 px
+    page: ids equal and the raw logits at the oracle's top-8 indices within 2e-3 of the committed fixture
+    (tests/golden/full_q4k_synthetic0.npz, make_full_golden.py --snapshot q4k: the oracle reading the
+    same snapshot)."""
+    import os
+    import dsocr
+    from dsocr import DecodeParameters, ModelLoadArgs, Page, VisionSettings, build_prompt_tokens, load_model
+    from dsocr.synth import BENCH_PROMPT, SyntheticTokenizer, synthetic_page, write_synthetic_snapshot
+    fxp = os.path.join(os.path.dirname(__file__), "golden", "full_q4k_synthetic0.npz")
+    fx = dict(np.load(fxp))
+    cfg = json.load(open(dsocr.FULL_CONFIG))
+    path = str(tmp_path / "full_q4k.dsq")
+    write_synthetic_snapshot(cfg, path, seed=0)
+    n = int(fx["max_new"])
+    eng = load_model(ModelLoadArgs(config_path=dsocr.FULL_CONFIG, synthetic_seed=int(fx["weights_seed"]), dtype="f16",
+                                   snapshot_path=path))
+    try:
+        page = Page(synthetic_page(0), VisionSettings(), eng)
+        ids, mask = build_prompt_tokens(SyntheticTokenizer(eng.vocab), BENCH_PROMPT, [page.n_image_tokens])
+        assert ids == fx["prompt_ids"].tolist()
+        outs, logits = eng.generate_trace([(ids, mask, page, None)], DecodeParameters(max_new_tokens=n), ignore_eos=True)
+    finally:
+        eng.close()
+    ref = fx["ids"].tolist()
+    bad = next((s for s, (a, b) in enumerate(zip(outs[0], ref)) if a != b), None)
+    assert outs[0] == ref, f"first divergent step {bad}, oracle margin there {fx['margin'][bad]:.3g}"
+    err = float(np.max(np.abs(np.take_along_axis(logits[0][:n], fx["top_idx"][:n], 1) - fx["top_val"][:n])))
+    print(f"q4k page: 64 ids equal, top-8 logit max-abs {err:.3g}")
+    assert err <= 2e-3, err

@@ -22,7 +22,7 @@ for step in "$@"; do
     prof1) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o b1 --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof1.log 2>&1 ;;
     prof8) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o b8 --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof8.log 2>&1 ;;
     profdots) run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profdots -o dots --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 1 > gpurun_out/profdots.log 2>&1 ;;
-    gpu_all) run 1100 python -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
+    gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
     bench_full) run 1100 python bench.py > gpurun_out/bench_full.log 2>&1 ;;
@@ -47,6 +47,10 @@ for step in "$@"; do
     gprof_full_maps) DSOCR_SEGV_MAPS=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_full_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/gprof_full_maps.log 2>&1 ;;
     katt) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k decode_attention > gpurun_out/katt.log 2>&1 ;;
     kb_attn) run 120 ./tools/kbench attn1 attn8 > gpurun_out/kb_attn.log 2>&1 ;;
+    # graph-mode kernel trace short enough that the AQL ring never wraps under the profiler
+    gprof64) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof64 -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline > gpurun_out/gprof64.log 2>&1 ;;
+    gprof64_8) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof64_8 -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline > gpurun_out/gprof64_8.log 2>&1 ;;
+    spans8t) run 600 python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/spans8t.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
