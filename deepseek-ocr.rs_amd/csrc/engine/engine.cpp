@@ -1059,12 +1059,26 @@ void Engine::decode_step(int B, int Lmax) {
         DecGemvArgs g;
         g.M = B; g.N = QKVN; g.K = H; g.W = d.qkv.W; g.ldw = H; g.wdtype = d.qkv.wdt; g.bias = d.qkv.b;
         g.y = QKV; g.ldy = QKVN; g.x = X; g.ldx = H; g.norm_w = d.in_norm.w; g.eps = L.rms_eps;
+        bool attn_done = false;
         if (B == 1 && !L.use_mla && L.rope_dim == hd) {
             DecRopeEpi re;
             re.kv_pos = kv_pos; re.cos = rope_cos_; re.sin = rope_sin_; re.hd = hd;
             re.rot_rows = (L.heads + L.kv_heads) * hd;
-            launch_dec_qkv_rope(g, re, st);
             da.prerot = 1;
+            if (qkv_attn_fused() && dec_qkv_attn_ok(g, re, da)) {
+                // one launch: the attention blocks stream their K / V chunk beside the projection
+                // (s_qkv stays sentinel-filled between launches; SKIP_ATTN, the profile's variant without
+                // attention, projects into a scratch row so the hand-off row keeps its sentinels)
+                if (step_skip_ & SKIP_ATTN) {
+                    g.y = wsf("p_qkv_skip", (size_t)QKVN);
+                    launch_dec_qkv_rope(g, re, st);
+                } else {
+                    stamped(SPAN_ATTN, l, [&] { launch_dec_qkv_attn(g, re, da, st); }, nullptr, 0);
+                }
+                attn_done = true;
+            } else {
+                launch_dec_qkv_rope(g, re, st);
+            }
         } else if (B <= 8) {
             launch_dec_gemv(g, st);
         } else {
@@ -1072,7 +1086,7 @@ void Engine::decode_step(int B, int Lmax) {
             g.x = XN; g.norm_w = nullptr;
             launch_dec_gemv(g, st);
         }
-        if (!(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
+        if (!attn_done && !(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
         // o_proj + residual
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
@@ -1171,6 +1185,13 @@ void Engine::ensure_mm_weights(int B) {
         }
     }
     HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+// one page: q/k/v projection + decode attention as one launch (dec_qkv_attn); DSOCR_QKV_ATTN=0 (A/B
+// switch, read once) keeps the two launches
+bool Engine::qkv_attn_fused() {
+    static const bool v = !(getenv("DSOCR_QKV_ATTN") && atoi(getenv("DSOCR_QKV_ATTN")) == 0);
+    return v;
 }
 
 // screened selection applies (lmhead.hip): int8 copy present, B <= 2, no repetition penalty
@@ -1411,6 +1432,10 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     {  // decode attention records: sentinel-filled before the first launch (the polling merge refills them)
         const size_t pf = dec_attn_workspace(B, L.heads, L.head_dim, Lmax) / 4 + 16;
         dec_attn_part_init(wsf("s_part", pf), pf * 4, st);
+        // the fused q/k/v + attention launch (one page) takes q / k / v by polling this row: sentinel-filled
+        const size_t qn = (size_t)B * layers_[0].qkv.N;
+        dec_qkv_sentinel_init(wsf("s_qkv", qn), qn, st);
+        wsf("p_qkv_skip", qn);  // the profile's variant without attention projects here (allocated before capture)
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
@@ -1749,6 +1774,10 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     HIP_CHECK(hipMemcpy(d_pos, pm1.data(), B * 4, hipMemcpyHostToDevice));
     prof.tokens = B;
     prof.kv_len = pm1[0] + 1;
+    {
+        const size_t qn = (size_t)B * layers_[0].qkv.N;
+        HIP_CHECK(hipMemsetAsync(wsf("p_qkv_attn", qn), 0, qn * 4, st));
+    }
     // n back-to-back launches captured in one hipGraph, replayed between two events on the
     // engine stream: per-launch time = span / n = device time + the dependent-kernel boundary
     // (eager launches go host-bound below ~3.5 us per kernel, MI355X_MICROARCH.md
@@ -1841,7 +1870,9 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         timed(prof.attention, n, [&](int i) {
             const int l = i % L.layers;
             DecAttn2Args da;
-            da.qkv = wsf("s_qkv", (size_t)B * QKVN); da.ld = QKVN; da.kv_pos = d_pos; da.B = B; da.heads = L.heads;
+            // a scratch q/k/v row (zeros): s_qkv holds the fused launch's sentinels, and the replays
+            // rewrite the K / V slot of pos - 1 from this row
+            da.qkv = wsf("p_qkv_attn", (size_t)B * QKVN); da.ld = QKVN; da.kv_pos = d_pos; da.B = B; da.heads = L.heads;
             da.kv_heads = L.kv_heads; da.hd = hd; da.rope_dim = L.rope_dim; da.use_mla = L.use_mla; da.max_len = Lmax;
             da.cos = rope_cos_; da.sin = rope_sin_;
             da.kc = kc_ + (long)l * B * page_stride_; da.vc = vc_ + (long)l * B * page_stride_;

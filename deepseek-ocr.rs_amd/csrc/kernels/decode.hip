@@ -515,13 +515,14 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
 // attention kernel's formula x*cos + sign*partner*sin.  One token (M = 1).
 // (Every wave normalising the row itself, without LDS or a block barrier, measured +0.75 us per layer:
 // the block-staged row is read from LDS, not re-read from L2 by each wave.)
-template <typename WT>
-__global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRopeEpi r) {
+// SC1: the rows are handed to attention blocks of the same launch (dec_qkv_attn): stored write-through
+template <typename WT, bool SC1>
+__device__ __forceinline__ void qkv_rope_body(const DecGemvArgs& a, const DecRopeEpi& r, int bid) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int U = 3, XR = 2;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int half = r.hd / 2;
-    const int p = blockIdx.x * 4 + wave;                 // pair index
+    const int p = bid * 4 + wave;                        // pair index
     const int npairs = a.N / 2;
     const bool active = p < npairs;
     const int pp = min(p, npairs - 1);
@@ -571,9 +572,19 @@ __global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRop
             y0 = o0;
             y1 = o1;
         }
-        a.y[n0] = y0;
-        a.y[n1] = y1;
+        if (SC1) {
+            __hip_atomic_store(a.y + n0, y0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.y + n1, y1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            a.y[n0] = y0;
+            a.y[n1] = y1;
+        }
     }
+}
+
+template <typename WT>
+__global__ __launch_bounds__(256) void dec_qkv_rope_kernel(DecGemvArgs a, DecRopeEpi r) {
+    qkv_rope_body<WT, false>(a, r, blockIdx.x);
 }
 
 bool dec_qkv_rope_ok(const DecGemvArgs& a, const DecRopeEpi& r) {
@@ -1048,9 +1059,13 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
-template <int HD, bool PREROT, bool POLL>
-__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
-    WaveSpan span_(a.span);
+// FUSED (dec_qkv_attn, one page, PREROT + POLL): q and the new k / v come from q/k/v blocks of the
+// same launch, stored write-through into a row that enters the launch sentinel-filled; this block
+// issues its K / V cache loads first, then polls its rows until no word holds the sentinel, and the
+// merging block (chunk 0) refills them once every chunk of the head has read them (its record is
+// written after that read).  The cache stream overlaps the projection's weight stream.
+template <int HD, bool PREROT, bool POLL, bool FUSED>
+__device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c, const int h, const int b) {
     constexpr int CH = DA_CH;
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
     constexpr int DPL = HD / LPK;                                // dims per lane when scoring
@@ -1063,7 +1078,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     __shared__ float red[8];
     __shared__ int last_s;
     __shared__ float4 o_s[384];  // P.V partials; reused by the combine (m, l per chunk + per-group sums)
-    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int k0 = c * CH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvh = h / (a.heads / a.kv_heads);
@@ -1102,7 +1116,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     };
     const float* row = a.qkv + (long)b * a.ld;
     float q_pre = 0.f, k_pre = 0.f, v_pre = 0.f;
-    if (PREROT) {  // unconditional (every thread loads a valid element): one round trip with pos
+    if (PREROT && !FUSED) {  // unconditional (every thread loads a valid element): one round trip with pos
         const int td = tid & (HD - 1);
         q_pre = row[h * HD + td];
         k_pre = row[a.heads * HD + kvh * HD + td];
@@ -1114,6 +1128,28 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     issue_k(k0, min(k0 + CH, len) - 1);
     issue_v(k0, min(k0 + CH, len) - 1);
     const bool own = pos >= k0 && pos < k0 + CH;
+    if constexpr (FUSED) {
+        // the head's q (and, owning the position, the new k / v) from this launch's projection blocks
+        const int td = tid & (HD - 1);
+        const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), (short)0,
+                                                          (a.heads + 2 * a.kv_heads) * HD * 4, 0x00020000);
+        const int oq = (h * HD + td) * 4, ok = ((a.heads + kvh) * HD + td) * 4,
+                  ov = ((a.heads + a.kv_heads + kvh) * HD + td) * 4;
+        for (unsigned it = 0;; ++it) {
+            asm volatile("" ::: "memory");
+            q_pre = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, oq, 0, 16));
+            k_pre = own ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok, 0, 16)) : 0.f;
+            v_pre = own ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ov, 0, 16)) : 0.f;
+            const bool pend = __float_as_uint(q_pre) == DA_SENT || __float_as_uint(k_pre) == DA_SENT ||
+                              __float_as_uint(v_pre) == DA_SENT;
+            if (!__syncthreads_or(pend)) break;
+            if (it > (1u << 20)) {
+                if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
     const int nc = (len + CH - 1) / CH;
     // 2. RoPE inputs
     const float* krow = row + a.heads * HD + kvh * HD;
@@ -1382,6 +1418,61 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
         for (int g = 0; g < KS; ++g) { at += accp[g * HD + tid]; lt += lp[g * HD + tid]; }
         a.o[(long)b * a.o_ld + (long)h * HD + tid] = at / lt;
     }
+    if constexpr (FUSED) {
+        // every chunk of this head has read its q / k / v (its record, merged above, came after): refill
+        if (tid < HD) {
+            const uint32_t sent = DA_SENT;
+            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), (short)0,
+                                                              (a.heads + 2 * a.kv_heads) * HD * 4, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(sent, rr, (h * HD + tid) * 4, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + kvh) * HD + tid) * 4, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + a.kv_heads + kvh) * HD + tid) * 4, 0, 16);
+        }
+    }
+}
+
+template <int HD, bool PREROT, bool POLL>
+__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
+    WaveSpan span_(a.span);
+    dec_attn_body<HD, PREROT, POLL, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// One page (MHA, 128-dim heads, <= 24 chunks): the q/k/v projection (qkv_rope_body, blocks [0, nq)) and
+// the decode attention (blocks nq + h * chunks + c) in ONE launch: the attention blocks stream their K / V
+// cache chunk while the projection blocks stream the q/k/v weights, then take q / k / v by polling
+// (FUSED above) - the kernel boundary between the two and the attention's load latency leave the chain.
+template <typename WT>
+__global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecGemvArgs g, DecRopeEpi r, DecAttn2Args a, int nq) {
+    WaveSpan span_(a.span);
+    if ((int)blockIdx.x < nq) {
+        qkv_rope_body<WT, true>(g, r, blockIdx.x);
+        return;
+    }
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    const int i = (int)blockIdx.x - nq;
+    dec_attn_body<128, true, true, true>(a, i % chunks, i / chunks, 0);
+}
+
+bool dec_qkv_attn_ok(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a) {
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    return dec_qkv_rope_ok(g, r) && a.B == 1 && a.hd == 128 && r.hd == 128 && a.heads == a.kv_heads && a.err &&
+           chunks <= 24 && a.max_len <= 512 * DA_CH && g.y == a.qkv && g.N == (a.heads + 2 * a.kv_heads) * a.hd &&
+           r.rot_rows == (a.heads + a.kv_heads) * a.hd;
+}
+
+void launch_dec_qkv_attn(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a, hipStream_t s) {
+    if (!dec_qkv_attn_ok(g, r, a)) throw std::runtime_error("EINVAL: dec_qkv_attn outside its range");
+    const int nq = (g.N / 2 + 3) / 4;
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    const size_t lds = stage_bytes(1, g.K);
+    dim3 grid(nq + chunks * a.heads);
+    if (g.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_qkv_attn_kernel<bf16_t>), grid, dim3(256), lds, s, g, r, a, nq);
+    else DSOCR_LAUNCH((dec_qkv_attn_kernel<f16_t>), grid, dim3(256), lds, s, g, r, a, nq);
+}
+
+void dec_qkv_sentinel_init(float* qkv, size_t floats, hipStream_t s) {
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(qkv), (int)DA_SENT, floats, s) != hipSuccess)
+        throw std::runtime_error("EINTERNAL: hipMemsetD32Async (q/k/v hand-off row)");
 }
 
 void dec_attn_part_init(float* part, size_t bytes, hipStream_t s) {

@@ -243,12 +243,14 @@ __device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
 // Wave layout: bf16 weights use 4 x 1 waves of 32 x 128 (each A row is split by exactly one wave; a
 // 2 x 2 layout splits every A fragment in two waves and the split VALU work, not the MFMAs, bounds
 // the k-step); f16 weights keep 2 x 2 of 64 x 64 (their W split would double instead).
-template <bool F16W, bool W22 = F16W>
+// NST = 1: one LDS stage (24 KB: four blocks per CU at <= 128 VGPRs), the latency of a block's stage
+// loads hidden by the other blocks of its CU instead of by a second stage
+template <bool F16W, bool W22 = F16W, int NST = 2>
 __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     constexpr int WN = W22 ? 2 : 1, WM = 4 / WN;     // waves along N / M
     constexpr int TI = FX_M / WM / 32, TJ = FX_N / WN / 32;
-    __shared__ __attribute__((aligned(16))) float a_lds[2 * FX_AS];
-    __shared__ __attribute__((aligned(16))) uint16_t w_lds[2 * FX_WS];
+    __shared__ __attribute__((aligned(16))) float a_lds[NST * FX_AS];
+    __shared__ __attribute__((aligned(16))) uint16_t w_lds[NST * FX_WS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int ntn = (g.N + FX_N - 1) / FX_N;
@@ -276,8 +278,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     // so the lane fetches the global chunk that the swizzle puts in that slot)
     auto issue = [&](int kt) {
         const int k0 = (kbeg + kt) * FX_K;
-        float* as = a_lds + (kt & 1) * FX_AS;
-        uint16_t* ws_ = w_lds + (kt & 1) * FX_WS;
+        float* as = a_lds + (NST == 1 ? 0 : (kt & 1) * FX_AS);
+        uint16_t* ws_ = w_lds + (NST == 1 ? 0 : (kt & 1) * FX_WS);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int R = (wave * 4 + i) * 8;
@@ -297,14 +299,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
                                              (lds_void*)(ws_ + R * FX_K), 16, 0, 0);
         }
     };
-    if (nk > 0) issue(0);
+    if (NST == 2 && nk > 0) issue(0);
     for (int kt = 0; kt < nk; ++kt) {
+        if (NST == 1) issue(kt);  // the stage is free: every wave passed the barrier after its last read
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage kt landed
         __builtin_amdgcn_s_barrier();  // every wave's stage kt landed; every wave is done with stage kt - 1
         asm volatile("" ::: "memory");
-        if (kt + 1 < nk) issue(kt + 1);  // into stage (kt - 1) & 1
-        const float* As = a_lds + (kt & 1) * FX_AS;
-        const uint16_t* Ws = w_lds + (kt & 1) * FX_WS;
+        if (NST == 2 && kt + 1 < nk) issue(kt + 1);  // into stage (kt - 1) & 1
+        const float* As = a_lds + (NST == 1 ? 0 : (kt & 1) * FX_AS);
+        const uint16_t* Ws = w_lds + (NST == 1 ? 0 : (kt & 1) * FX_WS);
 #pragma unroll
         for (int ks = 0; ks < FX_K / 16; ++ks) {
             const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of 4)
@@ -360,6 +363,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's reads done before the next barrier
+        if (NST == 1) {
+            __builtin_amdgcn_s_barrier();  // every wave's reads of the stage done before it is refilled
+            asm volatile("" ::: "memory");
+        }
     }
     const int half = lane >> 5, l32 = lane & 31;
     if (g.splits > 1) {
@@ -399,11 +406,14 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     }
 }
 
+// K slices: up to ~2 blocks per CU while every slice keeps >= 2 k-steps of 32 (tools/kbench vgemm: the CLIP
+// 257 / 404-row linears, the neck convolutions and the projector ran 1.2-1.3x faster at 4-8x the slices
+// of the former >= 16-step rule, the 6400-row K 3072 fc2 1.35x at 2 slices)
 int gemm_f32a_splits(int M, int N, int K) {
     const int tiles = ((M + FX_M - 1) / FX_M) * ((N + FX_N - 1) / FX_N);
     const int nk = K / FX_K;
     int sp = 1;
-    while (tiles * sp < 256 && nk / (sp * 2) >= 16) sp *= 2;
+    while (tiles * sp < 512 && nk / (sp * 2) >= 2) sp *= 2;
     return sp;
 }
 
@@ -412,16 +422,27 @@ bool gemm_f32a_ok(const GemmBf16Args& g) {
            (reinterpret_cast<uintptr_t>(g.W) & 15) == 0 && !g.out_bf16;
 }
 
+// DSOCR_GEMM_NST=2 (A/B switch, read once): the bf16-weight linears on the two-stage kernel
+static int gemm_nst_env() {
+    static const int v = getenv("DSOCR_GEMM_NST") ? atoi(getenv("DSOCR_GEMM_NST")) : 1;
+    return v;
+}
+
 void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     GemmBf16Args g = g0;
+    if (!g.variant) g.variant = gemm_nst_env();
     if (g.M <= 0 || g.N <= 0) return;
     if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
     // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once); f16 weights: 2 x 2 (their W split
     // would double under 4 x 1)
+    // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once), ONE LDS stage (24 KB, four blocks per
+    // CU: kbench vgemm 1.00-1.18x the two-stage kernel on the SAM linears, within 3 % elsewhere); f16
+    // weights: 2 x 2 (their W split would double under 4 x 1), two stages
     if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else if (g.variant == 2) hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 2>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 1>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) {
         const long n = (long)g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);

@@ -41,6 +41,7 @@ struct GemmBf16Args {
     // v = rnd(acc); bias: v = rnd(v + b); act: v = rnd(act(v)); accumulate: v = rnd(C + v)
     int out_bf16 = 0;
     int w_f16 = 0;  // gemm_f32a only: W holds f16 values (split into hi / lo bf16 in registers)
+    int variant = 0;  // gemm_f32a bf16 weights: 0 = default (one LDS stage), 2 = two stages (tools/kbench A/B)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
 int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)
@@ -248,6 +249,12 @@ struct DecRopeEpi {
 };
 bool dec_qkv_rope_ok(const DecGemvArgs& a, const DecRopeEpi& r);
 void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t s);
+// One page: q/k/v projection + RoPE and the decode attention in one launch (the attention blocks stream
+// their K / V chunk while the projection runs, then poll for q / k / v); the q/k/v row g.y == a.qkv must
+// enter the first launch sentinel-filled (dec_qkv_sentinel_init), every launch leaves it so
+bool dec_qkv_attn_ok(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a);
+void launch_dec_qkv_attn(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a, hipStream_t s);
+void dec_qkv_sentinel_init(float* qkv, size_t floats, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
 // the record buffer enters every dec_attn launch sentinel-filled (the polling merge refills what it reads)
 void dec_attn_part_init(float* part, size_t bytes, hipStream_t s);

@@ -383,12 +383,7 @@ def test_moe_decode_full_size_dispatch(gpu, T, H, E, topk, I, ns, norm):
     (H 1280, 64 experts, I 896, 2 shared = Is 1792) one token takes moe_gateup_mix + moe_down_mix,
     3..8 tokens the grouped kernels (each distinct expert streamed once) - vs the oracle's run_moe
     (block.rs:1215-1395), ids exact, outputs <= 1e-4."""
-    test_moe_decode_layer(gpu, _NoEnv(), T, H, E, topk, I, ns, norm, 0)
-
-
-class _NoEnv:
-    def setenv(self, *a):
-        pass
+    test_moe_decode_layer(gpu, T, H, E, topk, I, ns, norm)
 
 
 # ---------------------------------------------------------------- screened lm_head: ties / near ties

@@ -36,7 +36,7 @@ for step in "$@"; do
     spans1) run 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/spans1.log 2>&1 ;;
     spans8) run 600 python bench.py --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/spans8.log 2>&1 ;;
     # graph-mode kernel trace with the HIP runtime's graph packet capture off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0)
-    gprof_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_nopc -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_nopc.log 2>&1 ;;
+    gprof_nopc) DSOCR_SEGV_MAPS=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_nopc -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_nopc.log 2>&1 ;;
     gprof8_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8_nopc.log 2>&1 ;;
     # the round-2 crash reproduced with the maps dump (expected SIGSEGV: run it last)
     gprof_maps) DSOCR_SEGV_MAPS=1 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_maps.log 2>&1 ;;
@@ -51,6 +51,9 @@ for step in "$@"; do
     gprof64) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof64 -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline > gpurun_out/gprof64.log 2>&1 ;;
     gprof64_8) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof64_8 -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline > gpurun_out/gprof64_8.log 2>&1 ;;
     spans8t) run 600 python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/spans8t.log 2>&1 ;;
+    # tagged bench lines (TAG names the log; the caller's environment selects the A/B switches)
+    benchx) run 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench_${TAG:-x}.log 2>&1 ;;
+    bench8x) run 600 python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench8_${TAG:-x}.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done

@@ -301,6 +301,80 @@ static void case_lm(int M, hipStream_t s) {
     for (int i = 0; i < NB; ++i) { (void)hipFree(w[i]); (void)hipFree(ws[i]); }
 }
 
+// mean stream time of n back-to-back launches of an uninstrumented body (after one warm-up)
+static double time_plain(int n, const std::function<void()>& body, hipStream_t s) {
+    body();
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < n; ++i) body();
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    const double us = 1000.0 * ms_between(e0, e1) / n;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return us;
+}
+
+// vision linears (exact-f32 3-plane GEMM, bf16 weights) at the shapes one 1024 px page runs: every
+// pipeline variant (GemmBf16Args::variant) timed in interleaved rounds, outputs compared bitwise to
+// variant 1 (the k order per output element is the same in all of them)
+static void case_vgemm(hipStream_t s) {
+    struct Shape { int M, N, K; const char* what; };
+    const Shape shapes[] = {
+        {4900, 2304, 768, "sam1 qkv (windows)"}, {4096, 3072, 768, "sam1 fc1"}, {4096, 768, 3072, "sam1 fc2"},
+        {4900, 768, 768, "sam1 proj"}, {7056, 2304, 768, "sam4 qkv (windows)"}, {6400, 3072, 768, "sam4 fc1"},
+        {6400, 768, 3072, "sam4 fc2"}, {257, 3072, 1024, "clip1 qkv"}, {404, 4096, 1024, "clip4 fc1"},
+        {404, 1024, 4096, "clip4 fc2"}, {257, 1024, 1024, "clip1 out"}, {1024, 512, 2304, "net2"},
+        {256, 1024, 4608, "net3"}, {400, 1280, 2048, "projector"}};
+    // KB_VARIANTS: comma list of <variant>[x<split multiplier>] (e.g. 1,7,1x4,7x4)
+    const char* env = getenv("KB_VARIANTS");
+    std::vector<int> vars, smul;
+    for (const char* p = env ? env : "2,1,2x4,1x4"; *p;) {
+        vars.push_back(atoi(p));
+        while (*p && *p != ',' && *p != 'x') ++p;
+        smul.push_back(*p == 'x' ? atoi(p + 1) : 1);
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+    }
+    for (const Shape& sh : shapes) {
+        float* A = rand_f32((size_t)sh.M * sh.K);
+        uint16_t* W = rand_f16((size_t)sh.N * sh.K, 0.05f);  // bit patterns as bf16: any finite values do
+        float* bias = rand_f32(sh.N, 0.1f);
+        const int splits = gemm_f32a_splits(sh.M, sh.N, sh.K);
+        int max_mul = 1;
+        for (int m : smul) max_mul = std::max(max_mul, m);
+        float* part = (float*)dalloc((size_t)splits * max_mul * sh.M * sh.N * 4);
+        std::vector<float*> C(vars.size());
+        for (auto& c : C) c = (float*)dalloc((size_t)sh.M * sh.N * 4);
+        std::vector<std::vector<double>> us(vars.size());
+        const double flop = 2.0 * sh.M * sh.N * sh.K;
+        for (int round = 0; round < 3; ++round)
+            for (size_t v = 0; v < vars.size(); ++v) {
+                GemmBf16Args g;
+                g.M = sh.M; g.N = sh.N; g.K = sh.K; g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.bias = bias;
+                g.C = C[v]; g.ldc = sh.N; g.part = part; g.variant = vars[v];
+                g.splits = std::max(1, std::min(splits * smul[v], sh.K / 32 / 2));
+                us[v].push_back(time_plain(8, [&] { launch_gemm_f32a(g, s); }, s));
+            }
+        std::vector<float> ref((size_t)sh.M * sh.N), got(ref.size());
+        CK(hipMemcpy(ref.data(), C[0], ref.size() * 4, hipMemcpyDeviceToHost));
+        printf("vgemm %-20s M %5d N %5d K %5d splits %d:", sh.what, sh.M, sh.N, sh.K, splits);
+        for (size_t v = 0; v < vars.size(); ++v) {
+            CK(hipMemcpy(got.data(), C[v], got.size() * 4, hipMemcpyDeviceToHost));
+            const bool same = memcmp(ref.data(), got.data(), ref.size() * 4) == 0;
+            std::sort(us[v].begin(), us[v].end());
+            printf("  v%dx%d %7.1f us %5.0f TF%s", vars[v], smul[v], us[v][1], flop / us[v][1] / 1e6, same ? "" : " DIFF");
+        }
+        printf("\n");
+        fflush(stdout);
+        for (auto& c : C) (void)hipFree(c);
+        (void)hipFree(A); (void)hipFree(W); (void)hipFree(bias);
+        (void)hipFree(part);
+    }
+}
+
 int main(int argc, char** argv) {
     std::vector<std::string> cases;
     for (int i = 1; i < argc; ++i) cases.push_back(argv[i]);
@@ -316,6 +390,7 @@ int main(int argc, char** argv) {
         else if (c == "attn1") { case_attn(1, 706, s); case_attn(1, 1216, s); }
         else if (c == "attn8") { case_attn(8, 706, s); case_attn(8, 1216, s); }
         else if (c == "lm8") case_lm(8, s);
+        else if (c == "vgemm") case_vgemm(s);
         else fprintf(stderr, "unknown case %s\n", c.c_str());
         CK(hipStreamSynchronize(s));
     }
