@@ -312,12 +312,254 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
 #undef AT2_LSTORE
 }
 
+// attention_split: the same exact-f32 attention (64-dim heads, uniform sequences, no causal mask: the
+// SAM and CLIP towers) on the bf16 matrix cores.  Every f32 operand is split exactly into three bf16
+// planes x = hi + mid + lo (RNE at each step, residuals exact) and each product takes the six plane
+// pairs whose weight reaches the f32 rounding of the product (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi,
+// mid.mid; the dropped mid.lo, lo.mid, lo.lo are below 2^-24 of |x||y|): QK^T and P.V as 6 bf16 MFMA
+// passes each, 16x the f32-MFMA rate per pass, so 2.7x fewer MFMA cycles than attention_fwd2 for
+// the same f32-accurate result (summation order aside).  Layout as attention_bf16_tr_kernel: S^T = K.Q^T
+// (the lane's own query in the accumulator column), O^T = V^T.P^T with V stored row-major as planes and
+// read as the V^T operand through ds_read_b64_tr_b16; K / V planes split once per tile at staging
+// (the next tile's f32 loads in registers under the current tile's compute); SAM's decomposed rel-pos
+// bias from the block's table rows in LDS as in attention_fwd2.
+typedef __bf16 bf16x8s_t __attribute__((ext_vector_type(8)));
+typedef short v4i16s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16s_t lds_v4i16s;
+
+__device__ __forceinline__ void split3_bf16(float v, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)v;
+    const float r1 = v - (float)h;
+    m = (__bf16)r1;
+    l = (__bf16)(r1 - (float)m);
+}
+
+template <bool REL>
+__global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
+    constexpr int HD = 64, KT = 64;
+    constexpr int KP = HD + 8, VP = HD + 32;   // plane row pitches (bf16): VP keeps 4 rows on distinct banks
+    constexpr int QS = HD / 16, DC = HD / 32;
+    constexpr int F4 = KT * HD / 4 / 256;      // float4 per thread per operand per tile
+    __shared__ __attribute__((aligned(16))) uint16_t Kp[3][KT][KP];
+    __shared__ __attribute__((aligned(16))) uint16_t Vp[3][KT][VP];
+    __shared__ int rbh[KT], rbw[KT];
+    extern __shared__ __attribute__((aligned(16))) float rbs[];
+    const int s = blockIdx.z, h = blockIdx.y;
+    const int len = a.L;
+    const int qb0 = blockIdx.x * (4 * AT_Q);
+    if (qb0 >= len) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = lane >> 5, l32 = lane & 31;
+    const int kvh = h / (a.heads / a.kv_heads);
+    const float* Q = a.q.ptr + (long)s * a.L * a.q.row_stride + (long)h * a.q.head_stride;
+    const float* K = a.k.ptr + (long)s * a.L * a.k.row_stride + (long)kvh * a.k.head_stride;
+    const float* V = a.v.ptr + (long)s * a.L * a.v.row_stride + (long)kvh * a.v.head_stride;
+    const int q_lane = qb0 + wave * AT_Q + l32;
+    const bool q_valid = q_lane < len;
+    // this lane's query as three planes: dims 16 st + 8 half + j
+    bf16x8s_t qh[QS], qm[QS], ql[QS];
+    {
+        const float* qr = Q + (long)(q_valid ? q_lane : 0) * a.q.row_stride + 8 * half;
+#pragma unroll
+        for (int st = 0; st < QS; ++st) {
+            const float4 x0 = *reinterpret_cast<const float4*>(qr + 16 * st);
+            const float4 x1 = *reinterpret_cast<const float4*>(qr + 16 * st + 4);
+            const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __bf16 hh, mm, ll;
+                split3_bf16(xv[j], hh, mm, ll);
+                qh[st][j] = hh; qm[st][j] = mm; ql[st][j] = ll;
+            }
+        }
+    }
+    const int R = a.rel_h + a.rel_w, RP = R + 1;
+    const float* rb = nullptr;
+    if (REL) {
+        const float* tab = a.relbias + (((long)s * a.heads + h) * a.L) * R;
+        for (int i = tid; i < 4 * AT_Q * R; i += 256) {
+            const int qq = i / R, j = i % R;
+            rbs[qq * RP + j] = tab[(long)min(qb0 + qq, len - 1) * R + j];
+        }
+        rb = rbs + (wave * AT_Q + l32) * RP;
+    }
+    const int i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3, gd = 16 * ((lane >> 4) & 1);
+    float4 rk[F4], rv[F4];
+#define AS_GLOAD(K0)                                                                           \
+    _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
+        const int f = tid + 256 * j;                                                           \
+        const int key = min((K0) + f / (HD / 4), len - 1);                                     \
+        const int c4 = (f % (HD / 4)) * 4;                                                     \
+        rk[j] = *reinterpret_cast<const float4*>(K + (long)key * a.k.row_stride + c4);         \
+        rv[j] = *reinterpret_cast<const float4*>(V + (long)key * a.v.row_stride + c4);         \
+    }
+#define AS_PUT(P, KEY, C4, X)                                                                  \
+    {                                                                                          \
+        const float xv_[4] = {(X).x, (X).y, (X).z, (X).w};                                     \
+        uint16_t hb_[4], mb_[4], lb_[4];                                                       \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                        \
+            __bf16 hh, mm, ll;                                                                 \
+            split3_bf16(xv_[e], hh, mm, ll);                                                   \
+            __builtin_memcpy(&hb_[e], &hh, 2);                                                 \
+            __builtin_memcpy(&mb_[e], &mm, 2);                                                 \
+            __builtin_memcpy(&lb_[e], &ll, 2);                                                 \
+        }                                                                                      \
+        __builtin_memcpy(&P[0][KEY][C4], hb_, 8);                                              \
+        __builtin_memcpy(&P[1][KEY][C4], mb_, 8);                                              \
+        __builtin_memcpy(&P[2][KEY][C4], lb_, 8);                                              \
+    }
+#define AS_LSTORE(K0)                                                                          \
+    _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
+        const int f = tid + 256 * j;                                                           \
+        const int kr = f / (HD / 4), c4 = (f % (HD / 4)) * 4;                                  \
+        AS_PUT(Kp, kr, c4, rk[j]);                                                             \
+        AS_PUT(Vp, kr, c4, rv[j]);                                                             \
+    }                                                                                          \
+    if (REL && tid < KT) {                                                                     \
+        const int key = (K0) + tid;                                                            \
+        rbh[tid] = key / a.rel_w;                                                              \
+        rbw[tid] = a.rel_h + key % a.rel_w;                                                    \
+    }
+    f32x16 o[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    AS_GLOAD(0);
+    AS_LSTORE(0);
+    __syncthreads();
+    for (int k0 = 0; k0 < len; k0 += KT) {
+        AS_GLOAD(k0 + KT);  // unconditional (clamped keys): the next tile in flight under this one
+        f32x16 sc[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[u][r] = 0.f;
+#pragma unroll
+            for (int st = 0; st < QS; ++st) {
+                const int kr = u * 32 + l32, kc = 16 * st + 8 * half;
+                const bf16x8s_t kh = *reinterpret_cast<const bf16x8s_t*>(&Kp[0][kr][kc]);
+                const bf16x8s_t km = *reinterpret_cast<const bf16x8s_t*>(&Kp[1][kr][kc]);
+                const bf16x8s_t kl = *reinterpret_cast<const bf16x8s_t*>(&Kp[2][kr][kc]);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[st], sc[u], 0, 0, 0);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(km, qm[st], sc[u], 0, 0, 0);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], sc[u], 0, 0, 0);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(km, qh[st], sc[u], 0, 0, 0);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qm[st], sc[u], 0, 0, 0);
+                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], sc[u], 0, 0, 0);
+            }
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int kl = u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                float v = sc[u][r] * a.scale;
+                if (REL) v += rb[rbh[kl]] + rb[rbw[kl]];
+                if (k0 + kl >= len) v = -INFINITY;
+                sc[u][r] = v;
+                tmax = fmaxf(tmax, v);
+            }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = (m_new == -INFINITY) ? 0.f : __expf(sc[u][r] - m_new);
+                sc[u][r] = p;
+                psum += p;
+            }
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+        // O^T += V^T . P^T: the lane's P registers 8t .. 8t+7 of half u hold keys 32u + 16t + 4 half +
+        // {0..3, 8..11}; the transposed reads fetch exactly those rows of each V plane
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                bf16x8s_t ph, pm, pl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    __bf16 hh, mm, ll;
+                    split3_bf16(sc[u][8 * t + j], hh, mm, ll);
+                    ph[j] = hh; pm[j] = mm; pl[j] = ll;
+                }
+                const int kr0 = u * 32 + 16 * t + 4 * half + tq;
+#pragma unroll
+                for (int c = 0; c < DC; ++c) {
+                    const int d0 = c * 32 + gd + 4 * tp;
+                    bf16x8s_t vf[3];
+#pragma unroll
+                    for (int pl_ = 0; pl_ < 3; ++pl_) {
+                        const v4i16s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16s*)&Vp[pl_][kr0][d0]);
+                        const v4i16s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16s*)&Vp[pl_][kr0 + 8][d0]);
+                        __builtin_memcpy(&vf[pl_], &lo, 8);
+                        __builtin_memcpy(reinterpret_cast<char*>(&vf[pl_]) + 8, &hi, 8);
+                    }
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2], ph, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1], pm, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], pl, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1], ph, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], pm, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], ph, o[c], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // every wave is done with the tile before it is refilled
+        AS_LSTORE(k0 + KT);
+        __syncthreads();
+    }
+    if (q_valid) {
+        float* op = a.o + (long)s * a.L * a.o_row_stride + (long)q_lane * a.o_row_stride + (long)h * a.o_head_stride;
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) op[c * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = o[c][r] / l_run;
+    }
+#undef AS_GLOAD
+#undef AS_PUT
+#undef AS_LSTORE
+}
+
+// DSOCR_ATTN_SPLIT=0 (A/B switch, read once): the SAM / CLIP attention on the f32 MFMA (attention_fwd2)
+static bool attn_split_on() {
+    static const bool v = !(getenv("DSOCR_ATTN_SPLIT") && atoi(getenv("DSOCR_ATTN_SPLIT")) == 0);
+    return v;
+}
+
 void launch_attention(const AttnArgs& a, hipStream_t s) {
     int maxlen = a.L;
     dim3 grid((maxlen + 4 * AT_Q - 1) / (4 * AT_Q), a.heads, a.n_seq);
     if (grid.x == 0 || a.n_seq == 0) return;
     AttnArgs b = a;
     if (b.kv_heads == 0) b.kv_heads = b.heads;
+    if (a.hd == 64 && !a.causal && !a.seq_len && !a.q.seq_off && !a.k.seq_off && !a.v.seq_off && !a.o_seq_off &&
+        attn_split_on()) {
+        // the vision towers: exact-f32 products on the bf16 matrix cores (6 plane pairs)
+        const bool rel = b.relbias != nullptr;
+        const size_t lds = rel ? (size_t)4 * AT_Q * (b.rel_h + b.rel_w + 1) * 4 : 0;
+        static bool attr_s = false;
+        if (!attr_s) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_split_kernel<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 90 * 1024);
+            attr_s = true;
+        }
+        if (lds <= 90 * 1024) {
+            if (rel) hipLaunchKernelGGL((attention_split_kernel<true>), grid, dim3(256), lds, s, b);
+            else hipLaunchKernelGGL((attention_split_kernel<false>), grid, dim3(256), 0, s, b);
+            return;
+        }
+    }
     if (a.hd == 64 || a.hd == 128) {  // exact-f32 MFMA flash attention; other head dims: attention_fwd_kernel
         const bool rel = b.relbias != nullptr;
         const size_t lds = rel ? (size_t)4 * AT_Q * (b.rel_h + b.rel_w + 1) * 4 : 0;

@@ -11,9 +11,7 @@
 // Matrix cores), so the 3 + 1 passes cost a quarter of the f32-MFMA kernel's cycles.
 //
 // Layout: S^T = K . Q^T (the accumulator's column is the lane's own query: the online-softmax
-// rescale needs no cross-lane traffic), O^T = V^T . P^T with V staged transposed in LDS; the key
-// order inside each 16-key MFMA step is permuted (bits 2 and 3 of the key index swapped) so that the
-// 8 keys a lane's P registers hold are 8 contiguous LDS columns of V^T (one 16-byte read).
+// rescale needs no cross-lane traffic), O^T = V^T . P^T (V^T read from a row-major V image, below).
 // 4 waves x 32 queries per block, 64-key tiles in LDS, the next tile's global loads in registers
 // while the current one is consumed.
 #include <stdexcept>
@@ -28,9 +26,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 constexpr int AB_Q = 32;   // queries per wave
 constexpr int AB_KT = 64;  // keys per LDS tile
 
-// LDS column of key k (0..63) inside a V^T tile: within each 16-key step swap bits 2 and 3
-__device__ __forceinline__ int vt_col(int k) { return (k & ~15) | ((k & 4) << 1) | ((k & 8) >> 1) | (k & 3); }
-
 __device__ __forceinline__ uint16_t bf_bits(float v) {
     const __bf16 b = (__bf16)v;
     uint16_t u;
@@ -42,15 +37,26 @@ __device__ __forceinline__ uint16_t bf_bits(float v) {
 #define AB_EXP(x) __expf(x)
 #endif
 
+// V is staged ROW-major (16-byte writes, as loaded) and read as the V^T MFMA operand through
+// ds_read_b64_tr_b16 (the hardware transpose read, cdna_hip_programming.md T10): a 16-lane group reads 4
+// keys x 16 dims and each lane receives its dim's 4 keys; two reads give the 8 keys of the lane's P
+// registers (keys 16t + 4 half + {0..3, 8..11}: the accumulator order, no key permutation).  K and V
+// double-buffered in LDS: one barrier per tile.  V row pitch HD + 32 (4 consecutive rows on 4 distinct
+// 16-bank groups: the transposed reads are conflict-free).  Round 2's kernel staged V transposed with
+// 16-bit writes, two barriers per tile and spilled (256 VGPRs + 144 B scratch): 9.09 -> 5.86 ms per
+// layer at 2044 px (profiles/r03_bench_dots_*).
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16_t lds_v4i16;
+
 template <int HD>
-__global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) {
-    constexpr int KP = HD + 8, VP = AB_KT + 8;   // LDS row pitches (bf16 elements)
+__global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args a) {
+    constexpr int KP = HD + 8, VP = HD + 32;      // LDS row pitches (bf16 elements)
     constexpr int C8 = HD / 8;                    // 16-byte chunks per row
     constexpr int NCH = AB_KT * C8 / 256;         // chunks per thread per operand per tile
     constexpr int QS = HD / 16;                   // MFMA k-steps of the QK product
     constexpr int DC = HD / 32;                   // 32-dim output chunks
-    __shared__ __attribute__((aligned(16))) uint16_t Ks[AB_KT][KP];
-    __shared__ __attribute__((aligned(16))) uint16_t Vt[HD][VP];
+    __shared__ __attribute__((aligned(16))) uint16_t Ks[2][AB_KT][KP];
+    __shared__ __attribute__((aligned(16))) uint16_t Vs[2][AB_KT][VP];
     const int s = blockIdx.z, h = blockIdx.y;
     const int len = a.L;
     const int qb0 = blockIdx.x * (4 * AB_Q);
@@ -63,33 +69,28 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
     const uint16_t* V = a.v + (long)s * a.L * a.v_rs + (long)kvh * a.v_hs;
     const int q_lane = qb0 + wave * AB_Q + l32;
     const bool q_valid = q_lane < len;
-    // this lane's query: dims 16 st + 8 half .. + 8 for every k-step st
     bf16x8_t qreg[QS];
     {
         const uint16_t* qr = Q + (long)(q_valid ? q_lane : 0) * a.q_rs + 8 * half;
 #pragma unroll
         for (int st = 0; st < QS; ++st) qreg[st] = *reinterpret_cast<const bf16x8_t*>(qr + 16 * st);
     }
-    uint4 rk[NCH], rv[NCH];
-#define AB_GLOAD(K0)                                                                            \
+    // transposed-read lane roles: 16-lane group g16 (dims 16 (g16 & 1) + i), lane i = 4 q + p supplies
+    // row (key) q, dims 4 p .. 4 p + 3 of the group's 16-dim block
+    const int i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3, gd = 16 * ((lane >> 4) & 1);
+    // the next tile's K and V move through ONE register block in turn (K loaded before QK^T, stored
+    // before P.V; V loaded then, stored after P.V): 16 fewer live registers than both at once
+    uint4 rg[NCH];
+#define AB_GLOAD(P, RS, K0)                                                                     \
     _Pragma("unroll") for (int j = 0; j < NCH; ++j) {                                           \
         const int f = tid + 256 * j;                                                            \
         const int key = min((K0) + f / C8, len - 1);                                            \
-        const int c8 = f % C8;                                                                  \
-        rk[j] = *reinterpret_cast<const uint4*>(K + (long)key * a.k_rs + c8 * 8);               \
-        rv[j] = *reinterpret_cast<const uint4*>(V + (long)key * a.v_rs + c8 * 8);               \
+        rg[j] = *reinterpret_cast<const uint4*>((P) + (long)key * (RS) + (f % C8) * 8);         \
     }
-#define AB_LSTORE()                                                                             \
+#define AB_LSTORE(T)                                                                            \
     _Pragma("unroll") for (int j = 0; j < NCH; ++j) {                                           \
         const int f = tid + 256 * j;                                                            \
-        const int kr = f / C8, c8 = f % C8;                                                     \
-        *reinterpret_cast<uint4*>(&Ks[kr][c8 * 8]) = rk[j];                                     \
-        const int col = vt_col(kr);                                                             \
-        const uint32_t w4[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};                            \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                         \
-            Vt[c8 * 8 + 2 * i][col] = (uint16_t)(w4[i] & 0xffffu);                              \
-            Vt[c8 * 8 + 2 * i + 1][col] = (uint16_t)(w4[i] >> 16);                              \
-        }                                                                                       \
+        *reinterpret_cast<uint4*>(&(T)[f / C8][(f % C8) * 8]) = rg[j];                          \
     }
     f32x16 o[DC];
 #pragma unroll
@@ -97,12 +98,14 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
-    AB_GLOAD(0);
-    AB_LSTORE();
+    AB_GLOAD(K, a.k_rs, 0);
+    AB_LSTORE(Ks[0]);
+    AB_GLOAD(V, a.v_rs, 0);
+    AB_LSTORE(Vs[0]);
     __syncthreads();
-    for (int k0 = 0; k0 < len; k0 += AB_KT) {
-        AB_GLOAD(k0 + AB_KT);  // unconditional (clamped keys): the next tile's loads in flight
-        // S^T for the two 32-key halves of the tile
+    int buf = 0;
+    for (int k0 = 0; k0 < len; k0 += AB_KT, buf ^= 1) {
+        AB_GLOAD(K, a.k_rs, k0 + AB_KT);  // unconditional (clamped keys): in flight under QK^T and the softmax
         f32x16 sc[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
             for (int r = 0; r < 16; ++r) sc[u][r] = 0.f;
 #pragma unroll
             for (int st = 0; st < QS; ++st) {
-                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(&Ks[u * 32 + l32][16 * st + 8 * half]);
+                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(&Ks[buf][u * 32 + l32][16 * st + 8 * half]);
                 sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qreg[st], sc[u], 0, 0, 0);
             }
         }
@@ -127,8 +130,6 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
             }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float m_new = fmaxf(m_run, tmax);
-        // exp on the hardware exp2 with the log2(e) scale folded into one multiply (__expf: a few ulp
-        // from libm's expf; the tower's tolerance is set by its bf16 roundings)
         const float alpha = (m_new == -INFINITY) ? 1.f : AB_EXP(m_run - m_new);
         float psum = 0.f;
 #pragma unroll
@@ -146,8 +147,8 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
         for (int c = 0; c < DC; ++c)
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
-        // O^T += V^T . P^T: per 16-key step t of half u, the lane's P registers 8t .. 8t+7 (keys
-        // 32u + 16t + 4 half + {0..3, 8..11}) as three exact bf16 planes
+        AB_LSTORE(Ks[buf ^ 1]);            // the other buffer's last readers passed the previous barrier
+        AB_GLOAD(V, a.v_rs, k0 + AB_KT);   // in flight under P.V
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -163,17 +164,24 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_kernel(AttnBf16Args a) 
                     pm[j] = mi;
                     pl[j] = (__bf16)(r1 - (float)mi);
                 }
+                const int kr0 = u * 32 + 16 * t + 4 * half + tq;  // this lane's supplied row (+ 8 for j = 4..7)
 #pragma unroll
                 for (int c = 0; c < DC; ++c) {
-                    const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(&Vt[c * 32 + l32][u * 32 + 16 * t + 8 * half]);
+                    const int d0 = c * 32 + gd + 4 * tp;
+                    const v4i16_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)&Vs[buf][kr0][d0]);
+                    const v4i16_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)&Vs[buf][kr0 + 8][d0]);
+                    bf16x8_t vf;
+                    __builtin_memcpy(&vf, &lo, 8);
+                    __builtin_memcpy(reinterpret_cast<char*>(&vf) + 8, &hi, 8);
                     o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl, o[c], 0, 0, 0);
                     o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pm, o[c], 0, 0, 0);
                     o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, ph, o[c], 0, 0, 0);
                 }
             }
         }
-        __syncthreads();  // every wave is done with the tile before it is refilled
-        AB_LSTORE();
+        // the next tile into the other buffer (its last readers passed the previous barrier), then one
+        // barrier: the tile is visible and every wave is done with this buffer before it is refilled
+        AB_LSTORE(Vs[buf ^ 1]);
         __syncthreads();
     }
     if (q_valid) {
@@ -199,8 +207,8 @@ void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s) {
     if ((a.q_rs | a.k_rs | a.v_rs | a.q_hs | a.k_hs | a.v_hs) % 8)
         throw std::runtime_error("EINVAL: attention_bf16 needs 16-byte aligned rows");
     dim3 grid((a.L + 4 * AB_Q - 1) / (4 * AB_Q), a.heads, a.n_seq);
-    if (a.hd == 128) DSOCR_LAUNCH(attention_bf16_kernel<128>, grid, dim3(256), 0, s, a);
-    else DSOCR_LAUNCH(attention_bf16_kernel<64>, grid, dim3(256), 0, s, a);
+    if (a.hd == 128) DSOCR_LAUNCH(attention_bf16_tr_kernel<128>, grid, dim3(256), 0, s, a);
+    else DSOCR_LAUNCH(attention_bf16_tr_kernel<64>, grid, dim3(256), 0, s, a);
 }
 
 }  // namespace dsocr

@@ -245,21 +245,22 @@ __device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
 // the k-step); f16 weights keep 2 x 2 of 64 x 64 (their W split would double instead).
 // NST = 1: one LDS stage (24 KB: four blocks per CU at <= 128 VGPRs), the latency of a block's stage
 // loads hidden by the other blocks of its CU instead of by a second stage
-template <bool F16W, bool W22 = F16W, int NST = 2>
+template <bool F16W, bool W22 = F16W, int NST = 2, int BN = FX_N>  // (BN 256 measured slower on every vision shape)
 __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     constexpr int WN = W22 ? 2 : 1, WM = 4 / WN;     // waves along N / M
-    constexpr int TI = FX_M / WM / 32, TJ = FX_N / WN / 32;
+    constexpr int TI = FX_M / WM / 32, TJ = BN / WN / 32;
+    constexpr int WS = BN * FX_K;  // bf16 elements of a W stage
     __shared__ __attribute__((aligned(16))) float a_lds[NST * FX_AS];
-    __shared__ __attribute__((aligned(16))) uint16_t w_lds[NST * FX_WS];
+    __shared__ __attribute__((aligned(16))) uint16_t w_lds[NST * WS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
-    const int ntn = (g.N + FX_N - 1) / FX_N;
+    const int ntn = (g.N + BN - 1) / BN;
     const int nwg = gridDim.x;
     const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
     const int split = wgid % g.splits, tile = wgid / g.splits;
     const int bm = tile / ntn, bn = tile % ntn;
-    const int m0 = bm * FX_M, n0 = bn * FX_N;
+    const int m0 = bm * FX_M, n0 = bn * BN;
     const float* A = reinterpret_cast<const float*>(g.A);
     const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
     f32x16 acc[TI][TJ];
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     auto issue = [&](int kt) {
         const int k0 = (kbeg + kt) * FX_K;
         float* as = a_lds + (NST == 1 ? 0 : (kt & 1) * FX_AS);
-        uint16_t* ws_ = w_lds + (NST == 1 ? 0 : (kt & 1) * FX_WS);
+        uint16_t* ws_ = w_lds + (NST == 1 ? 0 : (kt & 1) * WS);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int R = (wave * 4 + i) * 8;
@@ -290,8 +291,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
                                              (lds_void*)(as + R * FX_K), 16, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int R = (wave * 2 + i) * 16;
+        for (int i = 0; i < BN / 64; ++i) {
+            const int R = (wave * (BN / 64) + i) * 16;
             const int r = R + (lane >> 2);
             const int j = (lane & 3) ^ ((r >> 2) & 3);
             const long row = min(n0 + r, g.N - 1);
@@ -307,14 +308,14 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
         asm volatile("" ::: "memory");
         if (NST == 2 && kt + 1 < nk) issue(kt + 1);  // into stage (kt - 1) & 1
         const float* As = a_lds + (NST == 1 ? 0 : (kt & 1) * FX_AS);
-        const uint16_t* Ws = w_lds + (NST == 1 ? 0 : (kt & 1) * FX_WS);
+        const uint16_t* Ws = w_lds + (NST == 1 ? 0 : (kt & 1) * WS);
 #pragma unroll
         for (int ks = 0; ks < FX_K / 16; ++ks) {
             const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of 4)
             bf16x8_v bfv[TJ], blo[TJ];
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
-                const int r = wn * (FX_N / WN) + j * 32 + (lane & 31);
+                const int r = wn * (BN / WN) + j * 32 + (lane & 31);
                 if constexpr (F16W) {
                     const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
                     float wv[8], wh[8], wl[8];
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
         for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
-                const int col = n0 + wn * (FX_N / WN) + j * 32 + l32;
+                const int col = n0 + wn * (BN / WN) + j * 32 + l32;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = m0 + wm * (FX_M / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     for (int i = 0; i < TI; ++i) {
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-            const int col = n0 + wn * (FX_N / WN) + j * 32 + l32;
+            const int col = n0 + wn * (BN / WN) + j * 32 + l32;
             if (col >= g.N) continue;
             const float bv = g.bias ? g.bias[col] : 0.f;
 #pragma unroll

@@ -18,7 +18,7 @@ for step in "$@"; do
     gprof) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof.log 2>&1 ;;
     gprof8) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8 -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8.log 2>&1 ;;
     dots) run 900 python -u -m pytest tests/test_dots.py -q -m gpu -rf -p no:cacheprovider --timeout 600 --timeout-method thread -s > gpurun_out/dots.log 2>&1 ;;
-    benchdots) run 900 python bench.py --workload dots2048 --steps 2 --warmup 1 > gpurun_out/benchdots.log 2>&1 ;;
+    benchdots) run 900 python bench.py --workload dots2048 --steps 2 --warmup 1 > gpurun_out/benchdots${TAG:+_$TAG}.log 2>&1 ;;
     prof1) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o b1 --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof1.log 2>&1 ;;
     prof8) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o b8 --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof8.log 2>&1 ;;
     profdots) run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profdots -o dots --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 1 > gpurun_out/profdots.log 2>&1 ;;
@@ -45,6 +45,7 @@ for step in "$@"; do
     gprof8_full) run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8_full -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/gprof8_full.log 2>&1 ;;
     gprof128) run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof128 -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 128 --no-cpu-baseline > gpurun_out/gprof128.log 2>&1 ;;
     gprof_full_maps) DSOCR_SEGV_MAPS=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_full_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/gprof_full_maps.log 2>&1 ;;
+    kattn) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "attention" > gpurun_out/kattn.log 2>&1 ;;
     katt) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k decode_attention > gpurun_out/katt.log 2>&1 ;;
     kb_attn) run 120 ./tools/kbench attn1 attn8 > gpurun_out/kb_attn.log 2>&1 ;;
     # graph-mode kernel trace short enough that the AQL ring never wraps under the profiler
