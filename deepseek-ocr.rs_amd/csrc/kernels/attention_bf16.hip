@@ -14,6 +14,7 @@
 // rescale needs no cross-lane traffic), O^T = V^T . P^T (V^T read from a row-major V image, below).
 // 4 waves x 32 queries per block, 64-key tiles in LDS, the next tile's global loads in registers
 // while the current one is consumed.
+#include <algorithm>
 #include <stdexcept>
 
 #include "dev_common.hpp"
@@ -79,33 +80,41 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
     // row (key) q, dims 4 p .. 4 p + 3 of the group's 16-dim block
     const int i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3, gd = 16 * ((lane >> 4) & 1);
     // the next tile's K and V move through ONE register block in turn (K loaded before QK^T, stored
-    // before P.V; V loaded then, stored after P.V): 16 fewer live registers than both at once
-    uint4 rg[NCH];
-#define AB_GLOAD(P, RS, K0)                                                                     \
-    _Pragma("unroll") for (int j = 0; j < NCH; ++j) {                                           \
-        const int f = tid + 256 * j;                                                            \
-        const int key = min((K0) + f / C8, len - 1);                                            \
-        rg[j] = *reinterpret_cast<const uint4*>((P) + (long)key * (RS) + (f % C8) * 8);         \
-    }
+    // before P.V; V loaded then, stored after P.V): 16 fewer live registers than both at once.  Buffer
+    // loads bounded at the sequence's last key: keys past it read as zeros (K: scores masked below; V:
+    // zero rows), so no tile clamps or branches; per lane one offset (row tid / C8 (+ 256 / C8 per j),
+    // 16-byte chunk tid % C8) plus the tile's uniform row offset.
+    u32x4 rg[NCH];
+    const auto rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(K), (short)0, len * a.k_rs * 2, 0x00020000);
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(V), (short)0, len * a.v_rs * 2, 0x00020000);
+    const int ko = ((tid / C8) * a.k_rs + (tid % C8) * 8) * 2;
+    const int vo = ((tid / C8) * a.v_rs + (tid % C8) * 8) * 2;
+#define AB_GLOAD(R, RS, OFF, K0)                                                                \
+    _Pragma("unroll") for (int j = 0; j < NCH; ++j)                                             \
+        rg[j] = __builtin_amdgcn_raw_buffer_load_b128((R), (OFF) + ((K0) + j * (256 / C8)) * (RS) * 2, 0, 0);
 #define AB_LSTORE(T)                                                                            \
     _Pragma("unroll") for (int j = 0; j < NCH; ++j) {                                           \
         const int f = tid + 256 * j;                                                            \
-        *reinterpret_cast<uint4*>(&(T)[f / C8][(f % C8) * 8]) = rg[j];                          \
+        *reinterpret_cast<u32x4*>(&(T)[f / C8][(f % C8) * 8]) = rg[j];                          \
     }
     f32x16 o[DC];
 #pragma unroll
     for (int c = 0; c < DC; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+    // softmax in the log2 domain: p = 2^(s * scale * log2 e - m), m the running max of s * scale * log2 e
+    // (one FMA per score before the exponential; every tile holds a valid key, so m is finite after the
+    // first and alpha = 2^(m_old - m_new) = 0 there)
+    const float c2 = a.scale * 1.4426950408889634f;
     float m_run = -INFINITY, l_run = 0.f;
-    AB_GLOAD(K, a.k_rs, 0);
+    AB_GLOAD(rk, a.k_rs, ko, 0);
     AB_LSTORE(Ks[0]);
-    AB_GLOAD(V, a.v_rs, 0);
+    AB_GLOAD(rv, a.v_rs, vo, 0);
     AB_LSTORE(Vs[0]);
     __syncthreads();
     int buf = 0;
     for (int k0 = 0; k0 < len; k0 += AB_KT, buf ^= 1) {
-        AB_GLOAD(K, a.k_rs, k0 + AB_KT);  // unconditional (clamped keys): in flight under QK^T and the softmax
+        AB_GLOAD(rk, a.k_rs, ko, k0 + AB_KT);  // in flight under QK^T and the softmax
         f32x16 sc[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -117,53 +126,62 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
                 sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qreg[st], sc[u], 0, 0, 0);
             }
         }
+        if (k0 + AB_KT > len) {  // the last, partial tile: keys past the end score -inf
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= len) sc[u][r] = -INFINITY;
+        }
         float tmax = -INFINITY;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                float v = sc[u][r] * a.scale;
-                if (key >= len) v = -INFINITY;
-                sc[u][r] = v;
-                tmax = fmaxf(tmax, v);
-            }
+            for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float m_new = fmaxf(m_run, tmax);
-        const float alpha = (m_new == -INFINITY) ? 1.f : AB_EXP(m_run - m_new);
+        const float m_new = fmaxf(m_run, tmax * c2);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         float psum = 0.f;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = (m_new == -INFINITY) ? 0.f : AB_EXP(sc[u][r] - m_new);
+                const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c2, -m_new));
                 sc[u][r] = p;
                 psum += p;
             }
         psum += __shfl_xor(psum, 32, 64);
         l_run = l_run * alpha + psum;
         m_run = m_new;
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {  // some query's max moved (rare after the first tiles)
 #pragma unroll
-        for (int c = 0; c < DC; ++c)
+            for (int c = 0; c < DC; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
-        AB_LSTORE(Ks[buf ^ 1]);            // the other buffer's last readers passed the previous barrier
-        AB_GLOAD(V, a.v_rs, k0 + AB_KT);   // in flight under P.V
+                for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+        }
+        AB_LSTORE(Ks[buf ^ 1]);                // the other buffer's last readers passed the previous barrier
+        AB_GLOAD(rv, a.v_rs, vo, k0 + AB_KT);   // in flight under P.V
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                bf16x8_t ph, pm, pl;
+                // p = hi + mid + lo exactly: hi = p with its low 16 bits cleared (bf16 truncation), mid the
+                // same of the exact residual, lo the remaining <= 8 significant bits (a bf16 exactly); two
+                // bf16 of a plane packed per register by one byte permute
+                u32x4 ph, pm, pl;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float p = sc[u][8 * t + j];
-                    const __bf16 hi = (__bf16)p;
-                    const float r1 = p - (float)hi;
-                    const __bf16 mi = (__bf16)r1;
-                    ph[j] = hi;
-                    pm[j] = mi;
-                    pl[j] = (__bf16)(r1 - (float)mi);
+                for (int q = 0; q < 4; ++q) {
+                    const float p0 = sc[u][8 * t + 2 * q], p1 = sc[u][8 * t + 2 * q + 1];
+                    const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
+                    const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
+                    const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+                    const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+                    ph[q] = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+                    pm[q] = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
+                    pl[q] = __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u);
                 }
+                const bf16x8_t fh = __builtin_bit_cast(bf16x8_t, ph), fm = __builtin_bit_cast(bf16x8_t, pm),
+                               fl = __builtin_bit_cast(bf16x8_t, pl);
                 const int kr0 = u * 32 + 16 * t + 4 * half + tq;  // this lane's supplied row (+ 8 for j = 4..7)
 #pragma unroll
                 for (int c = 0; c < DC; ++c) {
@@ -173,9 +191,9 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
                     bf16x8_t vf;
                     __builtin_memcpy(&vf, &lo, 8);
                     __builtin_memcpy(reinterpret_cast<char*>(&vf) + 8, &hi, 8);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pm, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, ph, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fl, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fm, o[c], 0, 0, 0);
+                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fh, o[c], 0, 0, 0);
                 }
             }
         }
@@ -206,6 +224,8 @@ void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s) {
     if (a.kv_heads <= 0 || a.heads % a.kv_heads) throw std::runtime_error("EINVAL: heads must be a multiple of kv_heads");
     if ((a.q_rs | a.k_rs | a.v_rs | a.q_hs | a.k_hs | a.v_hs) % 8)
         throw std::runtime_error("EINVAL: attention_bf16 needs 16-byte aligned rows");
+    if ((long)(a.L + AB_KT) * std::max(a.k_rs, a.v_rs) * 2 >= (1L << 31))
+        throw std::runtime_error("EINVAL: attention_bf16 sequence slice beyond 32-bit buffer offsets");
     dim3 grid((a.L + 4 * AB_Q - 1) / (4 * AB_Q), a.heads, a.n_seq);
     if (a.hd == 128) DSOCR_LAUNCH(attention_bf16_tr_kernel<128>, grid, dim3(256), 0, s, a);
     else DSOCR_LAUNCH(attention_bf16_tr_kernel<64>, grid, dim3(256), 0, s, a);

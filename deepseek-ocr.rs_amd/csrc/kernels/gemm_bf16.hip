@@ -64,8 +64,9 @@ __device__ __forceinline__ void bf16_store_epilogue(const GemmBf16Args& g, long 
     *cp = (__bf16)v;
 }
 
+template <int NST>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
-    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * TB_STAGE];
+    __shared__ __attribute__((aligned(16))) uint16_t smem[NST * TB_STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     // XCD-aware tile order (bijective; blocks b and b + 8 share an XCD): consecutive tiles of one
@@ -91,13 +92,16 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
     const int kbeg = (int)((long)nk_all * split / g.splits), kend = (int)((long)nk_all * (split + 1) / g.splits);
     const int nk = kend - kbeg;
     auto issue = [&](int kt) {
-        uint16_t* st = smem + (kt & 1) * TB_STAGE;
+        uint16_t* st = smem + (NST == 1 ? 0 : (kt & 1) * TB_STAGE);
         stage_tile(A, g.lda, m0, g.M - 1, (kbeg + kt) * TB_K, st, wave, lane);
         stage_tile(W, g.ldw, n0, g.N - 1, (kbeg + kt) * TB_K, st + TB_M * TB_K, wave, lane);
     };
-    if (nk > 0) issue(0);
+    if (NST == 2 && nk > 0) issue(0);
     for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) {
+        if (NST == 1) {  // one stage: the other blocks of the CU hide this block's stage loads
+            issue(kt);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (kt + 1 < nk) {
             issue(kt + 1);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage kt landed (8 DMAs of kt+1 in flight)
         } else {
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        const uint16_t* As = smem + (kt & 1) * TB_STAGE;
+        const uint16_t* As = smem + (NST == 1 ? 0 : (kt & 1) * TB_STAGE);
         const uint16_t* Bs = As + TB_M * TB_K;
 #pragma unroll
         for (int ks = 0; ks < TB_K / 16; ++ks) {
@@ -203,7 +207,10 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
         throw std::runtime_error("EINVAL: gemm_bf16 needs K % 64 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);
-    hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    // one LDS stage unless variant 2 (tools/kbench dgemm A/B: 1.2-1.4x on the dots.ocr linears,
+    // profiles/r03_kbench_dgemm.log; bitwise equal results)
+    if (g.variant == 2) hipLaunchKernelGGL(gemm_bf16_nt_kernel<2>, dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL(gemm_bf16_nt_kernel<1>, dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) {
         const long n = (long)g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);

@@ -375,6 +375,43 @@ static void case_vgemm(hipStream_t s) {
     }
 }
 
+// dots.ocr tower linears (bf16 x bf16 -> bf16 epilogue, gemm_bf16_nt) at the 2044 px page's 21316 rows:
+// variant 1 (one LDS stage, the default) vs 2 (two stages), interleaved rounds, outputs compared bitwise
+// (a 256 x 256 eight-wave tile measured 0.7x of variant 1 here and was dropped: profiles/r03_kbench_dgemm.log)
+static void case_dgemm(hipStream_t s) {
+    struct Shape { int M, N, K; const char* what; };
+    const Shape shapes[] = {{21316, 4608, 1536, "qkv"}, {21316, 1536, 1536, "proj"}, {21316, 8448, 1536, "fc1|fc3"},
+                            {21316, 1536, 4224, "fc2"}};
+    const int vars[2] = {1, 2};
+    for (const Shape& sh : shapes) {
+        uint16_t* A = rand_f16((size_t)sh.M * sh.K, 0.5f);
+        uint16_t* W = rand_f16((size_t)sh.N * sh.K, 0.05f);
+        float* bias = rand_f32(sh.N, 0.1f);
+        uint16_t* C[2] = {(uint16_t*)dalloc((size_t)sh.M * sh.N * 2), (uint16_t*)dalloc((size_t)sh.M * sh.N * 2)};
+        std::vector<double> us[2];
+        const double flop = 2.0 * sh.M * sh.N * sh.K;
+        for (int round = 0; round < 3; ++round)
+            for (int v = 0; v < 2; ++v) {
+                GemmBf16Args g;
+                g.M = sh.M; g.N = sh.N; g.K = sh.K; g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.bias = bias;
+                g.C = reinterpret_cast<float*>(C[v]); g.ldc = sh.N; g.out_bf16 = 1; g.variant = vars[v];
+                us[v].push_back(time_plain(4, [&] { launch_gemm_bf16(g, s); }, s));
+            }
+        std::vector<uint16_t> r1((size_t)sh.M * sh.N), r2(r1.size());
+        CK(hipMemcpy(r1.data(), C[0], r1.size() * 2, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(r2.data(), C[1], r2.size() * 2, hipMemcpyDeviceToHost));
+        printf("dgemm %-8s M %5d N %5d K %5d:", sh.what, sh.M, sh.N, sh.K);
+        for (int v = 0; v < 2; ++v) {
+            std::sort(us[v].begin(), us[v].end());
+            printf("  v%d %8.1f us %5.0f TF", vars[v], us[v][1], flop / us[v][1] / 1e6);
+        }
+        printf("  v1==v2 %s\n", memcmp(r1.data(), r2.data(), r1.size() * 2) ? "NO" : "yes");
+        fflush(stdout);
+        for (auto* c : C) (void)hipFree(c);
+        (void)hipFree(A); (void)hipFree(W); (void)hipFree(bias);
+    }
+}
+
 int main(int argc, char** argv) {
     std::vector<std::string> cases;
     for (int i = 1; i < argc; ++i) cases.push_back(argv[i]);
@@ -391,6 +428,7 @@ int main(int argc, char** argv) {
         else if (c == "attn8") { case_attn(8, 706, s); case_attn(8, 1216, s); }
         else if (c == "lm8") case_lm(8, s);
         else if (c == "vgemm") case_vgemm(s);
+        else if (c == "dgemm") case_dgemm(s);
         else fprintf(stderr, "unknown case %s\n", c.c_str());
         CK(hipStreamSynchronize(s));
     }
