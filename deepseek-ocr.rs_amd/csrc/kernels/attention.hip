@@ -12,6 +12,7 @@
 // 2. sam_relbias: per-query rel-pos dot products q.Rh / q.Rw.
 // 3. rope_kv: rotate_half RoPE (block.rs:1403-1471) + KV-cache append (prefill rows;
 //    the decode step fuses both into dec_attn_kernel, decode.hip).
+#include <algorithm>
 #include <cstdlib>
 
 #include "dev_common.hpp"
@@ -384,18 +385,22 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
         rb = rbs + (wave * AT_Q + l32) * RP;
     }
     const int i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3, gd = 16 * ((lane >> 4) & 1);
-    float4 rk[F4], rv[F4];
+    // next tile's K / V in registers: buffer loads bounded at the sequence's last key (keys past it read
+    // as zeros: no clamps), one per-lane offset plus the tile's uniform row offset
+    f32x4 rk[F4], rv[F4];
+    const auto rsk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(K), (short)0, len * a.k.row_stride * 4, 0x00020000);
+    const auto rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(V), (short)0, len * a.v.row_stride * 4, 0x00020000);
+    const int ko = ((tid / (HD / 4)) * a.k.row_stride + (tid % (HD / 4)) * 4) * 4;
+    const int vo = ((tid / (HD / 4)) * a.v.row_stride + (tid % (HD / 4)) * 4) * 4;
 #define AS_GLOAD(K0)                                                                           \
     _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
-        const int f = tid + 256 * j;                                                           \
-        const int key = min((K0) + f / (HD / 4), len - 1);                                     \
-        const int c4 = (f % (HD / 4)) * 4;                                                     \
-        rk[j] = *reinterpret_cast<const float4*>(K + (long)key * a.k.row_stride + c4);         \
-        rv[j] = *reinterpret_cast<const float4*>(V + (long)key * a.v.row_stride + c4);         \
+        const int kr_ = (K0) + j * (256 / (HD / 4));                                           \
+        rk[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsk, ko + kr_ * a.k.row_stride * 4, 0, 0)); \
+        rv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsv, vo + kr_ * a.v.row_stride * 4, 0, 0)); \
     }
 #define AS_PUT(P, KEY, C4, X)                                                                  \
     {                                                                                          \
-        const float xv_[4] = {(X).x, (X).y, (X).z, (X).w};                                     \
+        const float xv_[4] = {(X)[0], (X)[1], (X)[2], (X)[3]};                                 \
         uint16_t hb_[4], mb_[4], lb_[4];                                                       \
         _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                        \
             __bf16 hh, mm, ll;                                                                 \
@@ -425,12 +430,13 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
     for (int c = 0; c < DC; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+    const float c2 = (REL ? 1.f : a.scale) * 1.4426950408889634f;  // score -> log2 units
     float m_run = -INFINITY, l_run = 0.f;
     AS_GLOAD(0);
     AS_LSTORE(0);
     __syncthreads();
     for (int k0 = 0; k0 < len; k0 += KT) {
-        AS_GLOAD(k0 + KT);  // unconditional (clamped keys): the next tile in flight under this one
+        AS_GLOAD(k0 + KT);  // the next tile in flight under this one
         f32x16 sc[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -450,50 +456,71 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
                 sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], sc[u], 0, 0, 0);
             }
         }
-        float tmax = -INFINITY;
+        // softmax in the log2 domain (p = 2^(v c - m), one FMA before the exponential; every tile holds a
+        // valid key, so m is finite after the first tile and alpha = 0 there); SAM adds its rel-pos bias
+        // to the scaled score first, as the reference does
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int kl = u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                float v = sc[u][r] * a.scale;
-                if (REL) v += rb[rbh[kl]] + rb[rbw[kl]];
-                if (k0 + kl >= len) v = -INFINITY;
-                sc[u][r] = v;
-                tmax = fmaxf(tmax, v);
+                if (REL) sc[u][r] = fmaf(sc[u][r], a.scale, rb[rbh[kl]] + rb[rbw[kl]]);
             }
+        if (k0 + KT > len) {  // the last, partial tile
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= len) sc[u][r] = -INFINITY;
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float m_new = fmaxf(m_run, tmax);
-        const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+        const float m_new = fmaxf(m_run, tmax * c2);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         float psum = 0.f;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = (m_new == -INFINITY) ? 0.f : __expf(sc[u][r] - m_new);
+                const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c2, -m_new));
                 sc[u][r] = p;
                 psum += p;
             }
         psum += __shfl_xor(psum, 32, 64);
         l_run = l_run * alpha + psum;
         m_run = m_new;
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
-        for (int c = 0; c < DC; ++c)
+            for (int c = 0; c < DC; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+                for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+        }
         // O^T += V^T . P^T: the lane's P registers 8t .. 8t+7 of half u hold keys 32u + 16t + 4 half +
         // {0..3, 8..11}; the transposed reads fetch exactly those rows of each V plane
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                bf16x8s_t ph, pm, pl;
+                // p = hi + mid + lo exactly by truncation (low 16 bits cleared, twice; the rest has <= 8
+                // significant bits), two bf16 of a plane packed per register by one byte permute
+                f32x4 phv, pmv, plv;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    __bf16 hh, mm, ll;
-                    split3_bf16(sc[u][8 * t + j], hh, mm, ll);
-                    ph[j] = hh; pm[j] = mm; pl[j] = ll;
+                for (int q = 0; q < 4; ++q) {
+                    const float p0 = sc[u][8 * t + 2 * q], p1 = sc[u][8 * t + 2 * q + 1];
+                    const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
+                    const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
+                    const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+                    const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+                    phv[q] = __uint_as_float(__builtin_amdgcn_perm(b1, b0, 0x07060302u));
+                    pmv[q] = __uint_as_float(__builtin_amdgcn_perm(c1, c0, 0x07060302u));
+                    plv[q] = __uint_as_float(__builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u));
                 }
+                const bf16x8s_t ph = __builtin_bit_cast(bf16x8s_t, phv), pm = __builtin_bit_cast(bf16x8s_t, pmv),
+                                pl = __builtin_bit_cast(bf16x8s_t, plv);
                 const int kr0 = u * 32 + 16 * t + 4 * half + tq;
 #pragma unroll
                 for (int c = 0; c < DC; ++c) {
@@ -544,7 +571,7 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
     AttnArgs b = a;
     if (b.kv_heads == 0) b.kv_heads = b.heads;
     if (a.hd == 64 && !a.causal && !a.seq_len && !a.q.seq_off && !a.k.seq_off && !a.v.seq_off && !a.o_seq_off &&
-        attn_split_on()) {
+        (long)(a.L + 64) * std::max(a.k.row_stride, a.v.row_stride) * 4 < (1L << 31) && attn_split_on()) {
         // the vision towers: exact-f32 products on the bf16 matrix cores (6 plane pairs)
         const bool rel = b.relbias != nullptr;
         const size_t lds = rel ? (size_t)4 * AT_Q * (b.rel_h + b.rel_w + 1) * 4 : 0;

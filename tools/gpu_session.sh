@@ -55,6 +55,8 @@ for step in "$@"; do
     # tagged bench lines (TAG names the log; the caller's environment selects the A/B switches)
     benchx) run 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench_${TAG:-x}.log 2>&1 ;;
     bench8x) run 600 python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench8_${TAG:-x}.log 2>&1 ;;
+    benchq4k) run 900 python bench.py --snapshot q4k --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/benchq4k.log 2>&1 ;;
+    bench8i) run 900 python bench.py --pages-per-gpu 8 --steps 2 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench8i.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
