@@ -172,12 +172,13 @@ void* Engine::dev_alloc(size_t bytes) {
     return p;
 }
 
-void* Engine::ws(const std::string& name, size_t bytes) {
+void* Engine::ws(const std::string& name0, size_t bytes) {
+    const std::string name = ws_prefix_.empty() ? name0 : ws_prefix_ + name0;
     auto it = ws_.find(name);
     if (it != ws_.end() && it->second.second >= bytes) return it->second.first;
     if (capturing_) throw std::runtime_error("EINTERNAL: workspace growth during graph capture: " + name);
     if (it != ws_.end()) {
-        HIP_CHECK(hipStreamSynchronize(stream_));
+        HIP_CHECK(hipDeviceSynchronize());  // both vision streams may still read it
         HIP_CHECK(hipFree(it->second.first));
     }
     void* p = nullptr;
@@ -319,12 +320,16 @@ void Engine::prepare_page_device(const uint8_t* rgb, int w, int h, PagePixels& p
 
 Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (vstream_) (void)hipStreamSynchronize(vstream_);
     for (auto& e : span_ev_) (void)hipEventDestroy(e);
+    for (auto& e : vis_ev_)
+        if (e) (void)hipEventDestroy(e);
     for (auto& kv : pinned_) (void)hipHostFree(kv.second.first);
     for (auto& kv : winmaps_) { (void)hipFree(kv.second.first); (void)hipFree(kv.second.second); }
     for (auto& kv : ws_) (void)hipFree(kv.second.first);
     for (void* p : allocations_) (void)hipFree(p);
     if (stream_) (void)hipStreamDestroy(stream_);
+    if (vstream_) (void)hipStreamDestroy(vstream_);
 }
 
 void Engine::ensure_small(int n) {
@@ -675,6 +680,12 @@ float* Engine::clip_pos(int tokens) {
 }
 
 // ============================================================================ vision
+// DSOCR_VIS_STREAMS=0 (A/B switch, read once): every vision pass of a batch on the engine stream
+static bool vis_streams_on() {
+    static const bool v = !(getenv("DSOCR_VIS_STREAMS") && atoi(getenv("DSOCR_VIS_STREAMS")) == 0);
+    return v;
+}
+
 // SamBackbone::forward (sam.rs:210-289) + ClipVisionModel::forward (clip.rs:98-102) +
 // build_clip_sam_tokens + ImageProjector::project (model/mod.rs:604-650, 392-444).
 float* Engine::vision_pass(const float* imgs, int n, int Spx, const std::string& out) {
@@ -1327,27 +1338,76 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         if (host_copy) HIP_CHECK(hipStreamSynchronize(st));  // host sources may be pageable temporaries
         return d;
     };
+    // every pixel batch gathered first, then the passes: odd passes on the second vision stream
+    // (DSOCR_VIS_STREAMS=0: all on one stream), joined before the image rows are assembled
+    std::vector<float*> g_img, t_img;
+    std::vector<int> t_n;
     for (auto& kv : gsz) {
         const int S = kv.first;
-        float* dimg = gather(kv.second, false, kv.second.size() * 3 * (size_t)S * S);
-        std::string name = "vis_out" + std::to_string(pass_id++);
-        float* post = vision_pass(dimg, (int)kv.second.size(), S, name);
-        const int Sq = (S / 64) * (S / 64);
-        for (size_t i = 0; i < kv.second.size(); ++i) gpost[kv.second[i]] = post + (size_t)i * Sq * H;
+        g_img.push_back(gather(kv.second, false, kv.second.size() * 3 * (size_t)S * S));
+        ++pass_id;
     }
     for (auto& kv : tsz) {
         const int S = kv.first;
         int n = 0;
         for (int b : kv.second) n += reqs[b].page->n_tiles;
-        float* dimg = gather(kv.second, true, (size_t)n * 3 * S * S);
-        std::string name = "vis_out" + std::to_string(pass_id++);
-        float* post = vision_pass(dimg, n, S, name);
-        const int Sq = (S / 64) * (S / 64);
-        size_t off = 0;
-        for (int b : kv.second) {
-            lpost[b] = post + off * Sq * H;
-            off += reqs[b].page->n_tiles;
+        t_img.push_back(gather(kv.second, true, (size_t)n * 3 * S * S));
+        t_n.push_back(n);
+        ++pass_id;
+    }
+    const bool two = vis_streams_on() && gsz.size() + tsz.size() >= 2;
+    if (two && !vstream_) {
+        HIP_CHECK(hipStreamCreateWithFlags(&vstream_, hipStreamNonBlocking));
+        for (auto& e : vis_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (two) {
+        HIP_CHECK(hipEventRecord(vis_ev_[0], st));  // pixels gathered
+        HIP_CHECK(hipStreamWaitEvent(vstream_, vis_ev_[0], 0));
+    }
+    int vis_k = 0;
+    bool side = false;
+    auto run_pass = [&](float* dimg, int n, int S) -> float* {
+        const std::string name = "vis_out" + std::to_string(vis_k);
+        if (!two || (vis_k++ & 1) == 0) return vision_pass(dimg, n, S, name);
+        std::swap(stream_, vstream_);
+        ws_prefix_ = "vs1_";
+        float* r = nullptr;
+        try {
+            r = vision_pass(dimg, n, S, name);
+        } catch (...) {
+            std::swap(stream_, vstream_);
+            ws_prefix_.clear();
+            throw;
         }
+        std::swap(stream_, vstream_);
+        ws_prefix_.clear();
+        side = true;
+        return r;
+    };
+    {
+        size_t gi = 0;
+        for (auto& kv : gsz) {
+            const int S = kv.first;
+            float* post = run_pass(g_img[gi++], (int)kv.second.size(), S);
+            const int Sq = (S / 64) * (S / 64);
+            for (size_t i = 0; i < kv.second.size(); ++i) gpost[kv.second[i]] = post + (size_t)i * Sq * H;
+        }
+        size_t ti = 0;
+        for (auto& kv : tsz) {
+            const int S = kv.first;
+            float* post = run_pass(t_img[ti], t_n[ti], S);
+            ++ti;
+            const int Sq = (S / 64) * (S / 64);
+            size_t off = 0;
+            for (int b : kv.second) {
+                lpost[b] = post + off * Sq * H;
+                off += reqs[b].page->n_tiles;
+            }
+        }
+    }
+    if (side) {
+        HIP_CHECK(hipEventRecord(vis_ev_[1], vstream_));
+        HIP_CHECK(hipStreamWaitEvent(st, vis_ev_[1], 0));
     }
     HIP_CHECK(hipEventRecord(ev[1], st));
     timings_.vision_flops = flops_acc_;

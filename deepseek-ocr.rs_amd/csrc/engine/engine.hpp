@@ -221,6 +221,11 @@ class Engine {
     int device_ = 0;
     int dtype_ = 1;
     hipStream_t stream_ = nullptr;
+    // the page batch's second vision pass (tiles beside the global views) runs on vstream_ with its own
+    // workspaces (ws_prefix_): the two towers' small CLIP / norm kernels fill each other's idle CUs
+    hipStream_t vstream_ = nullptr;
+    hipEvent_t vis_ev_[2] = {nullptr, nullptr};
+    std::string ws_prefix_;
     std::vector<void*> allocations_;
     std::map<std::string, std::pair<void*, size_t>> ws_;
     bool capturing_ = false;

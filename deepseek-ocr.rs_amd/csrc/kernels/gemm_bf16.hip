@@ -190,6 +190,56 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmBf16Args g) {
     *cp = v;
 }
 
+// the same, four columns per thread (N % 4 == 0): 16-byte partial loads, one row per grid.y, no
+// index division, all slices in flight at once (the scalar kernel ran ~11 us per call on the CLIP /
+// projector shapes, 125 calls per vision pass)
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmBf16Args g) {
+    const int col = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const int row = blockIdx.y;
+    if (col >= g.N) return;
+    const long i = (long)row * g.N + col;
+    const long mn = (long)g.M * g.N;
+    const long orow = g.c_rows ? (long)g.c_rows[row] : (long)row;  // issued with the slice loads
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = g.bias[col + e];
+    // every slice's load issued before the first add (a runtime-bounded loop waited for each in turn:
+    // one HBM round trip per slice), then summed in slice order as before
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp0 = 0; sp0 < g.splits; sp0 += 8) {
+        float4 p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sp0 + j < g.splits) p[j] = *reinterpret_cast<const float4*>(g.part + (sp0 + j) * mn + i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sp0 + j < g.splits) { v.x += p[j].x; v.y += p[j].y; v.z += p[j].z; v.w += p[j].w; }
+    }
+    if (orow < 0) return;
+    const float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (g.out_bf16) {
+            bf16_store_epilogue(g, orow, col + e, r[e], bv[e]);
+            continue;
+        }
+        float x = apply_act(r[e] + bv[e], g.act);
+        float* cp = g.C + orow * g.ldc + col + e;
+        if (g.accumulate) x += *cp;
+        *cp = x;
+    }
+}
+
+static void launch_splitk_reduce(const GemmBf16Args& g, hipStream_t s) {
+    if (g.N % 4 == 0 && g.M <= 65535 && (reinterpret_cast<uintptr_t>(g.part) & 15) == 0) {
+        hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)((g.N / 4 + 255) / 256), (unsigned)g.M), dim3(256), 0, s, g);
+        return;
+    }
+    const long n = (long)g.M * g.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+}
+
 int gemm_bf16_splits(int M, int N, int K) {
     const int tiles = ((M + TB_M - 1) / TB_M) * ((N + TB_N - 1) / TB_N);
     const int nk = K / TB_K;
@@ -211,10 +261,7 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
     // profiles/r03_kbench_dgemm.log; bitwise equal results)
     if (g.variant == 2) hipLaunchKernelGGL(gemm_bf16_nt_kernel<2>, dim3(tiles * g.splits), dim3(256), 0, s, g);
     else hipLaunchKernelGGL(gemm_bf16_nt_kernel<1>, dim3(tiles * g.splits), dim3(256), 0, s, g);
-    if (g.splits > 1) {
-        const long n = (long)g.M * g.N;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
-    }
+    if (g.splits > 1) launch_splitk_reduce(g, s);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -443,18 +490,13 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
-    // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once); f16 weights: 2 x 2 (their W split
-    // would double under 4 x 1)
     // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once), ONE LDS stage (24 KB, four blocks per
     // CU: kbench vgemm 1.00-1.18x the two-stage kernel on the SAM linears, within 3 % elsewhere); f16
     // weights: 2 x 2 (their W split would double under 4 x 1), two stages
     if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else if (g.variant == 2) hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 2>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 1>), dim3(tiles * g.splits), dim3(256), 0, s, g);
-    if (g.splits > 1) {
-        const long n = (long)g.M * g.N;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
-    }
+    if (g.splits > 1) launch_splitk_reduce(g, s);
 }
 
 // ---------------------------------------------------------------------------------------
