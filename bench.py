@@ -130,8 +130,10 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
     (prompt + max_new - 1, the cache padded with copies of its own rows: attention and the cache
     append cost what they cost at that length).  Decode time is linear in the KV length, so the
     page's (max_new - 1) decode steps are the trapezoid of the two measured step times.
-    Timed twice: with BLAS on every core this process may run on (len(sched_getaffinity)), which is
-    the reported `value`, and with the pool the environment sets (OMP_NUM_THREADS), as `at_env_threads`."""
+    Timed twice: with BLAS on every core this process may run on (len(sched_getaffinity)) and with the
+    pool the environment sets (OMP_NUM_THREADS); the faster run is the reported `value` (on the shared
+    GPU box 256 visible CPUs oversubscribe the job's share: 0.011 vs 0.029 pages/s at 16 threads), the
+    other is kept as `other_threads`."""
     import dsocr
     from oracle.model import OracleModel
     from oracle.specs import tensor_names
@@ -163,14 +165,15 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
         r["cores"] = threads
         log(f"[cpu] {threads} BLAS threads: {r['value']:.4f} pages/s ({r['sample']})")
         runs.append(r)
-    best = runs[0]
+    best = max(runs, key=lambda r: r["value"])
+    other = [r for r in runs if r is not best]
     out = {"value": best["value"], "unit": "pages/s", "cores": best["cores"], "kind": "port",
            "port": "oracle/ numpy restatement of the reference page path (f32, BLAS-threaded); "
                    "the Rust reference cannot be built here",
            "decode_tok_s": best["decode_tok_s"], "host_cpus": os.cpu_count(), "allowed_cpus": all_cores,
            "cpu_model": cpu_model(), "sample": best["sample"]}
-    if len(runs) > 1:
-        out["at_env_threads"] = {k: runs[1][k] for k in ("value", "cores", "decode_tok_s", "sample")}
+    if other:
+        out["other_threads"] = {k: other[0][k] for k in ("value", "cores", "decode_tok_s", "sample")}
     return out
 
 
