@@ -57,7 +57,10 @@ def test_gemm(gpu, M, N, K, wdt, act, acc):
                                                       (77, 130, 96, 0, 0, 1, 3), (4096, 2304, 768, 0, 0, 0, 1),
                                                       (693, 1280, 2048, 0, 0, 0, 0), (706, 3840, 1280, 1, 0, 0, 0),
                                                       (706, 1280, 1280, 1, 0, 1, 0), (1412, 13696, 1280, 1, 3, 0, 0),
-                                                      (100, 64, 1280, 1, 0, 0, 2)])
+                                                      (100, 64, 1280, 1, 0, 0, 2),
+                                                      # split-K reduce over more than one batch of 8 slices,
+                                                      # four columns per thread, accumulate + activation
+                                                      (300, 512, 1152, 0, 1, 1, 9)])
 def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
     """Vision (bf16 weights: 3 exact bf16 planes of the f32 activations) and prefill (f16 weights, split into
     hi / lo bf16 as well: 5 products) linears on the fused-split kernel vs an f64 matmul, incl. split-K and
