@@ -1100,7 +1100,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         if constexpr (TK) {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                kreg[i] = *reinterpret_cast<const float4*>(Kc + (long)min(kb + tk_key(i), klim) * HD + tk_d4);
+                kreg[i] = ldg_nt_f4(Kc + (long)min(kb + tk_key(i), klim) * HD + tk_d4);
         } else {
             const float4* kp = reinterpret_cast<const float4*>(Kc + (long)min(kb + key, klim) * HD + sub * DPL);
 #pragma unroll
@@ -1111,7 +1111,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
 #pragma unroll
         for (int j = 0; j < KPG; ++j) {
             const int kk = min(kb + (TK ? tk_key(j) : kg * KPG + j), klim);
-            vreg[j] = *reinterpret_cast<const float4*>(Vc + (long)kk * HD + dg * 4);
+            vreg[j] = ldg_nt_f4(Vc + (long)kk * HD + dg * 4);
         }
     };
     const float* row = a.qkv + (long)b * a.ld;

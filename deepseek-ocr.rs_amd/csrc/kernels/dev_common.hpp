@@ -33,6 +33,12 @@ __device__ __forceinline__ uint4 ldg_nt16(const void* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// 16-byte streaming f32 load (the decode attention's K / V cache: read once per step)
+__device__ __forceinline__ float4 ldg_nt_f4(const float* p) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // Weight element types: checkpoints are bf16; the decoder keeps the reference's
 // `--dtype f16` rounding (fp16 storage).  Both widen exactly to f32.
 struct bf16_t { uint16_t v; };
