@@ -365,9 +365,9 @@ def run_dots(args, rank, world, local, dist):
         # runs them on the bf16 matrix cores (exact: 1 pass for QK^T, 3 bf16 planes of P for P.V), so the
         # peak is the dense bf16 MFMA rate and the issued MFMA work is 2x the algorithmic FLOPs
         "roofline": {"bound": "mfma", "achieved": round(attn_tf, 2), "peak": 2500.0, "unit": "TFLOP/s",
-                     "frac": round(attn_tf / 2500.0, 4), "traffic": None,
+                     "frac": round(attn_tf / 2500.0, 4), "traffic": pmc_traffic("attention_bf16_tr_kernel"),
                      "mfma_issued_tflops": round(2.0 * attn_tf, 2), "mfma_issued_frac": round(2.0 * attn_tf / 2500.0, 4),
-                     "kernel": "attention_bf16_kernel<128> (bidirectional flash attention over the page's 21316 tokens "
+                     "kernel": "attention_bf16_tr_kernel<128> (bidirectional flash attention over the page's 21316 tokens "
                                "on v_mfma_f32_32x32x16_bf16 with the reference's f32 math: exact bf16 q.k products, "
                                "P split into 3 exact bf16 planes for P.V)",
                      "avg_launch_us": round(attn_layer_ms * 1e3, 1),

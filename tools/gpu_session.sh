@@ -60,6 +60,8 @@ for step in "$@"; do
     pmc8t_fetch) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc8t_fetch -o pmc --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc8t_fetch.log 2>&1 ;;
     pmc8t_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc8t_write -o pmc --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc8t_write.log 2>&1 ;;
     gprof8t_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8t_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8t_nopc.log 2>&1 ;;
+    pmcdots_fetch) run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcdots_fetch -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmcdots_fetch.log 2>&1 ;;
+    pmcdots_write) run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcdots_write -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmcdots_write.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
