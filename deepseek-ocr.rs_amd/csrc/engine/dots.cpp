@@ -23,6 +23,8 @@ void launch_dots_layernorm(const void* x, long rows, int D, const float* w, cons
 void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
                       int out_bf16, hipStream_t s);
 void launch_dots_swiglu(const void* gu, long N, int I, void* h, hipStream_t s);
+void launch_dots_rope_qk(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
+                         hipStream_t s);
 void launch_dots_gelu(void* x, long n, hipStream_t s);
 void launch_dots_to_bf16(const float* x, long N, int D, long ldi, void* y, int ldo, hipStream_t s);
 void launch_dots_bf16_to_f32(const void* x, long n, float* y, hipStream_t s);
@@ -355,9 +357,10 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
         } else {
             // bf16 matrix cores with the same f32 math (attention_bf16.hip): rotated q / k stay bf16
             // (exactly the reference's rounding), the context is written as the bf16 tensor it becomes
-            launch_dots_rope(QKV, N, H, hd, d_cos, d_sin, QKVr, 1, st);
+            // rotated q / k into QKVr; v is read where the qkv GEMM wrote it
+            launch_dots_rope_qk(QKV, N, H, hd, d_cos, d_sin, QKVr, st);
             AttnBf16Args a;
-            a.q = (const uint16_t*)QKVr; a.k = (const uint16_t*)QKVr + D; a.v = (const uint16_t*)QKVr + 2 * D;
+            a.q = (const uint16_t*)QKVr; a.k = (const uint16_t*)QKVr + D; a.v = (const uint16_t*)QKV + 2 * D;
             a.q_rs = a.k_rs = a.v_rs = 3L * D; a.q_hs = a.k_hs = a.v_hs = hd;
             a.o = CTXb; a.o_rs = D; a.o_hs = hd; a.o_bf16 = 1;
             a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
