@@ -60,10 +60,24 @@ dsocr_status guarded(F&& f) {
 // (async-signal-safe: open/read/write only), then hand the signal back to the handler that was there
 // before (a profiler's or the default), so unsymbolised PCs in its stack dump resolve to library + offset.
 struct sigaction g_prev_segv;
+// "0x" + 16 hex digits of v into out (no libc formatting: snprintf is not async-signal-safe)
+size_t hex_u64(uint64_t v, char* out) {
+    static const char dig[] = "0123456789abcdef";
+    out[0] = '0';
+    out[1] = 'x';
+    for (int i = 0; i < 16; ++i) out[2 + i] = dig[(v >> (60 - 4 * i)) & 15];
+    return 18;
+}
 void segv_maps_handler(int sig, siginfo_t* si, void* uc) {
     char buf[4096];
-    int n = snprintf(buf, sizeof(buf), "\n[dsocr] SIGSEGV at %p; /proc/self/maps follows\n", si ? si->si_addr : nullptr);
-    if (n > 0) (void)!write(2, buf, (size_t)n);
+    static const char head[] = "\n[dsocr] SIGSEGV at ", tail[] = "; /proc/self/maps follows\n";
+    size_t n = 0;
+    memcpy(buf, head, sizeof(head) - 1);
+    n += sizeof(head) - 1;
+    n += hex_u64(si ? (uint64_t)(uintptr_t)si->si_addr : 0, buf + n);
+    memcpy(buf + n, tail, sizeof(tail) - 1);
+    n += sizeof(tail) - 1;
+    (void)!write(2, buf, n);
     const int fd = open("/proc/self/maps", O_RDONLY);
     if (fd >= 0) {
         ssize_t r;
@@ -612,6 +626,57 @@ dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, in
         check_hip(e, "decode attention");
         if (herr) throw std::runtime_error("EINTERNAL: decode attention merge timed out");
     });
+}
+dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int hd, int max_len, float scale,
+                                   float eps, const float* x, const float* norm_w, const void* Wqkv, int wdtype,
+                                   const float* cos, const float* sin, float* kc, float* vc, const int* kv_pos,
+                                   float* qkv_row, float* o, int* used_fused) {
+    return guarded([&] {
+        if (steps <= 0 || H <= 0 || heads <= 0 || hd != 128 || heads * hd != H)
+            throw std::runtime_error("EINVAL: qkv_attention needs 128-dim MHA heads with heads * hd == H");
+        if (wdtype != dsocr::WDT_F16 && wdtype != dsocr::WDT_BF16) throw std::runtime_error("EINVAL: 16-bit weights only");
+        const int QKVN = 3 * H;
+        float* part = nullptr;
+        int* cnt = nullptr;
+        const size_t pb = dsocr::dec_attn_workspace(1, heads, hd, max_len);
+        check_hip(hipMalloc(&part, pb), "hipMalloc");
+        check_hip(hipMalloc(&cnt, sizeof(int) * (heads + 1)), "hipMalloc");
+        check_hip(hipMemset(cnt, 0, sizeof(int) * (heads + 1)), "hipMemset");
+        dsocr::dec_attn_part_init(part, pb, nullptr);
+        bool took = false;
+        for (int s = 0; s < steps; ++s) {
+            dsocr::DecGemvArgs g;
+            g.M = 1; g.N = QKVN; g.K = H; g.W = Wqkv; g.ldw = H; g.wdtype = wdtype; g.y = qkv_row; g.ldy = QKVN;
+            g.x = x + (size_t)s * H; g.ldx = H; g.norm_w = norm_w; g.eps = eps;
+            dsocr::DecRopeEpi re;
+            re.kv_pos = kv_pos + s; re.cos = cos; re.sin = sin; re.hd = hd; re.rot_rows = 2 * H;
+            dsocr::DecAttn2Args a;
+            a.qkv = qkv_row; a.ld = QKVN; a.kv_pos = kv_pos + s; a.B = 1; a.heads = heads; a.kv_heads = heads;
+            a.hd = hd; a.rope_dim = hd; a.use_mla = 0; a.max_len = max_len; a.cos = cos; a.sin = sin;
+            a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd; a.page_stride = (long)heads * max_len * hd;
+            a.scale = scale; a.part = part; a.o = o + (size_t)s * H; a.o_ld = H; a.counters = cnt; a.err = cnt + heads;
+            a.prerot = 1;
+            if (!dsocr::dec_qkv_rope_ok(g, re)) throw std::runtime_error("EINVAL: q/k/v projection outside dec_qkv_rope's range");
+            if (fused && dsocr::dec_qkv_attn_ok(g, re, a)) {
+                dsocr::launch_dec_qkv_attn(g, re, a, nullptr);
+                took = true;
+            } else {
+                dsocr::launch_dec_qkv_rope(g, re, nullptr);
+                dsocr::launch_dec_attn(a, nullptr);
+            }
+        }
+        hipError_t e = hipDeviceSynchronize();
+        int herr = 0;
+        if (e == hipSuccess) e = hipMemcpy(&herr, cnt + heads, sizeof(int), hipMemcpyDeviceToHost);
+        (void)hipFree(part);
+        (void)hipFree(cnt);
+        check_hip(e, "qkv_attention");
+        if (herr) throw std::runtime_error("EINTERNAL: q/k/v hand-off or attention merge timed out");
+        if (used_fused) *used_fused = took ? 1 : 0;
+    });
+}
+int dsocr_k_poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus) {
+    return dsocr::poll_wait_fits(waiting_blocks, api_blocks_per_cu, cus) ? 1 : 0;
 }
 dsocr_status dsocr_k_moe(int T, int H, int E, int topk, int I, int Is, const float* x, const float* norm_w,
                          float eps, const void* router, const void* Wgu, const void* Wd, const void* sWgu,

@@ -1778,7 +1778,9 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
             // events only: the gate/up record takes its layer's expert count from the down record
             if (!(span_mode_ & SPAN_WAVES) && r < per_kind) spans_host_[r * SPAN_FIELDS + 2] = dev[(per_kind + r) * 4 + 2];
         }
-        span_rec_ = nullptr;  // profile_decode and later generates run unstamped unless re-enabled
+        spans_steps_ = span_cap_;  // reported with the records it sizes (a throwing generate leaves both)
+        // profile_decode runs unstamped; every later generate is stamped again while span_mode_ is set
+        span_rec_ = nullptr;
         span_slots_ = nullptr;
         span_step_ = nullptr;
     }
@@ -1838,6 +1840,24 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         const size_t qn = (size_t)B * layers_[0].qkv.N;
         HIP_CHECK(hipMemsetAsync(wsf("p_qkv_attn", qn), 0, qn * 4, st));
     }
+    // the replays rewrite the K / V slot of pos - 1 in every layer (the attention replays from a scratch
+    // row): keep those slots and put them back after the attention replays and at the end, so the
+    // step-graph replays and any later use of the engine state see the cache the generate left
+    const size_t slot_w = (size_t)hd * 4, n_slots = (size_t)L.layers * B * 2;
+    float* kv_saved = wsf("p_kv_saved", n_slots * L.kv_heads * hd);
+    auto kv_slots = [&](bool restore) {
+        for (int l = 0; l < L.layers; ++l)
+            for (int b = 0; b < B; ++b)
+                for (int kv = 0; kv < 2; ++kv) {
+                    float* base = (kv ? vc_ : kc_) + (long)l * B * page_stride_ + (long)b * page_stride_ + (long)pm1[b] * hd;
+                    float* keep = kv_saved + (((size_t)l * B + b) * 2 + kv) * L.kv_heads * hd;
+                    if (restore)
+                        HIP_CHECK(hipMemcpy2DAsync(base, head_stride_ * 4, keep, slot_w, slot_w, L.kv_heads, hipMemcpyDeviceToDevice, st));
+                    else
+                        HIP_CHECK(hipMemcpy2DAsync(keep, slot_w, base, head_stride_ * 4, slot_w, L.kv_heads, hipMemcpyDeviceToDevice, st));
+                }
+    };
+    kv_slots(false);
     // n back-to-back launches captured in one hipGraph, replayed between two events on the
     // engine stream: per-launch time = span / n = device time + the dependent-kernel boundary
     // (eager launches go host-bound below ~3.5 us per kernel, MI355X_MICROARCH.md
@@ -1942,6 +1962,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
             launch_dec_attn(da, st);
         });
+        kv_slots(true);
         // K and V of every attended key (f32 cache) + q/k/v row + context out
         prof.attention.bytes = (double)keys * L.kv_heads * hd * 4.0 * 2.0 + (double)B * (QKVN + H) * 4.0;
         prof.attention.flops = 4.0 * keys * L.heads * hd;
@@ -2085,6 +2106,8 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         HIP_CHECK(hipMemcpyAsync(X, X0, (size_t)B * H * 4, hipMemcpyDeviceToDevice, st));
         HIP_CHECK(hipStreamSynchronize(st));
     }
+    kv_slots(true);
+    HIP_CHECK(hipStreamSynchronize(st));
     return prof;
 }
 

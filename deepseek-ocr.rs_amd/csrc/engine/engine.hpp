@@ -172,7 +172,7 @@ class Engine {
     // dispatch duration in ns (HIP events recorded around the launch inside the replayed graph)} of the
     // last generate with spans on; step = tokens emitted before the step (1 .. steps - 1 are decode steps)
     const std::vector<unsigned long long>& spans() const { return spans_host_; }
-    int span_steps() const { return span_cap_; }
+    int span_steps() const { return spans_steps_; }  // the steps of spans_host_ (set with it)
     hipStream_t stream() const { return stream_; }
     void upload_page(PagePixels& pg);
     void prepare_page_device(const uint8_t* rgb, int w, int h, PagePixels& px);
@@ -275,6 +275,7 @@ class Engine {
     const int* span_step_ = nullptr;            // device step counter (out_len of page 0)
     int span_cap_ = 0;
     std::vector<unsigned long long> spans_host_;
+    int spans_steps_ = 0;
     std::vector<hipEvent_t> span_ev_;           // [SPAN_KINDS][layers][2]
     std::vector<double> span_ev_ns_;            // [SPAN_KINDS][layers][span_cap_]
     unsigned long long* span_rec(int kind, int layer) const {

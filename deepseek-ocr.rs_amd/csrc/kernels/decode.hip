@@ -1128,6 +1128,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     issue_k(k0, min(k0 + CH, len) - 1);
     issue_v(k0, min(k0 + CH, len) - 1);
     const bool own = pos >= k0 && pos < k0 + CH;
+    bool gave_up = false;
     if constexpr (FUSED) {
         // the head's q (and, owning the position, the new k / v) from this launch's projection blocks
         const int td = tid & (HD - 1);
@@ -1145,11 +1146,16 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             if (!__syncthreads_or(pend)) break;
             if (it > (1u << 20)) {
                 if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                gave_up = true;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
     }
+    // a block that gave up (the error flag is set; the host raises after the step) leaves the K / V cache
+    // untouched: sentinel q / k / v never enter the cache.  It still writes its record so the merge of its
+    // head does not wait out a second bounded spin.
+    const bool write_kv = own && !gave_up;
     const int nc = (len + CH - 1) / CH;
     // 2. RoPE inputs
     const float* krow = row + a.heads * HD + kvh * HD;
@@ -1161,7 +1167,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             if (own) {
                 knew[tid] = k_pre;
                 vnew[tid] = v_pre;
-                if (h == kvh * (a.heads / a.kv_heads)) {  // one writer per kv head
+                if (write_kv && h == kvh * (a.heads / a.kv_heads)) {  // one writer per kv head
                     Kc[(long)pos * HD + tid] = k_pre;
                     Vc[(long)pos * HD + tid] = v_pre;
                 }
@@ -1453,11 +1459,65 @@ __global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecGemvArgs g, DecRop
     dec_attn_body<128, true, true, true>(a, i % chunks, i / chunks, 0);
 }
 
+// ------------------------------------------------------------------ residency of the polled hand-offs
+// A polling block waits on blocks of its own grid.  HIP promises no dispatch order (MI355X_MICROARCH.md,
+// "Contract"), so such a launch is deadlock-free only if the blocks that can wait never hold every slot the
+// device has for the kernel: then a block that never waits always finds a slot, runs to completion, and
+// every producer eventually runs.  Rule: waiting < usable slots, with usable slots per CU =
+// min(API answer, 8) less one where the API may over-admit (the guide's residency note: at 82-98 SGPRs
+// the API reports one block per CU more than the hardware admits).  Blocks that can wait:
+//   dec_qkv_attn: every attention block (each polls its head's q / k / v row) = chunks * heads;
+//   dec_attn (POLL): the merging block of each (page, head) = B * heads.
+bool poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus) {
+    if (waiting_blocks <= 0) return true;
+    int per_cu = std::min(api_blocks_per_cu, 8);
+    if (per_cu >= 6) per_cu -= 1;
+    return per_cu > 0 && cus > 0 && waiting_blocks < (long)per_cu * cus;
+}
+
+namespace {
+int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+    }
+    return cus;
+}
+template <typename K>
+int blocks_per_cu(K kernel, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess) return 0;
+    return per_cu;
+}
+int qkv_attn_blocks_per_cu(int wdtype, size_t lds) {
+    static int bf = -1, f16 = -1;  // the dynamic LDS is stage_bytes(1, K): one model per process
+    int& v = wdtype == WDT_BF16 ? bf : f16;
+    if (v < 0) v = wdtype == WDT_BF16 ? blocks_per_cu(dec_qkv_attn_kernel<bf16_t>, lds) : blocks_per_cu(dec_qkv_attn_kernel<f16_t>, lds);
+    return v;
+}
+int attn_poll_blocks_per_cu(bool prerot) {
+    static int pr = -1, npr = -1;
+    int& v = prerot ? pr : npr;
+    if (v < 0) v = prerot ? blocks_per_cu(dec_attn_kernel<128, true, true>, 0) : blocks_per_cu(dec_attn_kernel<128, false, true>, 0);
+    return v;
+}
+}  // namespace
+
 bool dec_qkv_attn_ok(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a) {
     const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
-    return dec_qkv_rope_ok(g, r) && a.B == 1 && a.hd == 128 && r.hd == 128 && a.heads == a.kv_heads && a.err &&
-           chunks <= 24 && a.max_len <= 512 * DA_CH && g.y == a.qkv && g.N == (a.heads + 2 * a.kv_heads) * a.hd &&
-           r.rot_rows == (a.heads + a.kv_heads) * a.hd;
+    if (!(dec_qkv_rope_ok(g, r) && a.B == 1 && a.hd == 128 && r.hd == 128 && a.heads == a.kv_heads && a.err &&
+          chunks <= 24 && a.max_len <= 512 * DA_CH && g.y == a.qkv && g.N == (a.heads + 2 * a.kv_heads) * a.hd &&
+          r.rot_rows == (a.heads + a.kv_heads) * a.hd))
+        return false;
+    return poll_wait_fits((long)chunks * a.heads, qkv_attn_blocks_per_cu(g.wdtype, stage_bytes(1, g.K)), device_cus());
+}
+
+bool dec_attn_polled(const DecAttn2Args& a) {
+    const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
+    return a.err && a.hd == 128 && chunks <= 24 &&
+           poll_wait_fits((long)a.B * a.heads, attn_poll_blocks_per_cu(a.prerot != 0), device_cus());
 }
 
 void launch_dec_qkv_attn(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a, hipStream_t s) {
@@ -1492,8 +1552,9 @@ void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     const bool prerot = a.prerot != 0;
     dim3 g1(chunks, a.heads, a.B);
     // polling merge (no ticket): 128-dim heads, <= 24 chunks (one load round trip in the merge), a
-    // give-up flag, a sentinel-filled record buffer; otherwise the arrival ticket
-    if (a.err && a.hd == 128 && chunks <= 24) {
+    // give-up flag, a sentinel-filled record buffer, the merging blocks within the residency rule;
+    // otherwise the arrival ticket (no block waits)
+    if (dec_attn_polled(a)) {
         if (prerot) DSOCR_LAUNCH((dec_attn_kernel<128, true, true>), g1, dim3(256), 0, s, a);
         else DSOCR_LAUNCH((dec_attn_kernel<128, false, true>), g1, dim3(256), 0, s, a);
         return;

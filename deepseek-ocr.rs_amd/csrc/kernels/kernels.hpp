@@ -252,7 +252,16 @@ void launch_dec_qkv_rope(const DecGemvArgs& a, const DecRopeEpi& r, hipStream_t 
 // One page: q/k/v projection + RoPE and the decode attention in one launch (the attention blocks stream
 // their K / V chunk while the projection runs, then poll for q / k / v); the q/k/v row g.y == a.qkv must
 // enter the first launch sentinel-filled (dec_qkv_sentinel_init), every launch leaves it so
+// (includes the residency rule below: the launch is refused - the engine then takes the two-launch form -
+// when the polling attention blocks could fill every slot the device has for the kernel)
 bool dec_qkv_attn_ok(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a);
+// Residency rule of the in-launch polled hand-offs: waiting_blocks (the blocks that may spin on other
+// blocks of the same grid) < usable slots (min(api, 8), one fewer where the API may over-admit, x CUs).
+// Pure host decision (no device call); dec_qkv_attn_ok / dec_attn_polled apply it with the kernel's
+// occupancy query.
+bool poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus);
+// dec_attn takes the polling merge (else the arrival ticket)
+bool dec_attn_polled(const DecAttn2Args& a);
 void launch_dec_qkv_attn(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a, hipStream_t s);
 void dec_qkv_sentinel_init(float* qkv, size_t floats, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);

@@ -285,6 +285,22 @@ dsocr_status dsocr_k_attention_bf16(int n_seq, int L, int heads, int hd, float s
 dsocr_status dsocr_k_decode_attention(int B, int heads, int kv_heads, int hd, int rope_dim, int max_len, float scale,
                                       const float* qkv, const float* cos, const float* sin, float* kc, float* vc,
                                       const int* kv_pos, float* o, int prerot);
+/* One page's decode attention sub-layer as the engine runs it (block.rs:446-804 at seq_len 1): RMSNorm +
+ * q/k/v projection (Wqkv [3H][H], 16-bit) with RoPE in the epilogue, K/V append at kv_pos[s], softmax
+ * attention over positions 0..kv_pos[s], for `steps` launches back to back (x [steps][H], kv_pos [steps],
+ * o [steps][H]).  fused != 0: the one-launch form (dec_qkv_attn: attention blocks poll the q/k/v row, which
+ * must enter the first launch filled with DSOCR_HANDOFF_SENTINEL words and is left so by every launch);
+ * fused == 0 or the residency rule refusing it: projection and attention as two launches.  *used_fused
+ * reports which ran.  128-dim MHA heads only.  Device pointers. */
+#define DSOCR_HANDOFF_SENTINEL 0x7FBADBADu
+dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int hd, int max_len, float scale,
+                                   float eps, const float* x, const float* norm_w, const void* Wqkv, int wdtype,
+                                   const float* cos, const float* sin, float* kc, float* vc, const int* kv_pos,
+                                   float* qkv_row, float* o, int* used_fused);
+/* Residency rule of the polled in-launch hand-offs (pure host decision, no device call): 1 when
+ * waiting_blocks (blocks that may spin on blocks of the same grid) < usable slots = (min(api, 8), one fewer
+ * where the occupancy API may over-admit) x cus; else 0 (the engine then launches the non-polling form). */
+int dsocr_k_poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus);
 /* Decode MoE layer (the north-star kernel chain, block.rs:1215-1395): [RMSNorm] + router GEMV +
  * softmax top-k + grouping + grouped SwiGLU experts + shared experts + weighted combine,
  * out[T][H] += moe(xn), xn = rmsnorm(x; norm_w, eps) if norm_w != NULL else x.  Runs exactly the

@@ -293,6 +293,63 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot):
             assert np.max(np.abs(got[b, h * hd:(h + 1) * hd] - ref)) < 2e-5, (b, h)
 
 
+SENT = 0x7FBADBAD  # DSOCR_HANDOFF_SENTINEL
+
+
+@pytest.mark.parametrize("max_len,p0", [(1219, 1200), (1219, 700), (130, 60), (64 * 24, 64 * 24 - 3)])
+def test_qkv_attention_fused_back_to_back(gpu, max_len, p0):
+    """One page's q/k/v projection + decode attention as ONE launch (dec_qkv_attn: attention blocks poll the
+    sentinel-filled q/k/v row the projection blocks of the same grid write) for three launches back to back
+    (positions p0, p0+1, p0+2: the row and the merge records refilled by each launch are what the next one
+    polls), against the two-launch form (dec_qkv_rope + dec_attn) on the same inputs and against f64 math
+    (block.rs:446-804 at seq_len 1: RMSNorm, q/k/v = W x, RoPE, K/V append, softmax attention).  Checks the
+    outputs, the appended K / V slots, and that the row holds only sentinels again afterwards."""
+    from types import SimpleNamespace
+    from oracle.decoder import apply_rope, rope_tables
+    H, heads, hd, steps = 1280, 10, 128, 3
+    rng = np.random.default_rng(max_len + p0)
+    x = rng.standard_normal((steps, H)).astype(np.float32)
+    nw = (1.0 + 0.1 * rng.standard_normal(H)).astype(np.float32)
+    bits, w = _weights(rng, 3 * H, H, 1)
+    kc = rng.standard_normal((heads, max_len, hd)).astype(np.float32)
+    vc = rng.standard_normal((heads, max_len, hd)).astype(np.float32)
+    kc[:, p0:] = np.nan
+    vc[:, p0:] = np.nan
+    pos = np.arange(p0, p0 + steps, dtype=np.int32)
+    cos, sin = rope_tables(SimpleNamespace(rope_theta=10000.0), max_len, hd)
+    scale, eps = 1.0 / math.sqrt(hd), 1e-6
+    dW, dx, dn, dcos, dsin, dp = Dev(bits), Dev(x), Dev(nw), Dev(cos), Dev(sin), Dev(pos)
+    outs = {}
+    for fused in (1, 0):
+        row = Dev(np.full(3 * H, SENT, np.uint32))
+        dk, dv, do = Dev(kc), Dev(vc), Dev.zeros((steps, H))
+        used = C.c_int(-1)
+        check(lib().dsocr_k_qkv_attention(fused, steps, H, heads, hd, max_len, scale, eps, dx.ptr, dn.ptr, dW.ptr, 1,
+                                          dcos.ptr, dsin.ptr, dk.ptr, dv.ptr, dp.ptr, row.ptr, do.ptr, C.byref(used)))
+        assert used.value == fused, "the residency rule refused the fused launch at this size"
+        if fused:
+            assert np.all(row.get() == SENT), "the q/k/v hand-off row was not refilled with sentinels"
+        outs[fused] = (do.get(), dk.get(), dv.get())
+    (o1, k1, v1), (o0, k0, v0) = outs[1], outs[0]
+    assert np.array_equal(k1[:, p0:p0 + steps], k0[:, p0:p0 + steps])
+    assert np.array_equal(v1[:, p0:p0 + steps], v0[:, p0:p0 + steps])
+    assert np.max(np.abs(o1 - o0)) <= 1e-6, np.max(np.abs(o1 - o0))
+    K, V = kc.copy(), vc.copy()
+    for s in range(steps):
+        p = pos[s]
+        xn = rms_norm(x[s][None], nw, eps)[0]
+        qkv = (xn.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32)
+        cs, sn = cos[p][None], sin[p][None]
+        q = apply_rope(qkv[:H].reshape(heads, hd), cs, sn, False)
+        kn = apply_rope(qkv[H:2 * H].reshape(heads, hd), cs, sn, False)
+        vn = qkv[2 * H:].reshape(heads, hd)
+        assert np.max(np.abs(k1[:, p] - kn)) < 1e-4 and np.max(np.abs(v1[:, p] - vn)) < 1e-4
+        K[:, p], V[:, p] = k1[:, p], v1[:, p]
+        for h in range(heads):
+            ref = _attn_ref(q[h][None], K[h, :p + 1], V[h, :p + 1], scale)[0]
+            assert np.max(np.abs(o1[s, h * hd:(h + 1) * hd] - ref)) < 1e-4, (s, h)
+
+
 @pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(3, 256, 16, 6, 64, 2, False), (1, 256, 16, 6, 64, 2, True),
                                                   (2, 1280, 64, 6, 896, 2, True), (9, 128, 8, 3, 32, 1, False),
                                                   (4, 256, 16, 6, 64, 2, False)])

@@ -235,6 +235,44 @@ def test_full_screened_selection_equals_exact(full_engine, monkeypatch):
     assert screened == exact, (screened, exact)
 
 
+def test_full_spans_do_not_change_ids(full_engine):
+    """In-context launch spans (dsocr_engine_set_spans: 1 = wave spans stamped by every gate/up, down and
+    attention wave, 2 = HIP events around those launches inside the replayed step graph; the MoE is then
+    split into its route / gate-up / down launches with the fold kernels) record without changing what is
+    decoded: ids equal with spans off, mode 1 and mode 2, records present with the stated dims, and
+    profile_decode (whose replays rewrite the last K/V slot) leaves a following generate unchanged."""
+    tok = SyntheticTokenizer(129280)
+    page = Page(synthetic_page(2), VisionSettings())
+    ids, mask = build_prompt_tokens(tok, "<image>\n<|grounding|>Convert the document to markdown.", [page.n_image_tokens])
+    n = 24
+    p = DecodeParameters(max_new_tokens=n)
+    full_engine.set_spans(0)
+    ref = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
+    layers = json.load(open(FULL))["language_config"]["num_hidden_layers"]
+    try:
+        for mode in (1, 2):
+            full_engine.set_spans(mode)
+            got = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
+            assert got == ref, (mode, got, ref)
+            sp = full_engine.spans()
+            assert set(sp) >= {"moe_gateup", "moe_down", "attention"}, sp.keys()
+            for kind in ("moe_gateup", "moe_down", "attention"):
+                a = sp[kind]
+                assert a.shape == (layers, n, 5), (kind, a.shape)
+                moe = kind != "attention"
+                rows = a[1:, 1:n] if moe else a[:, 1:n]     # layer 0 is dense: no MoE launches
+                if mode == 1:
+                    assert np.all(rows[..., 1] > rows[..., 0]), kind   # exit after entry in every step
+                else:
+                    assert np.all(rows[..., 4] > 0), kind              # event duration in every step
+                if moe:
+                    assert np.all((rows[..., 2] >= 6) & (rows[..., 2] <= 64)), kind  # distinct experts
+    finally:
+        full_engine.set_spans(0)
+    full_engine.profile_decode(2)
+    assert full_engine.generate(ids, mask, page, None, p, ignore_eos=True) == ref
+
+
 def test_tiny_generate_without_cache(tiny_engine, tiny_oracle):
     """use_cache = false (generate_without_cache, model/mod.rs:2051-2283): every step re-runs the whole
     forward on prompt + generated tokens; ids equal the oracle's no-cache restatement and the cached path."""

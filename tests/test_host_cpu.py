@@ -194,6 +194,24 @@ def test_c_abi_exports_every_declared_symbol():
         assert hasattr(L, s), s
 
 
+@pytest.mark.parametrize("waiting,api,cus,fits", [
+    # dec_qkv_attn at its bound (24 chunks x 10 heads poll the q/k/v row): 4 blocks per CU (102 VGPRs) x 256 CUs
+    (24 * 10, 4, 256, 1),
+    # the same grid on a part that could hold one block per CU on 240 CUs: every slot could be a waiter
+    (24 * 10, 1, 240, 0), (24 * 10, 1, 241, 1),
+    # the 8-page polling merge: 8 pages x 10 heads merging blocks (the rest of the 1600-block grid never waits)
+    (8 * 10, 4, 256, 1),
+    # the API may over-admit one block per CU at 6..8: 7 reported -> 6 usable
+    (6 * 256, 7, 256, 0), (6 * 256 - 1, 7, 256, 1), (8 * 256 - 1, 12, 256, 0), (7 * 256 - 1, 12, 256, 1),
+    # no slot at all (occupancy query failed -> 0): never poll
+    (1, 0, 256, 0), (0, 0, 256, 1)])
+def test_poll_residency_rule(waiting, api, cus, fits):
+    """Residency rule of the in-launch polled hand-offs (dec_qkv_attn, the dec_attn polling merge): the launch
+    polls only if the blocks that may wait cannot fill every slot the device has for the kernel (HIP promises
+    no dispatch order), else the engine takes the non-polling form.  Pure host decision through the C ABI."""
+    assert _lib().dsocr_k_poll_wait_fits(waiting, api, cus) == fits
+
+
 def test_engine_load_errors_without_gpu_are_loud():
     """The product path must fail loudly (never fall back to CPU) when no device/config is usable."""
     from dsocr import DsocrError, ModelLoadArgs, load_model
