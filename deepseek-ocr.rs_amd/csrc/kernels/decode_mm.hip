@@ -642,12 +642,15 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
         if (c + 2 < nch) load(fa, c + 2);
         compute(fb, c + 1);
     }
-    // partial tile -> part[seg][t][j] (write-through); tokens outside the segment are zero columns
+    // partial tile -> part[seg][t][j]: one 16-byte write-through (sc1) store per lane (rows 4g .. 4g + 3
+    // of token column col); tokens outside the segment are zero columns
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(a.dn_part, (short)0, 0x7fffffff, 0x00020000);
     if (col < a.T) {
         const float sc = scl[col];
-        float* dst = a.dn_part + ((long)seg * MM_MT + col) * a.Hout + j0 + 4 * g;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) __hip_atomic_store(dst + i, acc[i] * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float v4[4] = {acc[0] * sc, acc[1] * sc, acc[2] * sc, acc[3] * sc};
+        u32x4 bits;
+        __builtin_memcpy(&bits, v4, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(bits, prs, (int)((((long)seg * MM_MT + col) * a.Hout + j0 + 4 * g) * 4), 0, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -663,27 +666,49 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
     // the last arriver: the ordered sum over segments.  A token's column of a segment it does not
     // belong to was computed from a zero B column, so it holds exact zeros and adding it leaves every
-    // partial sum unchanged; all segments are therefore summed unconditionally, with the loads of a
-    // batch of 24 in flight together (a per-segment membership test made every load its own L2 round
-    // trip: 17 in a row at 8 pages)
-    constexpr int SB = 24;
-    for (int i = tid; i < RT * MM_MT; i += NWV * 64) {
-        const int t = i / RT, j = tile * RT + i % RT;
-        if (t >= a.T) continue;
-        const float* src = a.dn_part + (long)t * a.Hout + j;
-        const long sstride = (long)MM_MT * a.Hout;
-        float v = 0.f;
-        for (int s0 = 0; s0 < n_seg; s0 += SB) {
-            float pv[SB];
+    // partial sum unchanged; all segments are therefore summed unconditionally.  Thread = (4 rows of one
+    // token, half of the segments): 16-byte sc1 loads of every segment of its half issued together (one
+    // L2 round trip; a per-segment test, or batches of scalar loads, made each batch its own round trip),
+    // summed in segment order; the second half's sum joins the first's through LDS:
+    // (s_0 + .. + s_{h-1}) + (s_h + .. + s_{n-1}), a fixed order.
+    static_assert(NWV == 4 && RT * MM_MT / 4 == 128, "tail layout: 128 row quads x 2 halves = 256 threads");
+    __shared__ float4 half_s[128];
+    const int q4 = tid & 127, hf = tid >> 7;
+    const int t = q4 / (RT / 4), j = tile * RT + (q4 % (RT / 4)) * 4;
+    const int nh = (n_seg + 1) >> 1;
+    const int sb = hf ? nh : 0, se = hf ? n_seg : nh;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < a.T) {
+        constexpr int SB = 18;  // segments in flight per batch (n_seg <= 72: at most 2 batches per half)
+        const long sstride = (long)MM_MT * a.Hout * 4;
+        const int base = (int)(((long)t * a.Hout + j) * 4);
+        for (int s0 = sb; s0 < se; s0 += SB) {
+            u32x4 pv[SB];
 #pragma unroll
             for (int q = 0; q < SB; ++q)
-                pv[q] = __hip_atomic_load(src + min(s0 + q, n_seg - 1) * sstride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pv[q] = __builtin_amdgcn_raw_buffer_load_b128(prs, base + (int)(min(s0 + q, se - 1) * sstride), 0, 16);
 #pragma unroll
-            for (int q = 0; q < SB; ++q)
-                if (s0 + q < n_seg) v += pv[q];
+            for (int q = 0; q < SB; ++q) {
+                if (s0 + q < se) {
+                    v.x += __uint_as_float(pv[q][0]);
+                    v.y += __uint_as_float(pv[q][1]);
+                    v.z += __uint_as_float(pv[q][2]);
+                    v.w += __uint_as_float(pv[q][3]);
+                }
+            }
         }
-        float* op = a.out + (long)t * a.Hout + j;
-        *op = *op + v;
+    }
+    if (hf) half_s[q4] = v;
+    __syncthreads();
+    if (!hf && t < a.T) {
+        const float4 u = half_s[q4];
+        float4* op = reinterpret_cast<float4*>(a.out + (long)t * a.Hout + j);
+        float4 o = *op;
+        o.x = o.x + (v.x + u.x);
+        o.y = o.y + (v.y + u.y);
+        o.z = o.z + (v.z + u.z);
+        o.w = o.w + (v.w + u.w);
+        *op = o;
     }
 }
 

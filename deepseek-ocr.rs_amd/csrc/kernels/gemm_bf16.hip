@@ -53,6 +53,28 @@ __device__ __forceinline__ bf16x8_v frag(const uint16_t* lds, int r, int kc) {
 
 __device__ __forceinline__ float rnd_bf16(float v) { return (float)(__bf16)v; }
 
+// tile -> (M band, N column) in grouped order: gm bands per group, consecutive tiles walk down the
+// group's bands of one column, then the next column (gm = 1: one band across every column)
+__device__ __forceinline__ void tile_coords(int tile, int ntm, int ntn, int gm, int& bm, int& bn) {
+    if (gm <= 1) {
+        bm = tile / ntn;
+        bn = tile % ntn;
+        return;
+    }
+    const int per_group = gm * ntn;
+    const int first = (tile / per_group) * gm;
+    const int gsz = min(ntm - first, gm);
+    const int t = tile % per_group;
+    bm = first + t % gsz;
+    bn = t / gsz;
+}
+
+static int gemm_group_m(int requested) {
+    if (requested >= 0) return requested;
+    static const int v = getenv("DSOCR_GEMM_GROUP_M") ? atoi(getenv("DSOCR_GEMM_GROUP_M")) : 8;
+    return v;
+}
+
 // bf16-output epilogue: each reference op rounds to bf16 on its own (matmul, + bias, activation,
 // + residual), so the rounding chain is rnd(rnd(rnd(acc) + b) ...)
 __device__ __forceinline__ void bf16_store_epilogue(const GemmBf16Args& g, long orow, int col, float acc, float bv) {
@@ -77,7 +99,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(GemmBf16Args g) {
     const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
     // split-K: wgid = tile * splits + split (a tile's K slices on one XCD, adjacent in time)
     const int split = wgid % g.splits, tile = wgid / g.splits;
-    const int bm = tile / ntn, bn = tile % ntn;
+    int bm, bn;
+    tile_coords(tile, (g.M + TB_M - 1) / TB_M, ntn, g.group_m, bm, bn);
     const int m0 = bm * TB_M, n0 = bn * TB_N;
     const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A);
     const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
@@ -256,6 +279,7 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
         (reinterpret_cast<uintptr_t>(g.W) & 15))
         throw std::runtime_error("EINVAL: gemm_bf16 needs K % 64 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
+    g.group_m = gemm_group_m(g.group_m);
     const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);
     // one LDS stage unless variant 2 (tools/kbench dgemm A/B: 1.2-1.4x on the dots.ocr linears,
     // profiles/r03_kbench_dgemm.log; bitwise equal results)
@@ -313,7 +337,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
     const int split = wgid % g.splits, tile = wgid / g.splits;
-    const int bm = tile / ntn, bn = tile % ntn;
+    int bm, bn;
+    tile_coords(tile, (g.M + FX_M - 1) / FX_M, ntn, g.group_m, bm, bn);
     const int m0 = bm * FX_M, n0 = bn * BN;
     const float* A = reinterpret_cast<const float*>(g.A);
     const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
@@ -489,6 +514,7 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return;
     if (!gemm_f32a_ok(g)) throw std::runtime_error("EINVAL: gemm_f32a needs K % 32 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
+    g.group_m = gemm_group_m(g.group_m);
     const int tiles = ((g.M + FX_M - 1) / FX_M) * ((g.N + FX_N - 1) / FX_N);
     // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once), ONE LDS stage (24 KB, four blocks per
     // CU: kbench vgemm 1.00-1.18x the two-stage kernel on the SAM linears, within 3 % elsewhere); f16

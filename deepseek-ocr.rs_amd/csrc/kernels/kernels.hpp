@@ -42,6 +42,11 @@ struct GemmBf16Args {
     int out_bf16 = 0;
     int w_f16 = 0;  // gemm_f32a only: W holds f16 values (split into hi / lo bf16 in registers)
     int variant = 0;  // gemm_f32a bf16 weights: 0 = default (one LDS stage), 2 = two stages (tools/kbench A/B)
+    // tile raster: consecutive tiles (of one XCD) walk group_m M row bands down one N column, then the next
+    // column (grouped order: ~group_m bands x (resident / group_m) columns live at once share their A and W
+    // k-slices in the XCD's L2); 1 = one band across all N tiles (the round-3 order); -1 = the default
+    // (DSOCR_GEMM_GROUP_M, else 8)
+    int group_m = -1;
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
 int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)

@@ -404,8 +404,9 @@ def test_full_q4k_snapshot_engine_matches_oracle(gpu, tmp_path):
 @pytest.mark.gpu
 def test_full_q4k_snapshot_page_matches_fixture(gpu, tmp_path):
     """configs[4] with a page: the full-size synthetic Q4_K snapshot (the projector from its Q8_0 record)
-    through vision -> projector -> 706-token prefill -> 64 greedy tokens on the bench's synthetic 1024 px
-    page: ids equal and the raw logits at the oracle's top-8 indices within 2e-3 of the committed fixture
+    through vision -> projector -> 706-token prefill -> the fixture's greedy tokens on the bench's synthetic 1024 px
+    page (512 tokens): ids equal and the raw logits at the oracle's top-8 and probe indices within 2e-3 of the
+    committed fixture
     (tests/golden/full_q4k_synthetic0.npz, make_full_golden.py --snapshot q4k: the oracle reading the
     same snapshot)."""
     import os
@@ -427,9 +428,5 @@ def test_full_q4k_snapshot_page_matches_fixture(gpu, tmp_path):
         outs, logits = eng.generate_trace([(ids, mask, page, None)], DecodeParameters(max_new_tokens=n), ignore_eos=True)
     finally:
         eng.close()
-    ref = fx["ids"].tolist()
-    bad = next((s for s, (a, b) in enumerate(zip(outs[0], ref)) if a != b), None)
-    assert outs[0] == ref, f"first divergent step {bad}, oracle margin there {fx['margin'][bad]:.3g}"
-    err = float(np.max(np.abs(np.take_along_axis(logits[0][:n], fx["top_idx"][:n], 1) - fx["top_val"][:n])))
-    print(f"q4k page: 64 ids equal, top-8 logit max-abs {err:.3g}")
-    assert err <= 2e-3, err
+    from test_full_parity import check_stream
+    check_stream("q4k_synthetic0", fx, outs[0], logits[0], n)

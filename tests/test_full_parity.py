@@ -15,7 +15,8 @@ by tests/golden/make_full_golden.py in the dev container: the GPU box never runs
   max are printed.  On any id divergence the test reports the first divergent step with the oracle's
   top-1 / top-2 margin there and both sides' logits of the two tokens.
 * configs[2] shape: eight distinct pages in one batch (the grouped 3..8-token decode kernels) give
-  every page's oracle ids (64-token fixtures for pages 1..7, the 512-token page 0 prefix).
+  every page's oracle ids and logits over all 512 steps (8 image pages; 8 text pages with distinct
+  decode streams).
 """
 import json
 import os
@@ -68,6 +69,30 @@ def _report(fx, logits, got, ref, s):
             f"oracle top-8 {list(zip(fx['top_idx'][s].tolist(), np.round(fx['top_val'][s], 6).tolist()))}")
 
 
+def check_stream(name, fx, got, logits, n):
+    """ids over n steps == the oracle's, logits (up to the first divergence: identical contexts) at the oracle's
+    top-8 and the 64 probe indices within LOGIT_TOL; on a divergence the first divergent step is reported with
+    the oracle's top-1 / top-2 margin there and both sides' logits of the two tokens."""
+    ref = fx["ids"][:n].tolist()
+    s = first_divergence(got, ref)
+    upto = n if s is None else s
+    rows = np.arange(upto)
+    d_top = np.abs(logits[rows[:, None], fx["top_idx"][:upto]] - fx["top_val"][:upto])
+    d_probe = np.abs(logits[rows[:, None], fx["probe_idx"][None, :]] - fx["probe_val"][:upto])
+    d = np.concatenate([d_top.ravel(), d_probe.ravel()])
+    stats = {"page": name, "steps_compared": int(upto), "logit_max_abs": float(d.max()),
+             "logit_p99_abs": float(np.percentile(d, 99)), "min_oracle_margin": float(fx["margin"][:upto].min()),
+             "distinct_ids": len(set(ref))}
+    print(json.dumps(stats))
+    if os.environ.get("DSOCR_PARITY_OUT"):
+        with open(os.environ["DSOCR_PARITY_OUT"], "a") as f:
+            f.write(json.dumps(stats) + "\n")
+    assert s is None, f"{name}: " + _report(fx, logits, got, ref, s)
+    assert d.max() <= REF_LOGIT_TOL
+    assert d.max() <= LOGIT_TOL, stats
+    return stats
+
+
 @pytest.mark.parametrize("name", ["synthetic0", "sample_1"])
 def test_full_page_512_tokens_ids_and_logits(engine, name):
     fx = fixture(name)
@@ -85,29 +110,13 @@ def test_full_page_512_tokens_ids_and_logits(engine, name):
     n = int(fx["max_new"])
     outs, logits = engine.generate_trace([(ids, mask, page, None)], DecodeParameters(max_new_tokens=n),
                                          ignore_eos=True)
-    got, ref = outs[0], fx["ids"].tolist()
-    logits = logits[0]
-    s = first_divergence(got, ref)
-    upto = n if s is None else s
-    # logits of every step up to the first divergence (identical contexts), at the oracle's top-8 and probes
-    rows = np.arange(upto)
-    d_top = np.abs(logits[rows[:, None], fx["top_idx"][:upto]] - fx["top_val"][:upto])
-    d_probe = np.abs(logits[rows[:, None], fx["probe_idx"][None, :]] - fx["probe_val"][:upto])
-    d = np.concatenate([d_top.ravel(), d_probe.ravel()])
-    stats = {"page": name, "steps_compared": int(upto), "logit_max_abs": float(d.max()),
-             "logit_p99_abs": float(np.percentile(d, 99)), "min_oracle_margin": float(fx["margin"][:upto].min())}
-    print(json.dumps(stats))
-    if os.environ.get("DSOCR_PARITY_OUT"):
-        with open(os.environ["DSOCR_PARITY_OUT"], "a") as f:
-            f.write(json.dumps(stats) + "\n")
-    assert s is None, _report(fx, logits, got, ref, s)
-    assert d.max() <= REF_LOGIT_TOL
-    assert d.max() <= LOGIT_TOL, stats
+    check_stream(name, fx, outs[0], logits[0], n)
 
 
 def test_full_batch8_equals_oracle(engine):
-    """configs[2] shape: 8 distinct pages in one generate_batch (grouped decode MoE at 8 tokens, the
-    exact lm_head, separate RMSNorms) -> each page's oracle ids."""
+    """configs[2] shape: 8 distinct image pages in one batch (the grouped matrix-core decode at 8 tokens, the
+    exact lm_head) -> every page's oracle ids over all 512 steps (KV 707 .. 1218), the traced logits at the
+    oracle's top-8 and probe indices within LOGIT_TOL, first-divergence report."""
     names = [f"synthetic{i}" for i in range(8)]
     fxs = [fixture(n) for n in names]
     n = min(int(f["max_new"]) for f in fxs)
@@ -118,17 +127,16 @@ def test_full_batch8_equals_oracle(engine):
         ids, mask = build_prompt_tokens(tok, PROMPT, [page.n_image_tokens])
         assert ids == fx["prompt_ids"].tolist()
         reqs.append((ids, mask, page, None))
-    got = engine.generate_batch(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
-    for name, fx, g in zip(names, fxs, got):
-        ref = fx["ids"][:n].tolist()
-        s = first_divergence(g, ref)
-        assert s is None, f"{name}: first divergent step {s}: engine {g[s]} oracle {ref[s]} margin {fx['margin'][s]:.3g}"
+    got, logits = engine.generate_trace(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
+    for name, fx, g, lg in zip(names, fxs, got, logits):
+        check_stream(name, fx, g, lg, n)
 
 
 def test_full_text_batch8_equals_oracle(engine):
     """The realistic-routing 8-page batch (bench --text-pages): 706-token text prompts whose decode streams
     differ page to page (~35 distinct experts per MoE layer and step, the grouped matrix-core MoE at its
-    widest) -> every page's 64 oracle ids, and the traced logits at the oracle's top-8 indices."""
+    widest) -> every page's oracle ids over all 512 steps, the traced logits at the oracle's top-8 and probe
+    indices within LOGIT_TOL, first-divergence report."""
     from dsocr.synth import text_page_prompt
     names = [f"text{i}" for i in range(8)]
     fxs = [fixture(n) for n in names]
@@ -139,14 +147,8 @@ def test_full_text_batch8_equals_oracle(engine):
         assert ids == fx["prompt_ids"].tolist()
         reqs.append((ids, None, None, None))
     got, logits = engine.generate_trace(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
-    worst = 0.0
     for name, fx, g, lg in zip(names, fxs, got, logits):
-        ref = fx["ids"][:n].tolist()
-        s = first_divergence(g, ref)
-        assert s is None, f"{name}: first divergent step {s}: engine {g[s]} oracle {ref[s]} margin {fx['margin'][s]:.3g}"
-        top = fx["top_idx"][:n]
-        worst = max(worst, float(np.max(np.abs(np.take_along_axis(lg[:n], top, 1) - fx["top_val"][:n]))))
-    assert worst <= LOGIT_TOL, worst
+        check_stream(name, fx, g, lg, n)
     assert len({t for g in got for t in g}) > 64  # distinct streams, not one repeated token
 
 
