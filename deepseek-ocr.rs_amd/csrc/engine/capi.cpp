@@ -781,14 +781,25 @@ dsocr_status dsocr_k_lmhead_screened(int B, int V, int K, const float* x, const 
         };
         try {
             // the engine's load-time quantisation and its per-step launches (Engine::decode_head)
+            // (B = 3..8: the one-stream matrix-core form, as the engine runs it at 3..8 pages)
+            const bool mm = B >= 3 && dsocr::lmhead_q8mm_ok(B, V, K);
+            if (B > 2 && !mm) throw std::runtime_error("EINVAL: screened lm_head for 3..8 rows needs K in {768, 1024, 1280, 1536}");
+            const size_t vp = (size_t)(V + 15) / 16 * 16;
             void* q = alloc((size_t)V * K);
-            float* scale = (float*)alloc(sizeof(float) * V);
-            float* bound = (float*)alloc(sizeof(float) * V);
-            dsocr::launch_lmhead_quantize(W, V, K, q, scale, bound, nullptr);
+            float* scale = (float*)alloc(sizeof(float) * vp);
+            float* bound = (float*)alloc(sizeof(float) * vp);
+            float* qnorm = mm ? (float*)alloc(sizeof(float) * vp) : nullptr;
+            void* qfrag = mm ? alloc(dsocr::lmhead_qfrag_bytes(V, K)) : nullptr;
+            check_hip(hipMemset(scale, 0, sizeof(float) * vp), "hipMemset");
+            check_hip(hipMemset(bound, 0, sizeof(float) * vp), "hipMemset");
+            if (qnorm) check_hip(hipMemset(qnorm, 0, sizeof(float) * vp), "hipMemset");
+            dsocr::launch_lmhead_quantize(W, V, K, q, scale, bound, nullptr, qnorm, qfrag);
             dsocr::LmHeadQ8Args a;
             a.x = x; a.ldx = K; a.norm_w = norm_w; a.eps = eps; a.q = q; a.scale = scale; a.bound = bound;
             a.B = B; a.N = V; a.K = K; a.ban = ban; a.ban_ld = ban ? ban_ld : 0;
-            dsocr::lmhead_q8_grid(V, K, B, &a.nblk, &a.slot);
+            a.qfrag = qfrag; a.qnorm = qnorm;
+            if (mm) dsocr::lmhead_q8mm_grid(V, K, B, &a.nblk, &a.slot);
+            else dsocr::lmhead_q8_grid(V, K, B, &a.nblk, &a.slot);
             a.blk_cnt = (int*)alloc(sizeof(int) * B * a.nblk);
             a.blk_t = (float*)alloc(sizeof(float) * B * a.nblk);
             a.cand = (int*)alloc(sizeof(int) * B * a.nblk * a.slot);

@@ -591,10 +591,20 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
     lm_head_ = lin("lm_head", L.vocab, H, false);
     if (lm_head_.wdt == WDT_BF16 && H % 16 == 0 && H <= 1536) {
         // int8 screening copy of the lm_head (per-row scale + rigorous error bound), lmhead.hip
+        // (+ for 3..8 pages: s ||Q|| per row and the fragment-ordered copy the int8 matrix cores read; the
+        // per-row arrays padded to whole 16-row tiles)
+        const size_t vp = (size_t)(L.vocab + 15) / 16 * 16;
         lmq_ = dev_alloc((size_t)L.vocab * H);
-        lmq_scale_ = (float*)dev_alloc((size_t)L.vocab * 4);
-        lmq_bound_ = (float*)dev_alloc((size_t)L.vocab * 4);
-        launch_lmhead_quantize(lm_head_.W, L.vocab, H, lmq_, lmq_scale_, lmq_bound_, nullptr);
+        lmq_scale_ = (float*)dev_alloc(vp * 4);
+        lmq_bound_ = (float*)dev_alloc(vp * 4);
+        HIP_CHECK(hipMemset(lmq_scale_, 0, vp * 4));
+        HIP_CHECK(hipMemset(lmq_bound_, 0, vp * 4));
+        if (lmhead_q8mm_ok(8, L.vocab, H)) {
+            lmq_qnorm_ = (float*)dev_alloc(vp * 4);
+            HIP_CHECK(hipMemset(lmq_qnorm_, 0, vp * 4));
+            lmq_frag_ = dev_alloc(lmhead_qfrag_bytes(L.vocab, H));
+        }
+        launch_lmhead_quantize(lm_head_.W, L.vocab, H, lmq_, lmq_scale_, lmq_bound_, nullptr, lmq_qnorm_, lmq_frag_);
         HIP_CHECK(hipDeviceSynchronize());
     }
 }
@@ -1148,18 +1158,29 @@ void Engine::decode_step(int B, int Lmax) {
     }
 }
 
-// workspaces of the screened head (allocated before a graph capture)
-void Engine::reserve_head_ws(int B) {
-    if (!lmq_ || B > 2) return;
+// the screened head's launch arguments for B rows of s_x (workspaces allocated here: call before a graph
+// capture): B <= 2 the single-token kernel per page, 3..8 one int8 stream on the matrix cores
+LmHeadQ8Args Engine::head_q8_args(int B) {
     const LangConfig& L = cfg_.lang;
-    int nblk = 0;
-    long slot = 0;
-    lmhead_q8_grid(L.vocab, L.hidden, B, &nblk, &slot);
-    wsi("s_blkcnt", (size_t)B * nblk);
-    wsf("s_blkt", (size_t)B * nblk);
-    wsi("s_cand", (size_t)B * nblk * slot);
-    wsf("s_candhi", (size_t)B * nblk * slot);
-    wsf("s_lmxn", (size_t)B * L.hidden);
+    const int H = L.hidden;
+    LmHeadQ8Args q;
+    q.x = wsf("s_x", (size_t)B * H); q.ldx = H; q.norm_w = final_norm_; q.eps = L.rms_eps;
+    q.q = lmq_; q.scale = lmq_scale_; q.bound = lmq_bound_; q.B = B; q.N = L.vocab; q.K = H;
+    if (B >= 3) {
+        q.qfrag = lmq_frag_; q.qnorm = lmq_qnorm_;
+        lmhead_q8mm_grid(L.vocab, H, B, &q.nblk, &q.slot);
+    } else {
+        lmhead_q8_grid(L.vocab, H, B, &q.nblk, &q.slot);
+    }
+    q.blk_cnt = wsi("s_blkcnt", (size_t)B * q.nblk); q.blk_t = wsf("s_blkt", (size_t)B * q.nblk);
+    q.cand = wsi("s_cand", (size_t)B * q.nblk * q.slot); q.cand_hi = wsf("s_candhi", (size_t)B * q.nblk * q.slot);
+    q.xn_out = wsf("s_lmxn", (size_t)B * H);
+    return q;
+}
+
+void Engine::reserve_head_ws(int B) {
+    if (!lmq_ || B > 8 || (B >= 3 && !lmq_frag_)) return;
+    (void)head_q8_args(B);
 }
 
 // 3..8 pages: fragment-ordered copies of the lm_head and of every MoE layer's experts for the
@@ -1205,12 +1226,13 @@ bool Engine::qkv_attn_fused() {
     return v;
 }
 
-// screened selection applies (lmhead.hip): int8 copy present, B <= 2, no repetition penalty
+// screened selection applies (lmhead.hip): int8 copy present, B <= 8 (3..8: the matrix-core form), no
+// repetition penalty
 // (DSOCR_SCREEN=0 forces the exact lm_head; read per generate call)
 bool Engine::screen_applies(int B, float rep_penalty) const {
     if (getenv("DSOCR_SCREEN") && atoi(getenv("DSOCR_SCREEN")) == 0) return false;
     const bool pen = rep_penalty > 0.f && fabsf(rep_penalty - 1.0f) > 1.1920929e-07f;
-    return lmq_ && B <= 2 && !pen;
+    return lmq_ && !pen && (B <= 2 || (B <= 8 && lmq_frag_ && lmhead_q8mm_ok(B, cfg_.lang.vocab, cfg_.lang.hidden)));
 }
 
 // final norm + lm_head + greedy selection + step bookkeeping for the B decode rows in s_x
@@ -1222,15 +1244,8 @@ void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
     if (sa.ban_out) {
         // screened selection: int8 lm_head intervals + running threshold, exact rescoring of the
         // few kept rows — the exact path's token from half the lm_head bytes
-        reserve_head_ws(B);
-        LmHeadQ8Args q;
-        q.x = SX; q.ldx = H; q.norm_w = final_norm_; q.eps = L.rms_eps;
-        q.q = lmq_; q.scale = lmq_scale_; q.bound = lmq_bound_; q.B = B; q.N = L.vocab; q.K = H;
+        LmHeadQ8Args q = head_q8_args(B);
         q.ban = sa.ban_out; q.ban_ld = sa.ban_ld;
-        lmhead_q8_grid(L.vocab, H, B, &q.nblk, &q.slot);
-        q.blk_cnt = wsi("s_blkcnt", (size_t)B * q.nblk); q.blk_t = wsf("s_blkt", (size_t)B * q.nblk);
-        q.cand = wsi("s_cand", (size_t)B * q.nblk * q.slot); q.cand_hi = wsf("s_candhi", (size_t)B * q.nblk * q.slot);
-        q.xn_out = wsf("s_lmxn", (size_t)B * H);
         launch_lmhead_q8(q, st);
         DecSampleArgs ss = sa;
         ss.blk_cnt = q.blk_cnt; ss.blk_t = q.blk_t; ss.cand = q.cand; ss.cand_hi = q.cand_hi; ss.nblk = q.nblk; ss.slot = q.slot;
@@ -1986,16 +2001,9 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         });
         prof.lm_head.bytes = (double)L.vocab * H * 2.0 + (double)B * (L.vocab + H) * 4.0;
         prof.lm_head.flops = 2.0 * B * (double)L.vocab * H;
-        if (lmq_ && B <= 2) {
+        if (screen_applies(B, 1.0f)) {
             // screened head: int8 lm_head + selection (no bookkeeping, no ban: side-effect free)
-            reserve_head_ws(B);
-            LmHeadQ8Args q;
-            q.x = SX; q.ldx = H; q.norm_w = final_norm_; q.eps = L.rms_eps;
-            q.q = lmq_; q.scale = lmq_scale_; q.bound = lmq_bound_; q.B = B; q.N = L.vocab; q.K = H;
-            lmhead_q8_grid(L.vocab, H, B, &q.nblk, &q.slot);
-            q.blk_cnt = wsi("s_blkcnt", (size_t)B * q.nblk); q.blk_t = wsf("s_blkt", (size_t)B * q.nblk);
-            q.cand = wsi("s_cand", (size_t)B * q.nblk * q.slot); q.cand_hi = wsf("s_candhi", (size_t)B * q.nblk * q.slot);
-            q.xn_out = wsf("s_lmxn", (size_t)B * H);
+            const LmHeadQ8Args q = head_q8_args(B);
             DecSampleArgs ss;
             ss.B = B; ss.V = L.vocab; ss.ld = L.vocab; ss.ctx = wsi("p_sctx", 64); ss.ctx_cap = 64;
             ss.ctx_len = wsi("p_ctxlen", B); ss.ngram = 0; ss.out_tok = wsi("p_tok", B);

@@ -213,6 +213,7 @@ class Engine {
     MoeDecodeArgs moe_args(int l, int B, float* X);
     void decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen);
     void reserve_head_ws(int B);
+    LmHeadQ8Args head_q8_args(int B);
     bool screen_applies(int B, float rep_penalty) const;
     void layer_forward_prefill(int l, int T, int B, const int* row_page, const int* row_pos, const long* q_off,
                                const long* kv_off, const long* o_off, const int* seq_len, int max_len, int Lmax);
@@ -246,6 +247,8 @@ class Engine {
     void* lmq_ = nullptr;            // int8 [vocab][hidden] screening copy of lm_head
     float* lmq_scale_ = nullptr;     // per-row scale
     float* lmq_bound_ = nullptr;     // per-row error-bound factor (times ||x||)
+    float* lmq_qnorm_ = nullptr;     // per-row s ||Q|| (3..8 pages: the token rows' int8 representation error)
+    void* lmq_frag_ = nullptr;       // the int8 rows in the int8 matrix cores' fragment order (3..8 pages)
     float* rope_cos_ = nullptr;
     float* rope_sin_ = nullptr;
     int rope_cap_ = 0;

@@ -420,11 +420,20 @@ struct LmHeadQ8Args {
     int* blk_cnt = nullptr; float* blk_t = nullptr; int* cand = nullptr; float* cand_hi = nullptr;
     int nblk = 0; long slot = 0;  // from lmhead_q8_grid
     float* xn_out = nullptr;  // [B][K]
+    // B = 3..8 (lmhead_q8mm): the fragment-ordered int8 copy and s_v ||Q_v|| per row (scale / bound / qnorm
+    // padded to whole 16-row tiles); the grid from lmhead_q8mm_grid
+    const void* qfrag = nullptr; const float* qnorm = nullptr;
 };
 void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s);
 // grid of the screened lm_head for B pages: blocks per page and the per-block slot length
 void lmhead_q8_grid(int N, int K, int B, int* nblk, long* slot);
-void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s);
+// B = 3..8: one int8 stream for every token on the int8 matrix cores (K % 64 == 0, K <= 1536)
+bool lmhead_q8mm_ok(int B, int N, int K);
+void lmhead_q8mm_grid(int N, int K, int B, int* nblk, long* slot);
+size_t lmhead_qfrag_bytes(int V, int K);
+// load time: int8 rows + scale + bound (+ optional s ||Q|| and the fragment-ordered copy for B = 3..8)
+void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s,
+                            float* qnorm = nullptr, void* qfrag = nullptr);
 
 // DSQ snapshot tensors (dsq.hip): dtype codes of crates/dsq/src/lib.rs:60-110; decode a record's
 // payload ([out][in], row-major blocks) into fp16 on the device

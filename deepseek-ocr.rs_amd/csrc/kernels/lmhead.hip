@@ -21,7 +21,7 @@ namespace dsocr {
 
 // ---------------------------------------------------------------- load time: quantise one row per block
 __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __restrict__ w, int K, int8_t* q,
-                                                              float* scale, float* bound) {
+                                                              float* scale, float* bound, float* qnorm, int8_t* qf) {
     __shared__ double red[256];
     const int v = blockIdx.x;
     const uint16_t* row = w + (long)v * K;
@@ -36,11 +36,16 @@ __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __
     const float s = red[0] > 0.0 ? (float)(red[0] / 127.0) : 1.f;
     __syncthreads();
     double e2 = 0.0, w2 = 0.0, q2 = 0.0;
+    int8_t* const qf_out = qf;
     for (int k = threadIdx.x; k < K; k += 256) {
         const float x = bf16_bits_to_f32(row[k]);
         float qf = rintf(x / s);
         qf = fminf(127.f, fmaxf(-127.f, qf));
         q[(long)v * K + k] = (int8_t)qf;
+        if (qf_out) {  // fragment order of the multi-token kernel: [v/16][k/64][lane = v%16 + 16 (k%64)/16][k%16]
+            const int kk = k & 63;
+            qf_out[(((long)(v >> 4) * (K >> 6) + (k >> 6)) * 64 + (v & 15) + 16 * (kk >> 4)) * 16 + (kk & 15)] = (int8_t)qf;
+        }
         const double e = (double)x - (double)s * (double)qf;
         e2 += e * e;
         w2 += (double)x * x;
@@ -64,13 +69,20 @@ __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __
         const double b = (sqrt(e2) + g * (sqrt(w2) + (double)s * sqrt(q2))) * (1.0 + 1e-6) + 1e-30;
         scale[v] = s;
         bound[v] = __double2float_ru(b);
+        if (qnorm) qnorm[v] = __double2float_ru((double)s * sqrt(q2) * (1.0 + 1e-6));  // s ||Q||, rounded up
     }
 }
 
-void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s) {
+void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s,
+                            float* qnorm, void* qfrag) {
+    if (qfrag && K % 64) throw std::runtime_error("EINVAL: fragment-ordered int8 lm_head needs K % 64 == 0");
+    if (qfrag && V % 16 && hipMemsetAsync(qfrag, 0, lmhead_qfrag_bytes(V, K), s) != hipSuccess)
+        throw std::runtime_error("EINTERNAL: hipMemsetAsync (int8 lm_head tail tile)");
     DSOCR_LAUNCH(lmhead_quantize_kernel, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
-                       reinterpret_cast<int8_t*>(q), scale, bound);
+                       reinterpret_cast<int8_t*>(q), scale, bound, qnorm, reinterpret_cast<int8_t*>(qfrag));
 }
+
+size_t lmhead_qfrag_bytes(int V, int K) { return (size_t)((V + 15) / 16) * 16 * K; }
 
 // ---------------------------------------------------------------- per step: screened lm_head
 // x staged once per block exactly as dec_gemv_stream stages it (RMSNorm fused); block 0 also
@@ -349,10 +361,270 @@ void lmhead_q8_grid(int N, int K, int B, int* nblk, long* slot) {
     *slot = (long)per_wave * 4 * LQ_RB;
 }
 
+
+
+// ---------------------------------------------------------------- 3..8 tokens: one int8 stream for all
+// The same intervals for B = 3..8 decode rows, with the int8 rows read ONCE for every token on the
+// int8 matrix cores (v_mfma_i32_16x16x64_i8: 16 vocabulary rows x 64 k as the A operand, straight from
+// the fragment-ordered copy, one 1 KiB block per wave load; the B operand = the token rows).  Each
+// token's normalised row x (staged as dec_gemv / the single-token kernel stage it, block 0 writes it for
+// the exact rescoring) is represented in two int8 planes, x~ = t1 Xh + t2 Xl (t1 = max|x| / 127,
+// Xh = rint(x / t1), t2 = t1 / 254, Xl = rint((x - t1 Xh) / t2)), so Ih = Xh.Q_v and Il = Xl.Q_v are exact
+// int32 dot products and A_v = s_v (t1 Ih + t2 Il) is formed in f64.  Bound (per row v, token t):
+//   L_v - A_v = [fl(x.W) - x.W] + [x.(W - s Q)] + [s (x - x~).Q] + [s x~.Q - A_v]
+//   |.| <= ||x|| bound_v + (s_v ||Q_v||) ||x - x~|| + (f64 rounding of A_v, covered by the margin)
+// with ||x||, ||x - x~|| summed in f64 and rounded up, s ||Q|| stored at load (lmhead_quantize).  The
+// kept-row lists, per-block thresholds and the final kernel (dec_screen_final) are the single-token
+// kernel's, one list per token (page).
+constexpr int LM_T = 8, LM_WV = 8, LM_LIST = 256, LM_KMAX = 1536, LM_BANS = 128, LM_TPB = LM_LIST / 16;
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int KS>  // k-steps of 64 held in registers: KS == K / 64
+__global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int tpb) {
+    __shared__ __attribute__((aligned(16))) int8_t xq[2][LM_T][LM_KMAX + 16];
+    __shared__ float t1_s[LM_T], t2_s[LM_T], nrm_s[LM_T], errn_s[LM_T];
+    __shared__ unsigned tkey_s[LM_T];
+    __shared__ int lst_n[LM_T], nban_s[LM_T];
+    __shared__ int lst_idx[LM_T][LM_LIST];
+    __shared__ float lst_hi[LM_T][LM_LIST];
+    __shared__ int ban_s[LM_T][LM_BANS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int ks = KS;
+    const int K = KS * 64, B = a.B, N = a.N;
+    const int ntiles = (N + 15) >> 4;
+    const int t_beg = blockIdx.x * tpb, t_end = min(ntiles, t_beg + tpb);
+    const v4i32* QF = reinterpret_cast<const v4i32*>(a.qfrag);
+    // weight fragments stream through a ring of PF k-steps per wave: step t + PF (of this tile, or of the
+    // wave's next tile) is issued as step t is consumed, so PF KiB stay in flight per wave across tile
+    // boundaries; the first tile's first PF steps go out before the staging (their latency overlaps it)
+    constexpr int PF = KS / 2;
+    v4i32 wa[PF];
+    auto ld = [&](int T_, int t) {
+        return __builtin_nontemporal_load(QF + ((long)min(T_, ntiles - 1) * ks + t) * 64 + lane);
+    };
+    int T = t_beg + wave;
+#pragma unroll
+    for (int t = 0; t < PF; ++t) wa[t] = ld(T, t);
+    if (tid < LM_T) { tkey_s[tid] = 0u; lst_n[tid] = 0; nban_s[tid] = 0; }
+    // ---- stage: wave w normalises token row w (K <= 1536: float4 chunks lane + 64 j), quantises it
+    // into the two planes and sums ||x||^2 and ||x - x~||^2 in f64
+    if (wave < B) {
+        // three passes over the row (L1-resident after the first): sum of squares; max |x|; quantise
+        const float* xr = a.x + (long)wave * a.ldx;
+        constexpr int J = LM_KMAX / 256;
+        if (a.ban) {
+            const int* bg = a.ban + (long)wave * a.ban_ld;
+            const int nb = bg[0];
+            for (int i = lane; i < min(nb, LM_BANS); i += 64) ban_s[wave][i] = bg[1 + i];
+            if (lane == 0) nban_s[wave] = nb;
+        }
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int k = (lane + 64 * j) * 4;
+            if (k < K) {
+                const float4 v = *reinterpret_cast<const float4*>(xr + k);
+                q += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+            }
+        }
+        q = wave_sum(q);
+        const float den = sqrtf(q / (float)K + a.eps);
+        auto xhat = [&](int k) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k), w = *reinterpret_cast<const float4*>(a.norm_w + k);
+            return make_float4((v.x / den) * w.x, (v.y / den) * w.y, (v.z / den) * w.z, (v.w / den) * w.w);
+        };
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int k = (lane + 64 * j) * 4;
+            if (k < K) {
+                const float4 o = xhat(k);
+                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+            }
+        }
+        mx = wave_max(mx);
+        const float t1 = mx > 0.f ? mx / 127.f : 1.f, t2 = t1 / 254.f;
+        double n2 = 0.0, e2 = 0.0;
+        for (int j = 0; j < J; ++j) {
+            const int k = (lane + 64 * j) * 4;
+            if (k < K) {
+                const float4 o = xhat(k);
+                const float xv[4] = {o.x, o.y, o.z, o.w};
+                uint32_t hw = 0, lw = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float h = fminf(127.f, fmaxf(-127.f, rintf(xv[e] / t1)));
+                    const float l = fminf(127.f, fmaxf(-127.f, rintf(fmaf(-t1, h, xv[e]) / t2)));
+                    hw |= (uint32_t)(uint8_t)(int8_t)h << (8 * e);
+                    lw |= (uint32_t)(uint8_t)(int8_t)l << (8 * e);
+                    const double d = (double)xv[e] - ((double)t1 * (double)h + (double)t2 * (double)l);
+                    e2 += d * d;
+                    n2 += (double)xv[e] * (double)xv[e];
+                }
+                *reinterpret_cast<uint32_t*>(&xq[0][wave][k]) = hw;
+                *reinterpret_cast<uint32_t*>(&xq[1][wave][k]) = lw;
+                if (blockIdx.x == 0 && a.xn_out) *reinterpret_cast<float4*>(a.xn_out + (long)wave * K + k) = o;
+            }
+        }
+        n2 = wave_sum_d(n2);
+        e2 = wave_sum_d(e2);
+        if (lane == 0) {
+            t1_s[wave] = t1;
+            t2_s[wave] = t2;
+            nrm_s[wave] = __double2float_ru(sqrt(n2) * (1.0 + 1e-9));
+            errn_s[wave] = __double2float_ru(sqrt(e2) * (1.0 + 1e-9) + 1e-30);
+        }
+    }
+    __syncthreads();
+    // ---- per lane: token column c (lanes of columns >= B compute on a clamped row and are dropped),
+    // rows 16 T + 4 g + i (the int32 accumulator layout of the 16x16 MFMA)
+    const int c = lane & 15, g = lane >> 4, cr = min(c, B - 1);
+    const bool col_ok = c < B;
+    const float t1 = t1_s[cr], t2 = t2_s[cr], nrm = nrm_s[cr], errn = errn_s[cr];
+    const int8_t* xh = &xq[0][cr][16 * g];
+    const int8_t* xl = &xq[1][cr][16 * g];
+    float Tw = -INFINITY;
+    for (; T < t_end; T += LM_WV) {
+        const int Tn = T + LM_WV;
+        // scale / bound / s||Q|| of this lane's 4 rows (the arrays are padded to whole tiles)
+        const int r0 = 16 * T + 4 * g;
+        const float4 sc4 = *reinterpret_cast<const float4*>(a.scale + r0);
+        const float4 bd4 = *reinterpret_cast<const float4*>(a.bound + r0);
+        const float4 qn4 = *reinterpret_cast<const float4*>(a.qnorm + r0);
+        v4i32 ch = {0, 0, 0, 0}, cl = {0, 0, 0, 0};
+        // the token planes are re-read from LDS per tile (kept live across tiles they would take 8 KS VGPRs)
+        const int8_t* ph = xh;
+        const int8_t* pl = xl;
+        asm volatile("" : "+v"(ph), "+v"(pl));
+#pragma unroll
+        for (int t = 0; t < KS; ++t) {
+            const v4i32 bh = *reinterpret_cast<const v4i32*>(ph + 64 * t);
+            const v4i32 bl = *reinterpret_cast<const v4i32*>(pl + 64 * t);
+            const v4i32 w = wa[t % PF];
+            ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(w, bh, ch, 0, 0, 0);
+            cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(w, bl, cl, 0, 0, 0);
+            // refill the slot: step t + PF of this tile, else step t + PF - KS of the next (clamped: a wave
+            // without a next tile re-reads its last tile's rows, never used)
+            wa[t % PF] = t + PF < KS ? ld(T, t + PF) : ld(Tn < t_end ? Tn : T, t + PF - KS);
+            __builtin_amdgcn_sched_barrier(0);  // keep each step's two LDS reads next to its MFMAs
+        }
+        const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w}, bdv[4] = {bd4.x, bd4.y, bd4.z, bd4.w},
+                    qnv[4] = {qn4.x, qn4.y, qn4.z, qn4.w};
+        float lo[4], hi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const double A = (double)scv[i] * ((double)t1 * (double)ch[i] + (double)t2 * (double)cl[i]);
+            const double e = ((double)nrm * (double)bdv[i] + (double)qnv[i] * (double)errn) * (1.0 + 1e-6) +
+                             fabs(A) * 1e-12 + 1e-30;
+            lo[i] = __double2float_rd(A - e);
+            hi[i] = __double2float_ru(A + e);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 16 * T + 4 * g + i;
+            const bool trig = col_ok && row < N && (lo[i] > Tw || hi[i] >= Tw);
+            unsigned long long m = __ballot(trig);
+            while (m) {
+                const int r = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const float lo_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lo[i]), r));
+                const float hi_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi[i]), r));
+                const float Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tw), r));
+                const int tc = r & 15, n = 16 * T + 4 * (r >> 4) + i;
+                if (!(lo_r > Tc) && !(hi_r >= Tc)) continue;
+                const int nb = __builtin_amdgcn_readfirstlane(nban_s[tc]);
+                bool banned = false;
+                if (nb <= LM_BANS) {
+                    for (int j = 0; j < nb; ++j) banned = banned || ban_s[tc][j] == n;
+                } else {
+                    const int* bg = a.ban + (long)tc * a.ban_ld + 1;
+                    for (int j = 0; j < nb; ++j) banned = banned || bg[j] == n;
+                }
+                if (banned) continue;
+                if (lo_r > Tc) {
+                    if (c == tc) Tw = lo_r;  // every lane of token tc
+                    if (lane == 0) atomicMax(&tkey_s[tc], fkey(lo_r));
+                }
+                if (lane == 0) {
+                    const int p = atomicAdd(&lst_n[tc], 1);
+                    lst_idx[tc][p] = n;
+                    lst_hi[tc][p] = hi_r;
+                }
+            }
+        }
+        Tw = fmaxf(Tw, fkey_dec(tkey_s[cr]));
+    }
+    __syncthreads();
+    // ---- every token's list against its block threshold -> cand[b][p][block] (the single-token layout)
+    for (int tk = wave; tk < B; tk += LM_WV) {
+        const int cnt = lst_n[tk];
+        const float Tb = fkey_dec(tkey_s[tk]);
+        const long sb = (long)tk * a.nblk * a.slot + blockIdx.x;
+        int kept = 0;
+        for (int i0 = 0; i0 < cnt; i0 += 64) {
+            const int i = i0 + lane;
+            const bool keep = i < cnt && lst_hi[tk][i] >= Tb;
+            const unsigned long long bm = __ballot(keep);
+            if (keep) {
+                const int p = kept + __popcll(bm & ((1ull << lane) - 1ull));
+                a.cand[sb + (long)p * a.nblk] = lst_idx[tk][i];
+                a.cand_hi[sb + (long)p * a.nblk] = lst_hi[tk][i];
+            }
+            kept += __popcll(bm);
+        }
+        if (lane == 0) {
+            a.blk_cnt[(long)tk * a.nblk + blockIdx.x] = kept;
+            a.blk_t[(long)tk * a.nblk + blockIdx.x] = Tb;
+        }
+    }
+}
+
+bool lmhead_q8mm_ok(int B, int N, int K) {
+    return B >= 1 && B <= LM_T && (K == 768 || K == 1024 || K == 1280 || K == 1536) && N >= 16;
+}
+
+void lmhead_q8mm_grid(int N, int K, int B, int* nblk, long* slot) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    (void)K;
+    (void)B;
+    const int tiles = (N + 15) / 16;
+    // two blocks of 8 waves per CU; a block's tiles (its rows) never exceed its LDS lists
+    int blocks = std::max(2 * cus, (tiles + LM_TPB - 1) / LM_TPB);
+    const int tpb = (tiles + blocks - 1) / blocks;
+    blocks = (tiles + tpb - 1) / tpb;
+    *nblk = blocks;
+    *slot = (long)tpb * 16;
+}
+
 void launch_lmhead_q8(const LmHeadQ8Args& a, hipStream_t s) {
     if (a.K % 16 || a.K > 1536 || a.K < 16) throw std::runtime_error("EINVAL: lmhead_q8 needs K % 16 == 0, K <= 1536");
     int nblk = 0;
     long slot = 0;
+    if (a.B >= 3 && a.qfrag) {  // one int8 stream for all B tokens on the matrix cores
+        if (!lmhead_q8mm_ok(a.B, a.N, a.K) || !a.qnorm) throw std::runtime_error("EINVAL: lmhead_q8mm outside its range");
+        lmhead_q8mm_grid(a.N, a.K, a.B, &nblk, &slot);
+        if (!a.blk_cnt || !a.blk_t || !a.cand || !a.cand_hi || a.nblk != nblk || a.slot != slot)
+            throw std::runtime_error("EINVAL: lmhead_q8mm block lists missing or not sized by lmhead_q8_grid");
+        if (a.ban && a.ban_ld < 2) throw std::runtime_error("EINVAL: lmhead_q8 ban list stride < 2");
+        const int tpb = (int)(slot / 16);
+        if (a.K == 1280) DSOCR_LAUNCH(lmhead_q8mm_kernel<20>, dim3(nblk), dim3(512), 0, s, a, tpb);
+        else if (a.K == 1536) DSOCR_LAUNCH(lmhead_q8mm_kernel<24>, dim3(nblk), dim3(512), 0, s, a, tpb);
+        else if (a.K == 1024) DSOCR_LAUNCH(lmhead_q8mm_kernel<16>, dim3(nblk), dim3(512), 0, s, a, tpb);
+        else DSOCR_LAUNCH(lmhead_q8mm_kernel<12>, dim3(nblk), dim3(512), 0, s, a, tpb);
+        return;
+    }
     lmhead_q8_grid(a.N, a.K, a.B, &nblk, &slot);
     if (!a.blk_cnt || !a.blk_t || !a.cand || !a.cand_hi || a.nblk != nblk || a.slot != slot)
         throw std::runtime_error("EINVAL: lmhead_q8 block lists missing or not sized by lmhead_q8_grid");

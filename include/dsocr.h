@@ -199,7 +199,8 @@ typedef struct dsocr_decode_profile {
     dsocr_kernel_profile router;      /* MoE router: dec_gemv logits at 1-2 pages (the mix kernels rank-select),
                                          dec_route_grp (RMSNorm + logits + top-k + expert records) at 3-8 */
     dsocr_kernel_profile layers_step; /* every decoder layer of one decode step, replayed as one hipGraph */
-    dsocr_kernel_profile lm_head_screened; /* int8 screened lm_head + exact rescoring selection (B <= 2, no penalty) */
+    dsocr_kernel_profile lm_head_screened; /* int8 screened lm_head + exact rescoring selection (B <= 8, no penalty;
+                                              3..8: one int8 stream on the int8 matrix cores) */
     const char* moe_gateup_kernel;    /* static strings: kernel names of the two MoE entries above */
     const char* moe_down_kernel;
 } dsocr_decode_profile;

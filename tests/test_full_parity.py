@@ -160,3 +160,18 @@ def test_full_screened_head_equals_traced_ids(engine):
     got = engine.generate(ids, mask, page, None, DecodeParameters(max_new_tokens=int(fx["max_new"])), ignore_eos=True)
     s = first_divergence(got, fx["ids"].tolist())
     assert s is None, f"first divergent step {s}"
+
+
+def test_full_text_batch8_screened_head_equals_oracle(engine):
+    """The bench path at 8 pages (no trace: the screened head, 3..8 rows on the int8 matrix cores + exact
+    rescoring, inside the replayed step graph) -> every text page's oracle ids over all 512 steps."""
+    from dsocr.synth import text_page_prompt
+    names = [f"text{i}" for i in range(8)]
+    fxs = [fixture(n) for n in names]
+    n = min(int(f["max_new"]) for f in fxs)
+    reqs = [(text_page_prompt(i, vocab=engine.vocab), None, None, None) for i in range(8)]
+    got = engine.generate_batch(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
+    for name, fx, g in zip(names, fxs, got):
+        ref = fx["ids"][:n].tolist()
+        s = first_divergence(g, ref)
+        assert s is None, f"{name}: first divergent step {s}: engine {g[s]} oracle {ref[s]} margin {fx['margin'][s]:.3g}"

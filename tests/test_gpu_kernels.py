@@ -447,13 +447,16 @@ def test_moe_decode_full_size_dispatch(gpu, T, H, E, topk, I, ns, norm):
 
 
 # ---------------------------------------------------------------- screened lm_head: ties / near ties
-def test_screened_head_ties_first_index(gpu):
+@pytest.mark.parametrize("B", [2, 3, 8])
+def test_screened_head_ties_first_index(gpu, B):
     """The screened selection (int8 intervals + exact rescoring) against the exact lm_head GEMV's
     first-index argmax (argmax_index, sampling.rs:104-118) on rows built to tie: two identical
     dominant rows (first index wins), a row one bf16 ulp away in one element (a near tie far below
-    the int8 quantisation error), and a ban list that removes the first of the tied rows."""
+    the int8 quantisation error), and a ban list that removes the first of the tied rows.  B = 2: the
+    single-token kernel per page; B = 3, 8: one int8 stream for every row on the int8 matrix cores (two int8
+    planes per token row, its representation error in the bound)."""
     rng = np.random.default_rng(99)
-    B, V, K = 3, 20000, 1280
+    V, K = 20000, 1280
     x = rng.standard_normal((B, K)).astype(np.float32)
     nw = (1.0 + 0.05 * rng.standard_normal(K)).astype(np.float32)
     w = (rng.standard_normal((V, K)) * 0.02).astype(np.float32)
@@ -472,6 +475,8 @@ def test_screened_head_ties_first_index(gpu):
     ban = np.zeros((B, ban_ld), np.int32)
     ban[1, 0], ban[1, 1] = 2, A            # page 1: A banned
     ban[1, 2] = Cn
+    if B > 3:
+        ban[B - 1, 0], ban[B - 1, 1:6] = 5, [int(t) for t in rng.integers(0, V, 5)]  # a longer list
     dx, dn, dW, dban, dt = Dev(x), Dev(nw), Dev(bits), Dev(ban), Dev.zeros(B, np.int32)
     check(lib().dsocr_k_lmhead_screened(B, V, K, dx.ptr, dn.ptr, 1e-6, dW.ptr, dban.ptr, ban_ld, dt.ptr))
     got = dt.get()
@@ -485,6 +490,37 @@ def test_screened_head_ties_first_index(gpu):
             row[t] = -np.inf
         assert got[b] == int(np.argmax(row)), (b, got[b], int(np.argmax(row)), row[[A, Bt, Cn, 4000]])
     assert got[1] != A and got[1] != Cn
+
+
+@pytest.mark.parametrize("B,V", [(3, 50000), (8, 129280), (5, 1000)])
+def test_screened_head_multi_token_random(gpu, B, V):
+    """3..8 rows on the int8 matrix cores over random rows (vocab sizes incl. the model's 129280 and a
+    partial last 16-row tile): the selected token of every row equals the exact GEMV's first-index argmax,
+    with each row's top candidates placed at tile edges and a ban list on one row."""
+    rng = np.random.default_rng(B * 7 + V)
+    K = 1280
+    x = rng.standard_normal((B, K)).astype(np.float32)
+    nw = (1.0 + 0.05 * rng.standard_normal(K)).astype(np.float32)
+    bits = bf16_round((rng.standard_normal((V, K)) * 0.02).astype(np.float32))
+    xn = rms_norm(x, nw, 1e-6)
+    for b in range(B):  # a strong row per page at a tile edge (row 16 t + 15) or the last row
+        r = V - 1 if b == 0 else (int(rng.integers(0, V // 16)) * 16 + 15) % V
+        bits[r] = bf16_round((xn[b] / np.linalg.norm(xn[b]) * 0.06 + rng.standard_normal(K) * 0.01).astype(np.float32))
+    ban_ld = 8
+    ban = np.zeros((B, ban_ld), np.int32)
+    dy = Dev.zeros((B, V))
+    dx, dn, dW = Dev(x), Dev(nw), Dev(bits)
+    check(lib().dsocr_k_gemv(B, V, K, dx.ptr, dn.ptr, 1e-6, dW.ptr, 0, None, dy.ptr, 0, 0))
+    ex = dy.get()
+    ban[B - 1, 0], ban[B - 1, 1] = 1, int(np.argmax(ex[B - 1]))  # the last row's best is banned
+    dban, dt = Dev(ban), Dev.zeros(B, np.int32)
+    check(lib().dsocr_k_lmhead_screened(B, V, K, dx.ptr, dn.ptr, 1e-6, dW.ptr, dban.ptr, ban_ld, dt.ptr))
+    got = dt.get()
+    for b in range(B):
+        row = ex[b].copy()
+        for t in ban[b, 1:1 + ban[b, 0]]:
+            row[t] = -np.inf
+        assert got[b] == int(np.argmax(row)), (b, got[b], int(np.argmax(row)))
 
 
 # ---------------------------------------------------------------- bf16-matrix-core attention (dots.ocr ViT)
