@@ -490,11 +490,31 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
     const float t1 = t1_s[cr], t2 = t2_s[cr], nrm = nrm_s[cr], errn = errn_s[cr];
     const int8_t* xh = &xq[0][cr][16 * g];
     const int8_t* xl = &xq[1][cr][16 * g];
-    float Tw = -INFINITY;
-    for (; T < t_end; T += LM_WV) {
-        const int Tn = T + LM_WV;
+    // ---- phase 1: every tile of the wave (at most TPW) -> the lane's row intervals, kept in registers, and
+    // the lane's best unbanned lower bound; the block threshold per token from those (LDS atomicMax)
+    // ---- phase 2: the lane's rows whose upper bound reaches the threshold (and not banned) join the list.
+    // No per-row serial path: a row is tested against the BLOCK's final threshold, not a running one.
+    constexpr int TPW = (LM_TPB + LM_WV - 1) / LM_WV;
+    float lo_a[TPW][4], hi_a[TPW][4];
+    auto banned = [&](int n) {
+        const int nb = nban_s[cr];
+        bool hit = false;
+        if (nb <= LM_BANS) {
+            for (int j = 0; j < nb; ++j) hit = hit || ban_s[cr][j] == n;
+        } else {
+            const int* bg = a.ban + (long)cr * a.ban_ld + 1;
+            for (int j = 0; j < nb; ++j) hit = hit || bg[j] == n;
+        }
+        return hit;
+    };
+    float best = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int Tu = T + u * LM_WV;
+        if (Tu >= t_end) break;  // wave-uniform
+        const int Tn = Tu + LM_WV;
         // scale / bound / s||Q|| of this lane's 4 rows (the arrays are padded to whole tiles)
-        const int r0 = 16 * T + 4 * g;
+        const int r0 = 16 * Tu + 4 * g;
         const float4 sc4 = *reinterpret_cast<const float4*>(a.scale + r0);
         const float4 bd4 = *reinterpret_cast<const float4*>(a.bound + r0);
         const float4 qn4 = *reinterpret_cast<const float4*>(a.qnorm + r0);
@@ -512,54 +532,42 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
             cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(w, bl, cl, 0, 0, 0);
             // refill the slot: step t + PF of this tile, else step t + PF - KS of the next (clamped: a wave
             // without a next tile re-reads its last tile's rows, never used)
-            wa[t % PF] = t + PF < KS ? ld(T, t + PF) : ld(Tn < t_end ? Tn : T, t + PF - KS);
+            wa[t % PF] = t + PF < KS ? ld(Tu, t + PF) : ld(Tn < t_end ? Tn : Tu, t + PF - KS);
             __builtin_amdgcn_sched_barrier(0);  // keep each step's two LDS reads next to its MFMAs
         }
         const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w}, bdv[4] = {bd4.x, bd4.y, bd4.z, bd4.w},
                     qnv[4] = {qn4.x, qn4.y, qn4.z, qn4.w};
-        float lo[4], hi[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const double A = (double)scv[i] * ((double)t1 * (double)ch[i] + (double)t2 * (double)cl[i]);
             const double e = ((double)nrm * (double)bdv[i] + (double)qnv[i] * (double)errn) * (1.0 + 1e-6) +
                              fabs(A) * 1e-12 + 1e-30;
-            lo[i] = __double2float_rd(A - e);
-            hi[i] = __double2float_ru(A + e);
+            const int row = r0 + i;
+            const bool ok = col_ok && row < N;
+            lo_a[u][i] = ok ? __double2float_rd(A - e) : -INFINITY;
+            hi_a[u][i] = ok ? __double2float_ru(A + e) : -INFINITY;
+            if (lo_a[u][i] > best && !banned(row)) best = lo_a[u][i];
         }
+    }
+    // the token's best over the wave's 4 lanes of that column (lanes c, c + 16, c + 32, c + 48), then the block
+    best = fmaxf(best, __shfl_xor(best, 16));
+    best = fmaxf(best, __shfl_xor(best, 32));
+    if (col_ok && g == 0 && best > -INFINITY) atomicMax(&tkey_s[c], fkey(best));
+    __syncthreads();
+    const float Tb = fkey_dec(tkey_s[cr]);
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int Tu = T + u * LM_WV;
+        if (Tu >= t_end) break;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int row = 16 * T + 4 * g + i;
-            const bool trig = col_ok && row < N && (lo[i] > Tw || hi[i] >= Tw);
-            unsigned long long m = __ballot(trig);
-            while (m) {
-                const int r = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const float lo_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lo[i]), r));
-                const float hi_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi[i]), r));
-                const float Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tw), r));
-                const int tc = r & 15, n = 16 * T + 4 * (r >> 4) + i;
-                if (!(lo_r > Tc) && !(hi_r >= Tc)) continue;
-                const int nb = __builtin_amdgcn_readfirstlane(nban_s[tc]);
-                bool banned = false;
-                if (nb <= LM_BANS) {
-                    for (int j = 0; j < nb; ++j) banned = banned || ban_s[tc][j] == n;
-                } else {
-                    const int* bg = a.ban + (long)tc * a.ban_ld + 1;
-                    for (int j = 0; j < nb; ++j) banned = banned || bg[j] == n;
-                }
-                if (banned) continue;
-                if (lo_r > Tc) {
-                    if (c == tc) Tw = lo_r;  // every lane of token tc
-                    if (lane == 0) atomicMax(&tkey_s[tc], fkey(lo_r));
-                }
-                if (lane == 0) {
-                    const int p = atomicAdd(&lst_n[tc], 1);
-                    lst_idx[tc][p] = n;
-                    lst_hi[tc][p] = hi_r;
-                }
+            const int row = 16 * Tu + 4 * g + i;
+            if (col_ok && row < N && hi_a[u][i] >= Tb && !banned(row)) {
+                const int p = atomicAdd(&lst_n[c], 1);
+                lst_idx[c][p] = row;
+                lst_hi[c][p] = hi_a[u][i];
             }
         }
-        Tw = fmaxf(Tw, fkey_dec(tkey_s[cr]));
     }
     __syncthreads();
     // ---- every token's list against its block threshold -> cand[b][p][block] (the single-token layout)

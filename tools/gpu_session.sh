@@ -29,6 +29,7 @@ for step in "$@"; do
     prof) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
     kbench) run 300 ./tools/kbench $KB_CASES > gpurun_out/kbench.log 2>&1 ;;
     mb) run 120 ./tools/mb_stream > gpurun_out/mb_stream.log 2>&1 ;;
+    mbb) run 120 ./tools/mb_barrier > gpurun_out/mb_barrier.log 2>&1 ;;
     pmc_fetch) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_fetch.log 2>&1 ;;
     pmc_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_write.log 2>&1 ;;
     pmc_calib) run 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_calib -o mb --output-format csv -- ./tools/mb_stream > gpurun_out/pmc_calib.log 2>&1 ;;
