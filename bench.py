@@ -123,97 +123,53 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps):
-    """The repo's CPU oracle (numpy restatement of the reference path, oracle/) on rank 0's host
-    cores.  Bounded sample = 1 page: vision + prefill timed whole, then `decode_steps` decode
-    forwards at the prompt's KV length and `decode_steps` more at the last step's KV length
-    (prompt + max_new - 1, the cache padded with copies of its own rows: attention and the cache
-    append cost what they cost at that length).  Decode time is linear in the KV length, so the
-    page's (max_new - 1) decode steps are the trapezoid of the two measured step times.
-    Timed twice: with BLAS on every core this process may run on (len(sched_getaffinity)) and with the
-    pool the environment sets (OMP_NUM_THREADS); the faster run is the reported `value` (on the shared
-    GPU box 256 visible CPUs oversubscribe the job's share: 0.011 vs 0.029 pages/s at 16 threads), the
-    other is kept as `other_threads`."""
+def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
+    """The repo's CPU restatement timed on rank 0's host cores, one whole page of the workload: the vision tower
+    by the numpy port (oracle/vision.py, BLAS-threaded), then the decoder by the C++ / OpenMP restatement
+    (oracle/cpu_ref.cpp: the same f32 math as the oracle; 16-bit weights widened at use): the 706-token
+    prefill and ALL (max_new - 1) decode forwards with the greedy 20-gram-ban selection, timed whole (no
+    extrapolation).  Threads: OMP_NUM_THREADS (the job's CPU share: 16 on the GPU box), bound to cores
+    (OMP_PROC_BIND=close unless set); BLAS at the same count.  Stage sums are reported like the reference's
+    bench (crates/cli/src/bench.rs:200-260: vision, prefill, decode)."""
+    import numpy as np
+
     import dsocr
+    from oracle import cpu_ref
     from oracle.model import OracleModel
-    from oracle.specs import tensor_names
-    from oracle.weights import Weights, synthetic_has
+    from oracle.weights import Weights
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PLACES", "cores")
     cfg = json.load(open(dsocr.FULL_CONFIG))
-    W = Weights(seed=0, dtype="f16")
     t = time.time()
-    for n, shape in tensor_names(cfg).items():   # materialise weights outside the timed sample
-        if synthetic_has(n):
-            W.get(n, shape)
-    log(f"[cpu] oracle weights ready in {time.time() - t:.1f}s")
-    orc = OracleModel(cfg, W)
-    env_threads = blas_threads()
-    try:
-        all_cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        all_cores = os.cpu_count() or 1
+    cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
+    log(f"[cpu] C++ decoder loaded in {time.time() - t:.1f}s ({threads} threads)")
+    orc = OracleModel(cfg, Weights(seed=0, dtype="f16"))
     try:
         from threadpoolctl import threadpool_limits
     except ImportError:
         threadpool_limits = None
-    runs = []
-    for threads in ([all_cores, env_threads] if all_cores != env_threads and threadpool_limits else [env_threads]):
-        if threadpool_limits:
-            with threadpool_limits(limits=threads, user_api="blas"):
-                r = _cpu_page_sample(orc, pages[0], tok_ids, mask, max_new, decode_steps)
-        else:
-            r = _cpu_page_sample(orc, pages[0], tok_ids, mask, max_new, decode_steps)
-        r["cores"] = threads
-        log(f"[cpu] {threads} BLAS threads: {r['value']:.4f} pages/s ({r['sample']})")
-        runs.append(r)
-    best = max(runs, key=lambda r: r["value"])
-    other = [r for r in runs if r is not best]
-    out = {"value": best["value"], "unit": "pages/s", "cores": best["cores"], "kind": "port",
-           "port": "oracle/ numpy restatement of the reference page path (f32, BLAS-threaded); "
-                   "the Rust reference cannot be built here",
-           "decode_tok_s": best["decode_tok_s"], "host_cpus": os.cpu_count(), "allowed_cpus": all_cores,
-           "cpu_model": cpu_model(), "sample": best["sample"]}
-    if other:
-        out["other_threads"] = {k: other[0][k] for k in ("value", "cores", "decode_tok_s", "sample")}
-    return out
-
-
-def _cpu_page_sample(orc, img, tok_ids, mask, max_new, decode_steps):
-    import numpy as np
     t0 = time.time()
-    emb, _ = orc.image_embeddings(img)
-    t1 = time.time()
-    orc.dec.reset()
-    lg = orc.dec.forward(orc.prefill_embeddings(tok_ids, mask, emb))
-    t2 = time.time()
-    nxt = int(np.argmax(lg[0]))
-
-    def steps():
-        nonlocal nxt, lg
-        ts = time.time()
-        for _ in range(decode_steps):
-            lg = orc.dec.forward(orc.dec.embed([nxt]))
-            nxt = int(np.argmax(lg[0]))
-        return (time.time() - ts) / decode_steps
-
-    l_first = orc.dec.past
-    step_first = steps()
-    l_last = len(tok_ids) + max_new - 1
-    pad = l_last - orc.dec.past
-    if pad > 0:
-        d = orc.dec
-        for li in range(len(d.k_cache)):
-            idx = np.arange(pad) % d.k_cache[li].shape[1]
-            d.k_cache[li] = np.concatenate([d.k_cache[li], d.k_cache[li][:, idx]], 1)
-            d.v_cache[li] = np.concatenate([d.v_cache[li], d.v_cache[li][:, idx]], 1)
-        d.past += pad
-    step_last = steps()
-    decode_s = (step_first + step_last) / 2 * (max_new - 1)
-    page_s = (t1 - t0) + (t2 - t1) + decode_s
-    return {"value": 1.0 / page_s, "decode_tok_s": (max_new - 1) / decode_s,
-            "sample": f"1 synthetic 1024x1024 page: vision {t1 - t0:.2f}s + prefill {t2 - t1:.2f}s "
-                      f"({len(tok_ids)} tok) + {decode_steps} decode steps at KV {l_first} "
-                      f"({step_first * 1e3:.0f} ms/step) and {decode_steps} at KV {l_last} "
-                      f"({step_last * 1e3:.0f} ms/step), {max_new - 1} decode steps by the trapezoid"}
+    if threadpool_limits:
+        with threadpool_limits(limits=threads, user_api="blas"):
+            emb, _ = orc.image_embeddings(pages[0])
+    else:
+        emb, _ = orc.image_embeddings(pages[0])
+    vision_s = time.time() - t0
+    ids, ms = cr.generate(np.asarray(tok_ids, np.int64), np.asarray(mask, np.uint8), emb, max_new, ngram=20)
+    cr.close()
+    prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3
+    page_s = vision_s + prefill_s + decode_s
+    return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads, "kind": "cpp",
+            "port": "oracle/cpu_ref.cpp: C++ / OpenMP restatement of the decoder (AVX-512 micro-kernels, f32 math, "
+                    "prefill + every decode step); the vision tower by the numpy port (oracle/vision.py, BLAS); "
+                    "the Rust reference cannot be built here",
+            "decode_tok_s": (max_new - 1) / decode_s, "host_cpus": os.cpu_count(),
+            "allowed_cpus": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+            "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
+            "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (numpy) + prefill {prefill_s:.2f}s "
+                      f"({len(tok_ids)} tok, C++) + {max_new - 1} decode steps {decode_s:.2f}s (C++, "
+                      f"{decode_s / max(1, max_new - 1) * 1e3:.1f} ms/step), {threads} threads; first ids {ids[:4]}"}
 
 
 SPAN_HZ = 100e6  # s_memrealtime
@@ -386,7 +342,7 @@ def main():
     ap.add_argument("--pages-per-gpu", type=int, default=1)
     ap.add_argument("--max-new-tokens", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-decode-steps", type=int, default=2)
+    ap.add_argument("--cpu-decode-steps", type=int, default=0, help="(unused: the C++ baseline times every decode step)")
     ap.add_argument("--roofline-iters", type=int, default=20)
     ap.add_argument("--workload", default="deepseek", choices=["deepseek", "dots2048"],
                     help="deepseek: configs[1]/[2] (default); dots2048: configs[3], the dots.ocr vision tower")
