@@ -675,32 +675,6 @@ dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int h
         if (used_fused) *used_fused = took ? 1 : 0;
     });
 }
-dsocr_status dsocr_k_oproj_route(int H, int K, int E, const float* ctx, const void* Wo, int wdtype, const float* bo,
-                                 float* x, const void* Wr, const float* norm_w, float eps, const float* rbias,
-                                 float* logits, float* xn) {
-    return guarded([&] {
-        if (wdtype != dsocr::WDT_F16 && wdtype != dsocr::WDT_BF16) throw std::runtime_error("EINVAL: 16-bit weights only");
-        float* wrnT = nullptr;
-        float* part = nullptr;
-        int* ticket = nullptr;
-        check_hip(hipMalloc(&wrnT, sizeof(float) * (size_t)H * E + 16), "hipMalloc");
-        check_hip(hipMalloc(&part, sizeof(float) * (size_t)(H / 16 + 1) * (E + 1)), "hipMalloc");
-        check_hip(hipMalloc(&ticket, sizeof(int)), "hipMalloc");
-        check_hip(hipMemset(ticket, 0, sizeof(int)), "hipMemset");
-        try {
-            dsocr::launch_router_fold(Wr, wdtype, norm_w, E, H, wrnT, nullptr);
-            dsocr::DecOprojRouteArgs a;
-            a.ctx = ctx; a.K = K; a.Wo = Wo; a.wdtype = wdtype; a.bo = bo; a.x = x; a.H = H; a.wrnT = wrnT; a.E = E;
-            a.norm_w = norm_w; a.eps = eps; a.rbias = rbias; a.part = part; a.ticket = ticket; a.logits = logits; a.xn = xn;
-            dsocr::launch_dec_oproj_route(a, nullptr);
-            check_hip(hipDeviceSynchronize(), "oproj_route");
-        } catch (...) {
-            (void)hipFree(wrnT); (void)hipFree(part); (void)hipFree(ticket);
-            throw;
-        }
-        (void)hipFree(wrnT); (void)hipFree(part); (void)hipFree(ticket);
-    });
-}
 int dsocr_k_poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus) {
     return dsocr::poll_wait_fits(waiting_blocks, api_blocks_per_cu, cus) ? 1 : 0;
 }

@@ -559,9 +559,6 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
             d.router.N = E;
             d.router.K = H;
             d.router.b = optvec(lp + "mlp.gate.e_score_correction_bias", E);
-            // the router's columns times the post-attention norm weight (dec_oproj_route, one page)
-            d.wrnT = (float*)dev_alloc((size_t)H * E * 4);
-            launch_router_fold(d.router.W, d.router.wdt, d.post_norm.w, E, H, d.wrnT, nullptr);
             HostMat gu, dn;
             gu.data.resize((size_t)E * 2 * I * H);
             dn.data.resize((size_t)E * H * I);
@@ -1111,26 +1108,11 @@ void Engine::decode_step(int B, int Lmax) {
             launch_dec_gemv(g, st);
         }
         if (!attn_done && !(step_skip_ & SKIP_ATTN)) stamped(SPAN_ATTN, l, [&] { launch_dec_attn(da, st); }, nullptr, 0);
-        // o_proj + residual (one page, MoE layer: with the router in the same launch, dec_oproj_route)
-        bool routed = false;
-        if (B == 1 && d.moe && d.wrnT && oproj_route_fused()) {
-            const MoeDecodeArgs ma = moe_args(l, B, X);
-            DecOprojRouteArgs oa;
-            oa.ctx = CTX; oa.K = L.heads * hd; oa.Wo = d.o.W; oa.wdtype = d.o.wdt; oa.bo = d.o.b; oa.x = X; oa.H = H;
-            oa.wrnT = d.wrnT; oa.E = L.n_routed; oa.norm_w = d.post_norm.w; oa.eps = L.rms_eps; oa.rbias = d.router.b;
-            oa.part = wsf("s_orpart", (size_t)(H / 16) * (L.n_routed + 1)); oa.ticket = wsi("s_orticket", 1);
-            oa.logits = ma.logits; oa.xn = ma.xn_router;
-            if (dec_oproj_route_ok(oa)) {
-                launch_dec_oproj_route(oa, st);
-                routed = true;
-            }
-        }
-        if (!routed) {
-            DecGemvArgs go;
-            go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
-            go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
-            launch_dec_gemv(go, st);
-        }
+        // o_proj + residual
+        DecGemvArgs go;
+        go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
+        go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
+        launch_dec_gemv(go, st);
         // MLP / MoE
         if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
             // dense MLP (layer 0) on the matrix cores: gate|up with the post-attention RMSNorm fused,
@@ -1164,13 +1146,12 @@ void Engine::decode_step(int B, int Lmax) {
             continue;
         }
         if (!span_rec_) {
-            const int parts = (routed ? 0 : MOE_ROUTE) | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) |
-                              ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
+            const int parts = MOE_ROUTE | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) | ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
             launch_moe_decode(moe_args(l, B, X), st, parts);
             continue;
         }
         MoeDecodeArgs ma = moe_args(l, B, X);
-        if (!routed) launch_moe_decode(ma, st, MOE_ROUTE);
+        launch_moe_decode(ma, st, MOE_ROUTE);
         ma.span = (span_mode_ & SPAN_WAVES) ? span_slots_ : nullptr;
         stamped(SPAN_GATEUP, l, [&] { launch_moe_decode(ma, st, MOE_GATEUP); }, ma.ids, B * ma.topk);
         stamped(SPAN_DOWN, l, [&] { launch_moe_decode(ma, st, MOE_DOWN); }, ma.ids, B * ma.topk);
@@ -1236,13 +1217,6 @@ void Engine::ensure_mm_weights(int B) {
         }
     }
     HIP_CHECK(hipStreamSynchronize(stream_));
-}
-
-// one page: o_proj + MoE router as one launch (dec_oproj_route); DSOCR_OPROJ_ROUTE=0 (A/B switch, read
-// once) keeps the two launches
-bool Engine::oproj_route_fused() {
-    static const bool v = !(getenv("DSOCR_OPROJ_ROUTE") && atoi(getenv("DSOCR_OPROJ_ROUTE")) == 0);
-    return v;
 }
 
 // one page: q/k/v projection + decode attention as one launch (dec_qkv_attn); DSOCR_QKV_ATTN=0 (A/B

@@ -71,7 +71,6 @@ struct DecLayer {
     bool moe = false;
     Lin gu, down;                 // dense MLP (layer 0) [2I][H], [H][I]
     Lin router;                   // [E][H]
-    float* wrnT = nullptr;        // [H][E] f32: router weight x post-attention norm weight (one-page fused router)
     float* router_bias = nullptr; // e_score_correction_bias
     void* e_gu = nullptr;         // [E][2Im][H]
     void* e_d = nullptr;          // [E][H][Im]
@@ -274,7 +273,6 @@ class Engine {
     enum StepSkip : int { SKIP_GATEUP = 1, SKIP_DOWN = 2, SKIP_ATTN = 4 };
     int step_skip_ = 0;
     static bool qkv_attn_fused();
-    static bool oproj_route_fused();
     unsigned long long* span_slots_ = nullptr;  // device [SPAN_SLOTS][2]
     unsigned long long* span_rec_ = nullptr;    // device [SPAN_KINDS][layers][span_cap_][4]
     const int* span_step_ = nullptr;            // device step counter (out_len of page 0)

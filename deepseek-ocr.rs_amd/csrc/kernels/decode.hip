@@ -1039,158 +1039,6 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 #undef DSOCR_RT
 }
 
-// ------------------------------------------------------------------ one page: o_proj + router, one launch
-// x[j] += Wo[j] . ctx (+ bo[j]) for all H rows (16 per block, 4 per wave: dec_gemv's chunk layout and
-// per-row arithmetic), and the MoE router of the updated row in the same launch.  The router's RMSNorm
-// needs all of x_new, but its logits are linear in x_new:
-//   logit_e = sum_j Wr[e][j] * (x_j / den) * w_j = (1 / den) * sum_j WrnT[j][e] * x_j,  WrnT[j][e] = Wr[e][j] w_j
-// (block.rs:1254-1301 after rms_norm_stable, block.rs:24-29), so every block adds its rows' share of the 64
-// sums (lane e of each wave) and of sum x_j^2 into a partial record, stored write-through with x_new; the
-// last block to take the ticket (MI355X_MICROARCH.md hand-offs, first row) sums the records in block order,
-// forms den = sqrt(sum / H + eps), the logits (/ den, + bias) and the normalised row x_n = (x / den) * w for
-// the gate/up kernel (the router launch's own outputs).  The logits are an f32 reassociation of the
-// reference's sum (parity: greedy ids over the full-length fixtures).
-constexpr int OR_RPW = 4, OR_RPB = 16;  // rows per wave / per block
-
-template <typename WT>
-__global__ __launch_bounds__(256) void dec_oproj_route_kernel(DecOprojRouteArgs a) {
-    constexpr int U = 3;  // K <= 1536
-    __shared__ float ps[4][64];
-    __shared__ float sqs[4];
-    __shared__ float red[256];
-    __shared__ int last_s;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int chunks = a.K >> 3;
-    const int j0 = blockIdx.x * OR_RPB + wave * OR_RPW;
-    const WT* W = reinterpret_cast<const WT*>(a.Wo);
-    // the weight rows first (the stream), then ctx, the old x and the folded router columns
-    uint4 wq[OR_RPW][U];
-#pragma unroll
-    for (int r = 0; r < OR_RPW; ++r)
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            wq[r][u] = ldg_nt16(W + (long)min(j0 + r, a.H - 1) * a.K + (min(u * 64 + lane, chunks - 1) << 3));
-    float cx[U][8];
-#pragma unroll
-    for (int u = 0; u < U; ++u) ld_x8(a.ctx + (min(u * 64 + lane, chunks - 1) << 3), cx[u]);
-    float xo[OR_RPW], wr[OR_RPW], bo[OR_RPW];
-#pragma unroll
-    for (int r = 0; r < OR_RPW; ++r) {
-        const int j = min(j0 + r, a.H - 1);
-        xo[r] = a.x[j];
-        wr[r] = lane < a.E ? a.wrnT[(long)j * a.E + lane] : 0.f;
-        bo[r] = a.bo ? a.bo[j] : 0.f;
-    }
-    float p = 0.f, sq = 0.f;
-    const auto xr = __builtin_amdgcn_make_buffer_rsrc(a.x, (short)0, a.H * 4, 0x00020000);
-#pragma unroll
-    for (int r = 0; r < OR_RPW; ++r) {
-        float acc = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (u * 64 + lane < chunks) {
-                float w8[8];
-                unpack8<WT>(wq[r][u], w8);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) acc = fmaf(cx[u][q], w8[q], acc);
-            }
-        }
-        const float xn = xo[r] + (wave_sum(acc) + bo[r]);  // dec_gemv's accumulate: y + (dot + bias)
-        if (j0 + r < a.H) {
-            if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xn), xr, (j0 + r) * 4, 0, 16);  // sc1
-            p = fmaf(wr[r], xn, p);
-            sq = fmaf(xn, xn, sq);
-        }
-    }
-    ps[wave][lane] = p;
-    if (lane == 0) sqs[wave] = sq;
-    __syncthreads();
-    // block partial record [E sums | sum of squares], write-through
-    float* rec = a.part + (long)blockIdx.x * (a.E + 1);
-    if (tid < a.E) __hip_atomic_store(rec + tid, (ps[0][tid] + ps[1][tid]) + (ps[2][tid] + ps[3][tid]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 64) __hip_atomic_store(rec + a.E, (sqs[0] + sqs[1]) + (sqs[2] + sqs[3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (int)gridDim.x - 1;
-        if (last) __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_s = last;
-    }
-    __syncthreads();
-    if (!last_s) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
-    // ---- the last arriver: every record and the updated row, all loads in flight together
-    const int nb = gridDim.x;
-    constexpr int PB = 24;  // records per thread group (4 groups x 64 lanes; nb <= 96)
-    const int e = lane, grp = wave;
-    float pv[PB];
-#pragma unroll
-    for (int i = 0; i < PB; ++i) {
-        const int b = grp * PB + i;
-        pv[i] = __hip_atomic_load(a.part + (long)min(b, nb - 1) * (a.E + 1) + min(e, a.E - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // wave 0: the records' sums of squares, lane l holding records l and l + 64
-    float s0 = 0.f, s1 = 0.f;
-    if (wave == 0) {
-        s0 = __hip_atomic_load(a.part + (long)min(lane, nb - 1) * (a.E + 1) + a.E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s1 = __hip_atomic_load(a.part + (long)min(lane + 64, nb - 1) * (a.E + 1) + a.E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    constexpr int XU = 6;  // H <= 1536
-    float xv[XU];
-#pragma unroll
-    for (int i = 0; i < XU; ++i)
-        xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, min(tid + 256 * i, a.H - 1) * 4, 0, 16));
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < PB; ++i)
-        if (grp * PB + i < nb) t += pv[i];
-    red[tid] = t;  // lane e of group g: expert e's sum over records g*PB .. g*PB + PB - 1
-    if (wave == 0) {
-        const float q = wave_sum((lane < nb ? s0 : 0.f) + (lane + 64 < nb ? s1 : 0.f));
-        if (lane == 0) sqs[0] = q;
-    }
-    __syncthreads();
-    const float SQ = sqs[0];
-    const float den = sqrtf(SQ / (float)a.H + a.eps);
-    if (tid < a.E) {
-        const float P = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
-        a.logits[tid] = P / den + (a.rbias ? a.rbias[tid] : 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < XU; ++i) {
-        const int j = tid + 256 * i;
-        if (j < a.H) a.xn[j] = (xv[i] / den) * a.norm_w[j];
-    }
-}
-
-bool dec_oproj_route_ok(const DecOprojRouteArgs& a) {
-    return a.H % OR_RPB == 0 && a.H / OR_RPB <= 96 && a.H <= 1536 && a.K % 8 == 0 && a.K <= 64 * 3 * 8 && a.E >= 1 &&
-           a.E <= 64 && a.wrnT && a.part && a.ticket && a.logits && a.xn && a.norm_w;
-}
-
-void launch_dec_oproj_route(const DecOprojRouteArgs& a, hipStream_t s) {
-    if (!dec_oproj_route_ok(a)) throw std::runtime_error("EINVAL: dec_oproj_route outside its range");
-    const dim3 grid(a.H / OR_RPB);
-    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_oproj_route_kernel<bf16_t>), grid, dim3(256), 0, s, a);
-    else DSOCR_LAUNCH((dec_oproj_route_kernel<f16_t>), grid, dim3(256), 0, s, a);
-}
-
-// WrnT[j][e] = Wr[e][j] * w[j] (f32; the router's RMSNorm weight folded into its columns)
-__global__ void router_fold_kernel(const uint16_t* wr, int wdtype, const float* w, int E, int H, float* out) {
-    const int j = blockIdx.x, e = threadIdx.x;
-    if (e >= E) return;
-    const uint32_t bits = wr[(long)e * H + j];
-    const float v = wdtype == WDT_BF16 ? bf16_bits_to_f32(bits) : f16_bits_to_f32(bits);
-    out[(long)j * E + e] = v * w[j];
-}
-
-void launch_router_fold(const void* wr, int wdtype, const float* w, int E, int H, float* out, hipStream_t s) {
-    if (E > 256) throw std::runtime_error("EINVAL: router fold supports <= 256 experts");
-    hipLaunchKernelGGL(router_fold_kernel, dim3(H), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(wr), wdtype, w, E, H,
-                       out);
-}
-
 // ------------------------------------------------------------------ decode attention
 // grid (chunks of 64 keys, heads, B).  The token being decoded sits at pos = kv_pos[b]: q and the new
 // k are rotated here (rotate_half RoPE, block.rs:1403-1471) unless the projection's epilogue already

@@ -190,20 +190,6 @@ struct DecGemvArgs {
     const void* w_swz = nullptr;  // optional: W in dec_mm's fragment order (launch_mm_swizzle), M = 3..8
 };
 void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s);
-// One page: o_proj (+ residual, in place) and the MoE router of the updated row in one launch (decode.hip):
-// logits[e] = (sum_j WrnT[j][e] x_j) / den (+ rbias[e]), xn = (x / den) * norm_w, den = sqrt(mean(x^2) + eps)
-struct DecOprojRouteArgs {
-    const float* ctx = nullptr; int K = 0;              // attention output [K]
-    const void* Wo = nullptr; int wdtype = WDT_F16; const float* bo = nullptr;  // [H][K]
-    float* x = nullptr; int H = 0;                      // residual row [H], updated in place
-    const float* wrnT = nullptr; int E = 0;             // [H][E]: router weight x post-attention norm weight
-    const float* norm_w = nullptr; float eps = 0.f; const float* rbias = nullptr;
-    float* part = nullptr; int* ticket = nullptr;       // [H / 16][E + 1] records; one counter (zero between launches)
-    float* logits = nullptr; float* xn = nullptr;       // [E], [H]
-};
-bool dec_oproj_route_ok(const DecOprojRouteArgs& a);
-void launch_dec_oproj_route(const DecOprojRouteArgs& a, hipStream_t s);
-void launch_router_fold(const void* wr, int wdtype, const float* w, int E, int H, float* out, hipStream_t s);
 // 3..8 tokens on the matrix cores (decode_mm.hip): weight rows as MFMA A operands, the (optionally
 // RMS-normalised) activation rows as three exact 16-bit planes (f16: per-row power-of-two scaled)
 bool dec_mm_ok(const DecGemvArgs& a);

@@ -298,14 +298,6 @@ dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int h
                                    float eps, const float* x, const float* norm_w, const void* Wqkv, int wdtype,
                                    const float* cos, const float* sin, float* kc, float* vc, const int* kv_pos,
                                    float* qkv_row, float* o, int* used_fused);
-/* One page's o_proj + MoE router in one launch (the decode step's form at one page): x[j] += Wo[j] . ctx
- * (+ bo[j]) for j < H (in place), then the router of the updated row (block.rs:1254-1301 after
- * rms_norm_stable): xn = (x / den) * norm_w, den = sqrt(mean(x^2) + eps), logits[e] = Wr[e] . xn (+ rbias[e]),
- * the logits formed as (sum_j Wr[e][j] norm_w[j] x_j) / den (an f32 reassociation).  Wo [H][K], Wr [E][H]
- * 16-bit (wdtype 0 bf16, 1 f16); E <= 64, H % 16 == 0, H <= 1536.  Device pointers. */
-dsocr_status dsocr_k_oproj_route(int H, int K, int E, const float* ctx, const void* Wo, int wdtype, const float* bo,
-                                 float* x, const void* Wr, const float* norm_w, float eps, const float* rbias,
-                                 float* logits, float* xn);
 /* Residency rule of the polled in-launch hand-offs (pure host decision, no device call): 1 when
  * waiting_blocks (blocks that may spin on blocks of the same grid) < usable slots = (min(api, 8), one fewer
  * where the occupancy API may over-admit) x cus; else 0 (the engine then launches the non-polling form). */
