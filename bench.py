@@ -128,8 +128,8 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
     by the numpy port (oracle/vision.py, BLAS-threaded), then the decoder by the C++ / OpenMP restatement
     (oracle/cpu_ref.cpp: the same f32 math as the oracle; 16-bit weights widened at use): the 706-token
     prefill and ALL (max_new - 1) decode forwards with the greedy 20-gram-ban selection, timed whole (no
-    extrapolation).  Threads: OMP_NUM_THREADS (the job's CPU share: 16 on the GPU box), bound to cores
-    (OMP_PROC_BIND=close unless set); BLAS at the same count.  Stage sums are reported like the reference's
+    extrapolation).  Threads: OMP_NUM_THREADS (the job's CPU share: 16 on the GPU box); BLAS at the same
+    count (no thread binding: a bound OpenMP master would pin the BLAS pool it spawns later to one core).  Stage sums are reported like the reference's
     bench (crates/cli/src/bench.rs:200-260: vision, prefill, decode)."""
     import numpy as np
 
@@ -137,25 +137,25 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
     from oracle import cpu_ref
     from oracle.model import OracleModel
     from oracle.weights import Weights
-    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
-    os.environ.setdefault("OMP_PROC_BIND", "close")
-    os.environ.setdefault("OMP_PLACES", "cores")
+    allowed = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS") or allowed)
     cfg = json.load(open(dsocr.FULL_CONFIG))
-    t = time.time()
-    cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
-    log(f"[cpu] C++ decoder loaded in {time.time() - t:.1f}s ({threads} threads)")
     orc = OracleModel(cfg, Weights(seed=0, dtype="f16"))
     try:
         from threadpoolctl import threadpool_limits
     except ImportError:
         threadpool_limits = None
-    t0 = time.time()
+    t0 = time.time()  # (vision first: no OpenMP pool of the C++ library competes with the BLAS pool)
     if threadpool_limits:
         with threadpool_limits(limits=threads, user_api="blas"):
             emb, _ = orc.image_embeddings(pages[0])
     else:
         emb, _ = orc.image_embeddings(pages[0])
     vision_s = time.time() - t0
+    del orc
+    t = time.time()
+    cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
+    log(f"[cpu] C++ decoder loaded in {time.time() - t:.1f}s ({threads} threads)")
     ids, ms = cr.generate(np.asarray(tok_ids, np.int64), np.asarray(mask, np.uint8), emb, max_new, ngram=20)
     cr.close()
     prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3
@@ -165,7 +165,7 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
                     "prefill + every decode step); the vision tower by the numpy port (oracle/vision.py, BLAS); "
                     "the Rust reference cannot be built here",
             "decode_tok_s": (max_new - 1) / decode_s, "host_cpus": os.cpu_count(),
-            "allowed_cpus": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+            "allowed_cpus": allowed, "cpu_model": cpu_model(),
             "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
             "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (numpy) + prefill {prefill_s:.2f}s "
                       f"({len(tok_ids)} tok, C++) + {max_new - 1} decode steps {decode_s:.2f}s (C++, "
