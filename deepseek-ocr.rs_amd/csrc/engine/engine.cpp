@@ -589,7 +589,7 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
     HIP_CHECK(hipDeviceSynchronize());
     final_norm_ = vecf("model.norm.weight", H);  // f32 copy (model/mod.rs:1008-1014)
     lm_head_ = lin("lm_head", L.vocab, H, false);
-    if (lm_head_.wdt == WDT_BF16 && H % 16 == 0 && H <= 1536) {
+    if ((lm_head_.wdt == WDT_BF16 || lm_head_.wdt == WDT_F16) && H % 16 == 0 && H <= 1536) {
         // int8 screening copy of the lm_head (per-row scale + rigorous error bound), lmhead.hip
         // (+ for 3..8 pages: s ||Q|| per row and the fragment-ordered copy the int8 matrix cores read; the
         // per-row arrays padded to whole 16-row tiles)
@@ -604,7 +604,8 @@ void Engine::load_weights(const std::string& path, uint64_t seed, const std::str
             HIP_CHECK(hipMemset(lmq_qnorm_, 0, vp * 4));
             lmq_frag_ = dev_alloc(lmhead_qfrag_bytes(L.vocab, H));
         }
-        launch_lmhead_quantize(lm_head_.W, L.vocab, H, lmq_, lmq_scale_, lmq_bound_, nullptr, lmq_qnorm_, lmq_frag_);
+        launch_lmhead_quantize(lm_head_.W, L.vocab, H, lmq_, lmq_scale_, lmq_bound_, nullptr, lmq_qnorm_, lmq_frag_,
+                               lm_head_.wdt);
         HIP_CHECK(hipDeviceSynchronize());
     }
 }
@@ -1112,7 +1113,19 @@ void Engine::decode_step(int B, int Lmax) {
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
         go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
-        launch_dec_gemv(go, st);
+        // one page, MoE layer: o_proj and the router in one launch (the router blocks poll the residual row
+        // the o_proj blocks hand over; DSOCR_OPROJ_ROUTE=0 is the A/B switch)
+        bool routed = false;
+        if (d.moe && B == 1 && oproj_route_fused()) {
+            const int prev = prev_moe_layer(l);
+            DecGemvArgs gr;
+            if (prev != l && moe_router_args(moe_args(l, B, X), &gr) && dec_oproj_route_ok(go, gr)) {
+                float* hand = wsf("s_hand", (size_t)L.layers * H);
+                launch_dec_oproj_route(go, gr, hand + (long)l * H, hand + (long)prev * H, err, st);
+                routed = true;
+            }
+        }
+        if (!routed) launch_dec_gemv(go, st);
         // MLP / MoE
         if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
             // dense MLP (layer 0) on the matrix cores: gate|up with the post-attention RMSNorm fused,
@@ -1146,12 +1159,13 @@ void Engine::decode_step(int B, int Lmax) {
             continue;
         }
         if (!span_rec_) {
-            const int parts = MOE_ROUTE | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) | ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
+            const int parts = (routed ? 0 : MOE_ROUTE) | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) |
+                              ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
             launch_moe_decode(moe_args(l, B, X), st, parts);
             continue;
         }
         MoeDecodeArgs ma = moe_args(l, B, X);
-        launch_moe_decode(ma, st, MOE_ROUTE);
+        if (!routed) launch_moe_decode(ma, st, MOE_ROUTE);
         ma.span = (span_mode_ & SPAN_WAVES) ? span_slots_ : nullptr;
         stamped(SPAN_GATEUP, l, [&] { launch_moe_decode(ma, st, MOE_GATEUP); }, ma.ids, B * ma.topk);
         stamped(SPAN_DOWN, l, [&] { launch_moe_decode(ma, st, MOE_DOWN); }, ma.ids, B * ma.topk);
@@ -1221,6 +1235,22 @@ void Engine::ensure_mm_weights(int B) {
 
 // one page: q/k/v projection + decode attention as one launch (dec_qkv_attn); DSOCR_QKV_ATTN=0 (A/B
 // switch, read once) keeps the two launches
+// read at every capture (tests switch it within one process)
+bool Engine::oproj_route_fused() const {
+    const char* e = getenv("DSOCR_OPROJ_ROUTE");
+    return !(e && atoi(e) == 0);
+}
+
+// the MoE layer before l in decode order, cyclically (l itself when it is the only one)
+int Engine::prev_moe_layer(int l) const {
+    const int n = (int)layers_.size();
+    for (int k = 1; k <= n; ++k) {
+        const int j = ((l - k) % n + n) % n;
+        if (layers_[j].moe) return j;
+    }
+    return l;
+}
+
 bool Engine::qkv_attn_fused() {
     static const bool v = !(getenv("DSOCR_QKV_ATTN") && atoi(getenv("DSOCR_QKV_ATTN")) == 0);
     return v;
@@ -1249,7 +1279,7 @@ void Engine::decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen) {
         launch_lmhead_q8(q, st);
         DecSampleArgs ss = sa;
         ss.blk_cnt = q.blk_cnt; ss.blk_t = q.blk_t; ss.cand = q.cand; ss.cand_hi = q.cand_hi; ss.nblk = q.nblk; ss.slot = q.slot;
-        ss.w_exact = lm_head_.W; ss.xn = q.xn_out; ss.K = H;
+        ss.w_exact = lm_head_.W; ss.w_exact_wdt = lm_head_.wdt; ss.xn = q.xn_out; ss.K = H;
         if (getenv("DSOCR_SCREEN_STATS")) ss.stats = reinterpret_cast<unsigned long long*>(wsi("s_scrstats", 32));
         launch_dec_sample(ss, st);
         return;
@@ -1511,6 +1541,9 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         const size_t qn = (size_t)B * layers_[0].qkv.N;
         dec_qkv_sentinel_init(wsf("s_qkv", qn), qn, st);
         wsf("p_qkv_skip", qn);  // the profile's variant without attention projects here (allocated before capture)
+        // the one-page o_proj -> router hand-off rows (one per layer): sentinel-filled, each launch refills
+        // the previous MoE layer's
+        dec_hand_init(wsf("s_hand", (size_t)L.layers * H), (size_t)L.layers * H, st);
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
@@ -2008,7 +2041,7 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
             ss.B = B; ss.V = L.vocab; ss.ld = L.vocab; ss.ctx = wsi("p_sctx", 64); ss.ctx_cap = 64;
             ss.ctx_len = wsi("p_ctxlen", B); ss.ngram = 0; ss.out_tok = wsi("p_tok", B);
             ss.blk_cnt = q.blk_cnt; ss.blk_t = q.blk_t; ss.cand = q.cand; ss.cand_hi = q.cand_hi; ss.nblk = q.nblk;
-            ss.slot = q.slot; ss.w_exact = lm_head_.W; ss.xn = q.xn_out; ss.K = H;
+            ss.slot = q.slot; ss.w_exact = lm_head_.W; ss.w_exact_wdt = lm_head_.wdt; ss.xn = q.xn_out; ss.K = H;
             HIP_CHECK(hipMemsetAsync(ss.ctx_len, 0, B * 4, st));
             timed(prof.lm_head_screened, iters, [&](int) {
                 launch_lmhead_q8(q, st);

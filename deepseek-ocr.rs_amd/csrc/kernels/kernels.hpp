@@ -269,6 +269,15 @@ bool poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus);
 bool dec_attn_polled(const DecAttn2Args& a);
 void launch_dec_qkv_attn(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a, hipStream_t s);
 void dec_qkv_sentinel_init(float* qkv, size_t floats, hipStream_t s);
+// One page, MoE layer: o_proj + residual (go: accumulate into the residual row) and the router GEMV (gr:
+// RMSNorm fused, xn_out for the gate/up waves) in one launch; the router blocks poll the residual row the
+// o_proj blocks store write-through into `hand` (sentinel-filled on entry); the launch refills `hand_prev`
+// (the previous MoE layer's row, whose readers finished in an earlier launch).  Outputs equal the
+// two-launch form bit for bit.  dec_oproj_route_ok includes the residency rule.
+bool dec_oproj_route_ok(const DecGemvArgs& go, const DecGemvArgs& gr);
+void launch_dec_oproj_route(const DecGemvArgs& go, const DecGemvArgs& gr, float* hand, float* hand_prev, int* err,
+                            hipStream_t s);
+void dec_hand_init(float* hand, size_t floats, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
 // the record buffer enters every dec_attn launch sentinel-filled (the polling merge refills what it reads)
 void dec_attn_part_init(float* part, size_t bytes, hipStream_t s);
@@ -374,6 +383,8 @@ struct MoeDecodeArgs {
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments
 void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down);
+// the router launch arguments of launch_moe_decode's one-page plan (false: the plan has no separate router GEMV)
+bool moe_router_args(const MoeDecodeArgs& a, DecGemvArgs* gr);
 void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts = MOE_ALL);
 // Greedy selection (ngram ban evaluated in-kernel) + step bookkeeping + KV advance.
 struct DecSampleArgs {
@@ -395,6 +406,7 @@ struct DecSampleArgs {
     const int* blk_cnt = nullptr; const float* blk_t = nullptr; const int* cand = nullptr; const float* cand_hi = nullptr;
     int nblk = 0; long slot = 0;
     const void* w_exact = nullptr; const float* xn = nullptr; int K = 0;
+    int w_exact_wdt = WDT_BF16;  // the exact rows' storage (bf16, or f16 from a snapshot's dequantised lm_head)
     unsigned long long* stats = nullptr;  // [steps, kept rows, survivors] accumulated (diagnostics)
     // stochastic selection (sampling.hip; do_sample && temperature > 0): per-page rand StdRng state
     // ([B][RNG_WORDS]), top-k (0: off), top-p (active in [0, 1)), scratch of st_ld >= V entries
@@ -431,9 +443,10 @@ void lmhead_q8_grid(int N, int K, int B, int* nblk, long* slot);
 bool lmhead_q8mm_ok(int B, int N, int K);
 void lmhead_q8mm_grid(int N, int K, int B, int* nblk, long* slot);
 size_t lmhead_qfrag_bytes(int V, int K);
-// load time: int8 rows + scale + bound (+ optional s ||Q|| and the fragment-ordered copy for B = 3..8)
+// load time: int8 rows + scale + bound (+ optional s ||Q|| and the fragment-ordered copy for B = 3..8);
+// w: bf16 or f16 rows (wdtype)
 void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s,
-                            float* qnorm = nullptr, void* qfrag = nullptr);
+                            float* qnorm = nullptr, void* qfrag = nullptr, int wdtype = WDT_BF16);
 
 // DSQ snapshot tensors (dsq.hip): dtype codes of crates/dsq/src/lib.rs:60-110; decode a record's
 // payload ([out][in], row-major blocks) into fp16 on the device

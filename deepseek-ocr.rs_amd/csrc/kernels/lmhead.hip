@@ -20,13 +20,15 @@
 namespace dsocr {
 
 // ---------------------------------------------------------------- load time: quantise one row per block
+// (WT: the lm_head's 16-bit storage — bf16 checkpoints, f16 where a DSQ snapshot's Q8_0 lm_head was dequantised)
+template <typename WT>
 __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __restrict__ w, int K, int8_t* q,
                                                               float* scale, float* bound, float* qnorm, int8_t* qf) {
     __shared__ double red[256];
     const int v = blockIdx.x;
     const uint16_t* row = w + (long)v * K;
     float mx = 0.f;
-    for (int k = threadIdx.x; k < K; k += 256) mx = fmaxf(mx, fabsf(bf16_bits_to_f32(row[k])));
+    for (int k = threadIdx.x; k < K; k += 256) mx = fmaxf(mx, fabsf(wbits_to_f32<WT>(row[k])));
     red[threadIdx.x] = mx;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __
     double e2 = 0.0, w2 = 0.0, q2 = 0.0;
     int8_t* const qf_out = qf;
     for (int k = threadIdx.x; k < K; k += 256) {
-        const float x = bf16_bits_to_f32(row[k]);
+        const float x = wbits_to_f32<WT>(row[k]);
         float qf = rintf(x / s);
         qf = fminf(127.f, fmaxf(-127.f, qf));
         q[(long)v * K + k] = (int8_t)qf;
@@ -74,12 +76,16 @@ __global__ __launch_bounds__(256) void lmhead_quantize_kernel(const uint16_t* __
 }
 
 void launch_lmhead_quantize(const void* w, int V, int K, void* q, float* scale, float* bound, hipStream_t s,
-                            float* qnorm, void* qfrag) {
+                            float* qnorm, void* qfrag, int wdtype) {
     if (qfrag && K % 64) throw std::runtime_error("EINVAL: fragment-ordered int8 lm_head needs K % 64 == 0");
     if (qfrag && V % 16 && hipMemsetAsync(qfrag, 0, lmhead_qfrag_bytes(V, K), s) != hipSuccess)
         throw std::runtime_error("EINTERNAL: hipMemsetAsync (int8 lm_head tail tile)");
-    DSOCR_LAUNCH(lmhead_quantize_kernel, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
-                       reinterpret_cast<int8_t*>(q), scale, bound, qnorm, reinterpret_cast<int8_t*>(qfrag));
+    if (wdtype == WDT_F16)
+        DSOCR_LAUNCH(lmhead_quantize_kernel<f16_t>, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
+                     reinterpret_cast<int8_t*>(q), scale, bound, qnorm, reinterpret_cast<int8_t*>(qfrag));
+    else
+        DSOCR_LAUNCH(lmhead_quantize_kernel<bf16_t>, dim3(V), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(w), K,
+                     reinterpret_cast<int8_t*>(q), scale, bound, qnorm, reinterpret_cast<int8_t*>(qfrag));
 }
 
 size_t lmhead_qfrag_bytes(int V, int K) { return (size_t)((V + 15) / 16) * 16 * K; }

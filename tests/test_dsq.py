@@ -387,6 +387,9 @@ def test_full_q4k_snapshot_engine_matches_oracle(gpu, tmp_path):
     try:
         params = DecodeParameters(max_new_tokens=n_new)
         ids1, logits = eng.generate_trace([(prompts[0], None, None, None)], params, ignore_eos=True)
+        # without the trace the screened head selects (the snapshot's lm_head is f16: int8 screening of the
+        # f16 rows, exact rescoring in f16): one page and the 8-page matrix-core form
+        ids1s = eng.generate_batch([(prompts[0], None, None, None)], params, ignore_eos=True)
         ids8 = eng.generate_batch([(p, None, None, None) for p in prompts], params, ignore_eos=True)
     finally:
         eng.close()
@@ -396,6 +399,7 @@ def test_full_q4k_snapshot_engine_matches_oracle(gpu, tmp_path):
                                   record_logits=(i == 0), ignore_eos=True)
         if i == 0:
             assert ids1[0] == ref
+            assert ids1s[0] == ref, (ids1s[0], ref)
             err = max(float(np.max(np.abs(logits[0, s] - lg[s]))) for s in range(n_new))
             assert err < 2e-3, err
         assert ids8[i] == ref, (i, ids8[i], ref)
@@ -426,7 +430,10 @@ def test_full_q4k_snapshot_page_matches_fixture(gpu, tmp_path):
         ids, mask = build_prompt_tokens(SyntheticTokenizer(eng.vocab), BENCH_PROMPT, [page.n_image_tokens])
         assert ids == fx["prompt_ids"].tolist()
         outs, logits = eng.generate_trace([(ids, mask, page, None)], DecodeParameters(max_new_tokens=n), ignore_eos=True)
+        # the bench path: the screened head over the f16 lm_head rows (no trace)
+        screened = eng.generate(ids, mask, page, None, DecodeParameters(max_new_tokens=n), ignore_eos=True)
     finally:
         eng.close()
     from test_full_parity import check_stream
     check_stream("q4k_synthetic0", fx, outs[0], logits[0], n)
+    assert screened == fx["ids"].tolist(), "screened selection over the f16 lm_head differs from the fixture"

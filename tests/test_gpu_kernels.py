@@ -354,6 +354,45 @@ def test_qkv_attention_fused_back_to_back(gpu, max_len, p0):
             assert np.max(np.abs(o1[s, h * hd:(h + 1) * hd] - ref)) < 1e-4, (s, h)
 
 
+@pytest.mark.parametrize("wdt", [1, 0])
+def test_oproj_route_fused_back_to_back(gpu, wdt):
+    """One page's o_proj + residual and MoE router GEMV as ONE launch (dec_oproj_route: the router blocks poll
+    the residual row the o_proj blocks store write-through into a sentinel-filled hand-off row) for five
+    launches back to back through two alternating rows (each launch refills the other one, as consecutive MoE
+    layers do), against the two dec_gemv launches on the same inputs: the residual row, the logits and the
+    normalised row handed to the gate/up waves equal bit for bit; the last row holds the final residual and
+    the other only sentinels.  Also against f64 math (block.rs:1215-1240: x + W_o ctx, RMSNorm, router logits)."""
+    H, Kc, E, steps, eps = 1280, 1280, 64, 5, 1e-6
+    rng = np.random.default_rng(11 + wdt)
+    ctx = rng.standard_normal((steps, Kc)).astype(np.float32)
+    x0 = rng.standard_normal(H).astype(np.float32)
+    nw = (1.0 + 0.1 * rng.standard_normal(H)).astype(np.float32)
+    bo, wo = _weights(rng, H, Kc, wdt)
+    br, wr = _weights(rng, E, H, wdt)
+    dctx, dWo, dWr, dn = Dev(ctx), Dev(bo), Dev(br), Dev(nw)
+    outs = {}
+    for fused in (1, 0):
+        dx, dl, dxn, dh = Dev(x0), Dev.zeros((steps, E)), Dev.zeros((steps, H)), Dev.zeros((2, H))
+        used = C.c_int(-1)
+        check(lib().dsocr_k_oproj_route(fused, steps, H, Kc, E, dctx.ptr, dWo.ptr, dWr.ptr, wdt, dn.ptr, eps, dx.ptr,
+                                        dl.ptr, dxn.ptr, dh.ptr, C.byref(used)))
+        assert used.value == fused, "the residency rule refused the fused launch"
+        outs[fused] = (dx.get(), dl.get(), dxn.get(), dh.get())
+    (x1, l1, n1, h1), (x0b, l0, n0, _) = outs[1], outs[0]
+    assert np.array_equal(x1, x0b) and np.array_equal(l1, l0) and np.array_equal(n1, n0)
+    last = (steps - 1) % 2
+    assert np.array_equal(h1[last], x1), "the last hand-off row is not the final residual row"
+    assert np.all(h1[1 - last].view(np.uint32) == SENT), "the other hand-off row was not refilled"
+    x = x0.astype(np.float64)
+    for s in range(steps):
+        x = x + wo.astype(np.float64) @ ctx[s].astype(np.float64)
+        xn = x / np.sqrt(np.mean(x * x) + eps) * nw
+        assert np.max(np.abs(n1[s] - xn)) < 1e-4 * (1 + np.max(np.abs(xn)))
+        lg = wr.astype(np.float64) @ xn
+        assert np.max(np.abs(l1[s] - lg)) < 1e-4 * (1 + np.max(np.abs(lg)))
+    assert np.max(np.abs(x1 - x)) < 1e-4 * (1 + np.max(np.abs(x)))
+
+
 @pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(3, 256, 16, 6, 64, 2, False), (1, 256, 16, 6, 64, 2, True),
                                                   (2, 1280, 64, 6, 896, 2, True), (9, 128, 8, 3, 32, 1, False),
                                                   (4, 256, 16, 6, 64, 2, False)])
