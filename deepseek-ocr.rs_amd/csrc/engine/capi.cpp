@@ -567,6 +567,12 @@ dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale,
         a.o = o; a.o_row_stride = C; a.o_head_stride = hd; a.n_seq = n_seq; a.L = L; a.heads = heads;
         a.kv_heads = heads; a.hd = hd; a.scale = scale; a.causal = causal;
         float* rb = nullptr;
+        float* part = nullptr;
+        if (causal) {  // the engine's prefill form: key pieces + combine
+            a.part_floats = dsocr::attention_causal_part_floats(n_seq, heads, L, hd);
+            check_hip(hipMalloc(&part, sizeof(float) * a.part_floats), "hipMalloc attention pieces");
+            a.part = part;
+        }
         if (relh && relw) {
             if (gh * gw != L) throw std::runtime_error("EINVAL: rel-pos grid does not match L");
             check_hip(hipMalloc(&rb, sizeof(float) * (size_t)n_seq * heads * L * (gh + gw)), "hipMalloc relbias");
@@ -576,6 +582,7 @@ dsocr_status dsocr_k_attention(int n_seq, int L, int heads, int hd, float scale,
         dsocr::launch_attention(a, nullptr);
         hipError_t e = hipDeviceSynchronize();
         if (rb) (void)hipFree(rb);
+        if (part) (void)hipFree(part);
         check_hip(e, "attention");
     });
 }

@@ -928,6 +928,8 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     a.heads = L.heads; a.kv_heads = L.kv_heads; a.hd = hd;
     a.scale = (float)(1.0 / std::sqrt((double)hd));
     a.causal = 1;
+    a.part_floats = attention_causal_part_floats(B, L.heads, max_len, hd);
+    a.part = wsf("d_attn_part", a.part_floats);
     for (int q = 0; q < B && q < (int)prefill_lens_.size(); ++q)
         flops_acc_ += 2.0 * (double)prefill_lens_[q] * (prefill_lens_[q] + 1) * hd * L.heads;
     launch_attention(a, st);

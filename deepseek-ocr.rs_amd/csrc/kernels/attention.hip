@@ -150,16 +150,41 @@ __global__ __launch_bounds__(256) void attention_fwd_kernel(AttnArgs a) {
 // every K fragment is a 16-byte LDS read, V staged transposed in LDS (16-byte reads of 4 keys),
 // K/V tile t+1 prefetched into registers while tile t is consumed (one barrier per tile), and the
 // rel-pos bias column indices of a tile computed once per tile in LDS (no per-score division).
-template <int HD, bool REL>
+//
+// SPLIT (the causal prefill, round 4): the keys of a 128-query block are split into pieces of AT_KSPLIT keys,
+// one block per (query block, piece) — at one 706-token page 60 blocks with 1..6 pieces of work became 210
+// blocks of one piece each — and every block writes its unnormalised partial (m, l, o) per query;
+// attention_merge_kernel combines a query's pieces in piece order (flash-decoding combine).
+constexpr int AT_KSPLIT = 128;
+
+// (query block, key piece) of pair p, pairs enumerated query-block-major over the grid's length L
+__device__ __forceinline__ void split_pair(int p, int L, int& qb, int& ks) {
+    for (qb = 0;; ++qb) {
+        const int n = (min(L, (qb + 1) * 4 * AT_Q) + AT_KSPLIT - 1) / AT_KSPLIT;
+        if (p < n || n == 0) { ks = p; return; }
+        p -= n;
+    }
+}
+// first pair of query block qb
+__device__ __host__ inline int split_first_pair(int qb, int L) {
+    int off = 0;
+    for (int j = 0; j < qb; ++j) off += (std::min(L, (j + 1) * 4 * AT_Q) + AT_KSPLIT - 1) / AT_KSPLIT;
+    return off;
+}
+
+template <int HD, bool REL, bool SPLIT = false>
 __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
     constexpr int KP = HD + 4, VP = AT_KT + 4;
     constexpr int F4 = AT_KT * HD / 4 / 256;  // float4 per thread per operand per tile
+    static_assert(!(SPLIT && REL), "the split form serves the causal prefill (no rel-pos bias)");
     __shared__ __attribute__((aligned(16))) float Ks[2][AT_KT][KP];
     __shared__ __attribute__((aligned(16))) float Vt[2][HD][VP];
     __shared__ int rbh[2][AT_KT], rbw[2][AT_KT];
     const int s = blockIdx.z, h = blockIdx.y;
     const int len = a.seq_len ? a.seq_len[s] : a.L;
-    const int qb0 = blockIdx.x * (4 * AT_Q);
+    int qblk = blockIdx.x, kpiece = 0;
+    if (SPLIT) split_pair(blockIdx.x, a.L, qblk, kpiece);
+    const int qb0 = qblk * (4 * AT_Q);
     if (qb0 >= len) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int half = lane >> 5, l32 = lane & 31;
@@ -197,6 +222,12 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
     }
     int kend = len;
     if (a.causal) kend = min(len, qb0 + 4 * AT_Q);
+    int kbeg = 0;
+    if (SPLIT) {
+        kbeg = kpiece * AT_KSPLIT;
+        if (kbeg >= kend) return;  // past this sequence's keys (a shorter sequence of the batch)
+        kend = min(kend, kbeg + AT_KSPLIT);
+    }
     // staging: thread covers float4 f = tid + 256 j of the tile: key f / (HD/4), cols (f % (HD/4)) * 4
     // (macros, not lambdas: a captured register array is demoted to scratch)
     float4 rk[F4], rv[F4];
@@ -229,11 +260,11 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
-    AT2_GLOAD(0);
-    AT2_LSTORE(0, 0);
+    AT2_GLOAD(kbeg);
+    AT2_LSTORE(0, kbeg);
     __syncthreads();
     int buf = 0;
-    for (int k0 = 0; k0 < kend; k0 += AT_KT, buf ^= 1) {
+    for (int k0 = kbeg; k0 < kend; k0 += AT_KT, buf ^= 1) {
         AT2_GLOAD(k0 + AT_KT);  // unconditional (clamped keys): a guarded prefetch demotes rk/rv to scratch
         // S^T = K . Q^T: lane (half, l32) feeds dims i + half*HD/2
         f32x16 sc;
@@ -301,6 +332,18 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
         AT2_LSTORE(buf ^ 1, k0 + AT_KT);
         __syncthreads();
     }
+    if (SPLIT) {  // unnormalised partial of this key piece: [m, l, o[HD]] per query of the block
+        if (q_valid) {
+            const int npairs = split_first_pair((a.L + 4 * AT_Q - 1) / (4 * AT_Q), a.L);
+            float* rec = a.part + ((((long)s * a.heads + h) * npairs + blockIdx.x) * (4 * AT_Q) + (q_lane - qb0)) * (HD + 2);
+            if (half == 0) { rec[0] = m_run; rec[1] = l_run; }
+#pragma unroll
+            for (int t = 0; t < HD / 32; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) rec[2 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = o[t][r];
+        }
+        return;
+    }
     // O^T accumulator: row = d (within t), column = this lane's query
     if (q_valid) {
         float* op = a.o + ooff + (long)q_lane * a.o_row_stride + (long)h * a.o_head_stride;
@@ -311,6 +354,39 @@ __global__ __launch_bounds__(256, 1) void attention_fwd2_kernel(AttnArgs a) {
     }
 #undef AT2_GLOAD
 #undef AT2_LSTORE
+}
+
+// combine of the key pieces (SPLIT above): thread (query, d); m = max m_i, l = sum l_i e^(m_i - m),
+// o = sum o_i e^(m_i - m), all in piece order; out = o / l
+template <int HD>
+__global__ __launch_bounds__(256) void attention_merge_kernel(AttnArgs a) {
+    const int s = blockIdx.z, h = blockIdx.y;
+    const int len = a.seq_len ? a.seq_len[s] : a.L;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    const int q = (int)(idx / HD), d = (int)(idx % HD);
+    if (q >= len) return;
+    const int qb = q / (4 * AT_Q), ql = q % (4 * AT_Q);
+    const int kend = a.causal ? min(len, (qb + 1) * 4 * AT_Q) : len;
+    const int n = (kend + AT_KSPLIT - 1) / AT_KSPLIT;
+    const int npairs = split_first_pair((a.L + 4 * AT_Q - 1) / (4 * AT_Q), a.L);
+    const float* rec0 = a.part + ((((long)s * a.heads + h) * npairs + split_first_pair(qb, a.L)) * (4 * AT_Q) + ql) * (HD + 2);
+    const long pstride = (long)(4 * AT_Q) * (HD + 2);
+    float m = -INFINITY;
+    for (int i = 0; i < n; ++i) m = fmaxf(m, rec0[i * pstride]);
+    float l = 0.f, acc = 0.f;
+    for (int i = 0; i < n; ++i) {
+        const float* r = rec0 + i * pstride;
+        const float w = r[0] == -INFINITY ? 0.f : __expf(r[0] - m);
+        l += r[1] * w;
+        acc += r[2 + d] * w;
+    }
+    const long ooff = a.o_seq_off ? a.o_seq_off[s] : (long)s * a.L * a.o_row_stride;
+    a.o[ooff + (long)q * a.o_row_stride + (long)h * a.o_head_stride + d] = acc / l;
+}
+
+size_t attention_causal_part_floats(int n_seq, int heads, int L, int hd) {
+    const int nqb = (L + 4 * AT_Q - 1) / (4 * AT_Q);
+    return (size_t)n_seq * heads * split_first_pair(nqb, L) * (4 * AT_Q) * (hd + 2);
 }
 
 // attention_split: the same exact-f32 attention (64-dim heads, uniform sequences, no causal mask: the
@@ -564,6 +640,12 @@ static bool attn_split_on() {
     return v;
 }
 
+// DSOCR_ATTN_KSPLIT=0 (A/B switch, read at every launch): the causal prefill without key pieces
+static bool attn_ksplit_on() {
+    const char* e = getenv("DSOCR_ATTN_KSPLIT");
+    return !(e && atoi(e) == 0);
+}
+
 void launch_attention(const AttnArgs& a, hipStream_t s) {
     int maxlen = a.L;
     dim3 grid((maxlen + 4 * AT_Q - 1) / (4 * AT_Q), a.heads, a.n_seq);
@@ -586,6 +668,21 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
             else hipLaunchKernelGGL((attention_split_kernel<false>), grid, dim3(256), 0, s, b);
             return;
         }
+    }
+    if ((a.hd == 64 || a.hd == 128) && a.causal && !a.relbias && a.part &&
+        a.part_floats >= attention_causal_part_floats(a.n_seq, a.heads, a.L, a.hd) && attn_ksplit_on()) {
+        // the causal prefill: one block per (query block, key piece), then the piece combine
+        const int nqb = (a.L + 4 * AT_Q - 1) / (4 * AT_Q);
+        const dim3 g1(split_first_pair(nqb, a.L), a.heads, a.n_seq);
+        const dim3 g2((unsigned)(((long)a.L * a.hd + 255) / 256), a.heads, a.n_seq);
+        if (a.hd == 64) {
+            hipLaunchKernelGGL((attention_fwd2_kernel<64, false, true>), g1, dim3(256), 0, s, b);
+            hipLaunchKernelGGL(attention_merge_kernel<64>, g2, dim3(256), 0, s, b);
+        } else {
+            hipLaunchKernelGGL((attention_fwd2_kernel<128, false, true>), g1, dim3(256), 0, s, b);
+            hipLaunchKernelGGL(attention_merge_kernel<128>, g2, dim3(256), 0, s, b);
+        }
+        return;
     }
     if (a.hd == 64 || a.hd == 128) {  // exact-f32 MFMA flash attention; other head dims: attention_fwd_kernel
         const bool rel = b.relbias != nullptr;

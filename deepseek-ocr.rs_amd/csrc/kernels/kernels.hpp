@@ -118,8 +118,13 @@ struct AttnArgs {
     int causal = 0;
     const float* relbias = nullptr;  // [seq][head][L][rel_h + rel_w]
     int rel_h = 0, rel_w = 0;
+    // causal (prefill): workspace for the key-piece partials (attention_causal_part_floats); without it
+    // one block walks all of a query block's keys
+    float* part = nullptr;
+    size_t part_floats = 0;
 };
 void launch_attention(const AttnArgs& a, hipStream_t s);
+size_t attention_causal_part_floats(int n_seq, int heads, int L, int hd);
 // Bidirectional attention on bf16-valued q / k / v with f32 math on the bf16 matrix cores
 // (attention_bf16.hip): n_seq uniform sequences of L rows; element (seq, row, head, d) of q at
 // q + seq*L*q_rs + row*q_rs + head*q_hs + d (likewise k, v with kv heads); o f32 or bf16 (o_bf16).
