@@ -78,6 +78,30 @@ def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
+@pytest.mark.parametrize("M,N,K,act,acc,splits", [(4096, 2304, 768, 0, 0, 0), (257, 3072, 1024, 1, 0, 0),
+                                                  (404, 1024, 4096, 0, 1, 0), (300, 512, 1152, 3, 1, 9), (77, 130, 192, 0, 0, 1)])
+def test_gemm_f32a_k64(gpu, monkeypatch, M, N, K, act, acc, splits):
+    """The vision linears' kernel with 64 k per LDS stage (DSOCR_GEMM_KT=64: 256-B A rows swizzled chunk ^ (r & 15),
+    128-B W rows chunk ^ ((r >> 1) & 7)) vs f64 and bitwise vs the 32-k form (same products, same order)."""
+    rng = np.random.default_rng(M + N + K)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    bits, w = _weights(rng, N, K, 0)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
+    dA, dW, dB = Dev(a), Dev(bits), Dev(bias)
+    got = {}
+    for kt in ("64", "32"):
+        monkeypatch.setenv("DSOCR_GEMM_KT", kt)
+        dC = Dev(c0)
+        check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, 0, dB.ptr, dC.ptr, act, acc, splits))
+        got[kt] = dC.get()
+    ref = ACTS[act]((a.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias) + (c0 if acc else 0)
+    bound = _bound(a, w) * (2.0 if act else 1.0)
+    assert np.all(np.abs(got["64"] - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got["64"] - ref))
+    # the k order of the accumulation is the same in both forms (16-k MFMA steps in increasing k)
+    assert np.array_equal(got["64"], got["32"])
+
+
 @pytest.mark.parametrize("T,E,topk,N,K,wdt,act,acc,kernel", [
     (300, 64, 6, 1792, 1280, 1, 0, 0, 1),   # one page's routed gate/up (~28 rows per expert)
     (300, 64, 6, 1280, 896, 1, 0, 1, 1),    # ... down, accumulate epilogue
