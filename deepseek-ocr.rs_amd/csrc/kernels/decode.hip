@@ -1159,6 +1159,14 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 // (block.rs:776-789) and uses them directly.  Each block issues its K and V cache loads first, then
 // builds q; the chunk partials of a (page, head) are merged by chunk 0's block polling them (POLL, <= 24
 // chunks of 128-dim heads) or by the last arriver of a ticket (flash-decoding combine).
+// phase clock (DecAttn2Args::stamps): one lane per block, 64-bit device-scope min / max
+__device__ __forceinline__ void da_stamp(unsigned long long* st, int slot, bool is_min = false) {
+    if (!st || threadIdx.x != 0) return;
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (is_min) __hip_atomic_fetch_min(st + slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_max(st + slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int DA_CH = 64;       // keys per block
 constexpr int DA2_CH_MIN = DA_CH;
 constexpr uint32_t DA_SENT = 0x7FBADBADu;  // "record word not written yet" (a NaN payload no arithmetic produces)
@@ -1264,6 +1272,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        da_stamp(a.stamps, 2);
     }
     // a block that gave up (the error flag is set; the host raises after the step) leaves the K / V cache
     // untouched: sentinel q / k / v never enter the cache.  It still writes its record so the merge of its
@@ -1428,6 +1437,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         __builtin_memcpy(&bits, ml, 16);
         __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
     }
+    if (FUSED) da_stamp(a.stamps, 3);
     // 6. POLL: no ticket.  Chunk 0's block merges: it polls the records of the other chunks until
     //    none of the words it needs still holds the sentinel (the record buffer enters every launch
     //    filled with it: dec_attn_part_init, then each merge refills what it read), so a writer
@@ -1490,6 +1500,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        if (FUSED) da_stamp(a.stamps, 4);
         if (POLL) {  // refill what was read (each word by exactly one thread) for the next launch
             const uint32_t sent = DA_SENT;
 #pragma unroll
@@ -1547,6 +1558,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + kvh) * HD + tid) * 4, 0, 16);
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + a.kv_heads + kvh) * HD + tid) * 4, 0, 16);
         }
+        da_stamp(a.stamps, 5);
     }
 }
 
@@ -1563,10 +1575,15 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
 template <typename WT>
 __global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecGemvArgs g, DecRopeEpi r, DecAttn2Args a, int nq) {
     WaveSpan span_(a.span);
+    da_stamp(a.stamps, 0, true);
     if ((int)blockIdx.x < nq) {
+        da_stamp(a.stamps, 7);
         qkv_rope_body<WT, true>(g, r, blockIdx.x);
+        da_stamp(a.stamps, 1);
         return;
     }
+    da_stamp(a.stamps, 6, true);
+    da_stamp(a.stamps, 8);
     const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
     const int i = (int)blockIdx.x - nq;
     dec_attn_body<128, true, true, true>(a, i % chunks, i / chunks, 0);

@@ -278,6 +278,68 @@ static void case_attn(int B, int pos, hipStream_t s) {
     for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); }
 }
 
+// one page's fused q/k/v projection + decode attention (dec_qkv_attn) at L = pos + 1, 12 layers' weights and
+// caches rotating, timed; then the phase clocks of three single launches (DecAttn2Args::stamps)
+static void case_qkvattn1(int pos, hipStream_t s) {
+    const int max_len = 1218;
+    constexpr int NLA = 12;
+    const long head_stride = (long)max_len * HD, page_stride = (long)HEADS * head_stride;
+    std::vector<float*> kc(NLA), vc(NLA);
+    std::vector<uint16_t*> wq(NLA);
+    for (int l = 0; l < NLA; ++l) {
+        kc[l] = rand_f32((size_t)page_stride); vc[l] = rand_f32((size_t)page_stride);
+        wq[l] = rand_f16((size_t)3 * H * H);
+    }
+    float* x = rand_f32(H);
+    float* nw = rand_f32(H, 0.2f, 1.f);
+    float* row = (float*)dalloc((size_t)3 * H * 4);
+    dec_qkv_sentinel_init(row, 3 * H, nullptr);
+    int* kv_pos = (int*)dalloc(16);
+    CK(hipMemcpy(kv_pos, &pos, 4, hipMemcpyHostToDevice));
+    float* cs = rand_f32((size_t)max_len * HD, 1.f);
+    float* sn = rand_f32((size_t)max_len * HD, 1.f);
+    const size_t pb = dec_attn_workspace(1, HEADS, HD, max_len);
+    float* part = (float*)dalloc(pb + 64);
+    dec_attn_part_init(part, pb, nullptr);
+    int* cnt = (int*)dalloc(HEADS * 4 + 16);
+    float* o = (float*)dalloc((size_t)HEADS * HD * 4);
+    DecGemvArgs g;
+    g.M = 1; g.N = 3 * H; g.K = H; g.ldw = H; g.wdtype = WDT_F16; g.y = row; g.ldy = 3 * H; g.x = x; g.ldx = H;
+    g.norm_w = nw; g.eps = 1e-6f;
+    DecRopeEpi re;
+    re.kv_pos = kv_pos; re.cos = cs; re.sin = sn; re.hd = HD; re.rot_rows = 2 * H;
+    DecAttn2Args a;
+    a.qkv = row; a.ld = 3 * H; a.kv_pos = kv_pos; a.B = 1; a.heads = HEADS; a.kv_heads = HEADS; a.hd = HD;
+    a.rope_dim = HD; a.max_len = max_len; a.cos = cs; a.sin = sn; a.page_stride = page_stride; a.head_stride = head_stride;
+    a.scale = 1.f / sqrtf((float)HD); a.part = part; a.counters = cnt; a.o = o; a.o_ld = HEADS * HD; a.prerot = 1;
+    a.err = cnt + HEADS;
+    auto set = [&](int i) { g.W = wq[i % NLA]; a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; };
+    if (!dec_qkv_attn_ok(g, re, a)) { printf("qkvattn1: fused launch refused\n"); return; }
+    char nm[96];
+    snprintf(nm, sizeof nm, "qkv+attn B=1 L=%d", pos + 1);
+    const double bytes = 3.0 * H * H * 2 + 2.0 * (pos + 1) * HEADS * HD * 4;
+    report(nm, timeit(4 * NLA, [&](int i) { set(i); launch_dec_qkv_attn(g, re, a, s); }, s), bytes);
+    auto* st = (unsigned long long*)dalloc(16 * 8);
+    const char* names[9] = {"entry", "proj stored", "q polled", "record stored", "merge polled", "merge exit",
+                            "attn entry(min)", "proj entry(max)", "attn entry(max)"};
+    for (int it = 0; it < 3; ++it) {
+        std::vector<unsigned long long> init(16, 0);
+        init[0] = init[6] = ~0ull;
+        CK(hipMemcpy(st, init.data(), 16 * 8, hipMemcpyHostToDevice));
+        set(it + 1);
+        a.stamps = st;
+        launch_dec_qkv_attn(g, re, a, s);
+        a.stamps = nullptr;
+        CK(hipStreamSynchronize(s));
+        unsigned long long h[16];
+        CK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
+        printf("qkv+attn stamps (us from first block entry):");
+        for (int i = 1; i < 9; ++i) printf(" %s %.2f |", names[i], ((long long)h[i] - (long long)h[0]) / 100.0);
+        printf("\n");
+    }
+    for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); (void)hipFree(wq[l]); }
+}
+
 static void case_lm(int M, hipStream_t s) {
     constexpr int NB = 2;  // 2 x 331 MB > the Infinity Cache
     std::vector<uint16_t*> w(NB);
@@ -426,6 +488,7 @@ int main(int argc, char** argv) {
         else if (c == "gemv8") case_gemv(8, s);
         else if (c == "attn1") { case_attn(1, 706, s); case_attn(1, 1216, s); }
         else if (c == "attn8") { case_attn(8, 706, s); case_attn(8, 1216, s); }
+        else if (c == "qkvattn1") { case_qkvattn1(706, s); case_qkvattn1(1216, s); }
         else if (c == "lm8") case_lm(8, s);
         else if (c == "vgemm") case_vgemm(s);
         else if (c == "dgemm") case_dgemm(s);
