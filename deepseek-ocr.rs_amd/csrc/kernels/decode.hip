@@ -1396,6 +1396,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         if (tid == 0) red[4] = l;
     }
     __syncthreads();
+    if (!FUSED) da_stamp(a.stamps, 2);  // standalone: the chunk's scores and softmax done (K landed)
     // 5. P.V over this thread's KPG keys
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -1437,7 +1438,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         __builtin_memcpy(&bits, ml, 16);
         __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
     }
-    if (FUSED) da_stamp(a.stamps, 3);
+    da_stamp(a.stamps, 3);
     // 6. POLL: no ticket.  Chunk 0's block merges: it polls the records of the other chunks until
     //    none of the words it needs still holds the sentinel (the record buffer enters every launch
     //    filled with it: dec_attn_part_init, then each merge refills what it read), so a writer
@@ -1500,7 +1501,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (FUSED) da_stamp(a.stamps, 4);
+        da_stamp(a.stamps, 4);
         if (POLL) {  // refill what was read (each word by exactly one thread) for the next launch
             const uint32_t sent = DA_SENT;
 #pragma unroll
@@ -1558,13 +1559,15 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + kvh) * HD + tid) * 4, 0, 16);
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + a.kv_heads + kvh) * HD + tid) * 4, 0, 16);
         }
-        da_stamp(a.stamps, 5);
     }
+    da_stamp(a.stamps, 5);
 }
 
 template <int HD, bool PREROT, bool POLL>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     WaveSpan span_(a.span);
+    da_stamp(a.stamps, 0, true);
+    da_stamp(a.stamps, 8);
     dec_attn_body<HD, PREROT, POLL, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 

@@ -248,10 +248,11 @@ struct DecAttn2Args {
     int* err = nullptr;                                 // polled merge: give-up flag (set instead of hanging)
     unsigned long long* span = nullptr;                 // launch-span slots (SPAN_SLOTS pairs) or null
     int prerot = 0;                                     // q / k rows already rotated (dec_qkv_rope)
-    // phase clocks of the fused q/k/v + attention launch (tools/kbench qkvattn1; null in the engine):
-    // [0] first block entry (min), [1] last projection store, [2] last q poll done, [3] last chunk record
-    // stored, [4] last merge poll done, [5] last merge exit, [6] first attention block entry (min),
-    // [7] last projection block entry, [8] last attention block entry (s_memrealtime, 100 MHz)
+    // phase clocks (tools/kbench qkvattn1 / attn8; null in the engine): [0] first block entry (min),
+    // [1] last projection store (fused), [2] last q poll done (fused) / last softmax done (standalone),
+    // [3] last chunk record stored, [4] last merge poll done, [5] last block exit, [6] first attention
+    // block entry (fused, min), [7] last projection block entry (fused), [8] last attention block entry
+    // (s_memrealtime, 100 MHz)
     unsigned long long* stamps = nullptr;
 };
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);

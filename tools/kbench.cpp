@@ -275,6 +275,22 @@ static void case_attn(int B, int pos, hipStream_t s) {
     snprintf(nm, sizeof nm, "attn B=%d L=%d", B, pos + 1);
     const double bytes = 2.0 * B * (pos + 1) * HEADS * HD * 4;
     report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
+    auto* st = (unsigned long long*)dalloc(16 * 8);
+    for (int it = 0; it < 2; ++it) {
+        std::vector<unsigned long long> init(16, 0);
+        init[0] = ~0ull;
+        CK(hipMemcpy(st, init.data(), 16 * 8, hipMemcpyHostToDevice));
+        a.kc = kc[it + 1]; a.vc = vc[it + 1]; a.stamps = st;
+        launch_dec_attn(a, s);
+        a.stamps = nullptr;
+        CK(hipStreamSynchronize(s));
+        unsigned long long h[16];
+        CK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
+        printf("attn stamps (us from first entry): last entry %.2f | last softmax %.2f | last record %.2f | last merge poll %.2f | last exit %.2f\n",
+               ((long long)h[8] - (long long)h[0]) / 100.0, ((long long)h[2] - (long long)h[0]) / 100.0,
+               ((long long)h[3] - (long long)h[0]) / 100.0, ((long long)h[4] - (long long)h[0]) / 100.0,
+               ((long long)h[5] - (long long)h[0]) / 100.0);
+    }
     for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); }
 }
 
