@@ -536,9 +536,11 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once), ONE LDS stage (24 KB, four blocks per
     // CU: kbench vgemm 1.00-1.18x the two-stage kernel on the SAM linears, within 3 % elsewhere); f16
     // weights: 2 x 2 (their W split would double under 4 x 1), two stages
-    if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    const bool kt64 = gemm_kt_env() == 64 && g.K % FX_K == 0 && (g.K / FX_K) % (2 * g.splits) == 0;  // same K slices as at 32
+    if (g.w_f16 && kt64) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true, true, 1, FX_N, 64>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    else if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else if (g.variant == 2) hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 2>), dim3(tiles * g.splits), dim3(256), 0, s, g);
-    else if (gemm_kt_env() == 64 && (g.K / FX_K) % (2 * g.splits) == 0 && g.K % FX_K == 0)  // same K slices as at 32
+    else if (kt64)
         hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 1, FX_N, 64>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 1>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) launch_splitk_reduce(g, s);

@@ -78,14 +78,17 @@ def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
-@pytest.mark.parametrize("M,N,K,act,acc,splits", [(4096, 2304, 768, 0, 0, 0), (257, 3072, 1024, 1, 0, 0),
-                                                  (404, 1024, 4096, 0, 1, 0), (300, 512, 1152, 3, 1, 9), (77, 130, 192, 0, 0, 1)])
-def test_gemm_f32a_k64(gpu, monkeypatch, M, N, K, act, acc, splits):
-    """The vision linears' kernel with 64 k per LDS stage (DSOCR_GEMM_KT=64: 256-B A rows swizzled chunk ^ (r & 15),
-    128-B W rows chunk ^ ((r >> 1) & 7)) vs f64 and bitwise vs the 32-k form (same products, same order)."""
+@pytest.mark.parametrize("M,N,K,act,acc,splits,wdt", [(4096, 2304, 768, 0, 0, 0, 0), (257, 3072, 1024, 1, 0, 0, 0),
+                                                      (404, 1024, 4096, 0, 1, 0, 0), (300, 512, 1152, 3, 1, 9, 0),
+                                                      (77, 130, 192, 0, 0, 1, 0), (706, 3840, 1280, 0, 0, 0, 1),
+                                                      (706, 1280, 1280, 0, 1, 0, 1)])
+def test_gemm_f32a_k64(gpu, monkeypatch, M, N, K, act, acc, splits, wdt):
+    """The vision (bf16) and prefill (f16) linears' kernel with 64 k per LDS stage (DSOCR_GEMM_KT=64: 256-B A rows
+    swizzled chunk ^ (r & 15), 128-B W rows chunk ^ ((r >> 1) & 7)) vs f64 and bitwise vs the 32-k form (same
+    products, same order)."""
     rng = np.random.default_rng(M + N + K)
     a = rng.standard_normal((M, K)).astype(np.float32)
-    bits, w = _weights(rng, N, K, 0)
+    bits, w = _weights(rng, N, K, wdt)
     bias = rng.standard_normal(N).astype(np.float32) * 0.1
     c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
     dA, dW, dB = Dev(a), Dev(bits), Dev(bias)
@@ -93,7 +96,7 @@ def test_gemm_f32a_k64(gpu, monkeypatch, M, N, K, act, acc, splits):
     for kt in ("64", "32"):
         monkeypatch.setenv("DSOCR_GEMM_KT", kt)
         dC = Dev(c0)
-        check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, 0, dB.ptr, dC.ptr, act, acc, splits))
+        check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, wdt, dB.ptr, dC.ptr, act, acc, splits))
         got[kt] = dC.get()
     ref = ACTS[act]((a.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias) + (c0 if acc else 0)
     bound = _bound(a, w) * (2.0 if act else 1.0)
