@@ -682,45 +682,6 @@ dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int h
         if (used_fused) *used_fused = took ? 1 : 0;
     });
 }
-dsocr_status dsocr_k_oproj_route(int fused, int steps, int H, int Kc, int E, const float* ctx, const void* Wo,
-                                 const void* Wr, int wdtype, const float* norm_w, float eps, float* x, float* logits,
-                                 float* xn, float* hand_out, int* used_fused) {
-    return guarded([&] {
-        if (steps <= 0 || H <= 0 || Kc <= 0 || E <= 0) throw std::runtime_error("EINVAL: bad o_proj / router shape");
-        if (wdtype != dsocr::WDT_F16 && wdtype != dsocr::WDT_BF16) throw std::runtime_error("EINVAL: 16-bit weights only");
-        float* hand = nullptr;  // two layers' hand-off rows: step s uses row s % 2 and refills the other
-        int* err = nullptr;
-        check_hip(hipMalloc(&hand, sizeof(float) * 2 * (size_t)H), "hipMalloc");
-        check_hip(hipMalloc(&err, sizeof(int)), "hipMalloc");
-        check_hip(hipMemset(err, 0, sizeof(int)), "hipMemset");
-        dsocr::dec_hand_init(hand, 2 * (size_t)H, nullptr);
-        bool took = false;
-        for (int s = 0; s < steps; ++s) {
-            dsocr::DecGemvArgs go;  // o_proj + residual (Engine::decode_step)
-            go.M = 1; go.N = H; go.K = Kc; go.x = ctx + (size_t)s * Kc; go.ldx = Kc; go.W = Wo; go.ldw = Kc;
-            go.wdtype = wdtype; go.y = x; go.ldy = H; go.accumulate = 1;
-            dsocr::DecGemvArgs gr;  // the one-page router (launch_moe_decode's mix plan)
-            gr.M = 1; gr.N = E; gr.K = H; gr.x = x; gr.ldx = H; gr.W = Wr; gr.ldw = H; gr.wdtype = wdtype;
-            gr.y = logits + (size_t)s * E; gr.ldy = E; gr.norm_w = norm_w; gr.eps = eps; gr.xn_out = xn + (size_t)s * H;
-            if (fused && dsocr::dec_oproj_route_ok(go, gr)) {
-                dsocr::launch_dec_oproj_route(go, gr, hand + (size_t)(s % 2) * H, hand + (size_t)((s + 1) % 2) * H, err, nullptr);
-                took = true;
-            } else {
-                dsocr::launch_dec_gemv(go, nullptr);
-                dsocr::launch_dec_gemv(gr, nullptr);
-            }
-        }
-        hipError_t e = hipDeviceSynchronize();
-        int herr = 0;
-        if (e == hipSuccess) e = hipMemcpy(&herr, err, sizeof(int), hipMemcpyDeviceToHost);
-        if (e == hipSuccess && hand_out) e = hipMemcpy(hand_out, hand, sizeof(float) * 2 * (size_t)H, hipMemcpyDeviceToDevice);
-        (void)hipFree(hand);
-        (void)hipFree(err);
-        check_hip(e, "oproj_route");
-        if (herr) throw std::runtime_error("EINTERNAL: o_proj -> router hand-off timed out");
-        if (used_fused) *used_fused = took ? 1 : 0;
-    });
-}
 int dsocr_k_poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus) {
     return dsocr::poll_wait_fits(waiting_blocks, api_blocks_per_cu, cus) ? 1 : 0;
 }

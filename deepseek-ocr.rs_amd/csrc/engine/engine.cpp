@@ -1115,19 +1115,7 @@ void Engine::decode_step(int B, int Lmax) {
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
         go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
-        // one page, MoE layer: o_proj and the router in one launch (the router blocks poll the residual row
-        // the o_proj blocks hand over; DSOCR_OPROJ_ROUTE=0 is the A/B switch)
-        bool routed = false;
-        if (d.moe && B == 1 && oproj_route_fused()) {
-            const int prev = prev_moe_layer(l);
-            DecGemvArgs gr;
-            if (prev != l && moe_router_args(moe_args(l, B, X), &gr) && dec_oproj_route_ok(go, gr)) {
-                float* hand = wsf("s_hand", (size_t)L.layers * H);
-                launch_dec_oproj_route(go, gr, hand + (long)l * H, hand + (long)prev * H, err, st);
-                routed = true;
-            }
-        }
-        if (!routed) launch_dec_gemv(go, st);
+        launch_dec_gemv(go, st);
         // MLP / MoE
         if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
             // dense MLP (layer 0) on the matrix cores: gate|up with the post-attention RMSNorm fused,
@@ -1161,13 +1149,12 @@ void Engine::decode_step(int B, int Lmax) {
             continue;
         }
         if (!span_rec_) {
-            const int parts = (routed ? 0 : MOE_ROUTE) | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) |
-                              ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
+            const int parts = MOE_ROUTE | ((step_skip_ & SKIP_GATEUP) ? 0 : MOE_GATEUP) | ((step_skip_ & SKIP_DOWN) ? 0 : MOE_DOWN);
             launch_moe_decode(moe_args(l, B, X), st, parts);
             continue;
         }
         MoeDecodeArgs ma = moe_args(l, B, X);
-        if (!routed) launch_moe_decode(ma, st, MOE_ROUTE);
+        launch_moe_decode(ma, st, MOE_ROUTE);
         ma.span = (span_mode_ & SPAN_WAVES) ? span_slots_ : nullptr;
         stamped(SPAN_GATEUP, l, [&] { launch_moe_decode(ma, st, MOE_GATEUP); }, ma.ids, B * ma.topk);
         stamped(SPAN_DOWN, l, [&] { launch_moe_decode(ma, st, MOE_DOWN); }, ma.ids, B * ma.topk);
@@ -1237,22 +1224,6 @@ void Engine::ensure_mm_weights(int B) {
 
 // one page: q/k/v projection + decode attention as one launch (dec_qkv_attn); DSOCR_QKV_ATTN=0 (A/B
 // switch, read once) keeps the two launches
-// read at every capture (tests switch it within one process)
-bool Engine::oproj_route_fused() const {
-    const char* e = getenv("DSOCR_OPROJ_ROUTE");
-    return !(e && atoi(e) == 0);
-}
-
-// the MoE layer before l in decode order, cyclically (l itself when it is the only one)
-int Engine::prev_moe_layer(int l) const {
-    const int n = (int)layers_.size();
-    for (int k = 1; k <= n; ++k) {
-        const int j = ((l - k) % n + n) % n;
-        if (layers_[j].moe) return j;
-    }
-    return l;
-}
-
 bool Engine::qkv_attn_fused() {
     static const bool v = !(getenv("DSOCR_QKV_ATTN") && atoi(getenv("DSOCR_QKV_ATTN")) == 0);
     return v;
@@ -1543,9 +1514,6 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         const size_t qn = (size_t)B * layers_[0].qkv.N;
         dec_qkv_sentinel_init(wsf("s_qkv", qn), qn, st);
         wsf("p_qkv_skip", qn);  // the profile's variant without attention projects here (allocated before capture)
-        // the one-page o_proj -> router hand-off rows (one per layer): sentinel-filled, each launch refills
-        // the previous MoE layer's
-        dec_hand_init(wsf("s_hand", (size_t)L.layers * H), (size_t)L.layers * H, st);
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag

@@ -171,33 +171,18 @@ constexpr size_t STAGE_LDS_MAX = 64 * 1024;
 // A wave owns RB rows.  Every lane issues its 16-byte weight loads for the first U*64
 // chunks BEFORE the block stages x through LDS, so the HBM latency of the weight
 // stream overlaps the norm prologue; K <= 64*U*8 is a single batch.
-//
-// HM (the one-page o_proj + router launch, dec_oproj_route): HM_PRODUCE — every output is also stored
-// write-through into the layer's sentinel-filled hand-off row h.hand, and the previous MoE layer's row
-// (every reader of it finished with the launch before this one) is refilled with the sentinel;
-// HM_POLL — the row x is taken from h.hand by polling (sc1 loads) until no word holds the sentinel,
-// then staged exactly as from x (same registers, same xstage arithmetic, same dot order), so the
-// fused launch's outputs equal the two-launch form's bit for bit.
-struct HandOff {
-    float* hand = nullptr;       // this layer's row (written by HM_PRODUCE, polled by HM_POLL)
-    float* hand_prev = nullptr;  // the previous MoE layer's row, refilled by HM_PRODUCE
-    int* err = nullptr;          // bounded-spin give-up flag
-};
-constexpr int HM_NONE = 0, HM_PRODUCE = 1, HM_POLL = 2;
-constexpr uint32_t HAND_SENT = 0x7FBADBADu;  // the decode attention's record sentinel (DA_SENT)
-
-template <typename WT, int MT, int RB, int U, int HM = HM_NONE>
-__device__ __forceinline__ void dec_gemv_body(const DecGemvArgs& a, const int bid, const HandOff& h) {
+template <typename WT, int MT, int RB, int U>
+__global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = (bid * 4 + wave) * RB;
+    const int n0 = (blockIdx.x * 4 + wave) * RB;
     const bool active = n0 < a.N;
     const WT* W = reinterpret_cast<const WT*>(a.W);
     const int chunks = a.K >> 3;
     constexpr int XR = 2;
-    const bool fast = HM == HM_POLL || a.K <= XR * 4 * 256;
+    const bool fast = a.K <= XR * 4 * 256;
     XRegs<MT, XR> xr;
-    if (HM != HM_POLL && fast) xload<MT, XR>(xr, a.x, a.ldx, nullptr, a.M, a.K, a.norm_w);
+    if (fast) xload<MT, XR>(xr, a.x, a.ldx, nullptr, a.M, a.K, a.norm_w);
     uint4 wq[U][RB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -208,35 +193,10 @@ __device__ __forceinline__ void dec_gemv_body(const DecGemvArgs& a, const int bi
             wq[u][r] = ldg_nt16(W + (long)n * a.ldw + (min(c, chunks - 1) << 3));
         }
     }
-    if constexpr (HM == HM_POLL) {
-        static_assert(MT == 1, "the polled row is one token");
-        // xload's addresses and norm-weight registers, the row words from the hand-off row
-        const int tid = threadIdx.x;
-        const float* nwp = a.norm_w ? a.norm_w : a.x;
-#pragma unroll
-        for (int i = 0; i < XR; ++i) xr.w[i] = *reinterpret_cast<const float4*>(nwp + min((tid + i * 256) * 4, a.K - 4));
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(h.hand, (short)0, a.K * 4, 0x00020000);
-        for (unsigned it = 0;; ++it) {
-            asm volatile("" ::: "memory");  // the row changes under us: re-load it every pass
-            bool pend = false;
-#pragma unroll
-            for (int i = 0; i < XR; ++i) {
-                const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, min((tid + i * 256) * 4, a.K - 4) * 4, 0, 16);
-                pend = pend || b[0] == HAND_SENT || b[1] == HAND_SENT || b[2] == HAND_SENT || b[3] == HAND_SENT;
-                __builtin_memcpy(&xr.v[0][i], &b, 16);
-            }
-            if (!__syncthreads_or(pend)) break;
-            if (it > (1u << 20)) {
-                if (tid == 0) __hip_atomic_store(h.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
     if (fast) xstage<MT, XR>(xr, a.M, a.K, a.norm_w != nullptr, a.eps, smem);
     else stage_rows(a.x, a.ldx, nullptr, a.M, a.K, a.norm_w, a.eps, smem);
     const float* xs = smem + XS_RED;
-    if (a.xn_out && bid == 0)  // hand the normalised rows to the next kernel
+    if (a.xn_out && blockIdx.x == 0)  // hand the normalised rows to the next kernel
         for (int i = threadIdx.x * 4; i < a.M * a.K; i += blockDim.x * 4)
             *reinterpret_cast<float4*>(a.xn_out + i) = *reinterpret_cast<const float4*>(xs + i);
     if (!active) return;
@@ -289,32 +249,8 @@ __device__ __forceinline__ void dec_gemv_body(const DecGemvArgs& a, const int bi
                 float* yp = a.y + (long)m * a.ldy + n;
                 if (a.accumulate) v = *yp + v;
                 *yp = v;
-                if constexpr (HM == HM_PRODUCE) {
-                    const auto rs = __builtin_amdgcn_make_buffer_rsrc(h.hand, (short)0, a.N * 4, 0x00020000);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, n * 4, 0, 16);
-                    if (h.hand_prev) {
-                        const auto rp = __builtin_amdgcn_make_buffer_rsrc(h.hand_prev, (short)0, a.N * 4, 0x00020000);
-                        __builtin_amdgcn_raw_buffer_store_b32(HAND_SENT, rp, n * 4, 0, 16);
-                    }
-                }
             }
         }
-}
-
-template <typename WT, int MT, int RB, int U>
-__global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
-    dec_gemv_body<WT, MT, RB, U>(a, blockIdx.x, HandOff());
-}
-
-// One page, MoE layer: o_proj + residual and the router in ONE launch.  Blocks [0, nr) are the router's
-// (dec_gemv<WT, 1, 1, 3> with the post-attention RMSNorm fused; block 0 hands x^ to the gate/up waves):
-// they issue their router rows and norm weights at launch start and poll the residual row x + W_o ctx
-// that the o_proj blocks [nr, nr + N/4) store write-through into the layer's hand-off row as they finish.
-// Removes the router's launch and its kernel boundary; the results are the two-launch form's, bit for bit.
-template <typename WT>
-__global__ __launch_bounds__(256) void dec_oproj_route_kernel(DecGemvArgs go, DecGemvArgs gr, HandOff h, int nr) {
-    if ((int)blockIdx.x < nr) dec_gemv_body<WT, 1, 1, 3, HM_POLL>(gr, blockIdx.x, h);
-    else dec_gemv_body<WT, 1, 1, 3, HM_PRODUCE>(go, (int)blockIdx.x - nr, h);
 }
 
 // Several tokens (M = 3..8): blocks of 4 waves, RB weight rows per wave (issued first), the M
@@ -569,55 +505,6 @@ void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s) {
         if (a.wdtype == WDT_BF16) dec_gemv_dispatch<bf16_t>(p, s);
         else dec_gemv_dispatch<f16_t>(p, s);
     }
-}
-
-namespace {
-template <typename K>
-int occupancy_blocks(K kernel, size_t lds) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess) return 0;
-    return per_cu;
-}
-int hip_device_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-    }
-    return cus;
-}
-}  // namespace
-
-bool dec_oproj_route_ok(const DecGemvArgs& go, const DecGemvArgs& gr) {
-    if (!(go.M == 1 && gr.M == 1 && go.wdtype == gr.wdtype && gr.K == go.N && gr.norm_w && !gr.accumulate &&
-          go.K % 8 == 0 && gr.K % 8 == 0 && go.K >= 8 && gr.K >= 8 && go.K <= 64 * 3 * 8 && gr.K <= 64 * 3 * 8 &&
-          go.N <= 16384 && gr.N <= 16384))
-        return false;
-    // the router blocks poll: they must never hold every slot the launch can have (poll_wait_fits)
-    static int bf = -1, f16 = -1;
-    int& v = go.wdtype == WDT_BF16 ? bf : f16;
-    const size_t lds = stage_bytes(1, std::max(go.K, gr.K));
-    if (v < 0)
-        v = go.wdtype == WDT_BF16 ? occupancy_blocks(dec_oproj_route_kernel<bf16_t>, lds)
-                                  : occupancy_blocks(dec_oproj_route_kernel<f16_t>, lds);
-    return poll_wait_fits((gr.N + 3) / 4, v, hip_device_cus());
-}
-
-void launch_dec_oproj_route(const DecGemvArgs& go, const DecGemvArgs& gr, float* hand, float* hand_prev, int* err,
-                            hipStream_t s) {
-    if (!hand || !err || !dec_oproj_route_ok(go, gr)) throw std::runtime_error("EINVAL: dec_oproj_route outside its range");
-    HandOff h;
-    h.hand = hand; h.hand_prev = hand_prev; h.err = err;
-    const int nr = (gr.N + 3) / 4, no = (go.N + 3) / 4;
-    const size_t lds = stage_bytes(1, std::max(go.K, gr.K));
-    if (go.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_oproj_route_kernel<bf16_t>), dim3(nr + no), dim3(256), lds, s, go, gr, h, nr);
-    else DSOCR_LAUNCH((dec_oproj_route_kernel<f16_t>), dim3(nr + no), dim3(256), lds, s, go, gr, h, nr);
-}
-
-void dec_hand_init(float* hand, size_t floats, hipStream_t s) {
-    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(hand), (int)HAND_SENT, floats, s) != hipSuccess)
-        throw std::runtime_error("EINTERNAL: hipMemsetD32Async (o_proj -> router hand-off rows)");
 }
 
 // ------------------------------------------------------------------ q/k/v projection + RoPE
@@ -1159,12 +1046,12 @@ void launch_dec_router(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_t s
 // (block.rs:776-789) and uses them directly.  Each block issues its K and V cache loads first, then
 // builds q; the chunk partials of a (page, head) are merged by chunk 0's block polling them (POLL, <= 24
 // chunks of 128-dim heads) or by the last arriver of a ticket (flash-decoding combine).
-// phase clock (DecAttn2Args::stamps): one lane per block, 64-bit device-scope min / max
-__device__ __forceinline__ void da_stamp(unsigned long long* st, int slot, bool is_min = false) {
+// phase clock (DecAttn2Args::stamps): thread 0 of each block stores s_memrealtime into the block's own
+// 8-word record (no atomics: 680 blocks on one word serialised the launch)
+__device__ __forceinline__ void da_stamp(unsigned long long* st, int slot) {
     if (!st || threadIdx.x != 0) return;
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    if (is_min) __hip_atomic_fetch_min(st + slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __hip_atomic_fetch_max(st + slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long blk = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+    st[blk * 8 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 constexpr int DA_CH = 64;       // keys per block
@@ -1566,8 +1453,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
 template <int HD, bool PREROT, bool POLL>
 __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     WaveSpan span_(a.span);
-    da_stamp(a.stamps, 0, true);
-    da_stamp(a.stamps, 8);
+    da_stamp(a.stamps, 0);
     dec_attn_body<HD, PREROT, POLL, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
@@ -1578,15 +1464,12 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
 template <typename WT>
 __global__ __launch_bounds__(256) void dec_qkv_attn_kernel(DecGemvArgs g, DecRopeEpi r, DecAttn2Args a, int nq) {
     WaveSpan span_(a.span);
-    da_stamp(a.stamps, 0, true);
+    da_stamp(a.stamps, 0);
     if ((int)blockIdx.x < nq) {
-        da_stamp(a.stamps, 7);
         qkv_rope_body<WT, true>(g, r, blockIdx.x);
         da_stamp(a.stamps, 1);
         return;
     }
-    da_stamp(a.stamps, 6, true);
-    da_stamp(a.stamps, 8);
     const int chunks = (a.max_len + DA_CH - 1) / DA_CH;
     const int i = (int)blockIdx.x - nq;
     dec_attn_body<128, true, true, true>(a, i % chunks, i / chunks, 0);
@@ -2979,13 +2862,6 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     return p;
 }
 }  // namespace
-
-bool moe_router_args(const MoeDecodeArgs& a, DecGemvArgs* gr) {
-    const MoePlan p = moe_plan(a);
-    if (p.mode != 0) return false;  // the one-page mix plan: router = dec_gemv(p.router)
-    *gr = p.router;
-    return true;
-}
 
 void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down) {
     const MoePlan p = moe_plan(a);

@@ -323,23 +323,12 @@ __device__ __forceinline__ bf16x8_v fx_pack(const float* v) {
 // the k-step); f16 weights keep 2 x 2 of 64 x 64 (their W split would double instead).
 // NST = 1: one LDS stage (24 KB: four blocks per CU at <= 128 VGPRs), the latency of a block's stage
 // loads hidden by the other blocks of its CU instead of by a second stage
-// KT: k per stage, 32 or 64 (64: 256-B A rows, one per LDS bank row, chunk ^ (r & 15); 128-B W rows,
-// chunk ^ ((r >> 1) & 7) — every ds_read_b128 lane group on 16 distinct slots as at 32)
-template <int KT>
-__device__ __forceinline__ int fx_asw(int r) { return KT == 32 ? ((r >> 1) & 7) : (r & 15); }
-template <int KT>
-__device__ __forceinline__ int fx_wsw(int r) { return KT == 32 ? ((r >> 2) & 3) : ((r >> 1) & 7); }
-
-template <bool F16W, bool W22 = F16W, int NST = 2, int BN = FX_N, int KT = FX_K>  // (BN 256 measured slower on every vision shape)
+template <bool F16W, bool W22 = F16W, int NST = 2, int BN = FX_N>  // (BN 256 measured slower on every vision shape)
 __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
     constexpr int WN = W22 ? 2 : 1, WM = 4 / WN;     // waves along N / M
     constexpr int TI = FX_M / WM / 32, TJ = BN / WN / 32;
-    static_assert(KT == 32 || KT == 64, "k per stage");
-    constexpr int AS = FX_M * KT;  // f32 elements of an A stage
-    constexpr int WS = BN * KT;    // bf16 elements of a W stage
-    constexpr int ACH = KT / 4, WCH = KT / 8;  // 16-byte chunks per A / W row
-    constexpr int AR = 64 / ACH, WR = 64 / WCH;  // rows per LDS-DMA instruction
-    __shared__ __attribute__((aligned(16))) float a_lds[NST * AS];
+    constexpr int WS = BN * FX_K;  // bf16 elements of a W stage
+    __shared__ __attribute__((aligned(16))) float a_lds[NST * FX_AS];
     __shared__ __attribute__((aligned(16))) uint16_t w_lds[NST * WS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
@@ -360,34 +349,34 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
         for (int j = 0; j < TJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int nk_all = g.K / KT;
+    const int nk_all = g.K / FX_K;
     const int kbeg = (int)((long)nk_all * split / g.splits), kend = (int)((long)nk_all * (split + 1) / g.splits);
     const int nk = kend - kbeg;
-    // A: 128 rows x KT f32 (ACH chunks of 16 B per row); instruction i of wave w fills rows (w (32/AR) + i) AR ..
-    // W: BN rows x KT bf16 (WCH chunks per row);        instruction i of wave w fills rows (w (BN/4/WR) + i) WR ..
-    // (LDS-DMA writes lane-linearly: lane L's 16 B land in row R + L / ACH (W: L / WCH), slot L % ACH (L % WCH),
+    // A: 128 rows x 32 f32 (8 chunks of 16 B per row); instruction i of wave w fills rows (4w + i) * 8 .. + 7
+    // W: 128 rows x 32 bf16 (4 chunks per row);     instruction i of wave w fills rows (2w + i) * 16 .. + 15
+    // (LDS-DMA writes lane-linearly: lane L's 16 B land in row R + L / 8 (W: L / 4), slot L % 8 (L % 4),
     // so the lane fetches the global chunk that the swizzle puts in that slot)
     auto issue = [&](int kt) {
-        const int k0 = (kbeg + kt) * KT;
-        float* as = a_lds + (NST == 1 ? 0 : (kt & 1) * AS);
+        const int k0 = (kbeg + kt) * FX_K;
+        float* as = a_lds + (NST == 1 ? 0 : (kt & 1) * FX_AS);
         uint16_t* ws_ = w_lds + (NST == 1 ? 0 : (kt & 1) * WS);
 #pragma unroll
-        for (int i = 0; i < 32 / AR; ++i) {
-            const int R = (wave * (32 / AR) + i) * AR;
-            const int r = R + lane / ACH;
-            const int j = (lane % ACH) ^ fx_asw<KT>(r);
+        for (int i = 0; i < 4; ++i) {
+            const int R = (wave * 4 + i) * 8;
+            const int r = R + (lane >> 3);
+            const int j = (lane & 7) ^ ((r >> 1) & 7);
             const long row = min(m0 + r, g.M - 1);
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(A + row * g.lda + k0 + j * 4),
-                                             (lds_void*)(as + R * KT), 16, 0, 0);
+                                             (lds_void*)(as + R * FX_K), 16, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < BN / 4 / WR; ++i) {
-            const int R = (wave * (BN / 4 / WR) + i) * WR;
-            const int r = R + lane / WCH;
-            const int j = (lane % WCH) ^ fx_wsw<KT>(r);
+        for (int i = 0; i < BN / 64; ++i) {
+            const int R = (wave * (BN / 64) + i) * 16;
+            const int r = R + (lane >> 2);
+            const int j = (lane & 3) ^ ((r >> 2) & 3);
             const long row = min(n0 + r, g.N - 1);
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(W + row * g.ldw + k0 + j * 8),
-                                             (lds_void*)(ws_ + R * KT), 16, 0, 0);
+                                             (lds_void*)(ws_ + R * FX_K), 16, 0, 0);
         }
     };
     if (NST == 2 && nk > 0) issue(0);
@@ -397,17 +386,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
         __builtin_amdgcn_s_barrier();  // every wave's stage kt landed; every wave is done with stage kt - 1
         asm volatile("" ::: "memory");
         if (NST == 2 && kt + 1 < nk) issue(kt + 1);  // into stage (kt - 1) & 1
-        const float* As = a_lds + (NST == 1 ? 0 : (kt & 1) * AS);
+        const float* As = a_lds + (NST == 1 ? 0 : (kt & 1) * FX_AS);
         const uint16_t* Ws = w_lds + (NST == 1 ? 0 : (kt & 1) * WS);
 #pragma unroll
-        for (int ks = 0; ks < KT / 16; ++ks) {
-            const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of KT / 8)
+        for (int ks = 0; ks < FX_K / 16; ++ks) {
+            const int kc = ks * 2 + (lane >> 5);  // this lane's 8-value k chunk (of 4)
             bf16x8_v bfv[TJ], blo[TJ];
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
                 const int r = wn * (BN / WN) + j * 32 + (lane & 31);
                 if constexpr (F16W) {
-                    const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * KT + ((kc ^ fx_wsw<KT>(r)) * 8));
+                    const uint4 raw = *reinterpret_cast<const uint4*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
                     float wv[8], wh[8], wl[8];
                     unpack8<f16_t>(raw, wv);
 #pragma unroll
@@ -418,15 +407,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32a_nt_kernel(GemmBf16Args g) {
                     bfv[j] = fx_pack(wh);
                     blo[j] = fx_pack(wl);
                 } else {
-                    bfv[j] = *reinterpret_cast<const bf16x8_v*>(Ws + r * KT + ((kc ^ fx_wsw<KT>(r)) * 8));
+                    bfv[j] = *reinterpret_cast<const bf16x8_v*>(Ws + r * FX_K + ((kc ^ ((r >> 2) & 3)) * 8));
                 }
             }
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
                 const int r = wm * (FX_M / WM) + i * 32 + (lane & 31);
-                const int sw = fx_asw<KT>(r);
-                const float4 lo4 = *reinterpret_cast<const float4*>(As + r * KT + (((2 * kc) ^ sw) * 4));
-                const float4 hi4 = *reinterpret_cast<const float4*>(As + r * KT + (((2 * kc + 1) ^ sw) * 4));
+                const int sw = (r >> 1) & 7;
+                const float4 lo4 = *reinterpret_cast<const float4*>(As + r * FX_K + (((2 * kc) ^ sw) * 4));
+                const float4 hi4 = *reinterpret_cast<const float4*>(As + r * FX_K + (((2 * kc + 1) ^ sw) * 4));
                 const float av[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
                 float h[8], m[8], l[8];
 #pragma unroll
@@ -519,12 +508,6 @@ static int gemm_nst_env() {
     return v;
 }
 
-// DSOCR_GEMM_KT=64 (A/B switch, read at every launch): the bf16-weight linears with 64 k per LDS stage
-static int gemm_kt_env() {
-    const char* e = getenv("DSOCR_GEMM_KT");
-    return e ? atoi(e) : 32;
-}
-
 void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     GemmBf16Args g = g0;
     if (!g.variant) g.variant = gemm_nst_env();
@@ -536,12 +519,8 @@ void launch_gemm_f32a(const GemmBf16Args& g0, hipStream_t s) {
     // bf16 weights: 4 x 1 waves of 32 x 128 (each A row split once), ONE LDS stage (24 KB, four blocks per
     // CU: kbench vgemm 1.00-1.18x the two-stage kernel on the SAM linears, within 3 % elsewhere); f16
     // weights: 2 x 2 (their W split would double under 4 x 1), two stages
-    const bool kt64 = gemm_kt_env() == 64 && g.K % FX_K == 0 && (g.K / FX_K) % (2 * g.splits) == 0;  // same K slices as at 32
-    if (g.w_f16 && kt64) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true, true, 1, FX_N, 64>), dim3(tiles * g.splits), dim3(256), 0, s, g);
-    else if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+    if (g.w_f16) hipLaunchKernelGGL((gemm_f32a_nt_kernel<true>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else if (g.variant == 2) hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 2>), dim3(tiles * g.splits), dim3(256), 0, s, g);
-    else if (kt64)
-        hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 1, FX_N, 64>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((gemm_f32a_nt_kernel<false, false, 1>), dim3(tiles * g.splits), dim3(256), 0, s, g);
     if (g.splits > 1) launch_splitk_reduce(g, s);
 }

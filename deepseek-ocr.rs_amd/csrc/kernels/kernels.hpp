@@ -248,11 +248,9 @@ struct DecAttn2Args {
     int* err = nullptr;                                 // polled merge: give-up flag (set instead of hanging)
     unsigned long long* span = nullptr;                 // launch-span slots (SPAN_SLOTS pairs) or null
     int prerot = 0;                                     // q / k rows already rotated (dec_qkv_rope)
-    // phase clocks (tools/kbench qkvattn1 / attn8; null in the engine): [0] first block entry (min),
-    // [1] last projection store (fused), [2] last q poll done (fused) / last softmax done (standalone),
-    // [3] last chunk record stored, [4] last merge poll done, [5] last block exit, [6] first attention
-    // block entry (fused, min), [7] last projection block entry (fused), [8] last attention block entry
-    // (s_memrealtime, 100 MHz)
+    // phase clocks (tools/kbench qkvattn1 / attn8; null in the engine): per block (linear index) 8 words,
+    // s_memrealtime (100 MHz) at [0] entry, [1] projection rows stored (fused), [2] q polled (fused) /
+    // softmax done (standalone), [3] chunk record stored, [4] merge poll done, [5] exit
     unsigned long long* stamps = nullptr;
 };
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
@@ -280,15 +278,6 @@ bool poll_wait_fits(long waiting_blocks, int api_blocks_per_cu, int cus);
 bool dec_attn_polled(const DecAttn2Args& a);
 void launch_dec_qkv_attn(const DecGemvArgs& g, const DecRopeEpi& r, const DecAttn2Args& a, hipStream_t s);
 void dec_qkv_sentinel_init(float* qkv, size_t floats, hipStream_t s);
-// One page, MoE layer: o_proj + residual (go: accumulate into the residual row) and the router GEMV (gr:
-// RMSNorm fused, xn_out for the gate/up waves) in one launch; the router blocks poll the residual row the
-// o_proj blocks store write-through into `hand` (sentinel-filled on entry); the launch refills `hand_prev`
-// (the previous MoE layer's row, whose readers finished in an earlier launch).  Outputs equal the
-// two-launch form bit for bit.  dec_oproj_route_ok includes the residency rule.
-bool dec_oproj_route_ok(const DecGemvArgs& go, const DecGemvArgs& gr);
-void launch_dec_oproj_route(const DecGemvArgs& go, const DecGemvArgs& gr, float* hand, float* hand_prev, int* err,
-                            hipStream_t s);
-void dec_hand_init(float* hand, size_t floats, hipStream_t s);
 size_t dec_attn_workspace(int B, int heads, int hd, int max_len);
 // the record buffer enters every dec_attn launch sentinel-filled (the polling merge refills what it reads)
 void dec_attn_part_init(float* part, size_t bytes, hipStream_t s);
@@ -394,8 +383,6 @@ struct MoeDecodeArgs {
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments
 void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down);
-// the router launch arguments of launch_moe_decode's one-page plan (false: the plan has no separate router GEMV)
-bool moe_router_args(const MoeDecodeArgs& a, DecGemvArgs* gr);
 void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts = MOE_ALL);
 // Greedy selection (ngram ban evaluated in-kernel) + step bookkeeping + KV advance.
 struct DecSampleArgs {

@@ -87,7 +87,6 @@ EXPORTS = [
     "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
     "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16", "dsocr_k_gemv_splitk",
     "dsocr_engine_set_spans", "dsocr_engine_spans", "dsocr_k_qkv_attention", "dsocr_k_poll_wait_fits",
-    "dsocr_k_oproj_route",
 ]
 
 _lib = None
@@ -156,7 +155,6 @@ def lib():
     L.dsocr_k_qkv_attention.argtypes = [i32, i32, i32, i32, i32, i32, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp,
                                         vp, C.POINTER(i32)]
     L.dsocr_k_poll_wait_fits.argtypes = [C.c_long, i32, i32]
-    L.dsocr_k_oproj_route.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, f32, vp, vp, vp, vp, C.POINTER(i32)]
     L.dsocr_k_moe.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, i32, i32, f32, vp, vp, vp]
     L.dsocr_k_sample_greedy.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, vp]
     L.dsocr_k_sample_stoch.argtypes = [i32, i32, vp, vp, i32, vp, i32, f32, C.c_double, C.c_size_t, C.c_double,

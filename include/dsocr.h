@@ -298,16 +298,6 @@ dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int h
                                    float eps, const float* x, const float* norm_w, const void* Wqkv, int wdtype,
                                    const float* cos, const float* sin, float* kc, float* vc, const int* kv_pos,
                                    float* qkv_row, float* o, int* used_fused);
-/* One page, MoE layer: o_proj + residual (x += Wo ctx) and the router GEMV (logits = Wr rmsnorm(x), xn = the
- * normalised row) for `steps` launches back to back, as ONE launch per step (fused = 1 and the residency
- * rule admits it: dec_oproj_route, the router blocks poll the residual row the o_proj blocks hand over) or as
- * the two dec_gemv launches (fused = 0).  Step s hands over through row s % 2 of a two-row buffer and refills
- * the other (two layers' rows, as in the decode step); hand_out (2*H floats, optional) receives both rows
- * after the last step.  ctx [steps][Kc], logits [steps][E], xn [steps][H]; x [H] is updated in place.
- * Device pointers; Wo [H][Kc], Wr [E][H] of wdtype (1 f16, 0 bf16).  *used_fused reports which form ran. */
-dsocr_status dsocr_k_oproj_route(int fused, int steps, int H, int Kc, int E, const float* ctx, const void* Wo,
-                                 const void* Wr, int wdtype, const float* norm_w, float eps, float* x, float* logits,
-                                 float* xn, float* hand_out, int* used_fused);
 /* Residency rule of the polled in-launch hand-offs (pure host decision, no device call): 1 when
  * waiting_blocks (blocks that may spin on blocks of the same grid) < usable slots = (min(api, 8), one fewer
  * where the occupancy API may over-admit) x cus; else 0 (the engine then launches the non-polling form). */

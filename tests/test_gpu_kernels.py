@@ -78,33 +78,6 @@ def test_gemm_f32a(gpu, M, N, K, wdt, act, acc, splits):
     assert np.all(np.abs(got - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got - ref))
 
 
-@pytest.mark.parametrize("M,N,K,act,acc,splits,wdt", [(4096, 2304, 768, 0, 0, 0, 0), (257, 3072, 1024, 1, 0, 0, 0),
-                                                      (404, 1024, 4096, 0, 1, 0, 0), (300, 512, 1152, 3, 1, 9, 0),
-                                                      (77, 130, 192, 0, 0, 1, 0), (706, 3840, 1280, 0, 0, 0, 1),
-                                                      (706, 1280, 1280, 0, 1, 0, 1)])
-def test_gemm_f32a_k64(gpu, monkeypatch, M, N, K, act, acc, splits, wdt):
-    """The vision (bf16) and prefill (f16) linears' kernel with 64 k per LDS stage (DSOCR_GEMM_KT=64: 256-B A rows
-    swizzled chunk ^ (r & 15), 128-B W rows chunk ^ ((r >> 1) & 7)) vs f64 and bitwise vs the 32-k form (same
-    products, same order)."""
-    rng = np.random.default_rng(M + N + K)
-    a = rng.standard_normal((M, K)).astype(np.float32)
-    bits, w = _weights(rng, N, K, wdt)
-    bias = rng.standard_normal(N).astype(np.float32) * 0.1
-    c0 = rng.standard_normal((M, N)).astype(np.float32) if acc else np.zeros((M, N), np.float32)
-    dA, dW, dB = Dev(a), Dev(bits), Dev(bias)
-    got = {}
-    for kt in ("64", "32"):
-        monkeypatch.setenv("DSOCR_GEMM_KT", kt)
-        dC = Dev(c0)
-        check(lib().dsocr_k_gemm_f32a(M, N, K, dA.ptr, dW.ptr, wdt, dB.ptr, dC.ptr, act, acc, splits))
-        got[kt] = dC.get()
-    ref = ACTS[act]((a.astype(np.float64) @ w.T.astype(np.float64)).astype(np.float32) + bias) + (c0 if acc else 0)
-    bound = _bound(a, w) * (2.0 if act else 1.0)
-    assert np.all(np.abs(got["64"] - ref) <= bound + 1e-5 * np.abs(ref)), np.max(np.abs(got["64"] - ref))
-    # the k order of the accumulation is the same in both forms (16-k MFMA steps in increasing k)
-    assert np.array_equal(got["64"], got["32"])
-
-
 @pytest.mark.parametrize("T,E,topk,N,K,wdt,act,acc,kernel", [
     (300, 64, 6, 1792, 1280, 1, 0, 0, 1),   # one page's routed gate/up (~28 rows per expert)
     (300, 64, 6, 1280, 896, 1, 0, 1, 1),    # ... down, accumulate epilogue
@@ -383,45 +356,6 @@ def test_qkv_attention_fused_back_to_back(gpu, max_len, p0):
         for h in range(heads):
             ref = _attn_ref(q[h][None], K[h, :p + 1], V[h, :p + 1], scale)[0]
             assert np.max(np.abs(o1[s, h * hd:(h + 1) * hd] - ref)) < 1e-4, (s, h)
-
-
-@pytest.mark.parametrize("wdt", [1, 0])
-def test_oproj_route_fused_back_to_back(gpu, wdt):
-    """One page's o_proj + residual and MoE router GEMV as ONE launch (dec_oproj_route: the router blocks poll
-    the residual row the o_proj blocks store write-through into a sentinel-filled hand-off row) for five
-    launches back to back through two alternating rows (each launch refills the other one, as consecutive MoE
-    layers do), against the two dec_gemv launches on the same inputs: the residual row, the logits and the
-    normalised row handed to the gate/up waves equal bit for bit; the last row holds the final residual and
-    the other only sentinels.  Also against f64 math (block.rs:1215-1240: x + W_o ctx, RMSNorm, router logits)."""
-    H, Kc, E, steps, eps = 1280, 1280, 64, 5, 1e-6
-    rng = np.random.default_rng(11 + wdt)
-    ctx = rng.standard_normal((steps, Kc)).astype(np.float32)
-    x0 = rng.standard_normal(H).astype(np.float32)
-    nw = (1.0 + 0.1 * rng.standard_normal(H)).astype(np.float32)
-    bo, wo = _weights(rng, H, Kc, wdt)
-    br, wr = _weights(rng, E, H, wdt)
-    dctx, dWo, dWr, dn = Dev(ctx), Dev(bo), Dev(br), Dev(nw)
-    outs = {}
-    for fused in (1, 0):
-        dx, dl, dxn, dh = Dev(x0), Dev.zeros((steps, E)), Dev.zeros((steps, H)), Dev.zeros((2, H))
-        used = C.c_int(-1)
-        check(lib().dsocr_k_oproj_route(fused, steps, H, Kc, E, dctx.ptr, dWo.ptr, dWr.ptr, wdt, dn.ptr, eps, dx.ptr,
-                                        dl.ptr, dxn.ptr, dh.ptr, C.byref(used)))
-        assert used.value == fused, "the residency rule refused the fused launch"
-        outs[fused] = (dx.get(), dl.get(), dxn.get(), dh.get())
-    (x1, l1, n1, h1), (x0b, l0, n0, _) = outs[1], outs[0]
-    assert np.array_equal(x1, x0b) and np.array_equal(l1, l0) and np.array_equal(n1, n0)
-    last = (steps - 1) % 2
-    assert np.array_equal(h1[last], x1), "the last hand-off row is not the final residual row"
-    assert np.all(h1[1 - last].view(np.uint32) == SENT), "the other hand-off row was not refilled"
-    x = x0.astype(np.float64)
-    for s in range(steps):
-        x = x + wo.astype(np.float64) @ ctx[s].astype(np.float64)
-        xn = x / np.sqrt(np.mean(x * x) + eps) * nw
-        assert np.max(np.abs(n1[s] - xn)) < 1e-4 * (1 + np.max(np.abs(xn)))
-        lg = wr.astype(np.float64) @ xn
-        assert np.max(np.abs(l1[s] - lg)) < 1e-4 * (1 + np.max(np.abs(lg)))
-    assert np.max(np.abs(x1 - x)) < 1e-4 * (1 + np.max(np.abs(x)))
 
 
 @pytest.mark.parametrize("T,H,E,topk,I,ns,norm", [(3, 256, 16, 6, 64, 2, False), (1, 256, 16, 6, 64, 2, True),

@@ -235,23 +235,6 @@ def test_full_screened_selection_equals_exact(full_engine, monkeypatch):
     assert screened == exact, (screened, exact)
 
 
-def test_full_oproj_route_fused_equals_two_launches(full_engine, monkeypatch):
-    """One page: the o_proj + router launch (dec_oproj_route, the default for MoE layers at one page) decodes
-    exactly what the two-launch form (DSOCR_OPROJ_ROUTE=0) does: ids and the raw logits of every step equal
-    bit for bit over 40 steps of a full-size page (the hand-off rows cycle through every MoE layer)."""
-    tok = SyntheticTokenizer(129280)
-    page = Page(synthetic_page(3), VisionSettings())
-    ids, mask = build_prompt_tokens(tok, "<image>\n<|grounding|>Convert the document to markdown.", [page.n_image_tokens])
-    p = DecodeParameters(max_new_tokens=40)
-    got = {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("DSOCR_OPROJ_ROUTE", v)
-        got[v] = full_engine.generate_trace([(ids, mask, page, None)], p, ignore_eos=True)
-    (o1, l1), (o0, l0) = got["1"], got["0"]
-    assert o1 == o0, (o1, o0)
-    assert np.array_equal(np.asarray(l1), np.asarray(l0))
-
-
 def test_full_spans_do_not_change_ids(full_engine):
     """In-context launch spans (dsocr_engine_set_spans: 1 = wave spans stamped by every gate/up, down and
     attention wave, 2 = HIP events around those launches inside the replayed step graph; the MoE is then

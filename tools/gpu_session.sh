@@ -41,7 +41,7 @@ for step in "$@"; do
     gprof8_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8_nopc.log 2>&1 ;;
     # the round-2 crash reproduced with the maps dump (expected SIGSEGV: run it last)
     gprof_maps) DSOCR_SEGV_MAPS=1 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_maps.log 2>&1 ;;
-    k_r4) run 400 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -k "oproj_route or qkv_attention or test_attention or lmhead or k64" -rf -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/k_r4.log 2>&1 ;;
+    k_r4) run 400 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -k "qkv_attention or test_attention or lmhead or screened" -rf -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/k_r4.log 2>&1 ;;
     m_r4) run 600 python -u -m pytest tests/test_gpu_model.py -q -m gpu -k "oproj_route or full_screened" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/m_r4.log 2>&1 ;;
     dsq_r4) run 900 python -u -m pytest tests/test_dsq.py -q -m gpu -k "full_q4k" -rf -p no:cacheprovider --timeout 600 --timeout-method thread > gpurun_out/dsq_r4.log 2>&1 ;;
     kb_qa) run 180 ./tools/kbench qkvattn1 > gpurun_out/kb_qkvattn.log 2>&1 ;;

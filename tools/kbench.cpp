@@ -250,6 +250,30 @@ static void case_gemv(int M, hipStream_t s) {
     for (int i = 0; i < NB; ++i) { (void)hipFree(wq[i]); (void)hipFree(wo[i]); }
 }
 
+// per-block phase records (DecAttn2Args::stamps): block range [p0, p1) = projection blocks, [a0, a1) = attention
+// blocks; times in us from the first block entry: entry (first / last), and per phase the time by which every
+// block that reached it had (max) and the median
+static void print_stamps(const char* what, const std::vector<unsigned long long>& h, int p0, int p1, int a0, int a1) {
+    unsigned long long t0 = ~0ull;
+    for (size_t b = 0; b * 8 < h.size(); ++b) if (h[b * 8] && h[b * 8] < t0) t0 = h[b * 8];
+    auto us = [&](unsigned long long t) { return ((long long)t - (long long)t0) / 100.0; };
+    auto stat = [&](int lo, int hi, int slot, const char* nm) {
+        std::vector<double> v;
+        for (int b = lo; b < hi; ++b) if (h[(size_t)b * 8 + slot]) v.push_back(us(h[(size_t)b * 8 + slot]));
+        if (v.empty()) return;
+        std::sort(v.begin(), v.end());
+        printf(" %s %.2f/%.2f/%.2f |", nm, v.front(), v[v.size() / 2], v.back());
+    };
+    printf("%s stamps us (min/median/max):", what);
+    if (p1 > p0) { stat(p0, p1, 0, "proj entry"); stat(p0, p1, 1, "proj stored"); }
+    stat(a0, a1, 0, "attn entry");
+    stat(a0, a1, 2, p1 > p0 ? "q polled" : "softmax");
+    stat(a0, a1, 3, "record");
+    stat(a0, a1, 4, "merge polled");
+    stat(a0, a1, 5, "exit");
+    printf("\n");
+}
+
 static void case_attn(int B, int pos, hipStream_t s) {
     const int max_len = 1218;
     constexpr int NLA = 12;
@@ -275,21 +299,17 @@ static void case_attn(int B, int pos, hipStream_t s) {
     snprintf(nm, sizeof nm, "attn B=%d L=%d", B, pos + 1);
     const double bytes = 2.0 * B * (pos + 1) * HEADS * HD * 4;
     report(nm, timeit(4 * NLA, [&](int i) { a.kc = kc[i % NLA]; a.vc = vc[i % NLA]; launch_dec_attn(a, s); }, s), bytes);
-    auto* st = (unsigned long long*)dalloc(16 * 8);
+    const int chunks = (max_len + 63) / 64, nb = chunks * HEADS * B;
+    auto* st = (unsigned long long*)dalloc((size_t)nb * 64);
     for (int it = 0; it < 2; ++it) {
-        std::vector<unsigned long long> init(16, 0);
-        init[0] = ~0ull;
-        CK(hipMemcpy(st, init.data(), 16 * 8, hipMemcpyHostToDevice));
+        CK(hipMemset(st, 0, (size_t)nb * 64));
         a.kc = kc[it + 1]; a.vc = vc[it + 1]; a.stamps = st;
         launch_dec_attn(a, s);
         a.stamps = nullptr;
         CK(hipStreamSynchronize(s));
-        unsigned long long h[16];
-        CK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
-        printf("attn stamps (us from first entry): last entry %.2f | last softmax %.2f | last record %.2f | last merge poll %.2f | last exit %.2f\n",
-               ((long long)h[8] - (long long)h[0]) / 100.0, ((long long)h[2] - (long long)h[0]) / 100.0,
-               ((long long)h[3] - (long long)h[0]) / 100.0, ((long long)h[4] - (long long)h[0]) / 100.0,
-               ((long long)h[5] - (long long)h[0]) / 100.0);
+        std::vector<unsigned long long> h((size_t)nb * 8);
+        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+        print_stamps("attn", h, 0, 0, 0, nb);
     }
     for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); }
 }
@@ -335,23 +355,18 @@ static void case_qkvattn1(int pos, hipStream_t s) {
     snprintf(nm, sizeof nm, "qkv+attn B=1 L=%d", pos + 1);
     const double bytes = 3.0 * H * H * 2 + 2.0 * (pos + 1) * HEADS * HD * 4;
     report(nm, timeit(4 * NLA, [&](int i) { set(i); launch_dec_qkv_attn(g, re, a, s); }, s), bytes);
-    auto* st = (unsigned long long*)dalloc(16 * 8);
-    const char* names[9] = {"entry", "proj stored", "q polled", "record stored", "merge polled", "merge exit",
-                            "attn entry(min)", "proj entry(max)", "attn entry(max)"};
+    const int nq = (3 * H / 2 + 3) / 4, nb = nq + ((max_len + 63) / 64) * HEADS;
+    auto* st = (unsigned long long*)dalloc((size_t)nb * 64);
     for (int it = 0; it < 3; ++it) {
-        std::vector<unsigned long long> init(16, 0);
-        init[0] = init[6] = ~0ull;
-        CK(hipMemcpy(st, init.data(), 16 * 8, hipMemcpyHostToDevice));
+        CK(hipMemset(st, 0, (size_t)nb * 64));
         set(it + 1);
         a.stamps = st;
         launch_dec_qkv_attn(g, re, a, s);
         a.stamps = nullptr;
         CK(hipStreamSynchronize(s));
-        unsigned long long h[16];
-        CK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
-        printf("qkv+attn stamps (us from first block entry):");
-        for (int i = 1; i < 9; ++i) printf(" %s %.2f |", names[i], ((long long)h[i] - (long long)h[0]) / 100.0);
-        printf("\n");
+        std::vector<unsigned long long> h((size_t)nb * 8);
+        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+        print_stamps("qkv+attn", h, 0, nq, nq, nb);
     }
     for (int l = 0; l < NLA; ++l) { (void)hipFree(kc[l]); (void)hipFree(vc[l]); (void)hipFree(wq[l]); }
 }
