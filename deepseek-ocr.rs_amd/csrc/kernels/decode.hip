@@ -1364,6 +1364,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     constexpr int KS = 256 / HD;
     const int dim = tid % HD, grp = tid / HD;
     float l = 0.f, acc = 0.f;
+    bool refill = false;
     constexpr int NJ = 12;  // o partials per thread held in registers (nc <= KS * NJ)
     if (nc <= KS * NJ && nc <= 256) {
         // ONE round trip: (m, l) of chunk tid and this thread's o partials (clamped indices,
@@ -1389,16 +1390,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             __builtin_amdgcn_s_sleep(1);
         }
         da_stamp(a.stamps, 4);
-        if (POLL) {  // refill what was read (each word by exactly one thread) for the next launch
-            const uint32_t sent = DA_SENT;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                if (grp + KS * j < nc) __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, ((grp + KS * j) * PR + 4 + dim) * 4, 0, 16);
-            if (tid < nc) {
-                __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR) * 4, 0, 16);
-                __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR + 1) * 4, 0, 16);
-            }
-        }
+        refill = POLL;  // the words this thread read are refilled at the very end (after the last barrier)
         if (tid < nc) { ms[tid] = mt; ls[tid] = lt0; }
         __syncthreads();
         float mm = -INFINITY;
@@ -1445,6 +1437,20 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, (h * HD + tid) * 4, 0, 16);
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + kvh) * HD + tid) * 4, 0, 16);
             __builtin_amdgcn_raw_buffer_store_b32(sent, rr, ((a.heads + a.kv_heads + kvh) * HD + tid) * 4, 0, 16);
+        }
+    }
+    if (POLL && refill) {
+        // refill the record words this thread read (each word by exactly one thread) for the next launch.
+        // Here, after the block's last barrier: a __syncthreads waits for the write-through acknowledgements
+        // of every store before it (kbench attn stamps: merge poll -> exit 2.5-3 us with the refill before
+        // the combine's barriers)
+        const uint32_t sent = DA_SENT;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            if (grp + KS * j < nc) __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, ((grp + KS * j) * PR + 4 + dim) * 4, 0, 16);
+        if (tid < nc) {
+            __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR) * 4, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR + 1) * 4, 0, 16);
         }
     }
     da_stamp(a.stamps, 5);
