@@ -1077,6 +1077,7 @@ void Engine::decode_step(int B, int Lmax) {
         da.scale = (float)(1.0 / std::sqrt((double)hd)); da.part = part; da.o = CTX; da.o_ld = H;
         da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
         da.err = err;
+        da.kv_delay = att_kv_delay();
         da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
         // q/k/v projection with the input RMSNorm fused; one page: RoPE in the projection's epilogue, so the
         // attention reads q / k already rotated (B <= 2: the row block-staged; 3..8: dec_gemv_lds / dec_mm)
@@ -1224,6 +1225,12 @@ void Engine::ensure_mm_weights(int B) {
 
 // one page: q/k/v projection + decode attention as one launch (dec_qkv_attn); DSOCR_QKV_ATTN=0 (A/B
 // switch, read once) keeps the two launches
+// DSOCR_ATT_KV_DELAY (ticks of 10 ns, read at every capture): the fused launch's K / V loads behind the projection
+int Engine::att_kv_delay() {
+    const char* e = getenv("DSOCR_ATT_KV_DELAY");
+    return e ? std::max(0, atoi(e)) : 0;
+}
+
 bool Engine::qkv_attn_fused() {
     static const bool v = !(getenv("DSOCR_QKV_ATTN") && atoi(getenv("DSOCR_QKV_ATTN")) == 0);
     return v;

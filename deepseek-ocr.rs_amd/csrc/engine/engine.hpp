@@ -273,6 +273,7 @@ class Engine {
     enum StepSkip : int { SKIP_GATEUP = 1, SKIP_DOWN = 2, SKIP_ATTN = 4 };
     int step_skip_ = 0;
     static bool qkv_attn_fused();
+    static int att_kv_delay();
     unsigned long long* span_slots_ = nullptr;  // device [SPAN_SLOTS][2]
     unsigned long long* span_rec_ = nullptr;    // device [SPAN_KINDS][layers][span_cap_][4]
     const int* span_step_ = nullptr;            // device step counter (out_len of page 0)

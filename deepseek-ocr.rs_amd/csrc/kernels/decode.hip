@@ -1133,6 +1133,12 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     const int pos = a.kv_pos[b];
     const int len = pos + 1;
     if (k0 >= len) return;
+    if (FUSED && a.kv_delay > 0) {
+        // the projection blocks' weight stream first: this block's K / V cache loads wait kv_delay ticks
+        // (s_memrealtime, 10 ns) so the two streams do not share HBM while q is still being computed
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)a.kv_delay) __builtin_amdgcn_s_sleep(2);
+    }
     issue_k(k0, min(k0 + CH, len) - 1);
     issue_v(k0, min(k0 + CH, len) - 1);
     const bool own = pos >= k0 && pos < k0 + CH;

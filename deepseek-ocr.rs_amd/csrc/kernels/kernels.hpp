@@ -252,6 +252,7 @@ struct DecAttn2Args {
     // s_memrealtime (100 MHz) at [0] entry, [1] projection rows stored (fused), [2] q polled (fused) /
     // softmax done (standalone), [3] chunk record stored, [4] merge poll done, [5] exit
     unsigned long long* stamps = nullptr;
+    int kv_delay = 0;  // fused q/k/v + attention: ticks (10 ns) the K / V cache loads wait behind the projection
 };
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s);
 // q/k/v projection of one token with RoPE applied in the epilogue (rows < rot_rows rotated at

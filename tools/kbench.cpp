@@ -355,6 +355,12 @@ static void case_qkvattn1(int pos, hipStream_t s) {
     snprintf(nm, sizeof nm, "qkv+attn B=1 L=%d", pos + 1);
     const double bytes = 3.0 * H * H * 2 + 2.0 * (pos + 1) * HEADS * HD * 4;
     report(nm, timeit(4 * NLA, [&](int i) { set(i); launch_dec_qkv_attn(g, re, a, s); }, s), bytes);
+    for (int dl : {50, 100, 150, 200, 300}) {  // K / V loads held back behind the projection (10 ns ticks)
+        a.kv_delay = dl;
+        snprintf(nm, sizeof nm, "qkv+attn B=1 L=%d kv_delay %d", pos + 1, dl);
+        report(nm, timeit(4 * NLA, [&](int i) { set(i); launch_dec_qkv_attn(g, re, a, s); }, s), bytes);
+    }
+    a.kv_delay = getenv("KB_KV_DELAY") ? atoi(getenv("KB_KV_DELAY")) : 0;
     const int nq = (3 * H / 2 + 3) / 4, nb = nq + ((max_len + 63) / 64) * HEADS;
     auto* st = (unsigned long long*)dalloc((size_t)nb * 64);
     for (int it = 0; it < 3; ++it) {
