@@ -1372,11 +1372,11 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     float l = 0.f, acc = 0.f;
     bool refill = false;
     constexpr int NJ = 12;  // o partials per thread held in registers (nc <= KS * NJ)
-    if (nc <= KS * NJ && nc <= 256) {
-        // ONE round trip: (m, l) of chunk tid and this thread's o partials (clamped indices,
-        // weight 0 past nc by a select) are all in flight together
+    if (nc <= KS * NJ && nc <= 64) {
+        // ONE round trip: (m, l) of chunk `lane` (every wave holds all of them) and this thread's o partials
+        // (clamped indices, weight 0 past nc by a select) are all in flight together
         float ov[NJ];
-        const int tc = min(tid, nc - 1);
+        const int tc = min(lane, nc - 1);
         float mt, lt0;
         for (unsigned it = 0;; ++it) {
             asm volatile("" ::: "memory");  // the records change under us: re-load them every pass
@@ -1397,16 +1397,16 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         }
         da_stamp(a.stamps, 4);
         refill = POLL;  // the words this thread read are refilled at the very end (after the last barrier)
-        if (tid < nc) { ms[tid] = mt; ls[tid] = lt0; }
-        __syncthreads();
-        float mm = -INFINITY;
-        for (int cc = 0; cc < nc; ++cc) mm = fmaxf(mm, ms[cc]);
+        // chunk maxima / sums straight from the lanes that hold them: a wave max and lane reads, no LDS round
+        // trips or barrier (kbench attn stamps: the LDS form took ~2.5 us from the last poll to the exit)
+        const float mm = wave_max(lane < nc ? mt : -INFINITY);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int cc = grp + KS * j;
+            const float mc = __shfl(mt, min(cc, 63)), lc = __shfl(lt0, min(cc, 63));
             if (cc < nc) {
-                const float w = expf(ms[cc] - mm);
-                l += ls[cc] * w;
+                const float w = expf(mc - mm);
+                l += lc * w;
                 acc += ov[j] * w;
             }
         }
