@@ -1225,10 +1225,12 @@ void Engine::ensure_mm_weights(int B) {
 
 // one page: q/k/v projection + decode attention as one launch (dec_qkv_attn); DSOCR_QKV_ATTN=0 (A/B
 // switch, read once) keeps the two launches
-// DSOCR_ATT_KV_DELAY (ticks of 10 ns, read at every capture): the fused launch's K / V loads behind the projection
+// the fused launch's K / V loads held back behind the projection's weight stream: 150 ticks (1.5 us) from the
+// attention block's entry (tools/kbench qkvattn1 sweep 0..300: 12.99 -> 12.49 us at L 1217, 11.36 -> 10.88 at
+// L 707; decode layers 417.9 -> 411.6 us per step).  DSOCR_ATT_KV_DELAY (ticks of 10 ns) overrides; 0 = off
 int Engine::att_kv_delay() {
     const char* e = getenv("DSOCR_ATT_KV_DELAY");
-    return e ? std::max(0, atoi(e)) : 0;
+    return e ? std::max(0, atoi(e)) : 150;
 }
 
 bool Engine::qkv_attn_fused() {

@@ -1072,9 +1072,7 @@ __device__ __forceinline__ float group_sum(float v) {
 // issues its K / V cache loads first, then polls its rows until no word holds the sentinel, and the
 // merging block (chunk 0) refills them once every chunk of the head has read them (its record is
 // written after that read).  The cache stream overlaps the projection's weight stream.
-// SEQV (several pages): the V loads are issued after the scores, in the registers K held, so a block holds
-// 32 KB of the cache instead of 64 KB and every block of an 8-page launch fits the chip at once (one round)
-template <int HD, bool PREROT, bool POLL, bool FUSED, bool SEQV = false>
+template <int HD, bool PREROT, bool POLL, bool FUSED>
 __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c, const int h, const int b) {
     constexpr int CH = DA_CH;
     constexpr int LPK = 256 / CH;                                // lanes per key when scoring
@@ -1142,7 +1140,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)a.kv_delay) __builtin_amdgcn_s_sleep(2);
     }
     issue_k(k0, min(k0 + CH, len) - 1);
-    if (!SEQV) issue_v(k0, min(k0 + CH, len) - 1);
+    issue_v(k0, min(k0 + CH, len) - 1);
     const bool own = pos >= k0 && pos < k0 + CH;
     bool gave_up = false;
     if constexpr (FUSED) {
@@ -1290,7 +1288,6 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         const float l = wave_sum(p);
         if (tid == 0) red[4] = l;
     }
-    if (SEQV) issue_v(k0, min(k0 + CH, len) - 1);
     __syncthreads();
     if (!FUSED) da_stamp(a.stamps, 2);  // standalone: the chunk's scores and softmax done (K landed)
     // 5. P.V over this thread's KPG keys
@@ -1472,15 +1469,6 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttn2Args a) {
     dec_attn_body<HD, PREROT, POLL, false>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-// several pages: SEQV at MINW waves per SIMD (5: <= 96 VGPRs, 6: <= 80; 6 blocks per CU hold the 1600 blocks
-// of 8 pages at L 1217 nearly in one round)
-template <int MINW>
-__global__ __launch_bounds__(256, MINW) void dec_attn_seqv_kernel(DecAttn2Args a) {
-    WaveSpan span_(a.span);
-    da_stamp(a.stamps, 0);
-    dec_attn_body<128, false, true, false, true>(a, blockIdx.x, blockIdx.y, blockIdx.z);
-}
-
 // One page (MHA, 128-dim heads, <= 24 chunks): the q/k/v projection (qkv_rope_body, blocks [0, nq)) and
 // the decode attention (blocks nq + h * chunks + c) in ONE launch: the attention blocks stream their K / V
 // cache chunk while the projection blocks stream the q/k/v weights, then take q / k / v by polling
@@ -1541,7 +1529,6 @@ int attn_poll_blocks_per_cu(bool prerot) {
     static int pr = -1, npr = -1;
     int& v = prerot ? pr : npr;
     if (v < 0) v = prerot ? blocks_per_cu(dec_attn_kernel<128, true, true>, 0) : blocks_per_cu(dec_attn_kernel<128, false, true>, 0);
-    // (the SEQV kernels admit more blocks per CU than dec_attn_kernel: the rule stays conservative)
     return v;
 }
 }  // namespace
@@ -1585,13 +1572,6 @@ size_t dec_attn_workspace(int B, int heads, int hd, int max_len) {
     return (size_t)B * heads * ((max_len + DA2_CH_MIN - 1) / DA2_CH_MIN) * (hd + 4) * sizeof(float);
 }
 
-// DSOCR_ATT_SEQV=5|6 (A/B switch, read at every launch): 3..8 pages, V loads after the scores (SEQV) at that
-// many waves per SIMD
-static int attn_seqv() {
-    const char* e = getenv("DSOCR_ATT_SEQV");
-    return e ? atoi(e) : 0;
-}
-
 void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     if (!a.counters) throw std::runtime_error("EINTERNAL: dec_attn needs a zeroed counter array");
     if (a.max_len > 512 * DA_CH) throw std::runtime_error("EINVAL: decode context too long for the attention combine");
@@ -1603,10 +1583,7 @@ void launch_dec_attn(const DecAttn2Args& a, hipStream_t s) {
     // give-up flag, a sentinel-filled record buffer, the merging blocks within the residency rule;
     // otherwise the arrival ticket (no block waits)
     if (dec_attn_polled(a)) {
-        const int sv = !prerot && a.B >= 3 ? attn_seqv() : 0;
-        if (sv == 5) DSOCR_LAUNCH(dec_attn_seqv_kernel<5>, g1, dim3(256), 0, s, a);
-        else if (sv == 6) DSOCR_LAUNCH(dec_attn_seqv_kernel<6>, g1, dim3(256), 0, s, a);
-        else if (prerot) DSOCR_LAUNCH((dec_attn_kernel<128, true, true>), g1, dim3(256), 0, s, a);
+        if (prerot) DSOCR_LAUNCH((dec_attn_kernel<128, true, true>), g1, dim3(256), 0, s, a);
         else DSOCR_LAUNCH((dec_attn_kernel<128, false, true>), g1, dim3(256), 0, s, a);
         return;
     }

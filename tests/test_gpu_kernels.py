@@ -297,33 +297,6 @@ def test_decode_attention(gpu, B, heads, kvh, hd, max_len, prerot):
             assert np.max(np.abs(got[b, h * hd:(h + 1) * hd] - ref)) < 2e-5, (b, h)
 
 
-@pytest.mark.parametrize("seqv", ["5", "6"])
-def test_decode_attention_seqv_equals_default(gpu, monkeypatch, seqv):
-    """Several pages (8 x 10 heads x 128, max_len 1218, mixed positions incl. 0 and 63): the V-after-scores form
-    (DSOCR_ATT_SEQV, 5 or 6 waves per SIMD) computes what the default kernel does, bit for bit (same products
-    and order; only the time V is loaded differs), incl. the appended K / V slot."""
-    B, heads, hd, max_len = 8, 10, 128, 1218
-    rng = np.random.default_rng(int(seqv))
-    qkv = rng.standard_normal((B, 3 * heads * hd)).astype(np.float32)
-    kc = rng.standard_normal((B, heads, max_len, hd)).astype(np.float32)
-    vc = rng.standard_normal((B, heads, max_len, hd)).astype(np.float32)
-    pos = rng.integers(0, max_len, B).astype(np.int32)
-    pos[0], pos[1], pos[2] = max_len - 1, 0, 63
-    from types import SimpleNamespace
-    from oracle.decoder import rope_tables
-    cos, sin = rope_tables(SimpleNamespace(rope_theta=10000.0), max_len, hd)
-    dqkv, dp, dcos, dsin = Dev(qkv), Dev(pos), Dev(cos), Dev(sin)
-    got = {}
-    for v in ("0", seqv):
-        monkeypatch.setenv("DSOCR_ATT_SEQV", v)
-        dk, dv, do = Dev(kc), Dev(vc), Dev.zeros((B, heads * hd))
-        check(lib().dsocr_k_decode_attention(B, heads, heads, hd, hd, max_len, 1.0 / math.sqrt(hd), dqkv.ptr, dcos.ptr,
-                                             dsin.ptr, dk.ptr, dv.ptr, dp.ptr, do.ptr, 0))
-        got[v] = (do.get(), dk.get(), dv.get())
-    for x, y in zip(got["0"], got[seqv]):
-        assert np.array_equal(x, y)
-
-
 SENT = 0x7FBADBAD  # DSOCR_HANDOFF_SENTINEL
 
 

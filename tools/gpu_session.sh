@@ -45,7 +45,6 @@ for step in "$@"; do
     m_r4) run 600 python -u -m pytest tests/test_gpu_model.py -q -m gpu -k "oproj_route or full_screened" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/m_r4.log 2>&1 ;;
     dsq_r4) run 900 python -u -m pytest tests/test_dsq.py -q -m gpu -k "full_q4k" -rf -p no:cacheprovider --timeout 600 --timeout-method thread > gpurun_out/dsq_r4.log 2>&1 ;;
     kb_qa) run 180 ./tools/kbench qkvattn1 > gpurun_out/kb_qkvattn.log 2>&1 ;;
-    kb_seqv) run 180 ./tools/kbench attn8 attn8seqv > gpurun_out/kb_seqv.log 2>&1 ;;
     gprof64_maps) DSOCR_SEGV_MAPS=1 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof64_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof64_maps.log 2>&1 ;;
     # graph-mode kernel trace of a whole bench line (512 tokens), default runtime settings
     gprof_full) run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_full -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/gprof_full.log 2>&1 ;;

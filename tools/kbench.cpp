@@ -525,14 +525,6 @@ int main(int argc, char** argv) {
         else if (c == "gemv8") case_gemv(8, s);
         else if (c == "attn1") { case_attn(1, 706, s); case_attn(1, 1216, s); }
         else if (c == "attn8") { case_attn(8, 706, s); case_attn(8, 1216, s); }
-        else if (c == "attn8seqv") {  // the V-after-scores form at 5 and 6 waves per SIMD
-            for (const char* v : {"5", "6"}) {
-                setenv("DSOCR_ATT_SEQV", v, 1);
-                printf("DSOCR_ATT_SEQV=%s\n", v);
-                case_attn(8, 706, s); case_attn(8, 1216, s);
-            }
-            unsetenv("DSOCR_ATT_SEQV");
-        }
         else if (c == "qkvattn1") { case_qkvattn1(706, s); case_qkvattn1(1216, s); }
         else if (c == "lm8") case_lm(8, s);
         else if (c == "vgemm") case_vgemm(s);
