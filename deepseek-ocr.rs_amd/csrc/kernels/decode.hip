@@ -183,6 +183,17 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
     const bool fast = a.K <= XR * 4 * 256;
     XRegs<MT, XR> xr;
     if (fast) xload<MT, XR>(xr, a.x, a.ldx, nullptr, a.M, a.K, a.norm_w);
+    // accumulate (residual) rows of one or two tokens: loaded now, with x, instead of after the wave sums
+    // (one dependent round trip fewer at the end of o_proj)
+    constexpr bool YPRE = MT <= 2;
+    float ypre[YPRE ? RB : 1][YPRE ? MT : 1];
+    if constexpr (YPRE) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                ypre[r][m] = a.accumulate ? a.y[(long)min(m, a.M - 1) * a.ldy + min(n0 + r, a.N - 1)] : 0.f;
+    }
     uint4 wq[U][RB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -247,7 +258,10 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
             if (lane == 0 && m < a.M && n < a.N) {
                 v = apply_act(v + (a.bias ? a.bias[n] : 0.f), a.act);
                 float* yp = a.y + (long)m * a.ldy + n;
-                if (a.accumulate) v = *yp + v;
+                if (a.accumulate) {
+                    if constexpr (YPRE) v = ypre[r][m] + v;
+                    else v = *yp + v;
+                }
                 *yp = v;
             }
         }
@@ -2401,6 +2415,8 @@ __global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
     const int nr = a.topk * cpi, nch = nr + cps;
     const int per = (nch + NW - 1) / NW;
     const int c0 = wave * per, c1 = min(nch, c0 + per);
+    // the residual rows, loaded first (not after the LDS combine: one dependent round trip fewer)
+    const float xres = a.out[min(j0 + (int)(threadIdx.x & (RPB - 1)), a.Hout - 1)];
     // 1. h of this wave's chunks (independent of the picks)
     f32x4 hv[U][2];
     int seg[U], off[U];
@@ -2453,8 +2469,7 @@ __global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
     if (threadIdx.x < RPB && j0 + threadIdx.x < a.Hout) {
         const int r = threadIdx.x;
         const float v = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) + ((part[4][r] + part[5][r]) + (part[6][r] + part[7][r]));
-        float* xp = a.out + j0 + r;
-        *xp = *xp + v;
+        a.out[j0 + r] = xres + v;
     }
 }
 
