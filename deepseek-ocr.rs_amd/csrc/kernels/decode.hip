@@ -909,11 +909,6 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
                 float* d = xs + (long)wave * a.K + (c << 3);
                 *reinterpret_cast<float4*>(d) = lo;
                 *reinterpret_cast<float4*>(d + 4) = hi;
-                if (blockIdx.x == 0 && a.xn_out) {
-                    float* g = a.xn_out + (long)wave * a.K + (c << 3);
-                    *reinterpret_cast<float4*>(g) = lo;
-                    *reinterpret_cast<float4*>(g + 4) = hi;
-                }
             }
         }
     }
@@ -1019,6 +1014,16 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
         }
         if (lane == 0) r.grp[0] = __popcll(bm);
     }
+    // the normalised rows for the expert kernels, from this (last) block's LDS after its last barrier: a global
+    // store before a barrier makes the barrier wait for its acknowledgement (block 0 stored them during the
+    // staging and reached the ticket ~1 us late)
+    if (a.xn_out && wave < a.M)
+        for (int c = lane; c < chunks; c += 64) {
+            const float* sp = xs + (long)wave * a.K + (c << 3);
+            float* g = a.xn_out + (long)wave * a.K + (c << 3);
+            *reinterpret_cast<float4*>(g) = *reinterpret_cast<const float4*>(sp);
+            *reinterpret_cast<float4*>(g + 4) = *reinterpret_cast<const float4*>(sp + 4);
+        }
     RG_STAMP(7);
 #undef RG_STAMP
 }
@@ -3098,6 +3103,7 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
     __shared__ int si2[NT / 64];
     __shared__ int nlist, nban_s, pm_n;
     __shared__ int pm_c1[SP_PM], pm_c2[SP_PM];
+    __shared__ int banv_s[SP_PM];
     float* xs = dyn;
     int* list = reinterpret_cast<int*>(dyn + a.K);
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3219,6 +3225,17 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
         waves_argmax(bv, bi, sv2, si2);
     }
     const int t = bi == 0x7fffffff ? 0 : bi;
+    // the next step's ban from the prefix matches into LDS first: the global stores below then need no barrier
+    // after them (a barrier waits for the acknowledgement of every store before it)
+    const bool ban_fast = a.ban_out && pm_n <= SP_PM;
+    if (ban_fast) {
+        for (int p = tid; p < pm_n; p += NT)
+            if (pm_c1[p] == t) {
+                const int q = atomicAdd(&nban_s, 1);
+                banv_s[q] = pm_c2[p] < 0 ? t : pm_c2[p];  // q < pm_n <= SP_PM
+            }
+        __syncthreads();
+    }
     if (tid == 0) {
         a.out_tok[b] = t;
         if (a.out_ids && !done0) {
@@ -3246,12 +3263,13 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
     if (!a.ban_out) return;
     // (a page that did not take the token is done: its later selections are never read)
     int* out = a.ban_out + (long)b * a.ban_ld;
-    if (pm_n <= SP_PM) {
-        for (int p = tid; p < pm_n; p += NT)
-            if (pm_c1[p] == t) {
-                const int q = atomicAdd(&nban_s, 1);
-                if (q + 1 < a.ban_ld) out[1 + q] = pm_c2[p] < 0 ? t : pm_c2[p];
-            }
+    if (ban_fast) {
+        const int nb = nban_s;
+        for (int q = tid; q < nb; q += NT)
+            if (q + 1 < a.ban_ld) out[1 + q] = banv_s[q];
+        if (tid == 0) out[0] = min(nb, (int)a.ban_ld - 1);
+        SP_STAMP(5)
+        return;
     } else {
         // too many prefix matches (tiny n-gram sizes): full scan of the updated context
         __syncthreads();

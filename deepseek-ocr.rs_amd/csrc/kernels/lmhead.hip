@@ -320,23 +320,27 @@ __global__ __launch_bounds__(256) void lmhead_q8_kernel(LmHeadQ8Args a) {
     // the block's list against its final threshold (most rows kept early fall out here)
     const int cnt = lst_n;
     const float Tb = fkey_dec(tkey_s);
-    // entry p of this block at [b][p][block] (the final kernel reads a row of blocks per load)
+    // entry p of this block at [b][p][block] (the final kernel reads a row of blocks per load); wave 0
+    // compacts the list by ballots and writes the count itself: no barrier after the global stores (a barrier
+    // waits for the acknowledgement of every store before it)
     const long sb = (long)b * a.nblk * a.slot + blockIdx.x;
-    __syncthreads();
-    if (tid == 0) lst_n = 0;
-    __syncthreads();
-    for (int i = tid; i < cnt; i += 256) {
-        const float h = lst_hi[i];
-        if (h >= Tb) {
-            const int p = atomicAdd(&lst_n, 1);
-            a.cand[sb + (long)p * a.nblk] = lst_idx[i];
-            a.cand_hi[sb + (long)p * a.nblk] = h;
+    if (wave == 0) {
+        int kept = 0;
+        for (int i0 = 0; i0 < cnt; i0 += 64) {
+            const int i = i0 + lane;
+            const bool keep = i < cnt && lst_hi[i] >= Tb;
+            const unsigned long long bm = __ballot(keep);
+            if (keep) {
+                const int p = kept + __popcll(bm & ((1ull << lane) - 1ull));
+                a.cand[sb + (long)p * a.nblk] = lst_idx[i];
+                a.cand_hi[sb + (long)p * a.nblk] = lst_hi[i];
+            }
+            kept += __popcll(bm);
         }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        a.blk_cnt[(long)b * a.nblk + blockIdx.x] = lst_n;
-        a.blk_t[(long)b * a.nblk + blockIdx.x] = Tb;
+        if (lane == 0) {
+            a.blk_cnt[(long)b * a.nblk + blockIdx.x] = kept;
+            a.blk_t[(long)b * a.nblk + blockIdx.x] = Tb;
+        }
     }
 }
 
