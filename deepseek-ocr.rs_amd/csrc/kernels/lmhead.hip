@@ -235,7 +235,6 @@ __global__ __launch_bounds__(256) void lmhead_q8_kernel(LmHeadQ8Args a) {
                 o.w = (v[i].w / den) * w[i].w;
                 *reinterpret_cast<float4*>(xs + LQ_XS + k) = o;
                 n2 += (o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w);
-                if (blockIdx.x == 0 && a.xn_out) *reinterpret_cast<float4*>(a.xn_out + (long)b * K + k) = o;
             }
         }
         n2 = wave_sum(n2);
@@ -342,6 +341,11 @@ __global__ __launch_bounds__(256) void lmhead_q8_kernel(LmHeadQ8Args a) {
             a.blk_t[(long)b * a.nblk + blockIdx.x] = Tb;
         }
     }
+    // block 0 hands the staged row to the final selection (exact rescoring) here, after its last barrier:
+    // stored during the staging, the staging's barriers waited for the stores and block 0 started ~1 us late
+    if (blockIdx.x == 0 && a.xn_out)
+        for (int k = tid * 4; k < K; k += 256 * 4)
+            *reinterpret_cast<float4*>(a.xn_out + (long)b * K + k) = *reinterpret_cast<const float4*>(x + k);
 }
 
 static int lq_tseg(int K) {
@@ -400,6 +404,7 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
     __shared__ __attribute__((aligned(16))) int8_t xq[2][LM_T][LM_KMAX + 16];
     __shared__ float t1_s[LM_T], t2_s[LM_T], nrm_s[LM_T], errn_s[LM_T];
     __shared__ unsigned tkey_s[LM_T];
+    __shared__ float den_s[LM_T];
     __shared__ int lst_n[LM_T], nban_s[LM_T];
     __shared__ int lst_idx[LM_T][LM_LIST];
     __shared__ float lst_hi[LM_T][LM_LIST];
@@ -446,6 +451,7 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
         }
         q = wave_sum(q);
         const float den = sqrtf(q / (float)K + a.eps);
+        if (lane == 0) den_s[wave] = den;
         auto xhat = [&](int k) {
             const float4 v = *reinterpret_cast<const float4*>(xr + k), w = *reinterpret_cast<const float4*>(a.norm_w + k);
             return make_float4((v.x / den) * w.x, (v.y / den) * w.y, (v.z / den) * w.z, (v.w / den) * w.w);
@@ -480,7 +486,6 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
                 }
                 *reinterpret_cast<uint32_t*>(&xq[0][wave][k]) = hw;
                 *reinterpret_cast<uint32_t*>(&xq[1][wave][k]) = lw;
-                if (blockIdx.x == 0 && a.xn_out) *reinterpret_cast<float4*>(a.xn_out + (long)wave * K + k) = o;
             }
         }
         n2 = wave_sum_d(n2);
@@ -600,6 +605,17 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
         if (lane == 0) {
             a.blk_cnt[(long)tk * a.nblk + blockIdx.x] = kept;
             a.blk_t[(long)tk * a.nblk + blockIdx.x] = Tb;
+        }
+    }
+    // block 0 hands the normalised rows to the final selection here, after its last barrier (recomputed with the
+    // staging's arithmetic: the same values), not during the staging, whose barriers would wait for the stores
+    if (blockIdx.x == 0 && a.xn_out && wave < B) {
+        const float* xr = a.x + (long)wave * a.ldx;
+        const float den = den_s[wave];
+        for (int k = lane * 4; k < K; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k), w = *reinterpret_cast<const float4*>(a.norm_w + k);
+            *reinterpret_cast<float4*>(a.xn_out + (long)wave * K + k) =
+                make_float4((v.x / den) * w.x, (v.y / den) * w.y, (v.z / den) * w.z, (v.w / den) * w.w);
         }
     }
 }
