@@ -678,6 +678,9 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
     const int nh = (n_seg + 1) >> 1;
     const int sb = hf ? nh : 0, se = hf ? n_seg : nh;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the residual quad, loaded with the segments (not after the halves meet: one round trip fewer)
+    float4* op = reinterpret_cast<float4*>(a.out + (long)min(t, a.T - 1) * a.Hout + j);
+    const float4 o_in = hf ? make_float4(0.f, 0.f, 0.f, 0.f) : *op;
     if (t < a.T) {
         constexpr int SB = 18;  // segments in flight per batch (n_seg <= 72: at most 2 batches per half)
         const long sstride = (long)MM_MT * a.Hout * 4;
@@ -702,8 +705,7 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
     __syncthreads();
     if (!hf && t < a.T) {
         const float4 u = half_s[q4];
-        float4* op = reinterpret_cast<float4*>(a.out + (long)t * a.Hout + j);
-        float4 o = *op;
+        float4 o = o_in;
         o.x = o.x + (v.x + u.x);
         o.y = o.y + (v.y + u.y);
         o.z = o.z + (v.z + u.z);
