@@ -1105,7 +1105,6 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     __shared__ float red[8];
     __shared__ int last_s;
     __shared__ float4 o_s[384];  // P.V partials; reused by the combine (m, l per chunk + per-group sums)
-    __shared__ float ml0_s[2];   // the merging block's own (m, l) (own_lds)
     const int k0 = c * CH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvh = h / (a.heads / a.kv_heads);
@@ -1335,34 +1334,21 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     const int chunks = (a.max_len + CH - 1) / CH;
     float* part0 = a.part + ((long)b * a.heads + h) * chunks * PR;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part0, (short)0, chunks * PR * 4, 0x00020000);
-    // the merging block's own partial (POLL, chunk 0, the lane-read merge below) stays in LDS: no record, and
-    // no wait for its stores' acknowledgement before the block starts polling the others
-    constexpr int KS = 256 / HD, NJ = 12;  // merge: thread groups per dim, o partials per thread (nc <= KS * NJ)
-    const bool own_lds = POLL && c == 0 && nc <= KS * NJ && nc <= 64;
     if (tid < DG) {
         float4 t = o_s[tid];
         for (int g = 1; g < KG; ++g) {
             const float4 u = o_s[g * DG + tid];
             t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
         }
-        if (own_lds) {
-            o_s[tid] = t;  // (slot tid is read by this thread only)
-        } else {
-            u32x4 bits;
-            __builtin_memcpy(&bits, &t, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (c * PR + 4 + tid * 4) * 4, 0, 16);
-        }
+        u32x4 bits;
+        __builtin_memcpy(&bits, &t, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (c * PR + 4 + tid * 4) * 4, 0, 16);
     }
     if (tid == 0) {
-        if (own_lds) {
-            ml0_s[0] = m;
-            ml0_s[1] = l_run;
-        } else {
-            const float ml[4] = {m, l_run, 0.f, 0.f};
-            u32x4 bits;
-            __builtin_memcpy(&bits, ml, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
-        }
+        const float ml[4] = {m, l_run, 0.f, 0.f};
+        u32x4 bits;
+        __builtin_memcpy(&bits, ml, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, c * PR * 4, 0, 16);
     }
     da_stamp(a.stamps, 3);
     // 6. POLL: no ticket.  Chunk 0's block merges: it polls the records of the other chunks until
@@ -1378,7 +1364,7 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     if constexpr (POLL) {
         if (c != 0) return;
     }
-    if (!own_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (POLL) {
         last_s = 1;
@@ -1400,29 +1386,23 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
     float* ls = ms + 512;
     float* accp = ms + 1024;
     float* lp = ms + 1280;
+    constexpr int KS = 256 / HD;
     const int dim = tid % HD, grp = tid / HD;
     float l = 0.f, acc = 0.f;
     bool refill = false;
+    constexpr int NJ = 12;  // o partials per thread held in registers (nc <= KS * NJ)
     if (nc <= KS * NJ && nc <= 64) {
         // ONE round trip: (m, l) of chunk `lane` (every wave holds all of them) and this thread's o partials
         // (clamped indices, weight 0 past nc by a select) are all in flight together
         float ov[NJ];
         const int tc = min(lane, nc - 1);
         float mt, lt0;
-        // chunk 0's own partial from LDS (own_lds)
-        const float o0 = own_lds ? reinterpret_cast<const float*>(o_s)[dim] : 0.f;
-        const float m0 = own_lds ? ml0_s[0] : 0.f, l0 = own_lds ? ml0_s[1] : 0.f;
         for (unsigned it = 0;; ++it) {
             asm volatile("" ::: "memory");  // the records change under us: re-load them every pass
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int cj = min(grp + KS * j, nc - 1);
-                const float v = ld1(cj * PR + 4 + dim);
-                ov[j] = own_lds && cj == 0 ? o0 : v;
-            }
+            for (int j = 0; j < NJ; ++j) ov[j] = ld1(min(grp + KS * j, nc - 1) * PR + 4 + dim);
             mt = ld1(tc * PR);
             lt0 = ld1(tc * PR + 1);
-            if (own_lds && tc == 0) { mt = m0; lt0 = l0; }
             if (!POLL) break;
             bool pend = __float_as_uint(mt) == DA_SENT || __float_as_uint(lt0) == DA_SENT;
 #pragma unroll
@@ -1490,12 +1470,10 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         // of every store before it (kbench attn stamps: merge poll -> exit 2.5-3 us with the refill before
         // the combine's barriers)
         const uint32_t sent = DA_SENT;
-        const int c0 = own_lds ? 1 : 0;  // chunk 0's words were never written (own_lds)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-            if (grp + KS * j < nc && grp + KS * j >= c0)
-                __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, ((grp + KS * j) * PR + 4 + dim) * 4, 0, 16);
-        if (tid < nc && tid >= c0) {
+            if (grp + KS * j < nc) __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, ((grp + KS * j) * PR + 4 + dim) * 4, 0, 16);
+        if (tid < nc) {
             __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR) * 4, 0, 16);
             __builtin_amdgcn_raw_buffer_store_b32(sent, rsrc, (tid * PR + 1) * 4, 0, 16);
         }
