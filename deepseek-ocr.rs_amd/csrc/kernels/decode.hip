@@ -1171,11 +1171,14 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
                   ov = ((a.heads + a.kv_heads + kvh) * HD + td) * 4;
         for (unsigned it = 0;; ++it) {
             asm volatile("" ::: "memory");
-            q_pre = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, oq, 0, 16));
-            k_pre = own ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok, 0, 16)) : 0.f;
-            v_pre = own ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ov, 0, 16)) : 0.f;
-            const bool pend = __float_as_uint(q_pre) == DA_SENT || __float_as_uint(k_pre) == DA_SENT ||
-                              __float_as_uint(v_pre) == DA_SENT;
+            bool pend = false;
+            if (tid < HD) {  // waves 0..HD/64-1 poll (the others only join the vote): half the polling traffic
+                q_pre = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, oq, 0, 16));
+                k_pre = own ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ok, 0, 16)) : 0.f;
+                v_pre = own ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, ov, 0, 16)) : 0.f;
+                pend = __float_as_uint(q_pre) == DA_SENT || __float_as_uint(k_pre) == DA_SENT ||
+                       __float_as_uint(v_pre) == DA_SENT;
+            }
             if (!__syncthreads_or(pend)) break;
             if (it > (1u << 20)) {
                 if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
