@@ -1399,33 +1399,18 @@ __device__ __forceinline__ void dec_attn_body(const DecAttn2Args& a, const int c
         // (clamped indices, weight 0 past nc by a select) are all in flight together
         float ov[NJ];
         const int tc = min(lane, nc - 1);
-        float mt = 0.f, lt0 = 0.f;
-        const bool lite = POLL && a.B > 2;
-        bool ml_in = false;
+        float mt, lt0;
         for (unsigned it = 0;; ++it) {
             asm volatile("" ::: "memory");  // the records change under us: re-load them every pass
-            // several pages (lite): the (m, l) words alone are polled and the o partials loaded once every
-            // chunk's (m, l) is in — the 80 merging blocks of 8 pages poll from the launch's start, and a full
-            // pass (14 loads per thread) competed with the K / V stream; one page keeps the single round trip
-            if (!lite || ml_in) {
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) ov[j] = ld1(min(grp + KS * j, nc - 1) * PR + 4 + dim);
-            }
-            if (!ml_in) {
-                mt = ld1(tc * PR);
-                lt0 = ld1(tc * PR + 1);
-            }
+            for (int j = 0; j < NJ; ++j) ov[j] = ld1(min(grp + KS * j, nc - 1) * PR + 4 + dim);
+            mt = ld1(tc * PR);
+            lt0 = ld1(tc * PR + 1);
             if (!POLL) break;
             bool pend = __float_as_uint(mt) == DA_SENT || __float_as_uint(lt0) == DA_SENT;
-            if (!lite || ml_in) {
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) pend = pend || __float_as_uint(ov[j]) == DA_SENT;
-            }
-            if (!__syncthreads_or(pend)) {
-                if (!lite || ml_in) break;
-                ml_in = true;  // every (m, l) present: load the o partials (their stores preceded them)
-                continue;
-            }
+            for (int j = 0; j < NJ; ++j) pend = pend || __float_as_uint(ov[j]) == DA_SENT;
+            if (!__syncthreads_or(pend)) break;
             if (it > (1u << 20)) {
                 if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
