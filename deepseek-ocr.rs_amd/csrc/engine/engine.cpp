@@ -1146,7 +1146,13 @@ void Engine::decode_step(int B, int Lmax) {
             m.hs = wsf("s_hh", (size_t)B * L.inter);
             m.n_active = wsi("s_nact", 1);
             launch_moe_gateup2(m, st);
-            launch_moe_down2(m, st);
+            // one page: the down projection split over the 8 waves of a block (moe_down_mix; all of K in flight
+            // at once) — moe_down2 walks each 6848-long row in four dependent load rounds
+            MoeDec2Args dn = m;
+            dn.slot_mode = 1;
+            dn.ids = wsi("s_dense_ids", 8);  // (no routed segments: read, never used)
+            if (B == 1 && moe_down_mix_ok(dn)) launch_moe_down_mix(dn, st);
+            else launch_moe_down2(m, st);
             continue;
         }
         if (!span_rec_) {
