@@ -2512,6 +2512,15 @@ void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s)
 }
 
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
+    if (a.T == 1 && a.slots == 0 && a.sWgu && a.Is > 0 && a.K % 8 == 0 && a.K <= 64 * 3 * 8) {
+        // one token through a dense / shared-only MLP (layer 0): one gate + up row pair per wave, 4 rows per
+        // block (moe_gateup_shared_kernel, RB = 1: twice the blocks of RB = 2, half as long)
+        MoeDec2Args sh = a;
+        const int ns = (a.Is + 3) / 4;
+        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_shared_kernel<bf16_t, 1, 1>), dim3(ns), dim3(256), stage_bytes(1, a.K), s, sh, 0);
+        else DSOCR_LAUNCH((moe_gateup_shared_kernel<f16_t, 1, 1>), dim3(ns), dim3(256), stage_bytes(1, a.K), s, sh, 0);
+        return;
+    }
     constexpr int RB = 2;
     const int units_r = (a.I + 4 * RB - 1) / (4 * RB);
     const int units_s = a.sWgu ? (a.Is + 4 * RB - 1) / (4 * RB) : 0;
