@@ -3221,6 +3221,19 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
     }
     float bv = -INFINITY;
     int bi = 0x7fffffff;
+    // at most one survivor per wave (the usual case: ~9 of 16 waves): each wave also loads its survivor's
+    // embedding row now, so the next step's input row is in registers when the argmax is known (the gather
+    // after the argmax was one more dependent round trip at the end of the step)
+    constexpr int EU = 3;  // 16-byte chunks per lane of the embedding row (H <= 64 * 8 * EU)
+    const bool emb_pre = a.table && nl <= NT / 64 && a.H % 8 == 0 && a.H <= 64 * 8 * EU;
+    uint4 erow[EU];
+    int ev = -1;
+    if (emb_pre && wave < nl) {
+        ev = list[wave];
+        const uint16_t* tab = reinterpret_cast<const uint16_t*>(a.table) + (long)ev * a.H;
+#pragma unroll
+        for (int u = 0; u < EU; ++u) erow[u] = ldg_nt16(tab + (min(u * 64 + lane, a.H / 8 - 1) << 3));
+    }
     screened_rescore(a, W, xs, list, nl, T, bc, sb, bv, bi);
     SP_STAMP(2)
     waves_argmax(bv, bi, sv2, si2);
@@ -3265,10 +3278,28 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
         }
     }
     if (a.table) {
-        const uint16_t* tab = reinterpret_cast<const uint16_t*>(a.table);
-        for (int c = tid; c < a.H; c += NT) {
-            const uint32_t bits = tab[(long)t * a.H + c];
-            a.x_next[(long)b * a.H + c] = a.table_dt == WDT_BF16 ? bf16_bits_to_f32(bits) : f16_bits_to_f32(bits);
+        const bool hit = emb_pre && bi != 0x7fffffff && t == bi && __syncthreads_or(ev == t);
+        if (hit) {  // the wave that holds the winner's row writes it
+            if (ev == t) {
+#pragma unroll
+                for (int u = 0; u < EU; ++u) {
+                    const int cc = u * 64 + lane;
+                    if (cc < a.H / 8) {
+                        float w8[8];
+                        if (a.table_dt == WDT_BF16) unpack8<bf16_t>(erow[u], w8);
+                        else unpack8<f16_t>(erow[u], w8);
+                        float* d = a.x_next + (long)b * a.H + (cc << 3);
+                        *reinterpret_cast<float4*>(d) = make_float4(w8[0], w8[1], w8[2], w8[3]);
+                        *reinterpret_cast<float4*>(d + 4) = make_float4(w8[4], w8[5], w8[6], w8[7]);
+                    }
+                }
+            }
+        } else {
+            const uint16_t* tab = reinterpret_cast<const uint16_t*>(a.table);
+            for (int c = tid; c < a.H; c += NT) {
+                const uint32_t bits = tab[(long)t * a.H + c];
+                a.x_next[(long)b * a.H + c] = a.table_dt == WDT_BF16 ? bf16_bits_to_f32(bits) : f16_bits_to_f32(bits);
+            }
         }
     }
     SP_STAMP(4)
