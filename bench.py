@@ -97,19 +97,23 @@ def reduce_over_ranks(dist, elapsed, tok_s):
     return float(t.item()), float(r.item())
 
 
-def pmc_traffic(kernel_prefix):
+def pmc_traffic(kernel_prefix, runs=None):
     """Per-launch HBM bytes of a kernel from the committed rocprofv3 PMC summary
     (latest profiles/rNN_pmc_traffic.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 (gfx950
-    reports half of wide streaming reads) + WRITE_SIZE, each from its own --pmc pass)."""
+    reports half of wide streaming reads) + WRITE_SIZE, each from its own --pmc pass).  `runs` names the
+    PMC runs whose workload matches this bench line (the MoE kernels' bytes follow the routing: the 8-page
+    figure was taken on 8 text pages, 30 experts per layer, and is not this kernel's traffic at 16);
+    a kernel measured only in another run gives None."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     try:
         d = json.load(open(paths[-1]))
     except Exception:
         return None
-    for name, v in d.get("kernels", {}).items():
-        if name.startswith(kernel_prefix):
-            return v.get("hbm_bytes_per_launch")
+    for table in ("kernels", "kernels_b8"):
+        for name, v in d.get(table, {}).items():
+            if name.startswith(kernel_prefix) and (runs is None or v.get("run") in runs):
+                return v.get("hbm_bytes_per_launch")
     return None
 
 
@@ -493,7 +497,7 @@ def main():
                     "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
         gu = ctx_line("moe_gateup")
         roofline = {"bound": "hbm", "achieved": gu["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gu["frac"],
-                    "traffic": pmc_traffic(kernel),
+                    "traffic": pmc_traffic(kernel, runs=("b1",) if ppg == 1 else (("b8",) if args.text_pages and ppg == 8 else ())),
                     "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
                     # avg_launch_us = in-context duration: (one decode step's layers replayed as a hipGraph - the
                     # same graph without the gate/up launches) / MoE layers, HIP events around the replays on the
