@@ -20,6 +20,7 @@
 // (8 staged; lanes of columns 8..15 read the rows of columns 0..7 and their results are dropped).
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "dev_common.hpp"
 #include "kernels.hpp"
@@ -368,26 +369,38 @@ void launch_dec_mm(const DecGemvArgs& a, hipStream_t s) {
 // the 16 gate rows and the 16 up rows over the full K, streamed as MFMA A fragments (PF k-steps of
 // both per batch, double-buffered, the next unit's first batch in flight behind the current one's
 // last); the 8 normalised token rows (xn) are the B operand as three f16 planes staged once per
-// block.  Persistent grid (resident blocks only): unit u goes to block u % grid, wave (u / grid) % 8,
-// so every CU streams the same share (a second round of blocks, or two blocks' rows on one CU, set
-// the launch's length before).  Epilogue per (row, token): g, u scaled back, h = silu(g) * u (candle
-// silu: x / (1 + exp(-x))), times the pick's routing weight for routed experts, to h[slot row]
-// (slot = t * topk + k) or hs[t]; tokens outside a record are computed (a 16-column tile costs the
-// same) and dropped.
-template <typename WT, int PF, bool SWZ>
+// block.  KS waves share a unit, each streaming K / KS of it (more, shorter streams: one wave per
+// 80 KB unit left CUs idle at 16 experts and drew 5.1 TB/s at 32, `tools/mb_units.hip`); the pieces
+// meet in LDS, summed in piece order by the unit's first wave, which runs the epilogue.  The waves of
+// a unit hand over through two LDS counters (pieces posted, pieces consumed) instead of a block
+// barrier: a barrier would wait for the next unit's loads already in flight.  Persistent grid
+// (resident blocks only): block b takes units b NU + w / KS, then + grid NU, ... (NU = 8 / KS).
+// Epilogue per (row, token): g, u scaled back, h = silu(g) * u (candle silu: x / (1 + exp(-x))),
+// times the pick's routing weight for routed experts, to h[slot row] (slot = t * topk + k) or hs[t];
+// tokens outside a record are computed (a 16-column tile costs the same) and dropped.
+__device__ __forceinline__ int lds_load_relaxed(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <typename WT, int PF, bool SWZ, int KS>
 __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
-    constexpr int NWV = 8;
+    constexpr int NWV = 8, NU = NWV / KS;
+    static_assert(NWV % KS == 0, "whole units per block");
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ f32x4 red[KS > 1 ? NWV : 1][2][64];  // pieces 1.. of each unit: gate, up partial tiles
+    __shared__ int hand[2 * NU];                      // [us]: pieces posted, [NU + us]: units consumed
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the hand-off branches are scalar
     const int col = lane & 15, g = lane >> 4;
+    const int piece = wave % KS, us = wave / KS;
     const int tiles_r = a.I >> 4, tiles_s = a.sWgu ? a.Is >> 4 : 0;
     const int n_units = tiles_s + a.grp[0] * tiles_r;
-    const int steps = a.K >> 5, nch = steps / PF;
-    const int stride = gridDim.x * NWV;
-    int unit = blockIdx.x + gridDim.x * wave;
+    const int steps = a.K >> 5, nch = steps / PF, nb = nch / KS, c0 = piece * nb;
+    const int stride = gridDim.x * NU;
+    int unit = blockIdx.x * NU + us;
     // unit -> (shared?, expert, first row) and the lane's two fragment streams
     struct Src {
         const WT* pg;
@@ -437,11 +450,12 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     // both weight batches of the first unit go out before the staging barrier (the stream would
     // otherwise idle behind it)
     if (unit < n_units) {
-        load(ga, ua, cur, 0);
-        if (nch > 1) load(gb, ub, cur, 1);
+        load(ga, ua, cur, c0);
+        if (nb > 1) load(gb, ub, cur, c0 + 1);
     }
     const int KP = mm_pitch(a.K);
     if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
+    if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
     __syncthreads();
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
     f32x4 accg = {0.f, 0.f, 0.f, 0.f}, accu = {0.f, 0.f, 0.f, 0.f};
@@ -458,54 +472,92 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
     };
     bool first = true;
-    for (; unit < n_units; unit += stride) {
+    for (int n = 0; unit < n_units; unit += stride, ++n) {
         const int nu = unit + stride;
         const bool more = nu < n_units;
         const Src nxt = more ? src(nu) : cur;
-        for (int c = 0; c < nch; c += 2) {
-            if (c + 1 < nch) { if (!(first && c == 0)) load(gb, ub, cur, c + 1); }
-            else if (more) load(gb, ub, nxt, 0);
-            compute(ga, ua, c);
-            if (c + 1 >= nch) break;
-            if (c + 2 < nch) load(ga, ua, cur, c + 2);
-            else if (more) load(ga, ua, nxt, 0);
-            compute(gb, ub, c + 1);
+        for (int c = 0; c < nb; c += 2) {
+            if (c + 1 < nb) { if (!(first && c == 0)) load(gb, ub, cur, c0 + c + 1); }
+            else if (more) load(gb, ub, nxt, c0);
+            compute(ga, ua, c0 + c);
+            if (c + 1 >= nb) break;
+            if (c + 2 < nb) load(ga, ua, cur, c0 + c + 2);
+            else if (more) load(ga, ua, nxt, c0);
+            compute(gb, ub, c0 + c + 1);
         }
-        // token col's slot row (routed: -1 when the token did not pick this expert) and weight
-        int slot = -1;
-        float wk = 1.f;
-        if (cur.shared) {
-            slot = col < a.T ? col : -1;
-        } else {
-            const int* rec = a.grp + MOE_GRP_REC * (1 + cur.s);
-            const int cnt = rec[1];
-            for (int q = 0; q < cnt; ++q) {
-                const int r = rec[2 + q];
-                if (r / a.topk == col) { slot = r; wk = __int_as_float(rec[10 + q]); }
-            }
-        }
-        if (slot >= 0) {
-            const float sc = scl[col];
-            float hv[4];
+        if (KS > 1) {
+            if (piece > 0) {
+                // the unit's first wave has read this slot's previous partials (almost never waits)
+                while (lds_load_relaxed(&hand[NU + us]) < n) __builtin_amdgcn_s_sleep(1);
+                red[wave][0][lane] = accg;
+                red[wave][1][lane] = accu;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partials are in LDS before the count
+                if (lane == 0) __hip_atomic_fetch_add(&hand[us], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                while (lds_load_relaxed(&hand[us]) < (n + 1) * (KS - 1)) __builtin_amdgcn_s_sleep(1);
+                asm volatile("" ::: "memory");
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float gs = accg[i] * sc, us = accu[i] * sc;
-                const float h = (gs / (1.0f + expf(-gs))) * us;
-                hv[i] = cur.shared ? h : h * wk;
+                for (int q = 1; q < KS; ++q) {
+                    const f32x4 pg = red[wave + q][0][lane], pu = red[wave + q][1][lane];
+                    accg[0] += pg[0]; accg[1] += pg[1]; accg[2] += pg[2]; accg[3] += pg[3];
+                    accu[0] += pu[0]; accu[1] += pu[1]; accu[2] += pu[2]; accu[3] += pu[3];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the slot is released
+                if (lane == 0) __hip_atomic_fetch_add(&hand[NU + us], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            float* dst = cur.shared ? a.hs + (long)slot * a.Is : a.h + (long)slot * a.I;
-            *reinterpret_cast<float4*>(dst + cur.i0 + 4 * g) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        }
+        if (piece == 0) {
+            // token col's slot row (routed: -1 when the token did not pick this expert) and weight
+            int slot = -1;
+            float wk = 1.f;
+            if (cur.shared) {
+                slot = col < a.T ? col : -1;
+            } else {
+                const int* rec = a.grp + MOE_GRP_REC * (1 + cur.s);
+                const int cnt = rec[1];
+                for (int q = 0; q < cnt; ++q) {
+                    const int r = rec[2 + q];
+                    if (r / a.topk == col) { slot = r; wk = __int_as_float(rec[10 + q]); }
+                }
+            }
+            if (slot >= 0) {
+                const float sc = scl[col];
+                float hv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float gs = accg[i] * sc, us_ = accu[i] * sc;
+                    const float h = (gs / (1.0f + expf(-gs))) * us_;
+                    hv[i] = cur.shared ? h : h * wk;
+                }
+                float* dst = cur.shared ? a.hs + (long)slot * a.Is : a.h + (long)slot * a.I;
+                *reinterpret_cast<float4*>(dst + cur.i0 + 4 * g) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+            }
         }
         accg = f32x4{0.f, 0.f, 0.f, 0.f};
         accu = f32x4{0.f, 0.f, 0.f, 0.f};
         cur = nxt;
-        if (nch & 1) {  // odd batch count: the next unit's first batch landed in the b buffers
+        if (nb & 1) {  // odd batch count: the next unit's first batch landed in the b buffers
 #pragma unroll
             for (int i = 0; i < PF; ++i) { ga[i] = gb[i]; ua[i] = ub[i]; }
         }
         first = false;
     }
 }
+
+// waves per unit: DSOCR_GU_KS = 1 / 2 / 4 (default 2; K / 32 / PF batches must divide by it).  Measured at
+// 8 pages (`profiles/r04_bench8*_gu_ks*.log`): 2 beats 1 (16 experts: 19.5 -> 15.6 us wave span, 30: 34.3 ->
+// 32.9) and 4 (one block per CU at this register count: 3.5 rounds of pieces); a 128-register budget (two
+// blocks per CU) spilled and ran 1.6x slower
+static int gu_ks() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DSOCR_GU_KS");
+        v = e ? atoi(e) : 2;
+        if (v != 1 && v != 2 && v != 4) v = 2;
+    }
+    return v;
+}
+
 
 bool moe_gateup_mm_ok(const MoeDec2Args& a) {
     const bool swz_ok = !a.Wgu_swz || !a.sWgu || a.sWgu_swz;
@@ -518,15 +570,36 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
     const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.K);
     const int slots = std::min(a.E, a.T * a.topk);
     const int max_units = (a.sWgu ? a.Is / 16 : 0) + slots * (a.I / 16);
-#define DSOCR_GM(WTY, SW)                                                                                       \
-    do {                                                                                                        \
-        static int resident = 0;                                                                                \
-        if (!resident) resident = mm_resident_blocks((const void*)moe_gateup_mm_kernel<WTY, 5, SW>, 512, lds);  \
-        const int blocks = std::max(1, std::min(resident, (max_units + 7) / 8));                               \
-        DSOCR_LAUNCH((moe_gateup_mm_kernel<WTY, 5, SW>), dim3(blocks), dim3(512), lds, s, a);                    \
+    int ks = gu_ks();
+    while (ks > 1 && ((a.K >> 5) / 5) % ks) ks >>= 1;
+#define DSOCR_GM(WTY, SW, KS)                                                                                          \
+    do {                                                                                                            \
+        static int resident = 0;                                                                                    \
+        if (!resident) {                                                                                            \
+            /* the pieces' LDS (16 KB) takes the block past 64 KB: allowed per kernel */                            \
+            (void)hipFuncSetAttribute((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS>,                            \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                       \
+            resident = mm_resident_blocks((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS>, 512, lds);             \
+        }                                                                                                           \
+        const int blocks = std::max(1, std::min(resident, (max_units + 8 / KS - 1) / (8 / KS)));                  \
+        DSOCR_LAUNCH((moe_gateup_mm_kernel<WTY, 5, SW, KS>), dim3(blocks), dim3(512), lds, s, a);                    \
+        static bool checked = false;                                                                                \
+        if (!checked) {                                                                                             \
+            const hipError_t e = hipPeekAtLastError();                                                              \
+            if (e != hipSuccess)                                                                                    \
+                throw std::runtime_error(std::string("EINTERNAL: moe_gateup_mm launch: ") + hipGetErrorString(e)); \
+            checked = true;                                                                                         \
+        }                                                                                                           \
     } while (0)
-    if (a.wdtype == WDT_BF16) { if (a.Wgu_swz) DSOCR_GM(bf16_t, true); else DSOCR_GM(bf16_t, false); }
-    else { if (a.Wgu_swz) DSOCR_GM(f16_t, true); else DSOCR_GM(f16_t, false); }
+#define DSOCR_GMK(WTY, SW)                  \
+    do {                                    \
+        if (ks == 4) DSOCR_GM(WTY, SW, 4);  \
+        else if (ks == 2) DSOCR_GM(WTY, SW, 2); \
+        else DSOCR_GM(WTY, SW, 1);          \
+    } while (0)
+    if (a.wdtype == WDT_BF16) { if (a.Wgu_swz) DSOCR_GMK(bf16_t, true); else DSOCR_GMK(bf16_t, false); }
+    else { if (a.Wgu_swz) DSOCR_GMK(f16_t, true); else DSOCR_GMK(f16_t, false); }
+#undef DSOCR_GMK
 #undef DSOCR_GM
 }
 

@@ -30,6 +30,7 @@ for step in "$@"; do
     kbench) run 300 ./tools/kbench $KB_CASES > gpurun_out/kbench.log 2>&1 ;;
     mb) run 120 ./tools/mb_stream > gpurun_out/mb_stream.log 2>&1 ;;
     mbb) run 120 ./tools/mb_barrier > gpurun_out/mb_barrier.log 2>&1 ;;
+    mbu) run 120 ./tools/mb_units > gpurun_out/mb_units.log 2>&1 ;;
     pmc_fetch) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_fetch.log 2>&1 ;;
     pmc_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc_write.log 2>&1 ;;
     pmc_calib) run 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_calib -o mb --output-format csv -- ./tools/mb_stream > gpurun_out/pmc_calib.log 2>&1 ;;
@@ -44,6 +45,7 @@ for step in "$@"; do
     k_r4) run 400 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -k "qkv_attention or test_attention or lmhead or screened" -rf -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/k_r4.log 2>&1 ;;
     m_r4) run 600 python -u -m pytest tests/test_gpu_model.py -q -m gpu -k "oproj_route or full_screened" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/m_r4.log 2>&1 ;;
     dsq_r4) run 900 python -u -m pytest tests/test_dsq.py -q -m gpu -k "full_q4k" -rf -p no:cacheprovider --timeout 600 --timeout-method thread > gpurun_out/dsq_r4.log 2>&1 ;;
+    kmoe) run 400 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -k "moe_decode" -rf -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/kmoe${TAG:+_$TAG}.log 2>&1 ;;
     kb_qa) run 180 ./tools/kbench qkvattn1 > gpurun_out/kb_qkvattn.log 2>&1 ;;
     gprof64_maps) DSOCR_SEGV_MAPS=1 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof64_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof64_maps.log 2>&1 ;;
     # graph-mode kernel trace of a whole bench line (512 tokens), default runtime settings
@@ -62,7 +64,7 @@ for step in "$@"; do
     benchx) run 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench_${TAG:-x}.log 2>&1 ;;
     bench8x) run 600 python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench8_${TAG:-x}.log 2>&1 ;;
     benchq4k) run 900 python bench.py --snapshot q4k --pages-per-gpu 8 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/benchq4k.log 2>&1 ;;
-    bench8i) run 900 python bench.py --pages-per-gpu 8 --steps 2 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench8i.log 2>&1 ;;
+    bench8i) run 900 python bench.py --pages-per-gpu 8 --steps 2 --warmup 1 --no-cpu-baseline --roofline-iters 8 > gpurun_out/bench8i${TAG:+_$TAG}.log 2>&1 ;;
     pmc8t_fetch) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc8t_fetch -o pmc --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc8t_fetch.log 2>&1 ;;
     pmc8t_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc8t_write -o pmc --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc8t_write.log 2>&1 ;;
     gprof8t_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8t_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8t_nopc.log 2>&1 ;;
