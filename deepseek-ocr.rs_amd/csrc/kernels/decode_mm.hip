@@ -613,15 +613,18 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
 // ticket completes the tile (every segment stored) sums the segments in order (records by expert id,
 // then the shared pieces) with sc1 loads and adds to out (split-K seam: MI355X_MICROARCH.md price list
 // 'splitk-seam'; hand-off: the sc1-load table's first row).
-template <typename WT, int PF, bool SWZ, int NWV>
-__global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a) {
+template <typename WT, int PF, bool SWZ, int NWV, int KS>
+__global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Args a) {
     WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
     constexpr int RT = 16 * NWV, U = 2;  // rows per unit (16 per wave), chunks per lane (I <= 1024)
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
     __shared__ int last_s;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NW = NWV * KS;  // KS waves per 16-row tile, each a K / KS piece (met in LDS)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rw = wave % NWV, piece = wave / NWV;
     const int col = lane & 15, g = lane >> 4;
     const int n_act = a.grp[0];
     const int n_sh = a.sWd ? a.Is / a.I : 0;
@@ -634,8 +637,8 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
     const int hpiece = seg - n_act;
     const int* rec = a.grp + MOE_GRP_REC * (1 + (shared ? 0 : seg));
     const int e = shared ? 0 : rec[0];
-    const int steps = a.I >> 5, nch = steps / PF;
-    const int j0 = tile * RT + 16 * wave;
+    const int steps = a.I >> 5, nch = steps / PF / KS, c0 = piece * nch;  // nch: batches of this piece
+    const int j0 = tile * RT + 16 * rw;
     // A stream: rows j0 .. j0 + 15 of the segment's down matrix over its I columns
     const WT* pa;
     long fs = 32;
@@ -673,16 +676,17 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
         }
         return p;
     };
-    constexpr int SPW = MM_MT / NWV;  // token columns staged per wave
+    constexpr int SPW = MM_MT / NW;  // token columns staged per wave
+    static_assert(SPW >= 1 && MM_MT % NW == 0, "whole token columns per wave");
     const float* srcrow[SPW];
     MmRowU<U> xr[SPW];
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
-        srcrow[q] = src_of(wave + q * NWV);
+        srcrow[q] = src_of(wave + q * NW);
         if (srcrow[q]) mm_row_load<false, U>(xr[q], srcrow[q], a.I, nullptr);
     }
-    load(fa, 0);
-    if (nch > 1) load(fb, 1);
+    load(fa, c0);
+    if (nch > 1) load(fb, c0 + 1);
     const int KP = mm_pitch(a.I);
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
@@ -692,7 +696,7 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) xr[q].v[u][j] = 0.f;
         }
-        mm_row_store<WT, false, U>(xr[q], a.I, 0.f, xp, KP, scl, wave + q * NWV);
+        mm_row_store<WT, false, U>(xr[q], a.I, 0.f, xp, KP, scl, wave + q * NW);
     }
     __syncthreads();
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
@@ -709,16 +713,27 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
         }
     };
     for (int c = 0; c < nch; c += 2) {
-        if (c + 1 < nch && c > 0) load(fb, c + 1);
-        compute(fa, c);
+        if (c + 1 < nch && c > 0) load(fb, c0 + c + 1);
+        compute(fa, c0 + c);
         if (c + 1 >= nch) break;
-        if (c + 2 < nch) load(fa, c + 2);
-        compute(fb, c + 1);
+        if (c + 2 < nch) load(fa, c0 + c + 2);
+        compute(fb, c0 + c + 1);
+    }
+    if (KS > 1) {  // the pieces of a row tile meet in LDS, summed in piece order by piece 0
+        __shared__ f32x4 red[KS > 1 ? KS - 1 : 1][NWV][64];
+        if (piece > 0) red[piece - 1][rw][lane] = acc;
+        __syncthreads();
+        if (piece == 0)
+#pragma unroll
+            for (int q = 0; q < KS - 1; ++q) {
+                const f32x4 o = red[q][rw][lane];
+                acc[0] += o[0]; acc[1] += o[1]; acc[2] += o[2]; acc[3] += o[3];
+            }
     }
     // partial tile -> part[seg][t][j]: one 16-byte write-through (sc1) store per lane (rows 4g .. 4g + 3
     // of token column col); tokens outside the segment are zero columns
     const auto prs = __builtin_amdgcn_make_buffer_rsrc(a.dn_part, (short)0, 0x7fffffff, 0x00020000);
-    if (col < a.T) {
+    if (piece == 0 && col < a.T) {
         const float sc = scl[col];
         const float v4[4] = {acc[0] * sc, acc[1] * sc, acc[2] * sc, acc[3] * sc};
         u32x4 bits;
@@ -746,7 +761,8 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
     // (s_0 + .. + s_{h-1}) + (s_h + .. + s_{n-1}), a fixed order.
     static_assert(NWV == 4 && RT * MM_MT / 4 == 128, "tail layout: 128 row quads x 2 halves = 256 threads");
     __shared__ float4 half_s[128];
-    const int q4 = tid & 127, hf = tid >> 7;
+    const int q4 = tid & 127, hf = tid >> 7;  // threads past 256 (KS > 1) take no part
+    const bool tl = tid < 256;
     const int t = q4 / (RT / 4), j = tile * RT + (q4 % (RT / 4)) * 4;
     const int nh = (n_seg + 1) >> 1;
     const int sb = hf ? nh : 0, se = hf ? n_seg : nh;
@@ -754,7 +770,7 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
     // the residual quad, loaded with the segments (not after the halves meet: one round trip fewer)
     float4* op = reinterpret_cast<float4*>(a.out + (long)min(t, a.T - 1) * a.Hout + j);
     const float4 o_in = hf ? make_float4(0.f, 0.f, 0.f, 0.f) : *op;
-    if (t < a.T) {
+    if (tl && t < a.T) {
         constexpr int SB = 18;  // segments in flight per batch (n_seg <= 72: at most 2 batches per half)
         const long sstride = (long)MM_MT * a.Hout * 4;
         const int base = (int)(((long)t * a.Hout + j) * 4);
@@ -774,7 +790,7 @@ __global__ __launch_bounds__(64 * NWV, 4) void moe_down_mm_kernel(MoeDec2Args a)
             }
         }
     }
-    if (hf) half_s[q4] = v;
+    if (hf == 1) half_s[q4] = v;
     __syncthreads();
     if (!hf && t < a.T) {
         const float4 u = half_s[q4];
@@ -799,13 +815,28 @@ size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H) {
 }
 
 // Units of 64 output rows (4 waves): 17 segments x 20 row tiles = 340 blocks at 8 pages, where 128-row
-// units (8 waves) left a third of the CUs idle (170 blocks).
+// units (8 waves) left a third of the CUs idle (170 blocks).  Two waves per 16-row tile, each half of K (8
+// waves per block; DSOCR_DN_KS = 1 for one): 16 experts 12.9 -> 12.0 us wave span, 30 unchanged (21.0 / 21.3:
+// 680 blocks of 512 threads take 1.3 residency rounds), `profiles/r04_bench8{t,i}_dn_ks{1,2}.log`.
+static int dn_ks() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DSOCR_DN_KS");
+        v = e && atoi(e) == 1 ? 1 : 2;
+    }
+    return v;
+}
+
 void launch_moe_down_mm(const MoeDec2Args& a, hipStream_t s) {
     if (!moe_down_mm_ok(a)) throw std::runtime_error("EINVAL: grouped decode down (matrix cores) outside its range");
     const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.I);
     const int max_seg = std::min(a.E, a.T * a.topk) + (a.sWd ? a.Is / a.I : 0);
     dim3 grid(max_seg * (a.Hout / 64));
-#define DSOCR_DM(WTY, SW) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 4>), grid, dim3(256), lds, s, a)
+#define DSOCR_DM(WTY, SW)                                                                              \
+    do {                                                                                               \
+        if (dn_ks() == 2 && ((a.I >> 5) / 7) % 2 == 0) DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 4, 2>), grid, dim3(512), lds, s, a); \
+        else DSOCR_LAUNCH((moe_down_mm_kernel<WTY, 7, SW, 4, 1>), grid, dim3(256), lds, s, a);          \
+    } while (0)
     if (a.wdtype == WDT_BF16) { if (a.Wd_swz) DSOCR_DM(bf16_t, true); else DSOCR_DM(bf16_t, false); }
     else { if (a.Wd_swz) DSOCR_DM(f16_t, true); else DSOCR_DM(f16_t, false); }
 #undef DSOCR_DM
