@@ -184,6 +184,7 @@ __global__ __launch_bounds__(64 * WR * WK) void dec_mm_kernel(DecGemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
     __shared__ f32x4 red[WK > 1 ? WK - 1 : 1][WR][64];
+    __shared__ float res_s[WR == 1 ? MM_MT : 1][16];  // one tile per block: its residual rows, loaded up front
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int KP = mm_pitch(a.K);
     constexpr int NW = WR * WK;
@@ -218,9 +219,17 @@ __global__ __launch_bounds__(64 * WR * WK) void dec_mm_kernel(DecGemvArgs a) {
     if (NW < MM_MT && m1 < a.M) mm_row_load<NORM>(r1, a.x + (long)m1 * a.ldx, a.K, a.norm_w);
     int bt = blockIdx.x;
     const WT* cur = rowp(bt);
+    // the residual rows of the block's one tile (WR == 1), with the first loads: the staging barrier waits
+    // for them together, and the epilogue reads LDS instead of a dependent global round trip (8 text pages:
+    // decode 638.8-639.2 -> 636.2-636.5 ms, `profiles/r04_bench8t_mm_respre{0,1}*.log`; held in LDS, not
+    // registers: the register version cost occupancy)
+    float rv = 0.f;
+    if (WR == 1 && a.accumulate && tid < 16 * MM_MT && (tid >> 4) < a.M)
+        rv = a.y[(long)(tid >> 4) * a.ldy + min(bt * 16 + (tid & 15), a.N - 1)];
     load(fa, cur, 0);
     if (m0 < a.M) mm_row_store<WT, NORM>(r0, a.K, a.eps, xp, KP, scl, m0);
     if (NW < MM_MT && m1 < a.M) mm_row_store<WT, NORM>(r1, a.K, a.eps, xp, KP, scl, m1);
+    if (WR == 1 && a.accumulate && tid < 16 * MM_MT) res_s[WR == 1 ? tid >> 4 : 0][tid & 15] = rv;
     __syncthreads();
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * Q * g;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(64 * WR * WK) void dec_mm_kernel(DecGemvArgs a) {
                 const int nn = tile * 16 + 4 * g + i;
                 if (nn < a.N) {
                     float v = apply_act(acc[i] * s + (a.bias ? a.bias[nn] : 0.f), a.act);
-                    if (a.accumulate) v = yr[nn] + v;
+                    if (a.accumulate) v = (WR == 1 ? res_s[WR == 1 ? col : 0][4 * g + i] : yr[nn]) + v;
                     yr[nn] = v;
                 }
             }
