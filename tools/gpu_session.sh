@@ -40,7 +40,8 @@ for step in "$@"; do
     # graph-mode kernel trace with the HIP runtime's graph packet capture off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0)
     gprof_nopc) DSOCR_SEGV_MAPS=1 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_nopc -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_nopc.log 2>&1 ;;
     gprof8_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8_nopc.log 2>&1 ;;
-    # the round-2 crash reproduced with the maps dump (expected SIGSEGV: run it last)
+    # graph-mode trace with packet capture on and the SIGSEGV maps dump armed (the round-2 crash; it no longer
+    # reproduces on the round-4 tree: profiles/r04_gprof{32,64}_packet_capture_on.log)
     gprof_maps) DSOCR_SEGV_MAPS=1 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof_maps -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 32 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof_maps.log 2>&1 ;;
     k_r4) run 400 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -k "qkv_attention or test_attention or lmhead or screened" -rf -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/k_r4.log 2>&1 ;;
     m_r4) run 600 python -u -m pytest tests/test_gpu_model.py -q -m gpu -k "oproj_route or full_screened" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/m_r4.log 2>&1 ;;
