@@ -3143,6 +3143,16 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
     const int jc = min(tid, a.nblk - 1);
     float T = bt[jc];
     const int c0 = bc[jc];
+    // block jc's first E kept rows: they do not depend on T, so they load in this round trip too
+    constexpr int E = 16;
+    float h[E];
+    int v[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        const long e = sb + (long)min(i, (int)a.slot - 1) * a.nblk + jc;
+        h[i] = a.cand_hi[e];
+        v[i] = a.cand[e];
+    }
     if (tid >= a.nblk) T = -INFINITY;
     for (int j = tid + NT; j < a.nblk; j += NT) T = fmaxf(T, bt[j]);
     const int lc = max(last_i, 0);
@@ -3156,17 +3166,8 @@ __global__ __launch_bounds__(NT) void dec_screen_final_kernel(DecSampleArgs a) {
 #pragma unroll
     for (int w = 1; w < NT / 64; ++w) T = fmaxf(T, sv[w]);
     SP_STAMP(0)
-    // ---- kept rows whose upper bound reaches T: a block's first E entries in one round trip
+    // ---- kept rows whose upper bound reaches T (a block's first E entries are already in registers)
     if (tid < a.nblk) {
-        constexpr int E = 16;
-        float h[E];
-        int v[E];
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-            const long e = sb + (long)min(i, (int)a.slot - 1) * a.nblk + tid;
-            h[i] = a.cand_hi[e];
-            v[i] = a.cand[e];
-        }
         if (a.stats) atomicAdd(&nban_s, c0);  // (diagnostics: kept rows, reset below)
 #pragma unroll
         for (int i = 0; i < E; ++i)
