@@ -851,17 +851,17 @@ __device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softm
 }
 
 // Decode router for T <= 8 tokens, E <= 64 experts: RMSNorm + router logits + greedy top-k +
-// expert records in one launch.  Blocks of 8 waves, one expert row per wave.  Wave w normalises
-// token row w in the GEMV chunk layout (lane: chunks lane, lane+64, lane+128; its squares summed
-// u-major then j, one wave sum, x / den * w — dec_gemv_rows' NORM form) into LDS (block 0 also
-// hands the rows to the expert kernels: xn_out), then every wave dots its expert row with the T
-// rows (dec_gemv's per-row arithmetic).  Logits are stored write-through (sc1); the last block to
+// expert records in one launch.  Blocks of 8 waves and 8 expert rows.  Wave w normalises token row w
+// in the GEMV chunk layout (lane: chunks lane, lane+64, lane+128; its squares summed u-major then j,
+// one wave sum, x / den * w — dec_gemv_rows' NORM form) in registers and puts expert row w of the
+// block into LDS; then wave w dots its token row with the block's 8 expert rows (dec_gemv's per-row
+// arithmetic; the last block also hands the rows to the expert kernels: xn_out).  Logits are stored write-through (sc1); the last block to
 // take its ticket reads them back with sc1 loads (MI355X_MICROARCH.md hand-offs, first row), routes
 // token w on wave w (topk_wave64) and wave 0 groups the picks by expert (MOE_GRP_* records).
 template <typename WT>
 __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRouteEpi r) {
     constexpr int U = 3, MT = 8;  // K <= 1536, T <= 8
-    extern __shared__ __attribute__((aligned(16))) float xs[];  // [MT][K]
+    extern __shared__ __attribute__((aligned(16))) uint4 ws[];  // [8 experts][K / 8] 16-bit weight chunks
     __shared__ float lg_s[MT][64];
     __shared__ float rank_s[MT][64];
     __shared__ int ids_s[64];
@@ -871,15 +871,20 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
 #define RG_STAMP(i)                                                      \
     if (r.stamps && tid == 0 && (blockIdx.x == 0 || (i) >= 5)) r.stamps[i] = __builtin_amdgcn_s_memrealtime();
     RG_STAMP(0);
-    const int n = blockIdx.x * MT + wave;
+    const int n0 = blockIdx.x * MT;
     const int chunks = a.K >> 3;
     const WT* W = reinterpret_cast<const WT*>(a.W);
+    // wave w: expert row n0 + w into LDS (16-bit, as stored) and token row w normalised in registers; then
+    // every wave dots its token row with the block's 8 expert rows.  The products and their order per
+    // (token, expert) are dec_gemv's (lane chunks u-major, then j; one wave sum); the LDS traffic is the
+    // 16-bit weights once per wave instead of the f32 token rows once per expert (half the bytes)
     uint4 wq[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        wq[u] = ldg_nt16(W + (long)min(n, a.N - 1) * a.ldw + (min(u * 64 + lane, chunks - 1) << 3));
+        wq[u] = ldg_nt16(W + (long)min(n0 + wave, a.N - 1) * a.ldw + (min(u * 64 + lane, chunks - 1) << 3));
+    float xv[U][8];
     if (wave < a.M) {
-        float xv[U][8], nw[U][8];
+        float nw[U][8];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int cc = min(u * 64 + lane, chunks - 1);
@@ -900,51 +905,42 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
 #pragma unroll
                 for (int j = 0; j < 8; ++j) xv[u][j] = (xv[u][j] / den) * nw[u][j];
         }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = u * 64 + lane;
+        if (c < chunks) ws[wave * chunks + c] = wq[u];
+    }
+    __syncthreads();
+    RG_STAMP(2);
+    RG_STAMP(3);
+    float mine = 0.f;  // lane e keeps expert n0 + e's logit for token `wave`
+    if (wave < a.M) {
+        float acc[MT];
+#pragma unroll
+        for (int e = 0; e < MT; ++e) acc[e] = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = u * 64 + lane;
             if (c < chunks) {
-                const float4 lo = make_float4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]);
-                const float4 hi = make_float4(xv[u][4], xv[u][5], xv[u][6], xv[u][7]);
-                float* d = xs + (long)wave * a.K + (c << 3);
-                *reinterpret_cast<float4*>(d) = lo;
-                *reinterpret_cast<float4*>(d + 4) = hi;
+#pragma unroll
+                for (int e = 0; e < MT; ++e) {
+                    float w8[8];
+                    unpack8<WT>(ws[e * chunks + c], w8);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[e] = fmaf(xv[u][j], w8[j], acc[e]);
+                }
             }
         }
-    }
-    __syncthreads();
-    RG_STAMP(2);
-    float w8[U][8];
 #pragma unroll
-    for (int u = 0; u < U; ++u) unpack8<WT>(wq[u], w8[u]);
-    RG_STAMP(3);
-    // every token row unconditionally (rows past M clamp to row M-1, discarded): the 8 FMA chains and
-    // wave sums are independent and interleave
-    float acc[MT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = 0.f;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int c = u * 64 + lane;
-        if (c < chunks) {
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                float xv[8];
-                ld_x8(xs + (long)min(m, a.M - 1) * a.K + (c << 3), xv);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[m] = fmaf(xv[j], w8[u][j], acc[m]);
-            }
+        for (int e = 0; e < MT; ++e) {
+            const float v = wave_sum(acc[e]) + (a.bias ? a.bias[min(n0 + e, a.N - 1)] : 0.f);
+            if (lane == e) mine = v;
         }
-    }
-    const float bias = a.bias ? a.bias[min(n, a.N - 1)] : 0.f;
-    float mine = 0.f;  // lane m keeps token m's logit
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-        const float v = wave_sum(acc[m]) + bias;
-        if (lane == m) mine = v;
     }
     RG_STAMP(4);
-    if (n < a.N && lane < a.M) __hip_atomic_store(a.y + (long)lane * a.ldy + n, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave < a.M && lane < MT && n0 + lane < a.N)
+        __hip_atomic_store(a.y + (long)wave * a.ldy + n0 + lane, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -1014,15 +1010,17 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
         }
         if (lane == 0) r.grp[0] = __popcll(bm);
     }
-    // the normalised rows for the expert kernels, from this (last) block's LDS after its last barrier: a global
-    // store before a barrier makes the barrier wait for its acknowledgement (block 0 stored them during the
-    // staging and reached the ticket ~1 us late)
+    // the normalised rows for the expert kernels, from this (last) block's registers after its last barrier: a
+    // global store before a barrier makes the barrier wait for its acknowledgement
     if (a.xn_out && wave < a.M)
-        for (int c = lane; c < chunks; c += 64) {
-            const float* sp = xs + (long)wave * a.K + (c << 3);
-            float* g = a.xn_out + (long)wave * a.K + (c << 3);
-            *reinterpret_cast<float4*>(g) = *reinterpret_cast<const float4*>(sp);
-            *reinterpret_cast<float4*>(g + 4) = *reinterpret_cast<const float4*>(sp + 4);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = u * 64 + lane;
+            if (c < chunks) {
+                float* g = a.xn_out + (long)wave * a.K + (c << 3);
+                *reinterpret_cast<float4*>(g) = make_float4(xv[u][0], xv[u][1], xv[u][2], xv[u][3]);
+                *reinterpret_cast<float4*>(g + 4) = make_float4(xv[u][4], xv[u][5], xv[u][6], xv[u][7]);
+            }
         }
     RG_STAMP(7);
 #undef RG_STAMP
@@ -1037,7 +1035,7 @@ void launch_dec_route_grp(const DecGemvArgs& a, const DecRouteEpi& r, hipStream_
     if (!dec_route_grp_ok(a.M, a.N, a.K, r.topk) || !r.ids || !r.w || !r.counter || !a.y)
         throw std::runtime_error("EINVAL: decode router (grouped) outside its range");
     dim3 grid((a.N + 7) / 8);
-    const size_t lds = sizeof(float) * 8 * (size_t)a.K;
+    const size_t lds = sizeof(uint16_t) * 8 * (size_t)a.K;
     if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((dec_route_grp_kernel<bf16_t>), grid, dim3(512), lds, s, a, r);
     else DSOCR_LAUNCH((dec_route_grp_kernel<f16_t>), grid, dim3(512), lds, s, a, r);
 }
