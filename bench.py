@@ -338,6 +338,69 @@ def run_dots(args, rank, world, local, dist):
     }
 
 
+def decode_roofline(eng, batch, params, ppg, args):
+    """The roofline object of the decode MoE gate/up (the north-star kernel) at this batch size, from three
+    extra generates of the first timed batch (rank 0, after the timed region):
+      1. HIP events around every gate/up / down / attention launch inside the replayed step graph (no extra
+         kernel in the step): the dispatch-level duration rocprofv3's kernel trace reports for the same
+         launch (previous launch's end -> this launch's end, i.e. its boundary included), over every decode
+         step -> `avg_launch_us`, `achieved`, `frac`;
+      2. in-kernel wave spans (first wave entry -> last wave exit, s_memrealtime) of the same launches, each
+         launch's distinct experts recorded -> `in_kernel_waves`, and the per-launch pricing of (1) (same
+         batch, same routing: the ids of the two generates are checked equal);
+      3. profile_decode: one step's layers replayed as a graph with and without the gate/up launches ->
+         `in_context` (secondary)."""
+    import dsocr
+    dims = lang_dims(json.load(open(dsocr.FULL_CONFIG)))
+    P = len(batch[0][0])
+    eng.set_spans(eng.SPAN_WAVES)
+    ids_w = eng.generate_batch(batch, params, ignore_eos=True)
+    spans_w = eng.spans()
+    eng.set_spans(eng.SPAN_EVENTS)
+    ids_e = eng.generate_batch(batch, params, ignore_eos=True)
+    spans_e = eng.spans()
+    eng.set_spans(0)
+    if ids_w != ids_e:
+        raise RuntimeError("span generates of one batch emitted different ids")
+    for k in spans_e:  # events-only records carry no expert counts: the wave-span generate's (same routing)
+        spans_e[k][..., 2] = spans_w[k][..., 2]
+    waves = span_roofline(spans_w, dims, ppg, P)
+    disp = span_roofline(spans_e, dims, ppg, P)
+    prof = eng.profile_decode(args.roofline_iters)
+    kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
+
+    def ctx_line(k):
+        p = prof[k]
+        return {"ctx_us": round(p["ctx_us"], 3), "bytes": p["bytes"],
+                "GB/s": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9, 1) if p["ctx_us"] > 0 else None,
+                "frac": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if p["ctx_us"] > 0 else None,
+                "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
+    gu = disp["moe_gateup"]
+    runs = ("b1",) if ppg == 1 else (("b8",) if args.text_pages and ppg == 8 else (("b8i",) if ppg == 8 else ()))
+    return {"bound": "hbm", "achieved": round(gu["GB/s"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gu["frac"], 4), "traffic": pmc_traffic(kernel, runs=runs),
+            "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
+            # avg_launch_us = mean dispatch duration over every gate/up launch of a whole generate (HIP events
+            # on the engine stream around each launch inside the replayed step graph: previous launch end ->
+            # this launch end, as rocprofv3 reports a back-to-back dispatch); achieved = the launches'
+            # algorithmic bytes (each priced at its own distinct experts) / their summed durations
+            "avg_launch_us": round(gu["avg_us"], 3), "bytes_per_launch": gu["bytes_per_launch"],
+            "launches": gu["launches"], "experts_mean": gu["experts_mean"],
+            "timing": "dispatch duration: HIP events around each launch in the replayed step graph, every decode step",
+            "dispatch": disp,
+            "in_kernel_waves": waves,
+            "down_kernel": prof["moe_down_kernel"],
+            # secondary: one step's layers replayed with and without the gate/up launches, (full - without) / layers
+            "in_context": {k: ctx_line(k) for k in ("moe_gateup", "moe_down", "attention")},
+            "experts_touched_profile_step": prof["experts_touched"],
+            "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
+                           "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
+                       for k in ("lm_head", "lm_head_screened", "qkv", "o_proj", "router")
+                       if prof.get(k, {}).get("avg_us", 0) > 0},
+            "layers_step_us": round(prof["layers_step"]["avg_us"], 1),
+            "kv_len": prof["kv_len"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -348,6 +411,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-decode-steps", type=int, default=0, help="(unused: the C++ baseline times every decode step)")
     ap.add_argument("--roofline-iters", type=int, default=20)
+    ap.add_argument("--trace-only", action="store_true",
+                    help="production-only run for a rocprofv3 kernel trace: the timed generates and nothing else "
+                         "(no span / event / profile_decode generates, no CPU baseline); roofline is null")
     ap.add_argument("--workload", default="deepseek", choices=["deepseek", "dots2048"],
                     help="deepseek: configs[1]/[2] (default); dots2048: configs[3], the dots.ocr vision tower")
     ap.add_argument("--dots-size", type=int, default=2048,
@@ -476,48 +542,9 @@ def main():
 
     result = None
     if rank == 0:
-        # in context: the first timed batch decoded once more with launch spans on (every step's graph
-        # replay; each stamped launch is followed by a one-block fold launch, outside its own span)
-        # in-kernel wave spans over a whole generate (the first timed batch decoded again with every
-        # MoE / attention launch's first-wave entry and last-wave exit recorded, expert counts per launch)
-        dims = lang_dims(json.load(open(dsocr.FULL_CONFIG)))
-        P = len(batches[args.warmup][1][0][0])
-        eng.set_spans(eng.SPAN_WAVES)
-        eng.generate_batch(batches[args.warmup][1], params, ignore_eos=True)
-        eng.set_spans(0)
-        waves = span_roofline(eng.spans(), dims, ppg, P)
-        prof = eng.profile_decode(args.roofline_iters)
-        kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
-
-        def ctx_line(k):
-            p = prof[k]
-            return {"ctx_us": round(p["ctx_us"], 3), "bytes": p["bytes"],
-                    "GB/s": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9, 1) if p["ctx_us"] > 0 else None,
-                    "frac": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if p["ctx_us"] > 0 else None,
-                    "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
-        gu = ctx_line("moe_gateup")
-        roofline = {"bound": "hbm", "achieved": gu["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gu["frac"],
-                    "traffic": pmc_traffic(kernel, runs=("b1",) if ppg == 1 else (("b8",) if args.text_pages and ppg == 8 else ())),
-                    "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
-                    # avg_launch_us = in-context duration: (one decode step's layers replayed as a hipGraph - the
-                    # same graph without the gate/up launches) / MoE layers, HIP events around the replays on the
-                    # engine stream: the kernel with its own dispatch inside the real dependent chain (what
-                    # rocprofv3's kernel trace reports as its duration there); bytes priced at the routing the
-                    # replayed step takes (experts_touched distinct experts)
-                    "avg_launch_us": gu["ctx_us"], "bytes_per_launch": gu["bytes"],
-                    "experts_touched": prof["experts_touched"], "timing": "in-context step-graph difference",
-                    "down_kernel": prof["moe_down_kernel"],
-                    "in_context": {k: ctx_line(k) for k in ("moe_gateup", "moe_down", "attention")},
-                    # the same launches' waves alone, over every decode step of a generate (no dispatch)
-                    "in_kernel_waves": waves,
-                    "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
-                                   "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
-                               for k in ("lm_head", "lm_head_screened", "qkv", "o_proj", "router")
-                               if prof.get(k, {}).get("avg_us", 0) > 0},
-                    "layers_step_us": round(prof["layers_step"]["avg_us"], 1),
-                    "kv_len": prof["kv_len"]}
+        roofline = None if args.trace_only else decode_roofline(eng, batches[args.warmup][1], params, ppg, args)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not snap and not args.text_pages:
+        if world == 1 and not (args.no_cpu_baseline or args.trace_only) and not snap and not args.text_pages:
             b = batches[args.warmup]
             try:
                 cpu = cpu_baseline(b[0], b[1][0][0], b[1][0][1], args.max_new_tokens, args.cpu_decode_steps)

@@ -1,6 +1,6 @@
 // Host helpers: half-precision conversions, safetensors mmap reader and the
 // deterministic synthetic-weight generator (same published recipe as the
-// oracle's synth.c; tests/test_synth.py checks byte equality).
+// oracle's synth.c; tests/test_host_cpu.py::test_synth_recipe_product_equals_oracle checks equality).
 #pragma once
 #include <fcntl.h>
 #include <sys/mman.h>

@@ -643,6 +643,14 @@ dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int h
             throw std::runtime_error("EINVAL: qkv_attention needs 128-dim MHA heads with heads * hd == H");
         if (wdtype != dsocr::WDT_F16 && wdtype != dsocr::WDT_BF16) throw std::runtime_error("EINVAL: 16-bit weights only");
         const int QKVN = 3 * H;
+        {  // range check once, before anything is allocated (it does not depend on the step)
+            dsocr::DecGemvArgs g;
+            g.M = 1; g.N = QKVN; g.K = H; g.W = Wqkv; g.ldw = H; g.wdtype = wdtype; g.y = qkv_row; g.ldy = QKVN;
+            g.x = x; g.ldx = H; g.norm_w = norm_w; g.eps = eps;
+            dsocr::DecRopeEpi re;
+            re.kv_pos = kv_pos; re.cos = cos; re.sin = sin; re.hd = hd; re.rot_rows = 2 * H;
+            if (!dsocr::dec_qkv_rope_ok(g, re)) throw std::runtime_error("EINVAL: q/k/v projection outside dec_qkv_rope's range");
+        }
         float* part = nullptr;
         int* cnt = nullptr;
         const size_t pb = dsocr::dec_attn_workspace(1, heads, hd, max_len);
@@ -663,7 +671,6 @@ dsocr_status dsocr_k_qkv_attention(int fused, int steps, int H, int heads, int h
             a.kc = kc; a.vc = vc; a.head_stride = (long)max_len * hd; a.page_stride = (long)heads * max_len * hd;
             a.scale = scale; a.part = part; a.o = o + (size_t)s * H; a.o_ld = H; a.counters = cnt; a.err = cnt + heads;
             a.prerot = 1;
-            if (!dsocr::dec_qkv_rope_ok(g, re)) throw std::runtime_error("EINVAL: q/k/v projection outside dec_qkv_rope's range");
             if (fused && dsocr::dec_qkv_attn_ok(g, re, a)) {
                 dsocr::launch_dec_qkv_attn(g, re, a, nullptr);
                 took = true;

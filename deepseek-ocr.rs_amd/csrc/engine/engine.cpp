@@ -928,8 +928,15 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     a.heads = L.heads; a.kv_heads = L.kv_heads; a.hd = hd;
     a.scale = (float)(1.0 / std::sqrt((double)hd));
     a.causal = 1;
-    a.part_floats = attention_causal_part_floats(B, L.heads, max_len, hd);
-    a.part = wsf("d_attn_part", a.part_floats);
+    // the key-piece workspace grows as L^2 (n_seq * heads * sum over query blocks of their pieces * 128 * (hd + 2)
+    // floats: 89 MB at 8 x 706 tokens, 2.8 GB at 8 x 4096); above 512 MB the prefill runs the one-block-per-
+    // query-block kernel, which needs none
+    constexpr size_t kPartCapFloats = (size_t)128 << 20;
+    const size_t part_floats = attention_causal_part_floats(B, L.heads, max_len, hd);
+    if (part_floats <= kPartCapFloats) {
+        a.part_floats = part_floats;
+        a.part = wsf("d_attn_part", a.part_floats);
+    }
     for (int q = 0; q < B && q < (int)prefill_lens_.size(); ++q)
         flops_acc_ += 2.0 * (double)prefill_lens_[q] * (prefill_lens_[q] + 1) * hd * L.heads;
     launch_attention(a, st);
@@ -1057,10 +1064,10 @@ void Engine::decode_step(int B, int Lmax) {
         if (events) HIP_CHECK(hipEventRecord(ev[0], st));
         launch();
         if (events) HIP_CHECK(hipEventRecord(ev[1], st));
-        // the fold: after every launch with wave spans; events only: once per MoE layer, after the
-        // down launch (its record carries the layer's distinct experts for both MoE launches)
-        if (waves || (kind == SPAN_DOWN && ids))
-            launch_span_reduce(span_slots_, span_rec(kind, l), span_step_, span_cap_, ids, n_ids, st);
+        // the fold (wave span + the launch's distinct experts): after every launch with wave spans only; an
+        // events-only generate runs no extra kernel, so its step is the production chain plus the event
+        // markers (bench.py prices its launches with the expert counts of a wave-span generate of the same batch)
+        if (waves) launch_span_reduce(span_slots_, span_rec(kind, l), span_step_, span_cap_, ids, n_ids, st);
     };
     for (int l = 0; l < L.layers; ++l) {
         DecLayer& d = layers_[l];
@@ -1150,7 +1157,8 @@ void Engine::decode_step(int B, int Lmax) {
             // at once) — moe_down2 walks each 6848-long row in four dependent load rounds
             MoeDec2Args dn = m;
             dn.slot_mode = 1;
-            dn.ids = wsi("s_dense_ids", 8);  // (no routed segments: read, never used)
+            dn.ids = wsi("s_dense_ids", 8);  // no routed segments at topk 0: moe_down_mix reads no id
+            if (dn.topk != 0) throw std::logic_error("dense layer with routed experts");
             if (B == 1 && moe_down_mix_ok(dn)) launch_moe_down_mix(dn, st);
             else launch_moe_down2(m, st);
             continue;
@@ -1804,12 +1812,9 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         std::vector<unsigned long long> dev(nrec * 4);
         HIP_CHECK(hipMemcpy(dev.data(), span_rec_, dev.size() * 8, hipMemcpyDeviceToHost));
         spans_host_.assign(nrec * SPAN_FIELDS, 0);
-        const size_t per_kind = (size_t)L.layers * span_cap_;
         for (size_t r = 0; r < nrec; ++r) {
             for (int f = 0; f < 4; ++f) spans_host_[r * SPAN_FIELDS + f] = dev[r * 4 + f];
             if (span_mode_ & SPAN_EVENTS) spans_host_[r * SPAN_FIELDS + 4] = (unsigned long long)llround(span_ev_ns_[r]);
-            // events only: the gate/up record takes its layer's expert count from the down record
-            if (!(span_mode_ & SPAN_WAVES) && r < per_kind) spans_host_[r * SPAN_FIELDS + 2] = dev[(per_kind + r) * 4 + 2];
         }
         spans_steps_ = span_cap_;  // reported with the records it sizes (a throwing generate leaves both)
         // profile_decode runs unstamped; every later generate is stamped again while span_mode_ is set

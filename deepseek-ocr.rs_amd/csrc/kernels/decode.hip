@@ -2440,7 +2440,7 @@ __global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
     uint4 q[RPB][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int e = a.ids[max(seg[u], 0)];  // (shared chunks ignore it)
+        const int e = seg[u] >= 0 ? a.ids[seg[u]] : 0;  // shared chunks (all of them at topk 0) read no id
 #pragma unroll
         for (int r = 0; r < RPB; ++r) {
             const int j = min(j0 + r, a.Hout - 1);

@@ -427,19 +427,22 @@ __global__ __launch_bounds__(512, 4) void lmhead_q8mm_kernel(LmHeadQ8Args a, int
     int T = t_beg + wave;
 #pragma unroll
     for (int t = 0; t < PF; ++t) wa[t] = ld(T, t);
-    if (tid < LM_T) { tkey_s[tid] = 0u; lst_n[tid] = 0; nban_s[tid] = 0; }
+    // nban_s[t] has ONE writer: the staging wave t < B below, lane t of wave 0 for the unused t >= B (a
+    // zeroing by wave 0 of every entry could land after a staging wave's count: no barrier between them)
+    if (tid < LM_T) { tkey_s[tid] = 0u; lst_n[tid] = 0; if (tid >= B) nban_s[tid] = 0; }
     // ---- stage: wave w normalises token row w (K <= 1536: float4 chunks lane + 64 j), quantises it
     // into the two planes and sums ||x||^2 and ||x - x~||^2 in f64
     if (wave < B) {
         // three passes over the row (L1-resident after the first): sum of squares; max |x|; quantise
         const float* xr = a.x + (long)wave * a.ldx;
         constexpr int J = LM_KMAX / 256;
+        int nb = 0;
         if (a.ban) {
             const int* bg = a.ban + (long)wave * a.ban_ld;
-            const int nb = bg[0];
+            nb = bg[0];
             for (int i = lane; i < min(nb, LM_BANS); i += 64) ban_s[wave][i] = bg[1 + i];
-            if (lane == 0) nban_s[wave] = nb;
         }
+        if (lane == 0) nban_s[wave] = nb;
         float q = 0.f;
 #pragma unroll
         for (int j = 0; j < J; ++j) {

@@ -211,7 +211,8 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
  * launches writes its entry / exit s_memrealtime (100 MHz) to a slot, a one-block fold launch after each
  * keeps the first entry / last exit), 2 = HIP events recorded on the stream around those launches inside
  * the replayed step graph (the dispatch-level duration rocprofv3's kernel trace reports; read back after
- * every step).  Either mode also records the distinct experts each MoE layer streamed.  The decode steps
+ * every step; no extra kernel runs, so the step is the production chain plus the event markers).  Mode 1
+ * also records the distinct experts each MoE launch streamed (mode 2 alone leaves that field 0).  The decode steps
  * of every following generate are recorded; dsocr_engine_spans copies the last such generate's records,
  * [kinds][layers][steps][5] uint64 {entry, exit, distinct experts, waves, event duration ns}, into out
  * (cap = capacity in uint64; DSOCR_EINVAL if short; out NULL: only the dimensions are returned);

@@ -71,6 +71,14 @@ for step in "$@"; do
     gprof8t_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8t_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8t_nopc.log 2>&1 ;;
     pmcdots_fetch) run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcdots_fetch -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmcdots_fetch.log 2>&1 ;;
     pmcdots_write) run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcdots_write -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmcdots_write.log 2>&1 ;;
+    # round 5
+    counters) run 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1 ;;
+    # MFMA utilisation of the vision / prefill kernels (eager launches; decode shortened to 8 tokens)
+    pmc_mfma) grep -q SQ_VALU_MFMA_BUSY_CYCLES gpurun_out/counters.txt && DSOCR_NO_GRAPH=1 run 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/pmc_mfma -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --max-new-tokens 8 --trace-only ${PMC_ARGS} > gpurun_out/pmc_mfma${TAG:+_$TAG}.log 2>&1 ;;
+    # production-only graph-mode kernel trace of the whole bench line (512 tokens): packet capture on (the
+    # runtime default), an AQL ring of 131072 packets so the profiler's ring-wrap read never happens
+    gprod) ROC_AQL_QUEUE_SIZE=131072 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprod${TAG:+_$TAG} -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --trace-only ${BENCH_ARGS} > gpurun_out/gprod${TAG:+_$TAG}.log 2>&1 ;;
+    benchr) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/benchr${TAG:+_$TAG}.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
