@@ -2318,7 +2318,7 @@ __device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int so
 }
 
 template <typename WT>
-__global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn) {
+__global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn, int routed_first) {
     constexpr int RB = 1;  // one gate + up row pair per wave (66 VGPRs: the 1792-block grid is resident at once)
     WaveSpan span_(a.span);
     __shared__ __attribute__((aligned(16))) float rank_lds[4][64];
@@ -2328,8 +2328,12 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
     const int wpr = (a.I + RB - 1) / RB;                 // routed waves per pick
     const int n_sh = a.sWgu ? (a.Is + RB - 1) / RB : 0;  // shared waves
     const int n_rt = a.topk * wpr;
-    const bool shared = wave == 0;
-    const int widx = shared ? b : 3 * b + wave - 1;
+    // wave roles: routed_first = 0: wave 0 of every block streams the shared expert, waves 1..3 a routed
+    // expert; 1: the first ceil(n_rt / 4) blocks are all routed and the shared blocks come last, so the waves
+    // with the longer chain (logits -> picks -> weights) are dispatched first and the ones without it last
+    const int nbr = (n_rt + 3) >> 2;
+    const bool shared = routed_first ? b >= nbr : wave == 0;
+    const int widx = routed_first ? (shared ? 4 * (b - nbr) + wave : 4 * b + wave) : (shared ? b : 3 * b + wave - 1);
     if (shared ? widx >= n_sh : widx >= n_rt) return;   // whole wave: no block barrier below
     const int chunks = a.K >> 3;
     const int sl = shared ? 0 : widx / wpr;
@@ -2499,14 +2503,22 @@ bool moe_gateup_mix_ok(const MoeDec2Args& a) {
            a.ids_out && a.w_out;
 }
 
+// DSOCR_GU_ORDER (A/B switch, read at every launch): 1 = routed blocks first, shared blocks last; 0 = one shared
+// wave per block
+static int gu_order() {
+    const char* e = getenv("DSOCR_GU_ORDER");
+    return e ? atoi(e) : 0;
+}
+
 void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s) {
     if (!moe_gateup_mix_ok(a) || !xn) throw std::runtime_error("EINVAL: moe_gateup_mix outside its range");
     // one gate + up row pair per wave: 9.46 -> 8.73 us against two (98 / 90 VGPRs), 3.47 -> 3.55 pages/s
     const int n_sh = a.sWgu ? a.Is : 0;
     const int n_rt = a.topk * a.I;
-    dim3 grid(std::max(n_sh, (n_rt + 2) / 3));
-    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t>), grid, dim3(256), 0, s, a, xn);
-    else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t>), grid, dim3(256), 0, s, a, xn);
+    const int rf = gu_order();
+    dim3 grid(rf ? (n_rt + 3) / 4 + (n_sh + 3) / 4 : std::max(n_sh, (n_rt + 2) / 3));
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t>), grid, dim3(256), 0, s, a, xn, rf);
+    else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t>), grid, dim3(256), 0, s, a, xn, rf);
 }
 
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {

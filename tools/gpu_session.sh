@@ -79,6 +79,9 @@ for step in "$@"; do
     # runtime default), an AQL ring of 131072 packets so the profiler's ring-wrap read never happens
     gprod) ROC_AQL_QUEUE_SIZE=131072 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/gprod${TAG:+_$TAG} -o g --output-format csv -- python bench.py --steps 1 --warmup 0 --trace-only ${BENCH_ARGS} > gpurun_out/gprod${TAG:+_$TAG}.log 2>&1 ;;
     benchr) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/benchr${TAG:+_$TAG}.log 2>&1 ;;
+    kb_moe1) KB_WAVES=1 run 180 ./tools/kbench moe1 > gpurun_out/kb_moe1_o0.log 2>&1 && DSOCR_GU_ORDER=1 KB_WAVES=1 run 180 ./tools/kbench moe1 > gpurun_out/kb_moe1_o1.log 2>&1 ;;
+    # same-process A/B under a graph-mode kernel trace (AB_VARIANTS: the --variant arguments)
+    ab) ROC_AQL_QUEUE_SIZE=131072 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/ab${TAG:+_$TAG} -o g --output-format csv -- python tools/ab_trace.py --out gpurun_out/ab${TAG:+_$TAG}/order.json ${AB_ARGS} > gpurun_out/ab${TAG:+_$TAG}.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done

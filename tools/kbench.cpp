@@ -225,6 +225,47 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_GATEUP); }, s), gub);
     snprintf(nm, sizeof nm, "moe%d down", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_DOWN); }, s), dnb);
+    if (T != 1 || !getenv("KB_WAVES")) return;
+    // per-wave entry / exit clocks (WaveSpan slots) of single gate/up and down launches after a fresh route,
+    // by role: the gate/up's shared-expert and routed waves, the down's routed and shared waves
+    auto* slots = (unsigned long long*)dalloc((size_t)SPAN_SLOTS * 16);
+    const int order = getenv("DSOCR_GU_ORDER") ? atoi(getenv("DSOCR_GU_ORDER")) : 0;
+    const int n_rt = TOPK * I, nbr = (n_rt + 3) / 4;
+    for (int it = 0; it < 3; ++it) {
+        for (int part : {MOE_GATEUP, MOE_DOWN}) {
+            set(it + 1);
+            launch_moe_decode(a, s, MOE_ROUTE);
+            CK(hipMemsetAsync(slots, 0, (size_t)SPAN_SLOTS * 16, s));
+            a.span = slots;
+            launch_moe_decode(a, s, part);
+            a.span = nullptr;
+            CK(hipStreamSynchronize(s));
+            std::vector<unsigned long long> h((size_t)SPAN_SLOTS * 2);
+            CK(hipMemcpy(h.data(), slots, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            for (size_t w = 0; w < (size_t)SPAN_SLOTS; ++w) if (h[2 * w] && h[2 * w] < t0) t0 = h[2 * w];
+            std::vector<double> ent[2], ext[2];
+            for (size_t w = 0; w < (size_t)SPAN_SLOTS; ++w) {
+                if (!h[2 * w]) continue;
+                int role;
+                if (part == MOE_GATEUP) role = order ? ((int)(w / 4) >= nbr ? 0 : 1) : (w % 4 == 0 ? 0 : 1);
+                else role = (w % 8) >= 6 ? 0 : 1;  // down: waves 6, 7 of a block hold the shared chunks
+                ent[role].push_back(((long long)h[2 * w] - (long long)t0) / 100.0);
+                ext[role].push_back(((long long)h[2 * w + 1] - (long long)t0) / 100.0);
+            }
+            printf("%s waves (us from first entry; min/p10/p50/p90/max):", part == MOE_GATEUP ? "gateup" : "down  ");
+            for (int r = 0; r < 2; ++r) {
+                for (auto* v : {&ent[r], &ext[r]}) {
+                    if (v->empty()) continue;
+                    std::sort(v->begin(), v->end());
+                    auto q = [&](double f) { return (*v)[(size_t)(f * (v->size() - 1))]; };
+                    printf(" %s %s %.2f/%.2f/%.2f/%.2f/%.2f |", r ? "routed" : "shared", v == &ent[r] ? "entry" : "exit",
+                           q(0), q(0.1), q(0.5), q(0.9), q(1));
+                }
+            }
+            printf(" n %zu/%zu\n", ent[0].size(), ent[1].size());
+        }
+    }
 }
 
 static void case_gemv(int M, hipStream_t s) {
