@@ -338,16 +338,60 @@ def run_dots(args, rank, world, local, dist):
     }
 
 
+def chain_roofline(chain, waves, d, B, P):
+    """Dispatch-level durations from a chain-span generate (dsocr_engine_set_spans 4): every layer's attention,
+    o_proj, router, gate/up and down launches stamp their waves (one fold per step, nothing between launches),
+    so duration = last wave exit of the launch - last wave exit of the launch before it (its boundary
+    included, as a back-to-back rocprofv3 dispatch record), boundary = its first wave entry - that exit.
+    MoE launches are priced at the distinct experts the wave-span generate of the same batch recorded."""
+    import numpy as np
+    pred = {"moe_gateup": ("router", 0), "moe_down": ("moe_gateup", 0), "o_proj": ("attention", 0),
+            "router": ("o_proj", 0), "attention": ("moe_down", -1)}
+    Hh, hd, heads = d["H"], d["hd"], d["heads"]
+    out = {}
+    for kind, (pk, dl) in pred.items():
+        a, b = chain.get(kind), chain.get(pk)
+        if a is None or b is None or (kind == "attention" and B > 1):  # (B > 1: an unstamped q/k/v launch precedes it)
+            continue
+        L, S = a.shape[0], a.shape[1]
+        durs, bnds, wv, by = [], [], [], []
+        for l in range(max(0, -dl), L):
+            for st in range(S):
+                e_in, e_out, p_out = int(a[l, st, 0]), int(a[l, st, 1]), int(b[l + dl, st, 1])
+                if not (e_in and e_out and p_out) or e_out <= p_out:
+                    continue
+                durs.append((e_out - p_out) / SPAN_HZ)
+                bnds.append((e_in - p_out) / SPAN_HZ)
+                wv.append((e_out - e_in) / SPAN_HZ)
+                if kind in ("moe_gateup", "moe_down"):
+                    ex = int(waves[kind][l, st, 2]) if kind in waves else d["K"] * B
+                    by.append(span_bytes(kind, d, B, P, ex, st))
+                elif kind == "attention":
+                    by.append(span_bytes(kind, d, B, P, 0, st) + 3 * Hh * Hh * 2)  # + the fused q/k/v weights (B = 1)
+                elif kind == "o_proj":
+                    by.append(heads * hd * Hh * 2 + B * (heads * hd + 2 * Hh) * 4)
+                else:
+                    by.append(64 * Hh * 2 + B * Hh * 4)
+        if not durs:
+            continue
+        du = np.array(durs)
+        bb = np.array(by, np.float64)
+        out[kind] = {"launches": len(durs), "avg_us": float(du.mean() * 1e6), "p50_us": float(np.median(du) * 1e6),
+                     "boundary_us": float(np.mean(bnds) * 1e6), "wave_us": float(np.mean(wv) * 1e6),
+                     "bytes_per_launch": float(bb.mean()), "GB/s": float(bb.sum() / du.sum() / 1e9),
+                     "frac": float(bb.sum() / du.sum() / 1e9 / HBM_PEAK_GBS)}
+    return out
+
+
 def decode_roofline(eng, batch, params, ppg, args):
-    """The roofline object of the decode MoE gate/up (the north-star kernel) at this batch size, from three
-    extra generates of the first timed batch (rank 0, after the timed region):
-      1. HIP events around every gate/up / down / attention launch inside the replayed step graph (no extra
-         kernel in the step): the dispatch-level duration rocprofv3's kernel trace reports for the same
-         launch (previous launch's end -> this launch's end, i.e. its boundary included), over every decode
-         step -> `avg_launch_us`, `achieved`, `frac`;
-      2. in-kernel wave spans (first wave entry -> last wave exit, s_memrealtime) of the same launches, each
-         launch's distinct experts recorded -> `in_kernel_waves`, and the per-launch pricing of (1) (same
-         batch, same routing: the ids of the two generates are checked equal);
+    """The roofline object of the decode MoE gate/up (the north-star kernel) at this batch size, from extra
+    generates of the first timed batch (rank 0, after the timed region):
+      1. chain spans (every layer's attention, o_proj, router, gate/up, down launches stamp their waves; one
+         fold per step; nothing else between the launches): each launch's dispatch-level duration = its last
+         wave exit - the previous launch's last wave exit, over every decode step -> `avg_launch_us`,
+         `achieved`, `frac` (rocprofv3 reports a back-to-back dispatch the same way: previous end -> end);
+      2. in-kernel wave spans with each MoE launch's distinct experts (one fold launch after each stamped
+         launch) -> `in_kernel_waves` and the pricing of (1) (same batch, same routing: ids checked equal);
       3. profile_decode: one step's layers replayed as a graph with and without the gate/up launches ->
          `in_context` (secondary)."""
     import dsocr
@@ -356,16 +400,14 @@ def decode_roofline(eng, batch, params, ppg, args):
     eng.set_spans(eng.SPAN_WAVES)
     ids_w = eng.generate_batch(batch, params, ignore_eos=True)
     spans_w = eng.spans()
-    eng.set_spans(eng.SPAN_EVENTS)
-    ids_e = eng.generate_batch(batch, params, ignore_eos=True)
-    spans_e = eng.spans()
+    eng.set_spans(eng.SPAN_CHAIN)
+    ids_c = eng.generate_batch(batch, params, ignore_eos=True)
+    spans_c = eng.spans()
     eng.set_spans(0)
-    if ids_w != ids_e:
+    if ids_w != ids_c:
         raise RuntimeError("span generates of one batch emitted different ids")
-    for k in spans_e:  # events-only records carry no expert counts: the wave-span generate's (same routing)
-        spans_e[k][..., 2] = spans_w[k][..., 2]
     waves = span_roofline(spans_w, dims, ppg, P)
-    disp = span_roofline(spans_e, dims, ppg, P)
+    chain = chain_roofline(spans_c, spans_w, dims, ppg, P)
     prof = eng.profile_decode(args.roofline_iters)
     kernel = prof["moe_gateup_kernel"]  # what the dispatch runs at this batch size
 
@@ -375,19 +417,19 @@ def decode_roofline(eng, batch, params, ppg, args):
                 "GB/s": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9, 1) if p["ctx_us"] > 0 else None,
                 "frac": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if p["ctx_us"] > 0 else None,
                 "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
-    gu = disp["moe_gateup"]
+    gu = chain["moe_gateup"]
     runs = ("b1",) if ppg == 1 else (("b8",) if args.text_pages and ppg == 8 else (("b8i",) if ppg == 8 else ()))
     return {"bound": "hbm", "achieved": round(gu["GB/s"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gu["frac"], 4), "traffic": pmc_traffic(kernel, runs=runs),
             "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
-            # avg_launch_us = mean dispatch duration over every gate/up launch of a whole generate (HIP events
-            # on the engine stream around each launch inside the replayed step graph: previous launch end ->
-            # this launch end, as rocprofv3 reports a back-to-back dispatch); achieved = the launches'
-            # algorithmic bytes (each priced at its own distinct experts) / their summed durations
+            # avg_launch_us = mean dispatch-level duration over every gate/up launch of a whole generate
+            # (router's last wave exit -> gate/up's last wave exit, in the production step chain); achieved =
+            # the launches' algorithmic bytes (each priced at its own distinct experts) / their summed durations
             "avg_launch_us": round(gu["avg_us"], 3), "bytes_per_launch": gu["bytes_per_launch"],
-            "launches": gu["launches"], "experts_mean": gu["experts_mean"],
-            "timing": "dispatch duration: HIP events around each launch in the replayed step graph, every decode step",
-            "dispatch": disp,
+            "launches": gu["launches"],
+            "timing": "dispatch duration: previous launch's last wave exit -> this launch's last wave exit, every "
+                      "decode step of one generate (chain spans)",
+            "chain": chain,
             "in_kernel_waves": waves,
             "down_kernel": prof["moe_down_kernel"],
             # secondary: one step's layers replayed with and without the gate/up launches, (full - without) / layers

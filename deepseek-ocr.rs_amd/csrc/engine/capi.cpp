@@ -399,7 +399,7 @@ dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap
         const auto& v = e->impl->spans();
         const size_t nl = e->impl->cfg().lang.layers;
         const size_t ns = v.empty() ? 0 : (size_t)e->impl->span_steps();
-        if (kinds) *kinds = dsocr::Engine::SPAN_KINDS;
+        if (kinds) *kinds = (size_t)e->impl->span_kinds();
         if (layers) *layers = nl;
         if (steps) *steps = ns;
         if (!out) return;  // size query

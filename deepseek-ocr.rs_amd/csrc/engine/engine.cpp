@@ -1055,7 +1055,7 @@ void Engine::decode_step(int B, int Lmax) {
     // launch spans (set_spans): HIP events on the stream around the launch (dispatch-level duration,
     // what rocprofv3's kernel trace reports) + the in-kernel wave span folded right after it
     auto stamped = [&](int kind, int l, const std::function<void()>& launch, const int* ids, int n_ids) {
-        if (!span_rec_) {
+        if (!span_rec_ || chain_active_) {  // (chain spans: the launch carries its own slot region)
             launch();
             return;
         }
@@ -1085,7 +1085,7 @@ void Engine::decode_step(int B, int Lmax) {
         da.counters = wsi("s_attn_cnt", (size_t)B * L.heads);
         da.err = err;
         da.kv_delay = att_kv_delay();
-        da.span = (span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr;
+        da.span = chain_active_ ? chain_slots(l, SPAN_ATTN) : ((span_rec_ && (span_mode_ & SPAN_WAVES)) ? span_slots_ : nullptr);
         // q/k/v projection with the input RMSNorm fused; one page: RoPE in the projection's epilogue, so the
         // attention reads q / k already rotated (B <= 2: the row block-staged; 3..8: dec_gemv_lds / dec_mm)
         DecGemvArgs g;
@@ -1122,7 +1122,7 @@ void Engine::decode_step(int B, int Lmax) {
         // o_proj + residual
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
-        go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1;
+        go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1; go.span = chain_slots(l, SPAN_OPROJ);
         launch_dec_gemv(go, st);
         // MLP / MoE
         if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
@@ -1169,9 +1169,11 @@ void Engine::decode_step(int B, int Lmax) {
             continue;
         }
         MoeDecodeArgs ma = moe_args(l, B, X);
+        ma.route_span = chain_slots(l, SPAN_ROUTER);
         launch_moe_decode(ma, st, MOE_ROUTE);
-        ma.span = (span_mode_ & SPAN_WAVES) ? span_slots_ : nullptr;
+        ma.span = chain_active_ ? chain_slots(l, SPAN_GATEUP) : ((span_mode_ & SPAN_WAVES) ? span_slots_ : nullptr);
         stamped(SPAN_GATEUP, l, [&] { launch_moe_decode(ma, st, MOE_GATEUP); }, ma.ids, B * ma.topk);
+        if (chain_active_) ma.span = chain_slots(l, SPAN_DOWN);
         stamped(SPAN_DOWN, l, [&] { launch_moe_decode(ma, st, MOE_DOWN); }, ma.ids, B * ma.topk);
     }
 }
@@ -1737,7 +1739,19 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         HIP_CHECK(hipEventRecord(ev[5], st));
         HIP_CHECK(hipStreamSynchronize(st));
     } else {
-    if (span_mode_) {
+    chain_active_ = false;
+    spans_kinds_ = SPAN_KINDS;
+    if (span_mode_ == SPAN_CHAIN) {
+        span_cap_ = (int)std::max<size_t>(p.max_new, 1) + 1;  // the fold records at (tokens emitted) <= max_new
+        const size_t nreg = (size_t)L.layers * SPAN_KINDS_CHAIN;
+        span_chain_ = (unsigned long long*)ws("s_span_chain", nreg * SPAN_SLOTS * 16);
+        span_chain_rec_ = (unsigned long long*)ws("s_span_chain_rec", (size_t)span_cap_ * nreg * 32);
+        span_tmark_ = (unsigned long long*)ws("s_span_tmark", 16);
+        span_rec_ = span_chain_rec_;  // (marks the generate as stamped)
+        span_step_ = d_outlen;
+        chain_active_ = true;
+        HIP_CHECK(hipMemsetAsync(span_chain_rec_, 0, (size_t)span_cap_ * nreg * 32, st));
+    } else if (span_mode_) {
         span_cap_ = (int)std::max<size_t>(p.max_new, 1);
         const size_t rec_bytes = (size_t)SPAN_KINDS * L.layers * span_cap_ * 4 * 8;
         span_slots_ = (unsigned long long*)ws("s_span_slots", (size_t)SPAN_SLOTS * 16);
@@ -1766,6 +1780,10 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
+    if (chain_active_) {  // the dry step's stamps must not join step 1's: clear the regions and the marks
+        HIP_CHECK(hipMemsetAsync(span_chain_, 0, (size_t)L.layers * SPAN_KINDS_CHAIN * SPAN_SLOTS * 16, st));
+        HIP_CHECK(hipMemsetAsync(span_tmark_, 0, 16, st));
+    }
     HIP_CHECK(hipMemcpyAsync(d_kvpos, kvpos.data(), B * 4, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_kvlen, kvlen.data(), B * 4, hipMemcpyHostToDevice, st));
     launch_embed_tokens(embed_, embed_dt_, d_tok, B, H, SX, H, st);
@@ -1778,6 +1796,10 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     auto step_body = [&]() {
         decode_step(B, Lmax);
         decode_head(B, sa, pen);
+        // chain spans: the step's one fold, after the head (the step counter has advanced: record at count - 1)
+        if (chain_active_)
+            launch_span_chain_fold(span_chain_, L.layers * SPAN_KINDS_CHAIN, span_chain_rec_, span_step_, span_cap_,
+                                   span_tmark_, st);
     };
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
@@ -1807,7 +1829,25 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipStreamSynchronize(st));
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
-    if (span_rec_) {
+    if (chain_active_) {
+        const size_t nreg = (size_t)L.layers * SPAN_KINDS_CHAIN;
+        std::vector<unsigned long long> dev((size_t)span_cap_ * nreg * 4);
+        HIP_CHECK(hipMemcpy(dev.data(), span_chain_rec_, dev.size() * 8, hipMemcpyDeviceToHost));
+        spans_host_.assign((size_t)SPAN_KINDS_CHAIN * L.layers * span_cap_ * SPAN_FIELDS, 0);
+        // fold at step s's end recorded at index (tokens emitted) = s + 1: shift back to s
+        for (int st_ = 1; st_ < span_cap_; ++st_)
+            for (int l = 0; l < L.layers; ++l)
+                for (int k = 0; k < SPAN_KINDS_CHAIN; ++k) {
+                    const unsigned long long* r = &dev[((size_t)st_ * nreg + (size_t)l * SPAN_KINDS_CHAIN + k) * 4];
+                    unsigned long long* o = &spans_host_[(((size_t)k * L.layers + l) * span_cap_ + st_ - 1) * SPAN_FIELDS];
+                    o[0] = r[0]; o[1] = r[1]; o[3] = r[2];
+                }
+        spans_steps_ = span_cap_;
+        spans_kinds_ = SPAN_KINDS_CHAIN;
+        chain_active_ = false;
+        span_rec_ = nullptr;
+        span_step_ = nullptr;
+    } else if (span_rec_) {
         const size_t nrec = (size_t)SPAN_KINDS * L.layers * span_cap_;
         std::vector<unsigned long long> dev(nrec * 4);
         HIP_CHECK(hipMemcpy(dev.data(), span_rec_, dev.size() * 8, hipMemcpyDeviceToHost));

@@ -164,10 +164,16 @@ class Engine {
     // records per layer the (first wave entry, last wave exit) of its MoE gate/up, MoE down and
     // attention launches, with the distinct experts the MoE launches streamed (WaveSpan +
     // span_reduce_kernel; one extra fold launch after each stamped launch, inside the replayed graph).
-    enum SpanKind : int { SPAN_GATEUP = 0, SPAN_DOWN = 1, SPAN_ATTN = 2, SPAN_KINDS = 3 };
+    // SPAN_CHAIN (alone): no fold or event between launches; the gate/up, down, attention, o_proj and router
+    // launches of every layer stamp their own slot region and one fold runs at the end of each step, so the
+    // step is the production chain plus the waves' slot stores: exit(k) - exit(k - 1) is a launch's
+    // dispatch-level duration (its boundary included, as a back-to-back rocprofv3 kernel-trace record)
+    enum SpanKind : int { SPAN_GATEUP = 0, SPAN_DOWN = 1, SPAN_ATTN = 2, SPAN_KINDS = 3, SPAN_OPROJ = 3, SPAN_ROUTER = 4,
+                          SPAN_KINDS_CHAIN = 5 };
     static constexpr int SPAN_FIELDS = 5;
-    enum SpanMode : int { SPAN_WAVES = 1, SPAN_EVENTS = 2 };  // bit mask; 0 = off
-    void set_spans(int mode) { span_mode_ = mode & (SPAN_WAVES | SPAN_EVENTS); }
+    enum SpanMode : int { SPAN_WAVES = 1, SPAN_EVENTS = 2, SPAN_CHAIN = 4 };  // bit mask; 0 = off
+    void set_spans(int mode) { span_mode_ = (mode & SPAN_CHAIN) ? SPAN_CHAIN : mode & (SPAN_WAVES | SPAN_EVENTS); }
+    int span_kinds() const { return spans_kinds_; }
     // [kind][layer][step][SPAN_FIELDS] u64 {entry, exit (100 MHz wall clock), distinct experts, waves,
     // dispatch duration in ns (HIP events recorded around the launch inside the replayed graph)} of the
     // last generate with spans on; step = tokens emitted before the step (1 .. steps - 1 are decode steps)
@@ -282,6 +288,14 @@ class Engine {
     int spans_steps_ = 0;
     std::vector<hipEvent_t> span_ev_;           // [SPAN_KINDS][layers][2]
     std::vector<double> span_ev_ns_;            // [SPAN_KINDS][layers][span_cap_]
+    int spans_kinds_ = SPAN_KINDS;
+    bool chain_active_ = false;                 // a SPAN_CHAIN generate is running
+    unsigned long long* span_chain_ = nullptr;  // device [layers * SPAN_KINDS_CHAIN][SPAN_SLOTS][2]
+    unsigned long long* span_chain_rec_ = nullptr;  // device [span_cap_][layers * SPAN_KINDS_CHAIN][4]
+    unsigned long long* span_tmark_ = nullptr;  // device [2]
+    unsigned long long* chain_slots(int layer, int kind) const {
+        return chain_active_ ? span_chain_ + ((size_t)layer * SPAN_KINDS_CHAIN + kind) * SPAN_SLOTS * 2 : nullptr;
+    }
     unsigned long long* span_rec(int kind, int layer) const {
         return span_rec_ + ((size_t)kind * cfg_.lang.layers + layer) * span_cap_ * 4;
     }

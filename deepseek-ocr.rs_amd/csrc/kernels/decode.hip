@@ -173,6 +173,7 @@ constexpr size_t STAGE_LDS_MAX = 64 * 1024;
 // stream overlaps the norm prologue; K <= 64*U*8 is a single batch.
 template <typename WT, int MT, int RB, int U>
 __global__ __launch_bounds__(256) void dec_gemv_kernel(DecGemvArgs a) {
+    WaveSpan span_(a.span);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = (blockIdx.x * 4 + wave) * RB;
@@ -860,6 +861,7 @@ __device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softm
 // token w on wave w (topk_wave64) and wave 0 groups the picks by expert (MOE_GRP_* records).
 template <typename WT>
 __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRouteEpi r) {
+    WaveSpan span_(a.span);
     constexpr int U = 3, MT = 8;  // K <= 1536, T <= 8
     extern __shared__ __attribute__((aligned(16))) uint4 ws[];  // [8 experts][K / 8] 16-bit weight chunks
     __shared__ float lg_s[MT][64];
@@ -2503,11 +2505,12 @@ bool moe_gateup_mix_ok(const MoeDec2Args& a) {
            a.ids_out && a.w_out;
 }
 
-// DSOCR_GU_ORDER (A/B switch, read at every launch): 1 = routed blocks first, shared blocks last; 0 = one shared
-// wave per block
+// DSOCR_GU_ORDER (A/B switch, read at every launch): 1 (default) = routed blocks first, shared blocks last; 0 = one
+// shared wave per block.  Same-process A/B under a graph-mode kernel trace (tools/ab_trace.py, 64 tokens x 3
+// rounds): 9.13 -> 8.77 us per launch (profiles/r05_ab_gu_order.txt); the waves' arithmetic is unchanged
 static int gu_order() {
     const char* e = getenv("DSOCR_GU_ORDER");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
 }
 
 void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s) {
@@ -2887,7 +2890,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     m.dn_part = a.dn_part; m.dn_tick = a.dn_tick; m.span = a.span;
     DecGemvArgs& gr = p.router;
     gr.M = T; gr.N = E; gr.K = a.H; gr.x = mx; gr.ldx = a.H; gr.W = a.router; gr.ldw = a.H; gr.wdtype = a.router_wdt;
-    gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps;
+    gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps; gr.span = a.route_span;
     if (T >= 3 && T <= 8 && dec_router_ok(T, E, a.H, K) && a.route_cnt && a.grp) {
         p.mode = 2;
         m.slot_mode = 1; m.slots = TK; m.grp = a.grp; m.aw = a.wts;

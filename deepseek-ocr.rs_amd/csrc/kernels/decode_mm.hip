@@ -176,6 +176,7 @@ __device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uin
 // 16-byte nontemporal loads straight into registers, PF k-steps per batch, double-buffered.
 template <typename WT, int WR, int WK, int PF, int Q, bool NORM, bool SWZ>
 __global__ __launch_bounds__(64 * WR * WK) void dec_mm_kernel(DecGemvArgs a) {
+    WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
     static_assert(PF % Q == 0, "a batch holds whole k groups");
     // k order inside each group of Q steps: step Q T + s gives lane group g the 8 k's

@@ -15,6 +15,11 @@ enum WDType : int { WDT_BF16 = 0, WDT_F16 = 1 };
 // folded by launch_span_reduce into rec[min(*step, cap - 1)] = {first entry, last exit, distinct ids
 // among ids[0..n_ids) (0 if none), waves seen} (100 MHz wall clock) and cleared for the next launch.
 constexpr long SPAN_SLOTS = 16384;
+// Chain spans (Engine::set_spans bit 4): every stamped launch of a decode step writes its waves' slots into its
+// own region of SPAN_SLOTS pairs; one fold at the end of the step writes rec[step][region] = {first entry, last
+// exit, waves, 0} over the slots stamped since the previous fold (tmark: two words, alternated by step parity).
+void launch_span_chain_fold(const unsigned long long* slots, int nreg, unsigned long long* rec, const int* step, int cap,
+                            unsigned long long* tmark, hipStream_t s);
 void launch_span_reduce(unsigned long long* slots, unsigned long long* rec, const int* step, int cap, const int* ids,
                         int n_ids, hipStream_t s);
 struct ProfEvents {
@@ -193,6 +198,7 @@ struct DecGemvArgs {
     float eps = 0.f;
     float* xn_out = nullptr;  // optional: block 0 writes the staged (normalised) rows [M][K] here
     const void* w_swz = nullptr;  // optional: W in dec_mm's fragment order (launch_mm_swizzle), M = 3..8
+    unsigned long long* span = nullptr;  // launch-span slots (dec_gemv, dec_mm, dec_route_grp) or null
 };
 void launch_dec_gemv(const DecGemvArgs& a, hipStream_t s);
 // 3..8 tokens on the matrix cores (decode_mm.hip): weight rows as MFMA A operands, the (optionally
@@ -380,6 +386,7 @@ struct MoeDecodeArgs {
     int* eoff = nullptr; int* arow = nullptr; int* apos = nullptr; int* active = nullptr;  // T > 8:
     int* n_active = nullptr; float* aw = nullptr;                                          // [E+1],[TK],[TK],[E],[1],[TK]
     unsigned long long* span = nullptr;  // launch-span slots for the gate/up and down launches (or null)
+    unsigned long long* route_span = nullptr;  // launch-span slots for the router launch (or null)
 };
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments

@@ -258,4 +258,53 @@ void launch_span_reduce(unsigned long long* slots, unsigned long long* rec, cons
     hipLaunchKernelGGL(span_reduce_kernel, dim3(1), dim3(1024), 0, s, slots, rec, step, cap, ids, n_ids);
 }
 
+// Chain spans: block r folds region r's slots stamped since the previous fold (entry > tmark[step & 1]); block 0
+// then stamps tmark[(step + 1) & 1] (read by the next step's fold, never by this one).
+__global__ __launch_bounds__(1024) void span_chain_fold_kernel(const unsigned long long* slots, unsigned long long* rec,
+                                                               const int* step, int cap, unsigned long long* tmark) {
+    __shared__ unsigned long long lo_s[16], hi_s[16];
+    __shared__ int cnt_s[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = blockIdx.x;
+    int k = step ? *step : 0;
+    k = k < 0 ? 0 : (k >= cap ? cap - 1 : k);
+    const unsigned long long since = tmark[k & 1];
+    const unsigned long long* sl = slots + (size_t)r * SPAN_SLOTS * 2;
+    unsigned long long lo = ~0ull, hi = 0;
+    int cnt = 0;
+    for (long i = tid; i < SPAN_SLOTS; i += 1024) {
+        const unsigned long long a = sl[2 * i], b = sl[2 * i + 1];
+        if (a > since) {
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+            ++cnt;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long l2 = __shfl_xor(lo, o), h2 = __shfl_xor(hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+        cnt += __shfl_xor(cnt, o);
+    }
+    if (lane == 0) { lo_s[wave] = lo; hi_s[wave] = hi; cnt_s[wave] = cnt; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 16; ++w) {
+            lo = lo_s[w] < lo ? lo_s[w] : lo;
+            hi = hi_s[w] > hi ? hi_s[w] : hi;
+            cnt += cnt_s[w];
+        }
+        unsigned long long* o = rec + ((size_t)k * gridDim.x + r) * 4;
+        o[0] = cnt ? lo : 0;
+        o[1] = cnt ? hi : 0;
+        o[2] = (unsigned long long)cnt;
+        o[3] = 0;
+        if (r == 0) tmark[(k + 1) & 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+void launch_span_chain_fold(const unsigned long long* slots, int nreg, unsigned long long* rec, const int* step, int cap,
+                            unsigned long long* tmark, hipStream_t s) {
+    hipLaunchKernelGGL(span_chain_fold_kernel, dim3(nreg), dim3(1024), 0, s, slots, rec, step, cap, tmark);
+}
+
 }  // namespace dsocr

@@ -279,13 +279,14 @@ class DeepseekOcrEngine:
         check(lib().dsocr_last_timings(self._h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in TimingsC._fields_}
 
-    SPAN_KINDS = ("moe_gateup", "moe_down", "attention")
+    SPAN_KINDS = ("moe_gateup", "moe_down", "attention", "o_proj", "router")  # the last two: chain spans only
 
-    SPAN_WAVES, SPAN_EVENTS = 1, 2
+    SPAN_WAVES, SPAN_EVENTS, SPAN_CHAIN = 1, 2, 4
 
     def set_spans(self, mode: int):
         """In-context launch spans for the following generates (dsocr_engine_set_spans): 0 off, bit 1 wave
-        spans, bit 2 HIP events around the launches inside the replayed step graph."""
+        spans, bit 2 HIP events around the launches inside the replayed step graph, 4 (alone) chain spans
+        (every layer's gate/up, down, attention, o_proj and router launches, one fold per step)."""
         check(lib().dsocr_engine_set_spans(self._h, int(mode)))
 
     def spans(self) -> dict:

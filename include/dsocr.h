@@ -211,7 +211,11 @@ dsocr_status dsocr_profile_decode(dsocr_engine* e, int iters, dsocr_decode_profi
  * launches writes its entry / exit s_memrealtime (100 MHz) to a slot, a one-block fold launch after each
  * keeps the first entry / last exit), 2 = HIP events recorded on the stream around those launches inside
  * the replayed step graph (the dispatch-level duration rocprofv3's kernel trace reports; read back after
- * every step; no extra kernel runs, so the step is the production chain plus the event markers).  Mode 1
+ * every step; no extra kernel runs, so the step is the production chain plus the event markers), 4 (alone)
+ * = chain spans: the gate/up, down, attention, o_proj (kind 3) and router (kind 4) launches of every layer
+ * stamp their waves into their own slot regions and ONE fold launch runs at the end of each step (no fold
+ * or event between launches), so exit(launch) - exit(previous launch) is the launch's dispatch-level
+ * duration with its boundary, as rocprofv3 records a back-to-back dispatch; kinds = 5 then.  Mode 1
  * also records the distinct experts each MoE launch streamed (mode 2 alone leaves that field 0).  The decode steps
  * of every following generate are recorded; dsocr_engine_spans copies the last such generate's records,
  * [kinds][layers][steps][5] uint64 {entry, exit, distinct experts, waves, event duration ns}, into out

@@ -27,6 +27,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -143,6 +145,55 @@ void linear_t(const float* X, int M, int K, const Tensor& w, const Tensor* b, fl
     }
 }
 
+// kind 3 (the vision tower's bf16 weights, round 5): packed 32-column panels for the large-M GEMMs.  Panel p holds
+// columns 32p .. 32p + 31 as [K][16] dwords, dword i = bf16(W[32p + i][k]) | bf16(W[32p + 16 + i][k]) << 16, so a
+// k-step is one 64-B load, a shift (columns 0..15) and a mask (16..31).  The micro-kernel keeps MR rows x 32
+// columns in 2 MR accumulators and broadcasts one activation per row and k (outer products), instead of the
+// dot-product tiles' per-tile horizontal reductions.
+template <int MR>
+inline void pk_tile(const float* X, long ldx, int K, const uint32_t* P, const float* bias, float* Y, long ldy, int nc) {
+    __m512 a0[MR], a1[MR];
+    for (int r = 0; r < MR; ++r) { a0[r] = _mm512_setzero_ps(); a1[r] = _mm512_setzero_ps(); }
+    const __m512i hi_mask = _mm512_set1_epi32((int)0xffff0000u);
+    for (int k = 0; k < K; ++k) {
+        const __m512i raw = _mm512_loadu_si512(P + (size_t)k * 16);
+        const __m512 w0 = _mm512_castsi512_ps(_mm512_slli_epi32(raw, 16));
+        const __m512 w1 = _mm512_castsi512_ps(_mm512_and_si512(raw, hi_mask));
+        for (int r = 0; r < MR; ++r) {
+            const __m512 xb = _mm512_set1_ps(X[(long)r * ldx + k]);
+            a0[r] = _mm512_fmadd_ps(xb, w0, a0[r]);
+            a1[r] = _mm512_fmadd_ps(xb, w1, a1[r]);
+        }
+    }
+    const __mmask16 m0 = nc >= 16 ? (__mmask16)0xffff : (__mmask16)((1u << nc) - 1);
+    const __mmask16 m1 = nc >= 32 ? (__mmask16)0xffff : (nc > 16 ? (__mmask16)((1u << (nc - 16)) - 1) : (__mmask16)0);
+    const __m512 b0 = bias ? _mm512_maskz_loadu_ps(m0, bias) : _mm512_setzero_ps();
+    const __m512 b1 = bias ? _mm512_maskz_loadu_ps(m1, bias + 16) : _mm512_setzero_ps();
+    for (int r = 0; r < MR; ++r) {
+        _mm512_mask_storeu_ps(Y + (long)r * ldy, m0, _mm512_add_ps(a0[r], b0));
+        _mm512_mask_storeu_ps(Y + (long)r * ldy + 16, m1, _mm512_add_ps(a1[r], b1));
+    }
+}
+
+void linear_packed(const float* X, int M, int K, const Tensor& w, const Tensor* b, float* Y, int N) {
+    const int np = (N + 31) / 32;
+    constexpr int MB = 96;  // rows per work item (8 tiles of 12): the panel stays in L1 / L2 across them
+    const int nmb = (M + MB - 1) / MB;
+    const uint32_t* P = reinterpret_cast<const uint32_t*>(w.h.data());
+#pragma omp parallel for schedule(dynamic, 2) collapse(2)
+    for (int mb = 0; mb < nmb; ++mb)
+        for (int p = 0; p < np; ++p) {
+            const uint32_t* pp = P + (size_t)p * K * 16;
+            const int nc = std::min(32, N - 32 * p);
+            const float* bias = b ? b->f.data() + 32 * p : nullptr;
+            int m = mb * MB;
+            const int me = std::min(M, m + MB);
+            for (; m + 12 <= me; m += 12) pk_tile<12>(X + (long)m * K, K, K, pp, bias, Y + (long)m * N + 32 * p, N, nc);
+            for (; m + 4 <= me; m += 4) pk_tile<4>(X + (long)m * K, K, K, pp, bias, Y + (long)m * N + 32 * p, N, nc);
+            for (; m < me; ++m) pk_tile<1>(X + (long)m * K, K, K, pp, bias, Y + (long)m * N + 32 * p, N, nc);
+        }
+}
+
 double g_lin_ms = 0, g_att_ms = 0;  // stage clocks (cr_profile)
 
 void linear(const float* X, int M, int K, const Tensor& w, const Tensor* b, float* Y, int N) {
@@ -151,7 +202,8 @@ void linear(const float* X, int M, int K, const Tensor& w, const Tensor* b, floa
         std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
         ~Clk() { g_lin_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count(); }
     } clk;
-    if (w.kind == 1) linear_t<1>(X, M, K, w, b, Y, N);
+    if (w.kind == 3) linear_packed(X, M, K, w, b, Y, N);
+    else if (w.kind == 1) linear_t<1>(X, M, K, w, b, Y, N);
     else if (w.kind == 2) linear_t<2>(X, M, K, w, b, Y, N);
     else linear_t<0>(X, M, K, w, b, Y, N);
 }
@@ -375,6 +427,388 @@ int select(const std::vector<float>& lg, const std::vector<int>& ctx, int ngram)
     return best < 0 ? 0 : best;
 }
 
+
+// ====================================================================== vision tower (round 5)
+// SAM-ViTDet-B + CLIP-L + linear projector, the same f32 math as the numpy oracle (oracle/vision.py), which
+// restates vision/sam.rs, vision/clip.rs and model/mod.rs:246-923:
+//   * patch embed (16x16 conv as im2col + linear)    sam.rs:210-246
+//   * SamBlock: LN -> (window partition, pad with zeros) -> attention with the decomposed rel-pos bias
+//     (sam.rs:804-888: scores * scale + q.Rh[qh][kh] + q.Rw[qw][kw]) -> unpartition -> residual -> LN ->
+//     fc1 -> GELU-erf -> fc2 -> residual                 sam.rs:731-748, 926-980
+//   * neck (1x1 conv, LN2d, 3x3 conv, LN2d) + two stride-2 3x3 convs      sam.rs:503-575
+//   * CLIP: class token + patches + position table, pre-LN, 24 x (LN, MHA, residual, LN, fc1, quick-GELU,
+//     fc2, residual)                                    clip.rs:98-102, 349-416
+//   * projector over [clip tokens 1.. | sam tokens]     model/mod.rs:392-444, 604-650
+// The position-embedding resizes and the rel-pos tables depend only on the weights and the grid: the Python
+// side (CpuVision) computes them once with the oracle's functions and hands them over as tensors.
+struct VCfg {
+    int embed, depth, heads, window, neck, c0, c1, patch;
+    float sam_eps;
+    int clip_h, clip_layers, clip_heads, clip_ffn;
+    float clip_eps;
+    int n_embed, in_dim;
+    std::vector<int> global;
+};
+VCfg g_v;
+double g_vis_prof[6];  // ms: layer norms, activations, window / im2col copies, residual adds (DSOCR_CV_PROF=1)
+struct VClk {
+    int slot;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    explicit VClk(int s) : slot(s) {}
+    ~VClk() { g_vis_prof[slot] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count(); }
+};
+
+const Tensor* opt(const std::string& n) { return has(n) ? &W(n) : nullptr; }
+
+void layer_norm_rows(const float* x, long M, int C, const float* w, const float* b, float eps, float* y) {
+    VClk clk(0);
+#pragma omp parallel for schedule(static)
+    for (long m = 0; m < M; ++m) {
+        const float* xr = x + m * C;
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += xr[c];
+        const float mean = s / (float)C;
+        float v = 0.f;
+        for (int c = 0; c < C; ++c) v += (xr[c] - mean) * (xr[c] - mean);
+        const float den = std::sqrt(v / (float)C + eps);
+        float* yr = y + m * C;
+        for (int c = 0; c < C; ++c) yr[c] = ((xr[c] - mean) / den) * w[c] + b[c];
+    }
+}
+
+// multi-head attention over n sequences of L rows: qkv [n][L][3C] (q | k | v, head-major inside each), ctx
+// [n][L][C]; optional decomposed rel-pos bias (L = h * w, tables [h][h][hd] and [w][w][hd]).  Scores for a
+// block of 4 query rows against every key by broadcast FMAs over K^T (built once per sequence and head),
+// softmax (exp(s - max) / sum), then P.V with the 4 rows' dims in registers.
+// exp on 16 lanes: n = round(x log2 e), r = x - n ln2 (two-part ln2), degree-6 polynomial, scaled by 2^n
+// (within ~2 ulp of expf over the softmax's range x <= 0; the vision leg's tolerance vs the oracle is 1e-4)
+inline __m512 exp16(__m512 x) {
+    x = _mm512_max_ps(x, _mm512_set1_ps(-87.3f));
+    const __m512 n = _mm512_roundscale_ps(_mm512_mul_ps(x, _mm512_set1_ps(1.44269504088896341f)), _MM_FROUND_TO_NEAREST_INT);
+    __m512 r = _mm512_fnmadd_ps(n, _mm512_set1_ps(0.693359375f), x);
+    r = _mm512_fnmadd_ps(n, _mm512_set1_ps(-2.12194440e-4f), r);
+    __m512 p = _mm512_set1_ps(1.3981999507e-3f);
+    p = _mm512_fmadd_ps(p, r, _mm512_set1_ps(8.3334519073e-3f));
+    p = _mm512_fmadd_ps(p, r, _mm512_set1_ps(4.1665795894e-2f));
+    p = _mm512_fmadd_ps(p, r, _mm512_set1_ps(1.6666665459e-1f));
+    p = _mm512_fmadd_ps(p, r, _mm512_set1_ps(5.0000001201e-1f));
+    p = _mm512_fmadd_ps(p, _mm512_mul_ps(r, r), _mm512_add_ps(r, _mm512_set1_ps(1.0f)));
+    return _mm512_scalef_ps(p, n);
+}
+
+// multi-head attention over n sequences of L rows: qkv [n][L][3C] (q | k | v, head-major inside each), ctx
+// [n][L][C]; optional decomposed rel-pos bias (L = h * w, tables [h][h][hd] and [w][w][hd]).  K^T and V are
+// copied once per (sequence, head) into contiguous [hd][Lp] / [L][hd] buffers; a work item is 16 query rows:
+// their scores against every key by broadcast FMAs over K^T, scale + bias, softmax (exp(s - max) / sum), then
+// P.V for 8 rows x 32 dims at a time.
+template <int ND>  // hd / 16
+void attention_core(const float* qkv, int n, int L, int C, int nh, const float* Rh, const float* Rw, int h, int w,
+                    float* ctx) {
+    constexpr int hd = ND * 16, QB = 16;
+    const int Lp = (L + 15) & ~15, C3 = 3 * C;
+    const float scale = 1.0f / std::sqrt((float)hd);
+    std::vector<float> kt((size_t)n * nh * hd * Lp, 0.f), vv((size_t)n * nh * L * hd);
+#pragma omp parallel for schedule(static) collapse(2)
+    for (int i = 0; i < n; ++i)
+        for (int hh = 0; hh < nh; ++hh) {
+            float* K = kt.data() + ((size_t)i * nh + hh) * hd * Lp;
+            float* V = vv.data() + ((size_t)i * nh + hh) * L * hd;
+            for (int k = 0; k < L; ++k) {
+                const float* kr = qkv + ((size_t)i * L + k) * C3 + C + hh * hd;
+                for (int d = 0; d < hd; ++d) K[(size_t)d * Lp + k] = kr[d];
+                memcpy(V + (size_t)k * hd, kr + C, hd * 4);
+            }
+        }
+    const int nqb = (L + QB - 1) / QB;
+#pragma omp parallel
+    {
+        std::vector<float> S((size_t)QB * Lp);
+        std::vector<float> rh((size_t)QB * std::max(h, 1)), rw((size_t)QB * std::max(w, 1));
+#pragma omp for schedule(dynamic, 2) collapse(3)
+        for (int i = 0; i < n; ++i)
+            for (int hh = 0; hh < nh; ++hh)
+                for (int qb = 0; qb < nqb; ++qb) {
+                    const int q0 = qb * QB, nq = std::min(QB, L - q0);
+                    const float* K = kt.data() + ((size_t)i * nh + hh) * hd * Lp;
+                    const float* V = vv.data() + ((size_t)i * nh + hh) * L * hd;
+                    const float* Q[QB];
+                    for (int r = 0; r < QB; ++r) Q[r] = qkv + ((size_t)i * L + q0 + std::min(r, nq - 1)) * C3 + hh * hd;
+                    // 8 query rows x 32 keys per pass (2 K^T loads + 8 broadcasts per 16 FMAs)
+                    for (int rh0 = 0; rh0 < QB; rh0 += 8)
+                        for (int kb = 0; kb < Lp; kb += 32) {
+                            const bool two = kb + 16 < Lp;
+                            __m512 a0[8], a1[8];
+                            for (int r = 0; r < 8; ++r) { a0[r] = _mm512_setzero_ps(); a1[r] = _mm512_setzero_ps(); }
+                            for (int d = 0; d < hd; ++d) {
+                                const __m512 k0 = _mm512_loadu_ps(K + (size_t)d * Lp + kb);
+                                const __m512 k1 = two ? _mm512_loadu_ps(K + (size_t)d * Lp + kb + 16) : _mm512_setzero_ps();
+                                for (int r = 0; r < 8; ++r) {
+                                    const __m512 qb_ = _mm512_set1_ps(Q[rh0 + r][d]);
+                                    a0[r] = _mm512_fmadd_ps(qb_, k0, a0[r]);
+                                    a1[r] = _mm512_fmadd_ps(qb_, k1, a1[r]);
+                                }
+                            }
+                            for (int r = 0; r < 8; ++r) {
+                                _mm512_storeu_ps(S.data() + (size_t)(rh0 + r) * Lp + kb, a0[r]);
+                                if (two) _mm512_storeu_ps(S.data() + (size_t)(rh0 + r) * Lp + kb + 16, a1[r]);
+                            }
+                        }
+                    if (Rh) {
+                        for (int r = 0; r < nq; ++r) {
+                            const int q = q0 + r, qh = q / w, qw = q % w;
+                            for (int kh = 0; kh < h; ++kh) {
+                                const float* t = Rh + ((size_t)qh * h + kh) * hd;
+                                __m512 a = _mm512_setzero_ps();
+                                for (int d = 0; d < hd; d += 16) a = _mm512_fmadd_ps(_mm512_loadu_ps(Q[r] + d), _mm512_loadu_ps(t + d), a);
+                                rh[r * h + kh] = _mm512_reduce_add_ps(a);
+                            }
+                            for (int kw = 0; kw < w; ++kw) {
+                                const float* t = Rw + ((size_t)qw * w + kw) * hd;
+                                __m512 a = _mm512_setzero_ps();
+                                for (int d = 0; d < hd; d += 16) a = _mm512_fmadd_ps(_mm512_loadu_ps(Q[r] + d), _mm512_loadu_ps(t + d), a);
+                                rw[r * w + kw] = _mm512_reduce_add_ps(a);
+                            }
+                        }
+                    }
+                    for (int r = 0; r < QB; ++r) {
+                        float* sr = S.data() + (size_t)r * Lp;
+                        if (r >= nq) { std::fill(sr, sr + Lp, 0.f); continue; }
+                        __m512 mv = _mm512_set1_ps(-INFINITY);
+                        const __m512 sc = _mm512_set1_ps(scale);
+                        for (int k = 0; k < Lp; k += 16) {
+                            const __mmask16 mk = (L - k) >= 16 ? (__mmask16)0xffff : (__mmask16)((1u << (L - k)) - 1);
+                            __m512 v = _mm512_mul_ps(_mm512_loadu_ps(sr + k), sc);
+                            if (Rh && w % 16 == 0) {  // the 16 keys share kh = k / w; kw = k % w .. + 15
+                                v = _mm512_add_ps(v, _mm512_add_ps(_mm512_set1_ps(rh[r * h + k / w]), _mm512_loadu_ps(&rw[r * w + k % w])));
+                            } else if (Rh) {
+                                alignas(64) float bias[16];
+                                for (int t = 0; t < 16; ++t) {
+                                    const int kk = std::min(k + t, L - 1);
+                                    bias[t] = rh[r * h + kk / w] + rw[r * w + kk % w];
+                                }
+                                v = _mm512_add_ps(v, _mm512_load_ps(bias));
+                            }
+                            v = _mm512_mask_blend_ps(mk, _mm512_set1_ps(-INFINITY), v);
+                            _mm512_storeu_ps(sr + k, v);
+                            mv = _mm512_max_ps(mv, v);
+                        }
+                        const __m512 mx = _mm512_set1_ps(_mm512_reduce_max_ps(mv));
+                        __m512 sv = _mm512_setzero_ps();
+                        for (int k = 0; k < Lp; k += 16) {
+                            const __mmask16 mk = (L - k) >= 16 ? (__mmask16)0xffff : (__mmask16)((1u << (L - k)) - 1);
+                            const __m512 e = _mm512_maskz_mov_ps(mk, exp16(_mm512_sub_ps(_mm512_loadu_ps(sr + k), mx)));
+                            _mm512_storeu_ps(sr + k, e);
+                            sv = _mm512_add_ps(sv, e);
+                        }
+                        const __m512 sum = _mm512_set1_ps(_mm512_reduce_add_ps(sv));
+                        for (int k = 0; k < Lp; k += 16) _mm512_storeu_ps(sr + k, _mm512_div_ps(_mm512_loadu_ps(sr + k), sum));
+                    }
+                    for (int r0 = 0; r0 < nq; r0 += 8) {
+                        for (int j = 0; j < ND; j += 2) {
+                            __m512 o0[8], o1[8];
+                            for (int r = 0; r < 8; ++r) { o0[r] = _mm512_setzero_ps(); o1[r] = _mm512_setzero_ps(); }
+                            for (int k = 0; k < L; ++k) {
+                                const __m512 v0 = _mm512_loadu_ps(V + (size_t)k * hd + 16 * j);
+                                const __m512 v1 = _mm512_loadu_ps(V + (size_t)k * hd + 16 * j + 16);
+                                for (int r = 0; r < 8; ++r) {
+                                    const __m512 pb = _mm512_set1_ps(S[(size_t)(r0 + r) * Lp + k]);
+                                    o0[r] = _mm512_fmadd_ps(pb, v0, o0[r]);
+                                    o1[r] = _mm512_fmadd_ps(pb, v1, o1[r]);
+                                }
+                            }
+                            for (int r = 0; r < 8 && r0 + r < nq; ++r) {
+                                float* orow = ctx + ((size_t)i * L + q0 + r0 + r) * C + hh * hd + 16 * j;
+                                _mm512_storeu_ps(orow, o0[r]);
+                                _mm512_storeu_ps(orow + 16, o1[r]);
+                            }
+                        }
+                    }
+                }
+    }
+}
+
+void attention_any(const float* qkv, int n, int L, int C, int nh, const float* Rh, const float* Rw, int h, int w,
+                   float* ctx) {
+    const int hd = C / nh;
+    if (hd == 64) attention_core<4>(qkv, n, L, C, nh, Rh, Rw, h, w, ctx);
+    else if (hd == 32) attention_core<2>(qkv, n, L, C, nh, Rh, Rw, h, w, ctx);
+    else if (hd == 128) attention_core<8>(qkv, n, L, C, nh, Rh, Rw, h, w, ctx);
+    else throw std::runtime_error("cpu_ref vision: head dim must be 32, 64 or 128");
+}
+
+inline float gelu_erf(float v) { return 0.5f * v * (1.0f + std::erf(v * 0.70710678118654752f)); }
+
+// conv (no bias) on NHWC x [B][H][W][C] with the weight re-laid [O][kh][kw][C] (CpuVision does it): im2col + linear
+void conv_nhwc(const float* x, int B, int H, int Wd, int C, const Tensor& w, int O, int k, int stride, int pad,
+               std::vector<float>& y, int& oh, int& ow) {
+    oh = (H + 2 * pad - k) / stride + 1;
+    ow = (Wd + 2 * pad - k) / stride + 1;
+    const long rows = (long)B * oh * ow, K = (long)k * k * C;
+    VClk clk2(2);
+    std::vector<float> cols((size_t)rows * K);
+#pragma omp parallel for schedule(static)
+    for (long r = 0; r < rows; ++r) {
+        const int b = (int)(r / ((long)oh * ow)), oy = (int)(r / ow % oh), ox = (int)(r % ow);
+        float* cr = cols.data() + (size_t)r * K;
+        for (int ky = 0; ky < k; ++ky)
+            for (int kx = 0; kx < k; ++kx) {
+                const int iy = oy * stride + ky - pad, ix = ox * stride + kx - pad;
+                float* dst = cr + ((size_t)ky * k + kx) * C;
+                if (iy < 0 || iy >= H || ix < 0 || ix >= Wd) std::fill(dst, dst + C, 0.f);
+                else memcpy(dst, x + (((size_t)b * H + iy) * Wd + ix) * C, (size_t)C * 4);
+            }
+    }
+    y.assign((size_t)rows * O, 0.f);
+    linear(cols.data(), (int)rows, (int)K, w, nullptr, y.data(), O);
+}
+
+// SamBackbone::forward: img [B][3][H][W] -> NHWC [B][H/64][W/64][c1] (out, resized)
+void sam_forward(const float* img, int B, int H, int Wd, std::vector<float>& out, int& oh, int& ow) {
+    const VCfg& v = g_v;
+    const std::string pre = "model.sam_model.";
+    const int ps = v.patch, gh = H / ps, gw = Wd / ps, C = v.embed, K0 = 3 * ps * ps;
+    const long T = (long)B * gh * gw;
+    std::vector<float> cols((size_t)T * K0), x((size_t)T * C);
+#pragma omp parallel for schedule(static)
+    for (long r = 0; r < T; ++r) {
+        const int b = (int)(r / ((long)gh * gw)), gy = (int)(r / gw % gh), gx = (int)(r % gw);
+        for (int c = 0; c < 3; ++c)
+            for (int ky = 0; ky < ps; ++ky)
+                memcpy(cols.data() + (size_t)r * K0 + ((size_t)c * ps + ky) * ps,
+                       img + (((size_t)b * 3 + c) * H + gy * ps + ky) * Wd + gx * ps, (size_t)ps * 4);
+    }
+    linear(cols.data(), (int)T, K0, W(pre + "patch_embed.proj.weight"), opt(pre + "patch_embed.proj.bias"), x.data(), C);
+    const std::string pk = "cv.sam.pos." + std::to_string(gh) + "x" + std::to_string(gw);
+    if (has(pk)) {
+        const float* pos = W(pk).f.data();
+        for (long r = 0; r < T; ++r)
+            for (int c = 0; c < C; ++c) x[(size_t)r * C + c] += pos[(size_t)(r % ((long)gh * gw)) * C + c];
+    }
+    std::vector<float> nrm((size_t)T * C), attn((size_t)T * C);
+    for (int blk = 0; blk < v.depth; ++blk) {
+        const std::string bp = pre + "blocks." + std::to_string(blk) + ".";
+        layer_norm_rows(x.data(), T, C, W(bp + "norm1.weight").f.data(), W(bp + "norm1.bias").f.data(), v.sam_eps, nrm.data());
+        const bool glob = std::find(v.global.begin(), v.global.end(), blk) != v.global.end();
+        const int ws = glob ? 0 : v.window;
+        int n, h, w;
+        std::vector<float> win;
+        const float* xin;
+        int hp = gh, wp = gw;
+        if (ws > 0) {
+            hp = gh + (ws - gh % ws) % ws;
+            wp = gw + (ws - gw % ws) % ws;
+            const int nwy = hp / ws, nwx = wp / ws;
+            n = B * nwy * nwx;
+            h = w = ws;
+            win.assign((size_t)n * ws * ws * C, 0.f);
+#pragma omp parallel for schedule(static) collapse(2)
+            for (int b = 0; b < B; ++b)
+                for (int y = 0; y < gh; ++y)
+                    for (int xx = 0; xx < gw; ++xx) {
+                        const int wi = (b * nwy + y / ws) * nwx + xx / ws, t = (y % ws) * ws + xx % ws;
+                        memcpy(win.data() + ((size_t)wi * ws * ws + t) * C, nrm.data() + (((size_t)b * gh + y) * gw + xx) * C,
+                               (size_t)C * 4);
+                    }
+            xin = win.data();
+        } else {
+            n = B;
+            h = gh;
+            w = gw;
+            xin = nrm.data();
+        }
+        const int L = h * w;
+        std::vector<float> qkv((size_t)n * L * 3 * C), ctx((size_t)n * L * C), y((size_t)n * L * C);
+        linear(xin, n * L, C, W(bp + "attn.qkv.weight"), opt(bp + "attn.qkv.bias"), qkv.data(), 3 * C);
+        const float *Rh = nullptr, *Rw = nullptr;
+        if (has(bp + "attn.rel_pos_h")) {
+            Rh = W("cv.sam.relh." + std::to_string(blk) + "." + std::to_string(h)).f.data();
+            Rw = W("cv.sam.relw." + std::to_string(blk) + "." + std::to_string(w)).f.data();
+        }
+        const auto ta = std::chrono::steady_clock::now();
+        attention_any(qkv.data(), n, L, C, v.heads, Rh, Rw, h, w, ctx.data());
+        g_att_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
+        linear(ctx.data(), n * L, C, W(bp + "attn.proj.weight"), opt(bp + "attn.proj.bias"), y.data(), C);
+        if (ws > 0) {
+            const int nwy = hp / ws, nwx = wp / ws;
+#pragma omp parallel for schedule(static) collapse(2)
+            for (int b = 0; b < B; ++b)
+                for (int yy = 0; yy < gh; ++yy)
+                    for (int xx = 0; xx < gw; ++xx) {
+                        const int wi = (b * nwy + yy / ws) * nwx + xx / ws, t = (yy % ws) * ws + xx % ws;
+                        memcpy(attn.data() + (((size_t)b * gh + yy) * gw + xx) * C, y.data() + ((size_t)wi * ws * ws + t) * C,
+                               (size_t)C * 4);
+                    }
+        } else {
+            attn.swap(y);
+            y.assign(attn.size(), 0.f);
+        }
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < x.size(); ++i) x[i] += attn[i];
+        layer_norm_rows(x.data(), T, C, W(bp + "norm2.weight").f.data(), W(bp + "norm2.bias").f.data(), v.sam_eps, nrm.data());
+        const std::string f1 = has(bp + "mlp.fc1.weight") ? "mlp.fc1" : "mlp.lin1";
+        const std::string f2 = has(bp + "mlp.fc2.weight") ? "mlp.fc2" : "mlp.lin2";
+        const int hid = (int)W(bp + f1 + ".weight").rows;
+        std::vector<float> h1((size_t)T * hid), h2((size_t)T * C);
+        linear(nrm.data(), (int)T, C, W(bp + f1 + ".weight"), opt(bp + f1 + ".bias"), h1.data(), hid);
+        {
+            VClk clk(1);
+#pragma omp parallel for schedule(static)
+            for (size_t i = 0; i < h1.size(); ++i) h1[i] = gelu_erf(h1[i]);
+        }
+        linear(h1.data(), (int)T, hid, W(bp + f2 + ".weight"), opt(bp + f2 + ".bias"), h2.data(), C);
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < x.size(); ++i) x[i] += h2[i];
+    }
+    // neck + downsample (NHWC; LN2d = LN over channels per position)
+    std::vector<float> a, bbuf;
+    int h1, w1;
+    conv_nhwc(x.data(), B, gh, gw, C, W("cv.sam.neck.0"), v.neck, 1, 1, 0, a, h1, w1);
+    bbuf.resize(a.size());
+    layer_norm_rows(a.data(), (long)B * h1 * w1, v.neck, W(pre + "neck.1.weight").f.data(), W(pre + "neck.1.bias").f.data(), 1e-6f, bbuf.data());
+    conv_nhwc(bbuf.data(), B, h1, w1, v.neck, W("cv.sam.neck.2"), v.neck, 3, 1, 1, a, h1, w1);
+    layer_norm_rows(a.data(), (long)B * h1 * w1, v.neck, W(pre + "neck.3.weight").f.data(), W(pre + "neck.3.bias").f.data(), 1e-6f, bbuf.data());
+    int h2, w2;
+    conv_nhwc(bbuf.data(), B, h1, w1, v.neck, W("cv.sam.net_2"), v.c0, 3, 2, 1, a, h2, w2);
+    conv_nhwc(a.data(), B, h2, w2, v.c0, W("cv.sam.net_3"), v.c1, 3, 2, 1, out, oh, ow);
+}
+
+// ClipVisionModel::forward with the SAM features as patch embeddings: sam [B][g*g][C] -> x [B][1+g*g][C]
+void clip_forward(const float* sam, int B, int G, std::vector<float>& x) {
+    const VCfg& v = g_v;
+    const std::string pre = "model.vision_model.";
+    const int C = v.clip_h, S = G + 1;
+    const long T = (long)B * S;
+    x.assign((size_t)T * C, 0.f);
+    const float* cls = W(pre + "embeddings.class_embedding").f.data();
+    const float* pos = W("cv.clip.pos." + std::to_string(S)).f.data();
+    for (int b = 0; b < B; ++b)
+        for (int t = 0; t < S; ++t)
+            for (int c = 0; c < C; ++c)
+                x[((size_t)b * S + t) * C + c] = (t == 0 ? cls[c] : sam[((size_t)b * G + t - 1) * C + c]) + pos[(size_t)t * C + c];
+    std::vector<float> n1((size_t)T * C);
+    layer_norm_rows(x.data(), T, C, W(pre + "pre_layrnorm.weight").f.data(), W(pre + "pre_layrnorm.bias").f.data(), v.clip_eps, n1.data());
+    x.swap(n1);
+    std::vector<float> qkv((size_t)T * 3 * C), ctx((size_t)T * C), y((size_t)T * C), h1((size_t)T * v.clip_ffn);
+    for (int li = 0; li < v.clip_layers; ++li) {
+        const std::string lp = pre + "transformer.layers." + std::to_string(li) + ".";
+        layer_norm_rows(x.data(), T, C, W(lp + "layer_norm1.weight").f.data(), W(lp + "layer_norm1.bias").f.data(), v.clip_eps, n1.data());
+        linear(n1.data(), (int)T, C, W(lp + "self_attn.qkv_proj.weight"), opt(lp + "self_attn.qkv_proj.bias"), qkv.data(), 3 * C);
+        const auto ta = std::chrono::steady_clock::now();
+        attention_any(qkv.data(), B, S, C, v.clip_heads, nullptr, nullptr, 0, 0, ctx.data());
+        g_att_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
+        linear(ctx.data(), (int)T, C, W(lp + "self_attn.out_proj.weight"), opt(lp + "self_attn.out_proj.bias"), y.data(), C);
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < x.size(); ++i) x[i] += y[i];
+        layer_norm_rows(x.data(), T, C, W(lp + "layer_norm2.weight").f.data(), W(lp + "layer_norm2.bias").f.data(), v.clip_eps, n1.data());
+        linear(n1.data(), (int)T, C, W(lp + "mlp.fc1.weight"), opt(lp + "mlp.fc1.bias"), h1.data(), v.clip_ffn);
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < h1.size(); ++i) h1[i] = (1.0f / (1.0f + std::exp(-(h1[i] * 1.702f)))) * h1[i];
+        linear(h1.data(), (int)T, v.clip_ffn, W(lp + "mlp.fc2.weight"), opt(lp + "mlp.fc2.bias"), y.data(), C);
+#pragma omp parallel for schedule(static)
+        for (size_t i = 0; i < x.size(); ++i) x[i] += y[i];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -391,13 +825,31 @@ int cr_init(int H, int heads, int kv_heads, int hd, int layers, int vocab, int i
     return 0;
 }
 
-// kind: 0 keep f32, 1 store f16 (values already f16-rounded), 2 store bf16 (values already bf16)
+// kind: 0 keep f32, 1 store f16 (values already f16-rounded), 2 store bf16 (values already bf16), 3 store bf16 as
+// the packed 32-column panels of linear_packed (rows = N outputs, cols = K)
 int cr_set(const char* name, const float* data, long rows, long cols, int kind) {
     Tensor t;
     t.kind = kind;
     t.rows = rows;
     t.cols = cols;
     const long n = rows * cols;
+    if (kind == 3) {
+        const long np = (rows + 31) / 32;
+        t.h.assign((size_t)np * cols * 32, 0);
+        uint32_t* P = reinterpret_cast<uint32_t*>(t.h.data());
+#pragma omp parallel for schedule(static)
+        for (long p = 0; p < np; ++p)
+            for (long k = 0; k < cols; ++k)
+                for (int i = 0; i < 32; ++i) {
+                    const long r = 32 * p + i;
+                    uint32_t bits = 0;
+                    if (r < rows) memcpy(&bits, data + r * cols + k, 4);
+                    const uint32_t v = bits >> 16;
+                    P[((size_t)p * cols + k) * 16 + (i & 15)] |= i < 16 ? v : (v << 16);
+                }
+        g_w[name] = std::move(t);
+        return 0;
+    }
     if (kind == 0) {
         t.f.assign(data, data + n);
     } else {
@@ -468,12 +920,74 @@ int cr_generate(const int64_t* ids, const uint8_t* mask, int P, const float* img
     }
 }
 
+
+// ---- vision (round 5).  cv_init keeps the tensors already set (the decoder's cr_init clears them).
+int cv_init(int embed, int depth, int heads, int window, const int* global_flags, int neck, int c0, int c1, int patch,
+            float sam_eps, int clip_h, int clip_layers, int clip_heads, int clip_ffn, float clip_eps, int n_embed,
+            int in_dim, int threads) {
+    g_v = VCfg{embed, depth, heads, window, neck, c0, c1, patch, sam_eps, clip_h, clip_layers, clip_heads, clip_ffn,
+               clip_eps, n_embed, in_dim, {}};
+    for (int i = 0; i < depth; ++i)
+        if (global_flags[i]) g_v.global.push_back(i);
+    if (threads > 0) omp_set_num_threads(threads);
+    return (embed % 16 || clip_h % 16 || in_dim % 16) ? 1 : 0;
+}
+
+// one batch of B same-size views [B][3][H][W] -> the projected tokens post [B][G][n_embed] (G = (H/64)(W/64)),
+// the pre-projection rows pre [B][G][in_dim] when non-null; ms = {sam, clip, projector}
+int cv_features(const float* img, int B, int H, int Wd, float* post, float* pre_out, double* ms) {
+    try {
+        const VCfg& v = g_v;
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<float> sam;
+        int oh, ow;
+        sam_forward(img, B, H, Wd, sam, oh, ow);
+        auto t1 = std::chrono::steady_clock::now();
+        if (oh != ow || v.c1 != v.clip_h) return 2;
+        const int G = oh * ow;
+        std::vector<float> clip;
+        clip_forward(sam.data(), B, G, clip);
+        auto t2 = std::chrono::steady_clock::now();
+        std::vector<float> pre((size_t)B * G * v.in_dim);
+        for (int b = 0; b < B; ++b)
+            for (int t = 0; t < G; ++t) {
+                float* r = pre.data() + ((size_t)b * G + t) * v.in_dim;
+                memcpy(r, clip.data() + ((size_t)b * (G + 1) + t + 1) * v.clip_h, (size_t)v.clip_h * 4);
+                memcpy(r + v.clip_h, sam.data() + ((size_t)b * G + t) * v.c1, (size_t)v.c1 * 4);
+            }
+        linear(pre.data(), B * G, v.in_dim, W("model.projector.layers.weight"), opt("model.projector.layers.bias"), post,
+               v.n_embed);
+        if (pre_out) memcpy(pre_out, pre.data(), pre.size() * 4);
+        if (getenv("DSOCR_CV_PROF")) {
+            fprintf(stderr, "[cv] ln %.0f act %.0f im2col %.0f ms\n", g_vis_prof[0], g_vis_prof[1], g_vis_prof[2]);
+            for (double& d : g_vis_prof) d = 0;
+        }
+        auto t3 = std::chrono::steady_clock::now();
+        ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        ms[2] = std::chrono::duration<double, std::milli>(t3 - t2).count();
+        return 0;
+    } catch (...) {
+        return 3;
+    }
+}
+
 void cr_free() {
     g_w.clear();
     g_kv.clear();
 }
 
 int cr_threads() { return omp_get_max_threads(); }
+
+// Y = X . W^T for a tensor set with cr_set (micro-benchmark of the linear kernel)
+int cr_linear(const char* wname, const float* X, int M, int K, float* Y, int N) {
+    try {
+        linear(X, M, K, W(wname), nullptr, Y, N);
+        return 0;
+    } catch (...) {
+        return 3;
+    }
+}
 
 // stage clocks since the last call (ms): linears, attention core
 void cr_profile(double* out) {

@@ -37,6 +37,8 @@ def _lib():
     L.cr_set.argtypes = [C.c_char_p, vp, C.c_long, C.c_long, i32]
     L.cr_generate.argtypes = [vp, vp, i32, vp, i32, i32, i32, vp, vp]
     L.cr_free.restype = None
+    L.cv_init.argtypes = [i32, i32, i32, i32, vp, i32, i32, i32, i32, f32, i32, i32, i32, i32, f32, i32, i32, i32]
+    L.cv_features.argtypes = [vp, i32, i32, i32, vp, vp, vp]
     return L
 
 
@@ -85,3 +87,94 @@ class CpuRef:
 
     def close(self):
         self.L.cr_free()
+
+
+class CpuVision:
+    """The vision tower (SAM-ViTDet-B + CLIP-L + projector) in C++ / OpenMP (cv_features in cpu_ref.cpp; oracle
+    restatement oracle/vision.py of sam.rs / clip.rs / model/mod.rs:246-923).  The weight-only tables (position
+    embeddings resized to each grid, rel-pos tables per block and grid) come from the oracle's own functions, once,
+    for the view sizes given; the conv weights are re-laid [O][kh][kw][C] for the NHWC im2col.  embeddings(rgb) =
+    Vision.embeddings with the features computed in C++; stage times in last_ms."""
+
+    def __init__(self, cfg, weights, threads=0, sizes=(1024, 640)):
+        from .config import clip_params, projector_params, sam_params
+        from .vision import Clip, Sam, Vision, get_rel_pos
+        self.L = _lib()
+        sp, cp, pp = sam_params(cfg), clip_params(cfg), projector_params(cfg)
+        self.sp, self.cp = sp, cp
+        self.n_embed, self.in_dim = pp["n_embed"], pp["input_dim"]
+        flags = (C.c_int * sp.depth)(*[1 if i in sp.global_attn_indexes else 0 for i in range(sp.depth)])
+        rc = self.L.cv_init(sp.embed_dim, sp.depth, sp.num_heads, sp.window_size, flags, sp.neck_channels,
+                            sp.out_channels[0], sp.out_channels[1], sp.patch_size, float(sp.norm_eps), cp.hidden_size,
+                            cp.num_layers, cp.num_heads, cp.ffn_hidden_size, float(cp.eps), self.n_embed, self.in_dim,
+                            int(threads))
+        if rc:
+            raise RuntimeError(f"cpu_ref vision init failed ({rc})")
+        from .specs import tensor_names
+        conv = {"model.sam_model.neck.0.weight": "cv.sam.neck.0", "model.sam_model.neck.2.weight": "cv.sam.neck.2",
+                "model.sam_model.net_2.weight": "cv.sam.net_2", "model.sam_model.net_3.weight": "cv.sam.net_3"}
+        for name, shape in tensor_names(cfg).items():
+            if not name.startswith(("model.sam_model.", "model.vision_model.", "model.projector.")) or not weights.has(name):
+                continue
+            a = np.asarray(weights.get(name, shape), np.float32)
+            if name in conv:
+                a = a.transpose(0, 2, 3, 1)
+                self._set(conv[name], a.reshape(a.shape[0], -1), 3)
+            elif len(shape) >= 2 and "pos" not in name and "rel_pos" not in name:
+                self._set(name, a.reshape(shape[0], -1), 3)  # bf16 values (exact), packed panels
+            else:
+                self._set(name, a.reshape(1, -1) if a.ndim < 2 else a.reshape(a.shape[0], -1), 0)
+        sam, clip = Sam(cfg, weights), Clip(cfg, weights)
+        self._vision = Vision(cfg, weights)
+        hd = sp.embed_dim // sp.num_heads
+        for size in sizes:
+            g = size // sp.patch_size
+            pos = sam.pos_embed(g, g)
+            if pos is not None:
+                self._set(f"cv.sam.pos.{g}x{g}", pos.reshape(g * g, -1), 0)
+            for blk in range(sp.depth):
+                pre = f"model.sam_model.blocks.{blk}.attn."
+                if not weights.has(pre + "rel_pos_h"):
+                    continue
+                win = 0 if blk in sp.global_attn_indexes else sp.window_size
+                n = g if win == 0 else win
+                tokens = win if win > 0 else sp.image_size // sp.patch_size
+                rel = (2 * tokens - 1, hd)
+                self._set(f"cv.sam.relh.{blk}.{n}", get_rel_pos(n, n, weights.get(pre + "rel_pos_h", rel)).reshape(n, -1), 0)
+                self._set(f"cv.sam.relw.{blk}.{n}", get_rel_pos(n, n, weights.get(pre + "rel_pos_w", rel)).reshape(n, -1), 0)
+            go = g // 4
+            self._set(f"cv.clip.pos.{go * go + 1}", clip.pos(go * go + 1), 0)
+        self.last_ms = {}
+
+    def _set(self, name, a, kind):
+        a = np.ascontiguousarray(a, np.float32)
+        self.L.cr_set(name.encode(), a.ctypes.data_as(C.c_void_p), a.shape[0], int(np.prod(a.shape[1:])), kind)
+
+    def features(self, img, want_pre=False):
+        """img [B,3,H,W] f32 -> (pre [B,G,in_dim] or None, post [B,G,n_embed])."""
+        img = np.ascontiguousarray(img, np.float32)
+        B, _, H, Wd = img.shape
+        G = (H // 64) * (Wd // 64)
+        post = np.zeros((B, G, self.n_embed), np.float32)
+        pre = np.zeros((B, G, self.in_dim), np.float32) if want_pre else None
+        ms = np.zeros(3, np.float64)
+        rc = self.L.cv_features(img.ctypes.data_as(C.c_void_p), B, H, Wd, post.ctypes.data_as(C.c_void_p),
+                                pre.ctypes.data_as(C.c_void_p) if want_pre else None, ms.ctypes.data_as(C.c_void_p))
+        if rc:
+            raise RuntimeError(f"cpu_ref vision failed ({rc})")
+        for k, v in zip(("sam_ms", "clip_ms", "projector_ms"), ms):
+            self.last_ms[k] = self.last_ms.get(k, 0.0) + float(v)
+        return pre, post
+
+    def embeddings(self, rgb, base=1024, image_size=640, crop_mode=True):
+        """OracleModel.image_embeddings with the tower in C++ (preprocessing and token formatting as the oracle)."""
+        from . import preprocess
+        glob, patches, crop = preprocess.prepare_vision_input(rgb, base, image_size, crop_mode)
+        self.last_ms = {}
+        v = self._vision
+        orig = v.features
+        v.features = lambda img: self.features(img)
+        try:
+            return v.embeddings(glob, patches, crop), crop
+        finally:
+            v.features = orig

@@ -128,3 +128,33 @@ def test_span_roofline_prices_each_launch():
     a = got["attention"]
     assert abs(a["GB/s"] - bench.span_bytes("attention", d, 8, 706, 0, 3) / 8e-6 / 1e9) < 1e-6
     assert bench.span_bytes("attention", d, 1, 706, 0, 3) == 709 * 10 * 128 * 8 + (3840 + 1280) * 4
+
+
+def test_chain_roofline_exit_to_exit():
+    """bench.chain_roofline: a launch's duration = its last wave exit - the previous launch's last exit (router ->
+    gate/up -> down, attention -> o_proj -> router, down of layer l - 1 -> attention of l at one page), boundary =
+    its first entry - that exit; MoE launches priced at the wave-span generate's expert counts."""
+    import numpy as np
+    d = bench.lang_dims({"hidden_size": 1280, "moe_intermediate_size": 896, "n_shared_experts": 2,
+                         "num_experts_per_tok": 6, "num_attention_heads": 10, "num_key_value_heads": 10})
+    K = ("moe_gateup", "moe_down", "attention", "o_proj", "router")
+    ch = {k: np.zeros((3, 4, 5), np.uint64) for k in K}
+    wv = {k: np.zeros((3, 4, 5), np.uint64) for k in K[:3]}
+    # layer 1, step 2 (100 MHz ticks): attention [0, 1100], o_proj [1250, 1500], router [1650, 1900],
+    # gate/up [2050, 2800], down [2950, 3600]; layer 2 attention [3750, 4800]
+    for k, (e, x) in {"attention": (0, 1100), "o_proj": (1250, 1500), "router": (1650, 1900),
+                      "moe_gateup": (2050, 2800), "moe_down": (2950, 3600)}.items():
+        ch[k][1, 2, 0], ch[k][1, 2, 1] = e, x
+    ch["attention"][2, 2, 0], ch["attention"][2, 2, 1] = 3750, 4800
+    wv["moe_gateup"][1, 2, 2] = 6
+    wv["moe_down"][1, 2, 2] = 6
+    got = bench.chain_roofline(ch, wv, d, 1, 706)
+    g = got["moe_gateup"]
+    assert g["launches"] == 1 and abs(g["avg_us"] - 9.0) < 1e-9 and abs(g["boundary_us"] - 1.5) < 1e-9
+    assert abs(g["wave_us"] - 7.5) < 1e-9
+    assert g["bytes_per_launch"] == bench.span_bytes("moe_gateup", d, 1, 706, 6, 2)
+    assert abs(got["moe_down"]["avg_us"] - 8.0) < 1e-9
+    assert abs(got["router"]["avg_us"] - 4.0) < 1e-9 and abs(got["o_proj"]["avg_us"] - 4.0) < 1e-9
+    assert got["attention"]["launches"] == 1 and abs(got["attention"]["avg_us"] - 12.0) < 1e-9
+    # 8 pages: the attention follows an unstamped q/k/v launch and is not priced
+    assert "attention" not in bench.chain_roofline(ch, wv, d, 8, 706)
