@@ -98,23 +98,26 @@ def reduce_over_ranks(dist, elapsed, tok_s):
 
 
 def pmc_traffic(kernel_prefix, runs=None):
-    """Per-launch HBM bytes of a kernel from the committed rocprofv3 PMC summary
-    (latest profiles/rNN_pmc_traffic.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 (gfx950
-    reports half of wide streaming reads) + WRITE_SIZE, each from its own --pmc pass).  `runs` names the
-    PMC runs whose workload matches this bench line (the MoE kernels' bytes follow the routing: the 8-page
-    figure was taken on 8 text pages, 30 experts per layer, and is not this kernel's traffic at 16);
-    a kernel measured only in another run gives None."""
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary (latest
+    profiles/rNN_pmc_traffic.json, tools/pmc_summary.py + tools/pmc_merge.py: FETCH_SIZE x 2 (gfx950 reports half of
+    wide streaming reads) + WRITE_SIZE, each from its own --pmc pass) -> (bytes, traffic / algorithmic or None).
+    `runs` names the PMC runs whose workload matches this bench line (b1: one page; b8: 8 text pages; b8i: 8 image
+    pages).  Round 5: the MoE launches of a run are priced one by one at their own distinct experts
+    (tools/pmc_decode.py), so bytes and ratio come from the same launches; a kernel measured only in another run
+    gives (None, None)."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     try:
         d = json.load(open(paths[-1]))
     except Exception:
-        return None
-    for table in ("kernels", "kernels_b8"):
+        return None, None
+    for table in ("kernels", "kernels_b8", "kernels_b8i"):
         for name, v in d.get(table, {}).items():
             if name.startswith(kernel_prefix) and (runs is None or v.get("run") in runs):
-                return v.get("hbm_bytes_per_launch")
-    return None
+                if v.get("priced_hbm_bytes_per_launch"):
+                    return v["priced_hbm_bytes_per_launch"], v.get("traffic_over_algorithmic")
+                return v.get("hbm_bytes_per_launch"), None
+    return None, None
 
 
 def cpu_model():
@@ -128,35 +131,29 @@ def cpu_model():
 
 
 def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
-    """The repo's CPU restatement timed on rank 0's host cores, one whole page of the workload: the vision tower
-    by the numpy port (oracle/vision.py, BLAS-threaded), then the decoder by the C++ / OpenMP restatement
-    (oracle/cpu_ref.cpp: the same f32 math as the oracle; 16-bit weights widened at use): the 706-token
-    prefill and ALL (max_new - 1) decode forwards with the greedy 20-gram-ban selection, timed whole (no
-    extrapolation).  Threads: OMP_NUM_THREADS (the job's CPU share: 16 on the GPU box); BLAS at the same
-    count (no thread binding: a bound OpenMP master would pin the BLAS pool it spawns later to one core).  Stage sums are reported like the reference's
-    bench (crates/cli/src/bench.rs:200-260: vision, prefill, decode)."""
+    """The repo's C++ / OpenMP CPU restatement of the page path (oracle/cpu_ref.cpp, test/bench infrastructure)
+    timed on rank 0's host cores, one whole page of the workload: the vision tower (cv_features: SAM-ViTDet-B +
+    CLIP-L + projector, packed-panel AVX-512 GEMMs, the oracle's numpy preprocessing and token formatting), then
+    the decoder (cr_generate: the 706-token prefill and ALL (max_new - 1) decode forwards with the greedy
+    20-gram-ban selection), timed whole (no extrapolation).  Threads: OMP_NUM_THREADS (the job's CPU share: 16 on
+    the GPU box).  Stage sums are reported like the reference's bench (crates/cli/src/bench.rs:200-260: vision,
+    prefill, decode); the vision embeddings are checked against the numpy oracle's in tests/test_cpu_ref.py."""
     import numpy as np
 
     import dsocr
     from oracle import cpu_ref
-    from oracle.model import OracleModel
     from oracle.weights import Weights
     allowed = len(os.sched_getaffinity(0))
     threads = int(os.environ.get("OMP_NUM_THREADS") or allowed)
     cfg = json.load(open(dsocr.FULL_CONFIG))
-    orc = OracleModel(cfg, Weights(seed=0, dtype="f16"))
-    try:
-        from threadpoolctl import threadpool_limits
-    except ImportError:
-        threadpool_limits = None
-    t0 = time.time()  # (vision first: no OpenMP pool of the C++ library competes with the BLAS pool)
-    if threadpool_limits:
-        with threadpool_limits(limits=threads, user_api="blas"):
-            emb, _ = orc.image_embeddings(pages[0])
-    else:
-        emb, _ = orc.image_embeddings(pages[0])
+    t = time.time()
+    cv = cpu_ref.CpuVision(cfg, Weights(seed=0, dtype="f16"), threads=threads)
+    log(f"[cpu] C++ vision tower loaded in {time.time() - t:.1f}s ({threads} threads)")
+    t0 = time.time()
+    emb, _ = cv.embeddings(pages[0])
     vision_s = time.time() - t0
-    del orc
+    vis_ms = dict(cv.last_ms)
+    del cv
     t = time.time()
     cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
     log(f"[cpu] C++ decoder loaded in {time.time() - t:.1f}s ({threads} threads)")
@@ -165,14 +162,14 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
     prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3
     page_s = vision_s + prefill_s + decode_s
     return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads, "kind": "cpp",
-            "port": "oracle/cpu_ref.cpp: C++ / OpenMP restatement of the decoder (AVX-512 micro-kernels, f32 math, "
-                    "prefill + every decode step); the vision tower by the numpy port (oracle/vision.py, BLAS); "
-                    "the Rust reference cannot be built here",
+            "port": "oracle/cpu_ref.cpp: C++ / OpenMP restatement of the whole page path (vision tower + decoder, "
+                    "AVX-512 micro-kernels, f32 math); the Rust reference cannot be built here",
             "decode_tok_s": (max_new - 1) / decode_s, "host_cpus": os.cpu_count(),
             "allowed_cpus": allowed, "cpu_model": cpu_model(),
             "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
-            "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (numpy) + prefill {prefill_s:.2f}s "
-                      f"({len(tok_ids)} tok, C++) + {max_new - 1} decode steps {decode_s:.2f}s (C++, "
+            "vision_ms": {k: round(v, 1) for k, v in vis_ms.items()},
+            "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (C++, incl. numpy preprocessing) + prefill "
+                      f"{prefill_s:.2f}s ({len(tok_ids)} tok, C++) + {max_new - 1} decode steps {decode_s:.2f}s (C++, "
                       f"{decode_s / max(1, max_new - 1) * 1e3:.1f} ms/step), {threads} threads; first ids {ids[:4]}"}
 
 
@@ -325,7 +322,7 @@ def run_dots(args, rank, world, local, dist):
         # runs them on the bf16 matrix cores (exact: 1 pass for QK^T, 3 bf16 planes of P for P.V), so the
         # peak is the dense bf16 MFMA rate and the issued MFMA work is 2x the algorithmic FLOPs
         "roofline": {"bound": "mfma", "achieved": round(attn_tf, 2), "peak": 2500.0, "unit": "TFLOP/s",
-                     "frac": round(attn_tf / 2500.0, 4), "traffic": pmc_traffic("attention_bf16_tr_kernel"),
+                     "frac": round(attn_tf / 2500.0, 4), "traffic": pmc_traffic("attention_bf16_tr_kernel")[0],
                      "mfma_issued_tflops": round(2.0 * attn_tf, 2), "mfma_issued_frac": round(2.0 * attn_tf / 2500.0, 4),
                      "kernel": "attention_bf16_tr_kernel<128> (bidirectional flash attention over the page's 21316 tokens "
                                "on v_mfma_f32_32x32x16_bf16 with the reference's f32 math: exact bf16 q.k products, "
@@ -384,16 +381,16 @@ def chain_roofline(chain, waves, d, B, P):
 
 
 def decode_roofline(eng, batch, params, ppg, args):
-    """The roofline object of the decode MoE gate/up (the north-star kernel) at this batch size, from extra
-    generates of the first timed batch (rank 0, after the timed region):
-      1. chain spans (every layer's attention, o_proj, router, gate/up, down launches stamp their waves; one
-         fold per step; nothing else between the launches): each launch's dispatch-level duration = its last
-         wave exit - the previous launch's last wave exit, over every decode step -> `avg_launch_us`,
-         `achieved`, `frac` (rocprofv3 reports a back-to-back dispatch the same way: previous end -> end);
-      2. in-kernel wave spans with each MoE launch's distinct experts (one fold launch after each stamped
-         launch) -> `in_kernel_waves` and the pricing of (1) (same batch, same routing: ids checked equal);
-      3. profile_decode: one step's layers replayed as a graph with and without the gate/up launches ->
-         `in_context` (secondary)."""
+    """The roofline object of the decode MoE gate/up (the north-star kernel) at this batch size (rank 0, after the
+    timed region, on the first timed batch):
+      1. profile_decode: one decode step's layers replayed as a graph with and without the gate/up launches, HIP
+         events around the replays -> `avg_launch_us`, `achieved`, `frac` (the launch's in-context dispatch cost;
+         the round-5 production rocprofv3 trace agrees with it, profiles/INDEX_r05.md);
+      2. chain spans over a whole generate (every layer's attention, o_proj, router, gate/up, down launches stamp
+         their waves; one fold per step, nothing between the launches): exit-to-exit durations with the boundary
+         before each launch -> `chain`;
+      3. in-kernel wave spans with each MoE launch's distinct experts (one fold launch after each stamped launch)
+         -> `in_kernel_waves` and the pricing of (2) (same batch, same routing: ids checked equal)."""
     import dsocr
     dims = lang_dims(json.load(open(dsocr.FULL_CONFIG)))
     P = len(batch[0][0])
@@ -417,24 +414,28 @@ def decode_roofline(eng, batch, params, ppg, args):
                 "GB/s": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9, 1) if p["ctx_us"] > 0 else None,
                 "frac": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if p["ctx_us"] > 0 else None,
                 "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
-    gu = chain["moe_gateup"]
+    gu = ctx_line("moe_gateup")
     runs = ("b1",) if ppg == 1 else (("b8",) if args.text_pages and ppg == 8 else (("b8i",) if ppg == 8 else ()))
-    return {"bound": "hbm", "achieved": round(gu["GB/s"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gu["frac"], 4), "traffic": pmc_traffic(kernel, runs=runs),
+    traffic, ratio = pmc_traffic(kernel, runs=runs)
+    return {"bound": "hbm", "achieved": gu["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gu["frac"], "traffic": traffic, "traffic_over_algorithmic": ratio,
             "kernel": kernel + " (decode MoE gate/up of one layer: routed top-6 experts per page + shared experts)",
-            # avg_launch_us = mean dispatch-level duration over every gate/up launch of a whole generate
-            # (router's last wave exit -> gate/up's last wave exit, in the production step chain); achieved =
-            # the launches' algorithmic bytes (each priced at its own distinct experts) / their summed durations
-            "avg_launch_us": round(gu["avg_us"], 3), "bytes_per_launch": gu["bytes_per_launch"],
-            "launches": gu["launches"],
-            "timing": "dispatch duration: previous launch's last wave exit -> this launch's last wave exit, every "
-                      "decode step of one generate (chain spans)",
+            # avg_launch_us = the launch's dispatch-level cost in the production chain, by HIP events on the engine
+            # stream: one decode step's layers captured as a graph twice (as the decode loop runs them, and without
+            # the gate/up launches), each replayed back to back between events; (full - without) / MoE layers.
+            # Round 5: the 512-token graph-mode rocprofv3 trace of the timed generate alone (packet capture on, AQL
+            # ring 131072) gives the same figure for the same tree (profiles/INDEX_r05.md); bytes priced at the
+            # routing the replayed step takes (experts_touched distinct experts)
+            "avg_launch_us": gu["ctx_us"], "bytes_per_launch": gu["bytes"],
+            "experts_touched": prof["experts_touched"],
+            "timing": "HIP events: step-graph replays with and without the gate/up launches (in-context dispatch cost)",
+            # the same launches over every decode step of a whole generate: exit-to-exit spans in the production
+            # chain (previous launch's last wave exit -> this launch's last wave exit: the boundary before the launch
+            # instead of rocprof's after it), and the in-kernel wave spans alone
             "chain": chain,
             "in_kernel_waves": waves,
             "down_kernel": prof["moe_down_kernel"],
-            # secondary: one step's layers replayed with and without the gate/up launches, (full - without) / layers
             "in_context": {k: ctx_line(k) for k in ("moe_gateup", "moe_down", "attention")},
-            "experts_touched_profile_step": prof["experts_touched"],
             "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
                            "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
                        for k in ("lm_head", "lm_head_screened", "qkv", "o_proj", "router")

@@ -33,3 +33,19 @@ def test_cpu_ref_matches_oracle_tiny(seed, P, n_img, max_new, ngram):
         cr.close()
     assert got == ref, (got, ref)
     assert ms["prefill_ms"] > 0 and ms["decode_ms"] > 0
+
+
+@pytest.mark.parametrize("seed", [7, 11])
+def test_cpu_vision_matches_oracle_tiny(seed):
+    """The C++ vision tower (cv_features: SAM blocks with windowed / global attention and the decomposed rel-pos
+    bias, neck, downsample, CLIP, projector) against the numpy oracle (oracle/vision.py) on a crop-mode page:
+    the formatted image rows within 1e-4 relative (f32 summation order only)."""
+    cfg = json.load(open(TINY))
+    img = np.random.default_rng(seed).integers(0, 256, (300, 420, 3), dtype=np.uint8)
+    orc = OracleModel(cfg, Weights(seed=seed, dtype="f16"))
+    ref, crop = orc.image_embeddings(img, 256, 128, True)
+    cv = cpu_ref.CpuVision(cfg, Weights(seed=seed, dtype="f16"), threads=4, sizes=(256, 128))
+    got, crop2 = cv.embeddings(img, 256, 128, True)
+    assert crop == crop2 and got.shape == ref.shape
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-4
+    assert cv.last_ms["sam_ms"] > 0 and cv.last_ms["clip_ms"] > 0

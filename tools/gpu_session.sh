@@ -82,6 +82,10 @@ for step in "$@"; do
     kb_moe1) KB_WAVES=1 run 180 ./tools/kbench moe1 > gpurun_out/kb_moe1_o0.log 2>&1 && DSOCR_GU_ORDER=1 KB_WAVES=1 run 180 ./tools/kbench moe1 > gpurun_out/kb_moe1_o1.log 2>&1 ;;
     # same-process A/B under a graph-mode kernel trace (AB_VARIANTS: the --variant arguments)
     ab) ROC_AQL_QUEUE_SIZE=131072 run 900 rocprofv3 --kernel-trace --stats -d gpurun_out/ab${TAG:+_$TAG} -o g --output-format csv -- python tools/ab_trace.py --out gpurun_out/ab${TAG:+_$TAG}/order.json ${AB_ARGS} > gpurun_out/ab${TAG:+_$TAG}.log 2>&1 ;;
+    # PMC traffic with every MoE launch priced at its own routing (tools/pmc_decode.py + pmc_summary.py --routing);
+    # PMC_RUN = b1 | b8 | b8i
+    pmcr) case ${PMC_RUN:-b1} in b1) A="--pages 1" ;; b8) A="--pages 8 --text-pages" ;; b8i) A="--pages 8" ;; esac
+          for C in FETCH_SIZE WRITE_SIZE; do DSOCR_NO_GRAPH=1 run 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${PMC_RUN:-b1}_$C -o pmc --output-format csv -- python tools/pmc_decode.py $A --tokens 16 --out gpurun_out/routing_${PMC_RUN:-b1}.json > gpurun_out/pmc_${PMC_RUN:-b1}_$C.log 2>&1 || exit 1; done ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done

@@ -8,7 +8,7 @@ so fetched bytes = 2 x FETCH_SIZE x 1024.  WRITE_SIZE is exact for 16 B/lane sto
 atomics.  A calibration stream (tools/mb_stream, known bytes) can be passed to check both.
 
 usage: pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
-                      [--calib <mb_fetch_counter_collection.csv>]
+                      [--calib <mb_fetch_counter_collection.csv>] [--routing <tools/pmc_decode.py json>] [--run b1|b8|b8i]
 """
 import csv
 import json
@@ -24,12 +24,41 @@ def short(name):
 
 
 def load(path, counter):
-    per = defaultdict(list)
+    """kernel -> counter values per dispatch, in dispatch order (values of one dispatch summed)."""
+    per = defaultdict(dict)
     for r in csv.DictReader(open(path)):
         if r.get("Counter_Name") != counter:
             continue
-        per[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return per
+        d = per[short(r["Kernel_Name"])]
+        i = int(r["Dispatch_Id"])
+        d[i] = d.get(i, 0.0) + float(r["Counter_Value"])
+    return {k: [v[i] for i in sorted(v)] for k, v in per.items()}
+
+
+def priced(kernels, fetch, write, routing):
+    """The MoE launches of the routing file's plain generate (the last ones of each MoE kernel in dispatch
+    order) priced one by one at their own distinct experts (bench.span_bytes): measured / algorithmic."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    cfgp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "deepseek-ocr.rs_amd", "dsocr",
+                        "configs", "deepseek-ocr.json")
+    d = bench.lang_dims(json.load(open(cfgp)))
+    B = routing["pages"]
+    for k in kernels:
+        kind = "moe_gateup" if k.startswith("moe_gateup_m") else ("moe_down" if k.startswith("moe_down_mm") else None)
+        if kind is None or kind not in routing:
+            continue
+        seq = routing[kind]
+        f, w = fetch.get(k, []), write.get(k, [])
+        if len(f) < len(seq) or len(w) < len(seq):
+            continue
+        meas = [2.0 * 1024 * a + 1024 * b for a, b in zip(f[-len(seq):], w[-len(seq):])]
+        alg = [bench.span_bytes(kind, d, B, 706, e, 0) for e in seq]
+        kernels[k].update({"priced_launches": len(seq), "experts_mean": sum(seq) / len(seq),
+                           "priced_hbm_bytes_per_launch": sum(meas) / len(meas),
+                           "algorithmic_bytes_per_launch": sum(alg) / len(alg),
+                           "traffic_over_algorithmic": sum(meas) / sum(alg)})
 
 
 def main():
@@ -50,6 +79,14 @@ def main():
     res = {"source": {"fetch": fetch_csv, "write": write_csv},
            "correction": "read = 2 x FETCH_SIZE[KiB] x 1024 (gfx950 half-count of wide streaming reads); write = WRITE_SIZE[KiB] x 1024",
            "kernels": kernels}
+    if "--routing" in sys.argv:
+        routing = json.load(open(sys.argv[sys.argv.index("--routing") + 1]))
+        priced(kernels, fetch, write, routing)
+        res["routing"] = {k: routing[k] for k in ("pages", "text_pages", "tokens")}
+    if "--run" in sys.argv:
+        run = sys.argv[sys.argv.index("--run") + 1]
+        for v in kernels.values():
+            v["run"] = run
     if "--calib" in sys.argv:
         cal = load(sys.argv[sys.argv.index("--calib") + 1], "FETCH_SIZE")
         res["calibration"] = {k: {"launches": len(v), "read_bytes_per_launch": 2.0 * 1024 * sum(v) / len(v)}
