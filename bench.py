@@ -111,7 +111,7 @@ def pmc_traffic(kernel_prefix, runs=None):
         d = json.load(open(paths[-1]))
     except Exception:
         return None, None
-    for table in ("kernels", "kernels_b8", "kernels_b8i"):
+    for table in ("kernels", "kernels_b8", "kernels_b8i", "kernels_dots"):
         for name, v in d.get(table, {}).items():
             if name.startswith(kernel_prefix) and (runs is None or v.get("run") in runs):
                 if v.get("priced_hbm_bytes_per_launch"):

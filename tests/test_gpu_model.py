@@ -237,9 +237,9 @@ def test_full_screened_selection_equals_exact(full_engine, monkeypatch):
 
 def test_full_spans_do_not_change_ids(full_engine):
     """In-context launch spans (dsocr_engine_set_spans: 1 = wave spans stamped by every gate/up, down and
-    attention wave, 2 = HIP events around those launches inside the replayed step graph; the MoE is then
-    split into its route / gate-up / down launches with the fold kernels) record without changing what is
-    decoded: ids equal with spans off, mode 1 and mode 2, records present with the stated dims, and
+    attention wave, 2 = HIP events around those launches inside the replayed step graph, 4 = chain spans: five
+    launches per layer stamped into their own regions, one fold per step) record without changing what is
+    decoded: ids equal with spans off and in every mode, records present with the stated dims, and
     profile_decode (whose replays rewrite the last K/V slot) leaves a following generate unchanged."""
     tok = SyntheticTokenizer(129280)
     page = Page(synthetic_page(2), VisionSettings())
@@ -250,23 +250,29 @@ def test_full_spans_do_not_change_ids(full_engine):
     ref = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
     layers = json.load(open(FULL))["language_config"]["num_hidden_layers"]
     try:
-        for mode in (1, 2):
+        for mode in (1, 2, 4):
             full_engine.set_spans(mode)
             got = full_engine.generate(ids, mask, page, None, p, ignore_eos=True)
             assert got == ref, (mode, got, ref)
             sp = full_engine.spans()
-            assert set(sp) >= {"moe_gateup", "moe_down", "attention"}, sp.keys()
-            for kind in ("moe_gateup", "moe_down", "attention"):
+            kinds = ("moe_gateup", "moe_down", "attention") + (("o_proj", "router") if mode == 4 else ())
+            assert set(sp) == set(kinds), sp.keys()
+            steps = n + 1 if mode == 4 else n
+            for kind in kinds:
                 a = sp[kind]
-                assert a.shape == (layers, n, 5), (kind, a.shape)
-                moe = kind != "attention"
+                assert a.shape == (layers, steps, 5), (kind, a.shape)
+                moe = kind in ("moe_gateup", "moe_down", "router")
                 rows = a[1:, 1:n] if moe else a[:, 1:n]     # layer 0 is dense: no MoE launches
-                if mode == 1:
+                if mode in (1, 4):
                     assert np.all(rows[..., 1] > rows[..., 0]), kind   # exit after entry in every step
                 else:
                     assert np.all(rows[..., 4] > 0), kind              # event duration in every step
-                if moe:
+                if moe and mode == 1:
                     assert np.all((rows[..., 2] >= 6) & (rows[..., 2] <= 64)), kind  # distinct experts
+            if mode == 4:  # one chain: every launch starts after its predecessor's last wave left
+                for k, pk in (("moe_gateup", "router"), ("moe_down", "moe_gateup"), ("o_proj", "attention"),
+                              ("router", "o_proj")):
+                    assert np.all(sp[k][1:, 1:n, 0] > sp[pk][1:, 1:n, 1]), (k, pk)
     finally:
         full_engine.set_spans(0)
     full_engine.profile_decode(2)
