@@ -791,66 +791,6 @@ bool dec_router_ok(int T, int E, int K, int topk) {
     return T <= 8 && E <= 256 && K <= 64 * 3 * 8 && topk <= 8 && T * topk <= 64;
 }
 
-// Greedy top-k of one token by one wave, lane e holding expert e's logit (E <= 64): the picks of
-// topk_write (softmax / sigmoid scores, descending, ties -> lower expert id, weights summed in
-// pick order, optional renormalise + scaling), by rank: every lane counts the scores that beat its
-// own from a 64-float LDS copy (16 broadcast reads).  lds: 64 floats private to the wave.  Lane 0
-// writes ids[k], w[k].
-__device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softmax_scoring, int norm_topk, float scaling,
-                                            float* lds, int* ids, float* w) {
-    const int lane = threadIdx.x & 63;
-    float sc;
-    if (softmax_scoring) {
-        const float v = lane < E ? logit : -INFINITY;
-        const float mx = wave_max(v);
-        const float ex = lane < E ? expf(v - mx) : 0.f;
-        const float sum = wave_sum(ex);
-        sc = lane < E ? ex / sum : -INFINITY;
-    } else {
-        sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
-    }
-    lds[lane] = sc;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    int rank = 0;
-#pragma unroll
-    for (int j4 = 0; j4 < 16; ++j4) {
-        const float4 o = reinterpret_cast<const float4*>(lds)[j4];
-        const float oj[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = j4 * 4 + q;
-            rank += (oj[q] > sc || (oj[q] == sc && j < lane)) ? 1 : 0;
-        }
-    }
-    if (lane >= E) rank = 1 << 20;
-    float wsum = 0.f;
-    int pe[8];
-    float pv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        pe[k] = 0;
-        pv[k] = 0.f;
-        if (k < K) {
-            const unsigned long long bm = __ballot(rank == k);
-            pe[k] = __builtin_ctzll(bm);
-            pv[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), pe[k]));
-            wsum += pv[k];
-        }
-    }
-    if (lane < K) {
-        float v = pv[0];
-        int e = pe[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k)
-            if (lane == k) { v = pv[k]; e = pe[k]; }
-        if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
-        if (scaling != 1.0f) v = v * scaling;
-        ids[lane] = e;
-        w[lane] = v;
-    }
-}
-
 // Decode router for T <= 8 tokens, E <= 64 experts: RMSNorm + router logits + greedy top-k +
 // expert records in one launch.  Blocks of 8 waves and 8 expert rows.  Wave w normalises token row w
 // in the GEMV chunk layout (lane: chunks lane, lane+64, lane+128; its squares summed u-major then j,
@@ -2871,7 +2811,16 @@ struct MoePlan {
                           // else dec_router's last-block epilogue writes the records
     bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
     bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
+    bool route_in_gu = false;  // grouped mode: the routing runs inside the gate/up launch (no router launch)
+    MoeDec2Args mr;            // ... its arguments
 };
+
+// DSOCR_ROUTE_FUSED (A/B switch, read at every plan): 1 (default) = at 3..8 tokens the router runs inside the
+// matrix-core gate/up launch (moe_gateup_mm_route_ok); 0 = dec_route_grp launch + gate/up
+static bool route_fused_on() {
+    const char* e = getenv("DSOCR_ROUTE_FUSED");
+    return !e || atoi(e) != 0;
+}
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
     const int T = a.T, E = a.E, K = a.topk, TK = T * K;
@@ -2900,6 +2849,14 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
         p.route1 = dec_route_grp_ok(T, E, a.H, K);
         p.gu_mm = moe_gateup_mm_ok(m);
         p.dn_mm = moe_down_mm_ok(m);
+        if (p.route1 && p.gu_mm && a.norm_w && a.router_wdt == a.wdtype && route_fused_on()) {
+            MoeDec2Args r = m;
+            r.x = a.x; r.norm_w = a.norm_w; r.eps = a.eps;
+            r.router = a.router; r.router_bias = a.router_bias;
+            r.softmax_scoring = a.softmax_scoring; r.norm_topk = a.norm_topk; r.scaling = a.scaling;
+            r.ids_out = a.ids; r.w_out = a.wts;
+            if (moe_gateup_mm_route_ok(r)) { p.route_in_gu = true; p.mr = r; }
+        }
     } else if (T <= 8) {
         // every gate/up block routes itself from the router logits (rank / serial greedy top-k)
         m.grp = nullptr;
@@ -2936,7 +2893,9 @@ void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const 
 void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     const MoePlan p = moe_plan(a);
     const MoeDec2Args& m = p.m;
-    if ((parts & MOE_ROUTE) && p.route1) {
+    if ((parts & MOE_ROUTE) && p.route_in_gu) {
+        // (the gate/up launch routes)
+    } else if ((parts & MOE_ROUTE) && p.route1) {
         // norm + logits + top-k + records in one block (the grouped kernels read a.xn)
         DecGemvArgs g = p.router;
         g.x = a.x; g.norm_w = a.norm_w; g.xn_out = a.norm_w ? a.xn : nullptr;
@@ -2964,6 +2923,7 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     }
     if (parts & MOE_GATEUP) {
         if (p.mode == 0) launch_moe_gateup_mix(m, a.xn_router, s);
+        else if (p.mode == 2 && p.route_in_gu) launch_moe_gateup_mm(p.mr, s);
         else if (p.mode == 2 && p.gu_mm) launch_moe_gateup_mm(m, s);
         else if (p.mode == 2) launch_moe_gateup_grp(m, s);
         else launch_moe_gateup2(m, s);

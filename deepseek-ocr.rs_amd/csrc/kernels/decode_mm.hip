@@ -101,7 +101,7 @@ __device__ __forceinline__ void mm_row_load(MmRowU<U>& r, const float* xr, int K
     }
 }
 
-template <typename WT, bool NORM, int U = 3>
+template <typename WT, bool NORM, int U = 3, bool DIVNORM = false>
 __device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uint16_t* xp, int KP, float* scl, int m) {
     const int lane = threadIdx.x & 63;
     const int chunks = K >> 3;
@@ -114,11 +114,19 @@ __device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uin
                 for (int j = 0; j < 8; ++j) q += r.v[u][j] * r.v[u][j];
         // one division per row: x * (1 / den) is within an ulp of the reference's x / den (the planes
         // below are exact, the GEMM sums in its own order: this path is tolerance-pinned, not bitwise)
-        const float inv = 1.0f / sqrtf(wave_sum(q) / (float)K + eps);
+        if (DIVNORM) {  // x / den * w: dec_route_grp's (and the reference's) form, bit for bit
+            const float den = sqrtf(wave_sum(q) / (float)K + eps);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+            for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) r.v[u][j] = (r.v[u][j] * inv) * r.w[u][j];
+                for (int j = 0; j < 8; ++j) r.v[u][j] = (r.v[u][j] / den) * r.w[u][j];
+        } else {
+            const float inv = 1.0f / sqrtf(wave_sum(q) / (float)K + eps);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) r.v[u][j] = (r.v[u][j] * inv) * r.w[u][j];
+        }
     }
     float s_inv = 1.f;
     if (MmT<WT>::scaled) {
@@ -392,24 +400,145 @@ __device__ __forceinline__ int lds_load_relaxed(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <typename WT, int PF, bool SWZ, int KS>
+template <typename WT, int PF, bool SWZ, int KS, bool ROUTE>
 __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
     constexpr int NWV = 8, NU = NWV / KS;
     static_assert(NWV % KS == 0, "whole units per block");
+    constexpr int GR = 18;  // ROUTE: the block's expert records in LDS: [0] expert, [1] n, [2..10) h rows, [10..18) weights
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
-    __shared__ f32x4 red[KS > 1 ? NWV : 1][2][64];  // pieces 1.. of each unit: gate, up partial tiles
+    // pieces 1.. of each unit (gate, up partial tiles) at [us * (KS - 1) + piece - 1]; ROUTE: the prologue's router
+    // k-half partials [4][64] f32x4, logits [8][64] and rank scratch [8][64] share the same LDS
+    constexpr int RED = NU * (KS - 1) * 2 * 64 * 4;
+    constexpr int SCR = ROUTE ? (RED > 2048 ? RED : 2048) : (RED > 4 ? RED : 4);
+    __shared__ __attribute__((aligned(16))) float scr[SCR];
+    f32x4(*red)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(scr);
     __shared__ int hand[2 * NU];                      // [us]: pieces posted, [NU + us]: units consumed
+    __shared__ int grp_s[ROUTE ? GR * 65 : 1];
+    __shared__ int ids_s[ROUTE ? 64 : 1];
+    __shared__ float w_s[ROUTE ? 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the hand-off branches are scalar
     const int col = lane & 15, g = lane >> 4;
     const int piece = wave % KS, us = wave / KS;
     const int tiles_r = a.I >> 4, tiles_s = a.sWgu ? a.Is >> 4 : 0;
-    const int n_units = tiles_s + a.grp[0] * tiles_r;
+    const int* grp = ROUTE ? grp_s : a.grp;
+    const int grec = ROUTE ? GR : MOE_GRP_REC;
     const int steps = a.K >> 5, nch = steps / PF, nb = nch / KS, c0 = piece * nb;
     const int stride = gridDim.x * NU;
+    const int KP = mm_pitch(a.K);
+    const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
+    if constexpr (ROUTE) {
+        // ---- the router of dec_route_grp, in every block: token row w normalised on wave w (x / den * w) and
+        // staged as the B planes (the gate/up below uses the same rows); the 64 x K router matrix from L2 as MFMA
+        // A fragments (wave w: rows 16 (w & 3) .., k-steps of half w >> 2), halves met in LDS; top-k per token
+        // (topk_wave64) and the expert records (wave 0), so no router launch runs before this one
+        constexpr int RB = 10;  // router k-steps per register batch
+        const int half = steps >> 1, nrb = half / RB;
+        const int tile = wave & 3, kh = wave >> 2;
+        const WT* R = reinterpret_cast<const WT*>(a.router) + (long)min(16 * tile + col, a.E - 1) * a.K + 8 * g +
+                      32L * kh * half;
+        frag ra[RB], rb[RB];
+        auto rload = [&](frag(&f)[RB], int bi) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) {
+                const uint4 q = *reinterpret_cast<const uint4*>(R + 32L * (bi * RB + i));
+                __builtin_memcpy(&f[i], &q, 16);
+            }
+        };
+        MmRow xr;
+        if (wave < a.T) mm_row_load<true>(xr, a.x + (long)wave * a.K, a.K, a.norm_w);
+        rload(ra, 0);
+        if (wave < a.T) mm_row_store<WT, true, 3, true>(xr, a.K, a.eps, xp, KP, scl, wave);
+        if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
+        __syncthreads();
+        f32x4 racc = {0.f, 0.f, 0.f, 0.f};
+        auto rcompute = [&](const frag(&f)[RB], int bi) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) {
+                const int k = 32 * (kh * half + bi * RB + i);
+#pragma unroll
+                for (int p = 2; p >= 0; --p) {
+                    const frag b = *reinterpret_cast<const frag*>(bbase + (long)p * MM_MT * KP + k);
+                    racc = MmT<WT>::mfma(f[i], b, racc);
+                }
+            }
+        };
+        for (int bi = 0; bi < nrb; bi += 2) {
+            if (bi + 1 < nrb) rload(rb, bi + 1);
+            rcompute(ra, bi);
+            if (bi + 1 >= nrb) break;
+            if (bi + 2 < nrb) rload(ra, bi + 2);
+            rcompute(rb, bi + 1);
+        }
+        f32x4* rpart = reinterpret_cast<f32x4*>(scr);  // [4 tiles][64 lanes]
+        float* lg_s = scr + 1024;                       // [8 tokens][64 experts]
+        float* rank_s = scr + 1536;                     // [8][64]
+        if (kh == 1) rpart[tile * 64 + lane] = racc;
+        __syncthreads();
+        if (kh == 0) {
+            const f32x4 o = rpart[tile * 64 + lane];
+            const float sc = scl[col & 7];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = 16 * tile + 4 * g + i;
+                if (col < a.T && e < a.E) lg_s[col * 64 + e] = (racc[i] + o[i]) * sc + (a.router_bias ? a.router_bias[e] : 0.f);
+            }
+        }
+        __syncthreads();
+        if (wave < a.T)
+            topk_wave64(lg_s[wave * 64 + lane], a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, rank_s + wave * 64,
+                        ids_s + wave * a.topk, w_s + wave * a.topk);
+        __syncthreads();
+        const int TK = a.T * a.topk;
+        if (blockIdx.x == 0 && tid < TK) {
+            a.ids_out[tid] = ids_s[tid];
+            a.w_out[tid] = w_s[tid];
+        }
+        // wave 0, lane e: the tokens that picked expert e (a token's picks are distinct), in increasing token
+        // order -> record sidx = number of picked experts below e (dec_route_grp's records)
+        if (wave == 0) {
+            const int K = a.topk;
+            int hit[MM_MT];
+            int cnt = 0;
+#pragma unroll
+            for (int t = 0; t < MM_MT; ++t) {
+                hit[t] = -1;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k < K && t < a.T && ids_s[min(t * K + k, 63)] == lane) hit[t] = t * K + k;
+                cnt += hit[t] >= 0 ? 1 : 0;
+            }
+            const bool act = cnt > 0 && lane < a.E;
+            const unsigned long long bm = __ballot(act);
+            const int sidx = __popcll(bm & ((1ull << lane) - 1ull));
+            if (act) {
+                int* rl = grp_s + GR * (1 + sidx);
+                int* rgl = const_cast<int*>(a.grp) + MOE_GRP_REC * (1 + sidx);
+                rl[0] = lane;
+                rl[1] = cnt;
+                if (blockIdx.x == 0) { rgl[0] = lane; rgl[1] = cnt; }
+                int q = 0;
+#pragma unroll
+                for (int t = 0; t < MM_MT; ++t)
+                    if (hit[t] >= 0) {
+                        const int wb = __float_as_int(w_s[hit[t]]);
+                        rl[2 + q] = hit[t];
+                        rl[10 + q] = wb;
+                        if (blockIdx.x == 0) { rgl[2 + q] = hit[t]; rgl[10 + q] = wb; }
+                        ++q;
+                    }
+            }
+            if (lane == 0) {
+                grp_s[0] = __popcll(bm);
+                if (blockIdx.x == 0) const_cast<int*>(a.grp)[0] = __popcll(bm);
+            }
+        }
+        __syncthreads();
+    }
+    const int n_units = tiles_s + grp[0] * tiles_r;
     int unit = blockIdx.x * NU + us;
     // unit -> (shared?, expert, first row) and the lane's two fragment streams
     struct Src {
@@ -429,7 +558,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
         r.i0 = t * 16;
         const int rows_I = r.shared ? a.Is : a.I;
-        const int e = r.shared ? 0 : a.grp[MOE_GRP_REC * (1 + r.s)];
+        const int e = r.shared ? 0 : grp[grec * (1 + r.s)];
         if (SWZ) {
             const WT* base = r.shared ? reinterpret_cast<const WT*>(a.sWgu_swz) : reinterpret_cast<const WT*>(a.Wgu_swz);
             const long tg = (r.shared ? 0L : (long)e * (2 * a.I / 16)) + t;
@@ -454,20 +583,23 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             __builtin_memcpy(&fu[i], &q1, 16);
         }
     };
-    MmRow xr;  // wave w stages token row w: its loads go out before the weight batch
-    if (wave < a.T) mm_row_load<false>(xr, a.x + (long)wave * a.K, a.K, nullptr);
     Src cur = src(min(unit, max(n_units - 1, 0)));
-    // both weight batches of the first unit go out before the staging barrier (the stream would
-    // otherwise idle behind it)
-    if (unit < n_units) {
+    if constexpr (!ROUTE) {
+        MmRow xr;  // wave w stages token row w: its loads go out before the weight batch
+        if (wave < a.T) mm_row_load<false>(xr, a.x + (long)wave * a.K, a.K, nullptr);
+        // both weight batches of the first unit go out before the staging barrier (the stream would
+        // otherwise idle behind it)
+        if (unit < n_units) {
+            load(ga, ua, cur, c0);
+            if (nb > 1) load(gb, ub, cur, c0 + 1);
+        }
+        if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
+        if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
+        __syncthreads();
+    } else if (unit < n_units) {
         load(ga, ua, cur, c0);
         if (nb > 1) load(gb, ub, cur, c0 + 1);
     }
-    const int KP = mm_pitch(a.K);
-    if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
-    if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
-    __syncthreads();
-    const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
     f32x4 accg = {0.f, 0.f, 0.f, 0.f}, accu = {0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const frag(&fg)[PF], const frag(&fu)[PF], int c) {
 #pragma unroll
@@ -497,10 +629,11 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
         if (KS > 1) {
             if (piece > 0) {
+                const int ri = us * (KS - 1) + piece - 1;
                 // the unit's first wave has read this slot's previous partials (almost never waits)
                 while (lds_load_relaxed(&hand[NU + us]) < n) __builtin_amdgcn_s_sleep(1);
-                red[wave][0][lane] = accg;
-                red[wave][1][lane] = accu;
+                red[ri][0][lane] = accg;
+                red[ri][1][lane] = accu;
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partials are in LDS before the count
                 if (lane == 0) __hip_atomic_fetch_add(&hand[us], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
@@ -508,7 +641,8 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
                 asm volatile("" ::: "memory");
 #pragma unroll
                 for (int q = 1; q < KS; ++q) {
-                    const f32x4 pg = red[wave + q][0][lane], pu = red[wave + q][1][lane];
+                    const int ri = us * (KS - 1) + q - 1;
+                    const f32x4 pg = red[ri][0][lane], pu = red[ri][1][lane];
                     accg[0] += pg[0]; accg[1] += pg[1]; accg[2] += pg[2]; accg[3] += pg[3];
                     accu[0] += pu[0]; accu[1] += pu[1]; accu[2] += pu[2]; accu[3] += pu[3];
                 }
@@ -523,7 +657,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             if (cur.shared) {
                 slot = col < a.T ? col : -1;
             } else {
-                const int* rec = a.grp + MOE_GRP_REC * (1 + cur.s);
+                const int* rec = grp + grec * (1 + cur.s);
                 const int cnt = rec[1];
                 for (int q = 0; q < cnt; ++q) {
                     const int r = rec[2 + q];
@@ -575,24 +709,35 @@ bool moe_gateup_mm_ok(const MoeDec2Args& a) {
            a.I % 16 == 0 && (!a.sWgu || a.Is % 16 == 0) && !a.norm_w && a.x && swz_ok;
 }
 
+// the routing inside (see the kernel): E <= 64 experts, T * topk <= 64, topk <= 8, K / 32 k-steps split in two halves
+// of whole 10-step register batches; the picks and records also go to ids_out / w_out / grp for the down launch
+bool moe_gateup_mm_route_ok(const MoeDec2Args& a) {
+    MoeDec2Args b = a;
+    b.norm_w = nullptr;
+    return moe_gateup_mm_ok(b) && a.norm_w && a.router && a.E >= a.topk && a.E <= 64 && a.topk <= 8 &&
+           a.T * a.topk <= 64 && ((a.K >> 5) % 20) == 0 && a.ids_out && a.w_out;
+}
+
 void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
-    if (!moe_gateup_mm_ok(a)) throw std::runtime_error("EINVAL: grouped decode gate/up (matrix cores) outside its range");
+    const bool route = a.router != nullptr;
+    if (route ? !moe_gateup_mm_route_ok(a) : !moe_gateup_mm_ok(a))
+        throw std::runtime_error("EINVAL: grouped decode gate/up (matrix cores) outside its range");
     const size_t lds = sizeof(uint16_t) * 3 * MM_MT * (size_t)mm_pitch(a.K);
     const int slots = std::min(a.E, a.T * a.topk);
     const int max_units = (a.sWgu ? a.Is / 16 : 0) + slots * (a.I / 16);
     int ks = gu_ks();
     while (ks > 1 && ((a.K >> 5) / 5) % ks) ks >>= 1;
-#define DSOCR_GM(WTY, SW, KS)                                                                                          \
+#define DSOCR_GM(WTY, SW, KS, RT)                                                                                      \
     do {                                                                                                            \
         static int resident = 0;                                                                                    \
         if (!resident) {                                                                                            \
-            /* the pieces' LDS (16 KB) takes the block past 64 KB: allowed per kernel */                            \
-            (void)hipFuncSetAttribute((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS>,                            \
+            /* the pieces' LDS takes the block past 64 KB: allowed per kernel */                                    \
+            (void)hipFuncSetAttribute((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS, RT>,                        \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                       \
-            resident = mm_resident_blocks((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS>, 512, lds);             \
+            resident = mm_resident_blocks((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS, RT>, 512, lds);         \
         }                                                                                                           \
         const int blocks = std::max(1, std::min(resident, (max_units + 8 / KS - 1) / (8 / KS)));                  \
-        DSOCR_LAUNCH((moe_gateup_mm_kernel<WTY, 5, SW, KS>), dim3(blocks), dim3(512), lds, s, a);                    \
+        DSOCR_LAUNCH((moe_gateup_mm_kernel<WTY, 5, SW, KS, RT>), dim3(blocks), dim3(512), lds, s, a);                \
         static bool checked = false;                                                                                \
         if (!checked) {                                                                                             \
             const hipError_t e = hipPeekAtLastError();                                                              \
@@ -601,11 +746,17 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
             checked = true;                                                                                         \
         }                                                                                                           \
     } while (0)
-#define DSOCR_GMK(WTY, SW)                  \
-    do {                                    \
-        if (ks == 4) DSOCR_GM(WTY, SW, 4);  \
-        else if (ks == 2) DSOCR_GM(WTY, SW, 2); \
-        else DSOCR_GM(WTY, SW, 1);          \
+#define DSOCR_GMK(WTY, SW)                                                  \
+    do {                                                                    \
+        if (route) {                                                        \
+            if (ks == 4) DSOCR_GM(WTY, SW, 4, true);                        \
+            else if (ks == 2) DSOCR_GM(WTY, SW, 2, true);                   \
+            else DSOCR_GM(WTY, SW, 1, true);                                \
+        } else {                                                            \
+            if (ks == 4) DSOCR_GM(WTY, SW, 4, false);                       \
+            else if (ks == 2) DSOCR_GM(WTY, SW, 2, false);                  \
+            else DSOCR_GM(WTY, SW, 1, false);                               \
+        }                                                                   \
     } while (0)
     if (a.wdtype == WDT_BF16) { if (a.Wgu_swz) DSOCR_GMK(bf16_t, true); else DSOCR_GMK(bf16_t, false); }
     else { if (a.Wgu_swz) DSOCR_GMK(f16_t, true); else DSOCR_GMK(f16_t, false); }

@@ -167,6 +167,66 @@ struct WaveSpan {
     }
 };
 
+// Greedy top-k of one token by one wave, lane e holding expert e's logit (E <= 64): the picks of
+// topk_write (softmax / sigmoid scores, descending, ties -> lower expert id, weights summed in
+// pick order, optional renormalise + scaling), by rank: every lane counts the scores that beat its
+// own from a 64-float LDS copy (16 broadcast reads).  lds: 64 floats private to the wave.  Lane 0
+// writes ids[k], w[k].
+__device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softmax_scoring, int norm_topk, float scaling,
+                                            float* lds, int* ids, float* w) {
+    const int lane = threadIdx.x & 63;
+    float sc;
+    if (softmax_scoring) {
+        const float v = lane < E ? logit : -INFINITY;
+        const float mx = wave_max(v);
+        const float ex = lane < E ? expf(v - mx) : 0.f;
+        const float sum = wave_sum(ex);
+        sc = lane < E ? ex / sum : -INFINITY;
+    } else {
+        sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
+    }
+    lds[lane] = sc;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    int rank = 0;
+#pragma unroll
+    for (int j4 = 0; j4 < 16; ++j4) {
+        const float4 o = reinterpret_cast<const float4*>(lds)[j4];
+        const float oj[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = j4 * 4 + q;
+            rank += (oj[q] > sc || (oj[q] == sc && j < lane)) ? 1 : 0;
+        }
+    }
+    if (lane >= E) rank = 1 << 20;
+    float wsum = 0.f;
+    int pe[8];
+    float pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        pe[k] = 0;
+        pv[k] = 0.f;
+        if (k < K) {
+            const unsigned long long bm = __ballot(rank == k);
+            pe[k] = __builtin_ctzll(bm);
+            pv[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), pe[k]));
+            wsum += pv[k];
+        }
+    }
+    if (lane < K) {
+        float v = pv[0];
+        int e = pe[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k)
+            if (lane == k) { v = pv[k]; e = pe[k]; }
+        if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
+        if (scaling != 1.0f) v = v * scaling;
+        ids[lane] = e;
+        w[lane] = v;
+    }
+}
+
 // order-preserving float <-> unsigned key (atomicMax over floats); key 0 sorts below every
 // float and decodes to -inf
 __device__ __forceinline__ unsigned fkey(float f) {

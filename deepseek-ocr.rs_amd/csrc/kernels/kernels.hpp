@@ -331,6 +331,9 @@ struct MoeDec2Args {
     // matrix-core grouped down: per-segment partial tiles [segments][8][Hout] and per-128-row
     // arrival tickets [Hout / 128] (zero between launches; the last arriver resets them)
     float* dn_part = nullptr; int* dn_tick = nullptr;
+    // grouped gate/up with the routing inside (moe_gateup_mm_route_ok): the router rows [E][K] (wdtype), an
+    // optional logit bias; x is then the raw residual stream, normalised with norm_w in every block
+    const void* router = nullptr; const float* router_bias = nullptr;
 };
 // Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams
 // shared-expert rows from its first instruction, 3 of 4 route themselves (rank-based top-k of
@@ -352,6 +355,10 @@ void launch_moe_down_grp(const MoeDec2Args& a, hipStream_t s);
 // the grouped gate/up on the matrix cores (decode_mm.hip): expert rows as MFMA A fragments, the
 // token rows as three exact f16 planes
 bool moe_gateup_mm_ok(const MoeDec2Args& a);
+// the same with the router in every block (no dec_route_grp launch before it): RMSNorm of x with norm_w
+// (x / den * w, as dec_route_grp), the E <= 64 router logits on the matrix cores, greedy top-k per token,
+// the expert records (block 0 also writes them to grp, with the picks to ids_out / w_out, for the down launch)
+bool moe_gateup_mm_route_ok(const MoeDec2Args& a);
 void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s);
 bool moe_down_mm_ok(const MoeDec2Args& a);
 size_t moe_down_mm_part_floats(int E, int T, int topk, int I, int Is, int H);
