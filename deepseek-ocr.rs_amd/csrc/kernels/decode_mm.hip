@@ -424,7 +424,12 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     const int col = lane & 15, g = lane >> 4;
     const int piece = wave % KS, us = wave / KS;
     const int tiles_r = a.I >> 4, tiles_s = a.sWgu ? a.Is >> 4 : 0;
-    const int* grp = ROUTE ? grp_s : a.grp;
+    // record words: LDS (ds_read) with the routing inside, global otherwise — never through one generic pointer (a
+    // flat load also counts in vmcnt, so waiting for it would wait for every weight load in flight)
+    auto grp = [&](int i) -> int {
+        if constexpr (ROUTE) return grp_s[i];
+        else return a.grp[i];
+    };
     const int grec = ROUTE ? GR : MOE_GRP_REC;
     const int steps = a.K >> 5, nch = steps / PF, nb = nch / KS, c0 = piece * nb;
     const int stride = gridDim.x * NU;
@@ -538,7 +543,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
         __syncthreads();
     }
-    const int n_units = tiles_s + grp[0] * tiles_r;
+    const int n_units = tiles_s + grp(0) * tiles_r;
     int unit = blockIdx.x * NU + us;
     // unit -> (shared?, expert, first row) and the lane's two fragment streams
     struct Src {
@@ -558,7 +563,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
         r.i0 = t * 16;
         const int rows_I = r.shared ? a.Is : a.I;
-        const int e = r.shared ? 0 : grp[grec * (1 + r.s)];
+        const int e = r.shared ? 0 : grp(grec * (1 + r.s));
         if (SWZ) {
             const WT* base = r.shared ? reinterpret_cast<const WT*>(a.sWgu_swz) : reinterpret_cast<const WT*>(a.Wgu_swz);
             const long tg = (r.shared ? 0L : (long)e * (2 * a.I / 16)) + t;
@@ -657,11 +662,11 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             if (cur.shared) {
                 slot = col < a.T ? col : -1;
             } else {
-                const int* rec = grp + grec * (1 + cur.s);
-                const int cnt = rec[1];
+                const int rb = grec * (1 + cur.s);
+                const int cnt = grp(rb + 1);
                 for (int q = 0; q < cnt; ++q) {
-                    const int r = rec[2 + q];
-                    if (r / a.topk == col) { slot = r; wk = __int_as_float(rec[10 + q]); }
+                    const int r = grp(rb + 2 + q);
+                    if (r / a.topk == col) { slot = r; wk = __int_as_float(grp(rb + 10 + q)); }
                 }
             }
             if (slot >= 0) {

@@ -88,6 +88,7 @@ for step in "$@"; do
           for C in FETCH_SIZE WRITE_SIZE; do DSOCR_NO_GRAPH=1 run 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${PMC_RUN:-b1}_$C -o pmc --output-format csv -- python tools/pmc_decode.py $A --tokens 16 --out gpurun_out/routing_${PMC_RUN:-b1}.json > gpurun_out/pmc_${PMC_RUN:-b1}_$C.log 2>&1 || exit 1; done ;;
     envab) run 900 tools/env_ab.sh ${ENV_AB} > gpurun_out/envab${TAG:+_$TAG}.log 2>&1 ;;
     kb_router8) run 180 ./tools/kbench router8 > gpurun_out/kb_router8${TAG:+_$TAG}.log 2>&1 ;;
+    parity8) DSOCR_PARITY_OUT=gpurun_out/parity8${TAG:+_$TAG}.jsonl run 900 python -u -m pytest tests/test_full_parity.py -q -m gpu -rf -p no:cacheprovider --timeout 400 --timeout-method thread -k "batch8" > gpurun_out/parity8${TAG:+_$TAG}.log 2>&1 ;;
     *) echo "unknown step $step" >> gpurun_out/rc.log ;;
   esac
 done
