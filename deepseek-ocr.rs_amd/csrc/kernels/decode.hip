@@ -2836,7 +2836,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
     m.topk = K; m.E = E; m.I = a.I; m.Wgu = a.Wgu; m.Wd = a.Wd; m.wdtype = a.wdtype; m.h = a.h; m.ids = a.ids;
     if (a.sWgu && a.sWd && a.Is > 0) { m.Is = a.Is; m.sWgu = a.sWgu; m.sWd = a.sWd; m.hs = a.hs; }
     m.Wgu_swz = a.Wgu_swz; m.sWgu_swz = a.sWgu_swz; m.Wd_swz = a.Wd_swz; m.sWd_swz = a.sWd_swz;
-    m.dn_part = a.dn_part; m.dn_tick = a.dn_tick; m.span = a.span;
+    m.dn_part = a.dn_part; m.dn_tick = a.dn_tick; m.span = a.span; m.stamps = a.stamps;
     DecGemvArgs& gr = p.router;
     gr.M = T; gr.N = E; gr.K = a.H; gr.x = mx; gr.ldx = a.H; gr.W = a.router; gr.ldw = a.H; gr.wdtype = a.router_wdt;
     gr.bias = a.router_bias; gr.y = a.logits; gr.ldy = E; gr.norm_w = mnorm; gr.eps = a.eps; gr.span = a.route_span;
@@ -2854,7 +2854,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
             r.x = a.x; r.norm_w = a.norm_w; r.eps = a.eps;
             r.router = a.router; r.router_bias = a.router_bias;
             r.softmax_scoring = a.softmax_scoring; r.norm_topk = a.norm_topk; r.scaling = a.scaling;
-            r.ids_out = a.ids; r.w_out = a.wts;
+            r.ids_out = a.ids; r.w_out = a.wts; r.logits = a.logits;  // (block 0 also writes the logits)
             if (moe_gateup_mm_route_ok(r)) { p.route_in_gu = true; p.mr = r; }
         }
     } else if (T <= 8) {

@@ -406,7 +406,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     typedef typename MmT<WT>::frag frag;
     constexpr int NWV = 8, NU = NWV / KS;
     static_assert(NWV % KS == 0, "whole units per block");
-    constexpr int GR = 18;  // ROUTE: the block's expert records in LDS: [0] expert, [1] n, [2..10) h rows, [10..18) weights
+    constexpr int GREC = 65 * MOE_GRP_REC;  // the layer's expert records (count + <= 64 records) kept in LDS
     extern __shared__ __attribute__((aligned(16))) uint16_t xp[];  // [3][MT][KP]
     __shared__ float scl[MM_MT];
     // pieces 1.. of each unit (gate, up partial tiles) at [us * (KS - 1) + piece - 1]; ROUTE: the prologue's router
@@ -415,8 +415,11 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     constexpr int SCR = ROUTE ? (RED > 2048 ? RED : 2048) : (RED > 4 ? RED : 4);
     __shared__ __attribute__((aligned(16))) float scr[SCR];
     f32x4(*red)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(scr);
-    __shared__ int hand[2 * NU];                      // [us]: pieces posted, [NU + us]: units consumed
-    __shared__ int grp_s[ROUTE ? GR * 65 : 1];
+    __shared__ int hand[2 * NU];  // [us]: pieces posted, [NU + us]: units consumed
+    // Every record word the unit loop reads comes from LDS (ds_read: lgkmcnt).  A global load there would be
+    // waited on with vmcnt, i.e. behind every weight load in flight (the double-buffered stream drained at each
+    // unit: measured in the round-4 kernel's ISA, `s_waitcnt vmcnt(0)` after each record load).
+    __shared__ __attribute__((aligned(16))) int grp_s[GREC];
     __shared__ int ids_s[ROUTE ? 64 : 1];
     __shared__ float w_s[ROUTE ? 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -424,17 +427,13 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     const int col = lane & 15, g = lane >> 4;
     const int piece = wave % KS, us = wave / KS;
     const int tiles_r = a.I >> 4, tiles_s = a.sWgu ? a.Is >> 4 : 0;
-    // record words: LDS (ds_read) with the routing inside, global otherwise — never through one generic pointer (a
-    // flat load also counts in vmcnt, so waiting for it would wait for every weight load in flight)
-    auto grp = [&](int i) -> int {
-        if constexpr (ROUTE) return grp_s[i];
-        else return a.grp[i];
-    };
-    const int grec = ROUTE ? GR : MOE_GRP_REC;
     const int steps = a.K >> 5, nch = steps / PF, nb = nch / KS, c0 = piece * nb;
     const int stride = gridDim.x * NU;
     const int KP = mm_pitch(a.K);
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
+#define GU_STAMP(i) \
+    if (a.stamps && tid == 0) a.stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();
+    GU_STAMP(0);
     if constexpr (ROUTE) {
         // ---- the router of dec_route_grp, in every block: token row w normalised on wave w (x / den * w) and
         // staged as the B planes (the gate/up below uses the same rows); the 64 x K router matrix from L2 as MFMA
@@ -459,6 +458,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         if (wave < a.T) mm_row_store<WT, true, 3, true>(xr, a.K, a.eps, xp, KP, scl, wave);
         if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
         __syncthreads();
+        GU_STAMP(1);
         f32x4 racc = {0.f, 0.f, 0.f, 0.f};
         auto rcompute = [&](const frag(&f)[RB], int bi) {
 #pragma unroll
@@ -478,6 +478,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             if (bi + 2 < nrb) rload(ra, bi + 2);
             rcompute(rb, bi + 1);
         }
+        GU_STAMP(2);
         f32x4* rpart = reinterpret_cast<f32x4*>(scr);  // [4 tiles][64 lanes]
         float* lg_s = scr + 1024;                       // [8 tokens][64 experts]
         float* rank_s = scr + 1536;                     // [8][64]
@@ -497,13 +498,11 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             topk_wave64(lg_s[wave * 64 + lane], a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, rank_s + wave * 64,
                         ids_s + wave * a.topk, w_s + wave * a.topk);
         __syncthreads();
-        const int TK = a.T * a.topk;
-        if (blockIdx.x == 0 && tid < TK) {
-            a.ids_out[tid] = ids_s[tid];
-            a.w_out[tid] = w_s[tid];
-        }
+        GU_STAMP(3);
         // wave 0, lane e: the tokens that picked expert e (a token's picks are distinct), in increasing token
-        // order -> record sidx = number of picked experts below e (dec_route_grp's records)
+        // order -> record sidx = number of picked experts below e (dec_route_grp's records); block 0 also writes
+        // them, the picks and the logits to global memory (for the down launch and the tools), after its last
+        // barrier
         if (wave == 0) {
             const int K = a.topk;
             int hit[MM_MT];
@@ -520,90 +519,97 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             const unsigned long long bm = __ballot(act);
             const int sidx = __popcll(bm & ((1ull << lane) - 1ull));
             if (act) {
-                int* rl = grp_s + GR * (1 + sidx);
-                int* rgl = const_cast<int*>(a.grp) + MOE_GRP_REC * (1 + sidx);
+                int* rl = grp_s + MOE_GRP_REC * (1 + sidx);
                 rl[0] = lane;
                 rl[1] = cnt;
-                if (blockIdx.x == 0) { rgl[0] = lane; rgl[1] = cnt; }
                 int q = 0;
 #pragma unroll
                 for (int t = 0; t < MM_MT; ++t)
                     if (hit[t] >= 0) {
-                        const int wb = __float_as_int(w_s[hit[t]]);
                         rl[2 + q] = hit[t];
-                        rl[10 + q] = wb;
-                        if (blockIdx.x == 0) { rgl[2 + q] = hit[t]; rgl[10 + q] = wb; }
+                        rl[10 + q] = __float_as_int(w_s[hit[t]]);
                         ++q;
                     }
             }
-            if (lane == 0) {
-                grp_s[0] = __popcll(bm);
-                if (blockIdx.x == 0) const_cast<int*>(a.grp)[0] = __popcll(bm);
-            }
+            if (lane == 0) grp_s[0] = __popcll(bm);
         }
         __syncthreads();
+        GU_STAMP(4);
+        if (blockIdx.x == 0) {
+            const int TK = a.T * a.topk;
+            if (tid < TK) {
+                a.ids_out[tid] = ids_s[tid];
+                a.w_out[tid] = w_s[tid];
+            }
+            if (a.logits && (tid >> 6) < a.T && (tid & 63) < a.E)
+                const_cast<float*>(a.logits)[(tid >> 6) * a.E + (tid & 63)] = lg_s[(tid >> 6) * 64 + (tid & 63)];
+            int* gg = const_cast<int*>(a.grp);
+            const int nw = MOE_GRP_REC * (1 + grp_s[0]);
+            for (int i = tid; i < nw; i += 512) gg[i] = grp_s[i];
+        }
     }
-    const int n_units = tiles_s + grp(0) * tiles_r;
+    // ---- the records (ROUTE: in LDS already; else copied from the router's global records once, behind the
+    // x loads and ahead of the weight stream) and the first unit's stream
+    MmRow xr;  // non-ROUTE: wave w stages token row w: its loads go out before the weight batch
+    if constexpr (!ROUTE) {
+        if (wave < a.T) mm_row_load<false>(xr, a.x + (long)wave * a.K, a.K, nullptr);
+        static_assert(GREC / 4 <= 2 * 512, "two int4 per thread cover the records");
+        const int4* gsrc = reinterpret_cast<const int4*>(a.grp);
+        const int n4 = min(GREC / 4, MOE_GRP_REC / 4 * (1 + min(a.slots, 64)));
+        const int i0 = tid, i1 = tid + 512;
+        int4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+        if (i0 < n4) r0 = gsrc[i0];
+        if (i1 < n4) r1 = gsrc[i1];
+        if (i0 < n4) reinterpret_cast<int4*>(grp_s)[i0] = r0;
+        if (i1 < n4) reinterpret_cast<int4*>(grp_s)[i1] = r1;
+        if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
+        if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
+        __syncthreads();
+    }
+    const int n_units = tiles_s + grp_s[0] * tiles_r;
     int unit = blockIdx.x * NU + us;
-    // unit -> (shared?, expert, first row) and the lane's two fragment streams
-    struct Src {
-        const WT* pg;
-        const WT* pu;
-        int i0, s;
-        bool shared;
-    };
-    auto src = [&](int uu) {
-        Src r;
-        r.shared = uu < tiles_s;
+    // unit -> the lane's two fragment streams (gate, up), first row, record, shared?  Kept as plain variables
+    // (a struct select between the current and the next unit went through scratch, i.e. through vmcnt)
+    constexpr long FS = SWZ ? 512 : 32;  // elements between a lane's consecutive k-step fragments
+    auto src = [&](int uu, const WT*& pg, const WT*& pu, int& i0, int& rs, int& sh) {
+        sh = uu < tiles_s ? 1 : 0;
         int t = uu;
-        r.s = 0;
-        if (!r.shared) {
-            r.s = (uu - tiles_s) / tiles_r;
+        rs = 0;
+        if (!sh) {
+            rs = (uu - tiles_s) / tiles_r;
             t = (uu - tiles_s) % tiles_r;
         }
-        r.i0 = t * 16;
-        const int rows_I = r.shared ? a.Is : a.I;
-        const int e = r.shared ? 0 : grp(grec * (1 + r.s));
+        i0 = t * 16;
+        const int rows_I = sh ? a.Is : a.I;
+        const int e = sh ? 0 : grp_s[MOE_GRP_REC * (1 + rs)];
         if (SWZ) {
-            const WT* base = r.shared ? reinterpret_cast<const WT*>(a.sWgu_swz) : reinterpret_cast<const WT*>(a.Wgu_swz);
-            const long tg = (r.shared ? 0L : (long)e * (2 * a.I / 16)) + t;
-            r.pg = base + (tg * steps) * 512 + lane * 8;
-            r.pu = base + ((tg + rows_I / 16) * steps) * 512 + lane * 8;
+            const WT* base = sh ? reinterpret_cast<const WT*>(a.sWgu_swz) : reinterpret_cast<const WT*>(a.Wgu_swz);
+            const long tg = (sh ? 0L : (long)e * (2 * a.I / 16)) + t;
+            pg = base + (tg * steps) * 512 + lane * 8;
+            pu = base + ((tg + rows_I / 16) * steps) * 512 + lane * 8;
         } else {
-            const WT* Wg = r.shared ? reinterpret_cast<const WT*>(a.sWgu)
-                                    : reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
-            r.pg = Wg + (long)(r.i0 + col) * a.K + 8 * g;
-            r.pu = r.pg + (long)rows_I * a.K;
+            const WT* Wg = sh ? reinterpret_cast<const WT*>(a.sWgu)
+                              : reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
+            pg = Wg + (long)(i0 + col) * a.K + 8 * g;
+            pu = pg + (long)rows_I * a.K;
         }
-        return r;
     };
-    constexpr long FS = SWZ ? 512 : 32;  // elements between a lane's consecutive k-step fragments
     frag ga[PF], ua[PF], gb[PF], ub[PF];
-    auto load = [&](frag(&fg)[PF], frag(&fu)[PF], const Src& r, int c) {
+    auto load = [&](frag(&fg)[PF], frag(&fu)[PF], const WT* pg, const WT* pu, int c) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
-            const uint4 q0 = ldg_nt16(r.pg + FS * (c * PF + i));
-            const uint4 q1 = ldg_nt16(r.pu + FS * (c * PF + i));
+            const uint4 q0 = ldg_nt16(pg + FS * (c * PF + i));
+            const uint4 q1 = ldg_nt16(pu + FS * (c * PF + i));
             __builtin_memcpy(&fg[i], &q0, 16);
             __builtin_memcpy(&fu[i], &q1, 16);
         }
     };
-    Src cur = src(min(unit, max(n_units - 1, 0)));
-    if constexpr (!ROUTE) {
-        MmRow xr;  // wave w stages token row w: its loads go out before the weight batch
-        if (wave < a.T) mm_row_load<false>(xr, a.x + (long)wave * a.K, a.K, nullptr);
-        // both weight batches of the first unit go out before the staging barrier (the stream would
-        // otherwise idle behind it)
-        if (unit < n_units) {
-            load(ga, ua, cur, c0);
-            if (nb > 1) load(gb, ub, cur, c0 + 1);
-        }
-        if (wave < a.T) mm_row_store<WT, false>(xr, a.K, 0.f, xp, KP, scl, wave);
-        if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
-        __syncthreads();
-    } else if (unit < n_units) {
-        load(ga, ua, cur, c0);
-        if (nb > 1) load(gb, ub, cur, c0 + 1);
+    const WT *cpg, *cpu;
+    int ci0, crs, csh;
+    src(min(unit, max(n_units - 1, 0)), cpg, cpu, ci0, crs, csh);
+    if (unit < n_units) {
+        load(ga, ua, cpg, cpu, c0);
+        if (nb > 1) load(gb, ub, cpg, cpu, c0 + 1);
     }
     f32x4 accg = {0.f, 0.f, 0.f, 0.f}, accu = {0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const frag(&fg)[PF], const frag(&fu)[PF], int c) {
@@ -619,17 +625,21 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
     };
     bool first = true;
+    GU_STAMP(5);
     for (int n = 0; unit < n_units; unit += stride, ++n) {
         const int nu = unit + stride;
         const bool more = nu < n_units;
-        const Src nxt = more ? src(nu) : cur;
+        const WT *npg = cpg, *npu = cpu;
+        int ni0 = ci0, nrs = crs, nsh = csh;
+        if (more) src(nu, npg, npu, ni0, nrs, nsh);
         for (int c = 0; c < nb; c += 2) {
-            if (c + 1 < nb) { if (!(first && c == 0)) load(gb, ub, cur, c0 + c + 1); }
-            else if (more) load(gb, ub, nxt, c0);
+            if (c + 1 < nb) { if (!(first && c == 0)) load(gb, ub, cpg, cpu, c0 + c + 1); }
+            else if (more) load(gb, ub, npg, npu, c0);
             compute(ga, ua, c0 + c);
+            if (first && c == 0) GU_STAMP(6);
             if (c + 1 >= nb) break;
-            if (c + 2 < nb) load(ga, ua, cur, c0 + c + 2);
-            else if (more) load(ga, ua, nxt, c0);
+            if (c + 2 < nb) load(ga, ua, cpg, cpu, c0 + c + 2);
+            else if (more) load(ga, ua, npg, npu, c0);
             compute(gb, ub, c0 + c + 1);
         }
         if (KS > 1) {
@@ -659,14 +669,14 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             // token col's slot row (routed: -1 when the token did not pick this expert) and weight
             int slot = -1;
             float wk = 1.f;
-            if (cur.shared) {
+            if (csh) {
                 slot = col < a.T ? col : -1;
             } else {
-                const int rb = grec * (1 + cur.s);
-                const int cnt = grp(rb + 1);
+                const int rb = MOE_GRP_REC * (1 + crs);
+                const int cnt = grp_s[rb + 1];
                 for (int q = 0; q < cnt; ++q) {
-                    const int r = grp(rb + 2 + q);
-                    if (r / a.topk == col) { slot = r; wk = __int_as_float(grp(rb + 10 + q)); }
+                    const int r = grp_s[rb + 2 + q];
+                    if (r / a.topk == col) { slot = r; wk = __int_as_float(grp_s[rb + 10 + q]); }
                 }
             }
             if (slot >= 0) {
@@ -676,21 +686,23 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
                 for (int i = 0; i < 4; ++i) {
                     const float gs = accg[i] * sc, us_ = accu[i] * sc;
                     const float h = (gs / (1.0f + expf(-gs))) * us_;
-                    hv[i] = cur.shared ? h : h * wk;
+                    hv[i] = csh ? h : h * wk;
                 }
-                float* dst = cur.shared ? a.hs + (long)slot * a.Is : a.h + (long)slot * a.I;
-                *reinterpret_cast<float4*>(dst + cur.i0 + 4 * g) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+                float* dst = csh ? a.hs + (long)slot * a.Is : a.h + (long)slot * a.I;
+                *reinterpret_cast<float4*>(dst + ci0 + 4 * g) = make_float4(hv[0], hv[1], hv[2], hv[3]);
             }
         }
         accg = f32x4{0.f, 0.f, 0.f, 0.f};
         accu = f32x4{0.f, 0.f, 0.f, 0.f};
-        cur = nxt;
+        cpg = npg; cpu = npu; ci0 = ni0; crs = nrs; csh = nsh;
         if (nb & 1) {  // odd batch count: the next unit's first batch landed in the b buffers
 #pragma unroll
             for (int i = 0; i < PF; ++i) { ga[i] = gb[i]; ua[i] = ub[i]; }
         }
         first = false;
     }
+    GU_STAMP(7);
+#undef GU_STAMP
 }
 
 // waves per unit: DSOCR_GU_KS = 1 / 2 / 4 (default 2; K / 32 / PF batches must divide by it).  Measured at

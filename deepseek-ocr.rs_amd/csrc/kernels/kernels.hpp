@@ -334,6 +334,7 @@ struct MoeDec2Args {
     // grouped gate/up with the routing inside (moe_gateup_mm_route_ok): the router rows [E][K] (wdtype), an
     // optional logit bias; x is then the raw residual stream, normalised with norm_w in every block
     const void* router = nullptr; const float* router_bias = nullptr;
+    unsigned long long* stamps = nullptr;  // dev (tools/kbench moe8): per block 8 words of s_memrealtime at phase points
 };
 // Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams
 // shared-expert rows from its first instruction, 3 of 4 route themselves (rank-based top-k of
@@ -394,6 +395,7 @@ struct MoeDecodeArgs {
     int* n_active = nullptr; float* aw = nullptr;                                          // [E+1],[TK],[TK],[E],[1],[TK]
     unsigned long long* span = nullptr;  // launch-span slots for the gate/up and down launches (or null)
     unsigned long long* route_span = nullptr;  // launch-span slots for the router launch (or null)
+    unsigned long long* stamps = nullptr;      // dev: the grouped gate/up's phase clocks (MoeDec2Args::stamps)
 };
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments

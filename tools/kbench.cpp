@@ -181,9 +181,17 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
         a.Wgu_swz = w.gu_s; a.sWgu_swz = w.sgu_s; a.Wd_swz = w.d_s; a.sWd_swz = w.sd_s;
     };
     const int n = 4 * NL;
+    CK(hipDeviceSynchronize());  // the fills ran on the null stream; s does not wait for it
     set(0);
     launch_moe_decode(a, s, MOE_ALL);
     CK(hipStreamSynchronize(s));
+    {
+        std::vector<float> lg((size_t)T * E);
+        CK(hipMemcpy(lg.data(), a.logits, lg.size() * 4, hipMemcpyDeviceToHost));
+        printf("logits[0][0..7]:");
+        for (int e = 0; e < 8; ++e) printf(" %.4f", lg[e]);
+        printf("\n");
+    }
     std::vector<int> ids(T * TOPK);
     CK(hipMemcpy(ids.data(), a.ids, ids.size() * 4, hipMemcpyDeviceToHost));
     std::vector<char> seen(E, 0);
@@ -191,11 +199,14 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     for (int v : ids) if (v >= 0 && v < E && !seen[v]) { seen[v] = 1; ++touched; }
     const char *gun, *dnn;
     moe_decode_kernel_names(a, &gun, &dnn);
-    printf("moe T=%d: %d distinct experts, kernels %s / %s\n", T, touched, gun, dnn);
+    printf("moe T=%d: %d distinct experts, kernels %s / %s; ids", T, touched, gun, dnn);
+    for (int v : ids) printf(" %d", v);
+    printf("\n");
     char nm[96];
+    const bool fused = T >= 3 && !(getenv("DSOCR_ROUTE_FUSED") && atoi(getenv("DSOCR_ROUTE_FUSED")) == 0);
     snprintf(nm, sizeof nm, "moe%d route", T);
-    report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_ROUTE); }, s), (double)E * H * 2);
-    if (route_only) {
+    if (!fused) report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_ROUTE); }, s), (double)E * H * 2);
+    if (route_only && !fused) {
         // phase clocks of the one-block router (wall clock, 100 MHz)
         auto* st = (unsigned long long*)dalloc(128);
         for (int it = 0; it < 3; ++it) {
@@ -225,6 +236,33 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_GATEUP); }, s), gub);
     snprintf(nm, sizeof nm, "moe%d down", T);
     report(nm, timeit(n, [&](int i) { set(i); launch_moe_decode(a, s, MOE_DOWN); }, s), dnb);
+    if (T >= 3) {
+        // phase clocks of the grouped gate/up (per block: entry, staged, router MFMAs, top-k, records, unit loop,
+        // first unit batch computed, exit), us from the first block's entry: min / median / max over blocks
+        auto* st = (unsigned long long*)dalloc(1024 * 8 * 8);
+        for (int it = 0; it < 3; ++it) {
+            CK(hipMemset(st, 0, 1024 * 64));
+            set(it + 1);
+            launch_moe_decode(a, s, MOE_ROUTE);
+            a.stamps = st;
+            launch_moe_decode(a, s, MOE_GATEUP);
+            a.stamps = nullptr;
+            CK(hipStreamSynchronize(s));
+            std::vector<unsigned long long> h(1024 * 8);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            for (int b = 0; b < 1024; ++b) if (h[b * 8] && h[b * 8] < t0) t0 = h[b * 8];
+            printf("gateup%d stamps (us; min/med/max):", T);
+            for (int i = 0; i < 8; ++i) {
+                std::vector<double> v;
+                for (int b = 0; b < 1024; ++b) if (h[b * 8 + i]) v.push_back(((long long)h[b * 8 + i] - (long long)t0) / 100.0);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                printf(" %d:%.2f/%.2f/%.2f", i, v.front(), v[v.size() / 2], v.back());
+            }
+            printf("\n");
+        }
+    }
     if (T != 1 || !getenv("KB_WAVES")) return;
     // per-wave entry / exit clocks (WaveSpan slots) of single gate/up and down launches after a fresh route,
     // by role: the gate/up's shared-expert and routed waves, the down's routed and shared waves
