@@ -342,14 +342,18 @@ def chain_roofline(chain, waves, d, B, P):
     included, as a back-to-back rocprofv3 dispatch record), boundary = its first wave entry - that exit.
     MoE launches are priced at the distinct experts the wave-span generate of the same batch recorded."""
     import numpy as np
-    pred = {"moe_gateup": ("router", 0), "moe_down": ("moe_gateup", 0), "o_proj": ("attention", 0),
-            "router": ("o_proj", 0), "attention": ("moe_down", -1)}
+    # the launch before each kind (layer offset); at 3..8 pages the gate/up launch routes itself (no router launch):
+    # its predecessor is then the o_proj launch
+    pred = {"moe_gateup": (("router", 0), ("o_proj", 0)), "moe_down": (("moe_gateup", 0),),
+            "o_proj": (("attention", 0),), "router": (("o_proj", 0),), "attention": (("moe_down", -1),)}
     Hh, hd, heads = d["H"], d["hd"], d["heads"]
     out = {}
-    for kind, (pk, dl) in pred.items():
-        a, b = chain.get(kind), chain.get(pk)
-        if a is None or b is None or (kind == "attention" and B > 1):  # (B > 1: an unstamped q/k/v launch precedes it)
+    for kind, cands in pred.items():
+        a = chain.get(kind)
+        cands = [(chain[pk], dl) for pk, dl in cands if pk in chain and np.any(chain[pk][..., 1] > 0)]
+        if a is None or not cands or (kind == "attention" and B > 1):  # (B > 1: an unstamped q/k/v launch precedes it)
             continue
+        b, dl = cands[0]
         L, S = a.shape[0], a.shape[1]
         durs, bnds, wv, by = [], [], [], []
         for l in range(max(0, -dl), L):

@@ -2111,8 +2111,9 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         std::vector<int> moe_l;
         for (int l = 0; l < L.layers; ++l)
             if (layers_[l].moe) moe_l.push_back(l);
-        if (!moe_l.empty()) {
-            // the routing launches of the dispatch ([RMSNorm +] router GEMV [+ routing / grouping])
+        if (!moe_l.empty() && moe_decode_route_launch(moe_args(moe_l[0], B, XO))) {
+            // the routing launches of the dispatch ([RMSNorm +] router GEMV [+ routing / grouping]; none when the
+            // gate/up launch routes itself)
             timed(prof.router, iters * (int)moe_l.size(), [&](int i) {
                 MoeDecodeArgs ma = moe_args(moe_l[i % moe_l.size()], B, XO);
                 ma.x = SX;

@@ -2877,6 +2877,8 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
 }
 }  // namespace
 
+bool moe_decode_route_launch(const MoeDecodeArgs& a) { return !moe_plan(a).route_in_gu; }
+
 void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down) {
     const MoePlan p = moe_plan(a);
     const char* gu = "moe_gateup2_kernel";

@@ -399,6 +399,8 @@ struct MoeDecodeArgs {
 };
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments
+// false when the routing runs inside the gate/up launch (3..8 tokens, DSOCR_ROUTE_FUSED): MOE_ROUTE launches nothing
+bool moe_decode_route_launch(const MoeDecodeArgs& a);
 void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down);
 void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts = MOE_ALL);
 // Greedy selection (ngram ban evaluated in-kernel) + step bookkeeping + KV advance.
