@@ -431,8 +431,11 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     const int stride = gridDim.x * NU;
     const int KP = mm_pitch(a.K);
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
+    // phase clocks kept in LDS and written out at the end (a global store before a barrier would make the barrier
+    // wait for its acknowledgement and stretch the phase it measures)
+    __shared__ unsigned long long st_s[8];
 #define GU_STAMP(i) \
-    if (a.stamps && tid == 0) a.stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();
+    if (a.stamps && tid == 0) st_s[i] = __builtin_amdgcn_s_memrealtime();
     GU_STAMP(0);
     if constexpr (ROUTE) {
         // ---- the router of dec_route_grp, in every block: token row w normalised on wave w (x / den * w) and
@@ -702,6 +705,8 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         first = false;
     }
     GU_STAMP(7);
+    if (a.stamps && tid == 0)
+        for (int i = 0; i < 8; ++i) a.stamps[blockIdx.x * 8 + i] = (!ROUTE && i >= 1 && i <= 4) ? 0ull : st_s[i];
 #undef GU_STAMP
 }
 
