@@ -809,17 +809,26 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rw = wave % NWV, piece = wave / NWV;
     const int col = lane & 15, g = lane >> 4;
-    const int n_act = a.grp[0];
     const int n_sh = a.sWd ? a.Is / a.I : 0;
-    const int n_seg = n_act + n_sh;
     const int tiles = a.Hout / RT;
     const int unit = blockIdx.x;
-    if (unit >= n_seg * tiles) return;  // block-uniform, before any barrier
     const int seg = unit / tiles, tile = unit % tiles;
+    // the record count and this segment's record (expert, picks, their h rows) in ONE round trip: the record is
+    // read as if the segment were routed (in bounds either way) and dropped when it is a shared piece
+    int rw_[10];
+    {
+        const int* recg = a.grp + MOE_GRP_REC * (1 + min(seg, 64));
+        const int4 q0 = *reinterpret_cast<const int4*>(recg), q1 = *reinterpret_cast<const int4*>(recg + 4);
+        const int2 q2 = *reinterpret_cast<const int2*>(recg + 8);
+        rw_[0] = q0.x; rw_[1] = q0.y; rw_[2] = q0.z; rw_[3] = q0.w;
+        rw_[4] = q1.x; rw_[5] = q1.y; rw_[6] = q1.z; rw_[7] = q1.w; rw_[8] = q2.x; rw_[9] = q2.y;
+    }
+    const int n_act = a.grp[0];
+    const int n_seg = n_act + n_sh;
+    if (unit >= n_seg * tiles) return;  // block-uniform, before any barrier
     const bool shared = seg >= n_act;
     const int hpiece = seg - n_act;
-    const int* rec = a.grp + MOE_GRP_REC * (1 + (shared ? 0 : seg));
-    const int e = shared ? 0 : rec[0];
+    const int e = shared ? 0 : rw_[0];
     const int steps = a.I >> 5, nch = steps / PF / KS, c0 = piece * nch;  // nch: batches of this piece
     const int j0 = tile * RT + 16 * rw;
     // A stream: rows j0 .. j0 + 15 of the segment's down matrix over its I columns
@@ -852,10 +861,11 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         if (t >= a.T) return nullptr;
         if (shared) return a.hs + (long)t * a.Is + (long)hpiece * a.I;
         const float* p = nullptr;
-        const int cnt = rec[1];
-        for (int q = 0; q < cnt; ++q) {
-            const int r = rec[2 + q];
-            if (r / a.topk == t) p = a.h + (long)r * a.I;
+        const int cnt = rw_[1];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int r = rw_[2 + q];
+            if (q < cnt && r / a.topk == t) p = a.h + (long)r * a.I;
         }
         return p;
     };
