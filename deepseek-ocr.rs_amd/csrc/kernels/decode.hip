@@ -805,7 +805,7 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
     constexpr int U = 3, MT = 8;  // K <= 1536, T <= 8
     extern __shared__ __attribute__((aligned(16))) uint4 ws[];  // [8 experts][K / 8] 16-bit weight chunks
     __shared__ float lg_s[MT][64];
-    __shared__ float rank_s[MT][64];
+    __shared__ __attribute__((aligned(16))) float rank_s[MT][128];
     __shared__ int ids_s[64];
     __shared__ float w_s[64];
     __shared__ int last_s;
@@ -914,44 +914,8 @@ __global__ __launch_bounds__(512) void dec_route_grp_kernel(DecGemvArgs a, DecRo
     }
     // wave 0, lane e: the tokens that picked expert e (a token's picks are distinct, so at most one
     // per token), in increasing token order -> record s = number of picked experts below e
-    if (wave == 0 && r.grp) {
-        const int K = r.topk;
-        int pk[MT][8];  // picks, read unconditionally (clamped index) so the LDS reads batch
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pk[t][k] = ids_s[min(t * K + k, 63)];
-        int hit[MT];
-        int cnt = 0;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            hit[t] = -1;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (k < K && t < a.M && pk[t][k] == lane) hit[t] = t * K + k;
-            cnt += hit[t] >= 0 ? 1 : 0;
-        }
-        float hw[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) hw[t] = w_s[max(hit[t], 0)];
-        const bool act = cnt > 0 && lane < a.N;
-        const unsigned long long bm = __ballot(act);
-        const int sidx = __popcll(bm & ((1ull << lane) - 1ull));
-        if (act) {
-            int* rec = r.grp + MOE_GRP_REC * (1 + sidx);
-            rec[0] = lane;
-            rec[1] = cnt;
-            int q = 0;
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-                if (hit[t] >= 0) {
-                    rec[2 + q] = hit[t];
-                    rec[10 + q] = __float_as_int(hw[t]);
-                    ++q;
-                }
-        }
-        if (lane == 0) r.grp[0] = __popcll(bm);
-    }
+    if (wave == 0 && r.grp)  // scratch: wave 0's rank keys (read by now)
+        group_picks_wave64<0>(ids_s, w_s, a.M, r.topk, a.N, r.grp, reinterpret_cast<int*>(&rank_s[0][0]));
     // the normalised rows for the expert kernels, from this (last) block's registers after its last barrier: a
     // global store before a barrier makes the barrier wait for its acknowledgement
     if (a.xn_out && wave < a.M)
@@ -2212,9 +2176,14 @@ __global__ __launch_bounds__(256) void moe_down_slot_kernel(MoeDec2Args a) {
 // Rank form of the greedy top-k (block.rs:1254-1301: softmax, stable descending sort, ties ->
 // lower expert id): lane e holds score s_e; rank_e = #{j : s_j > s_e or (s_j == s_e and j < e)};
 // pick k is the lane whose rank is k.  Identical picks to topk_select, no serial argmax rounds.
-// lds: 64 floats private to the calling wave.  Returns (expert, weight) of pick `want`.
+// lds: 128 floats private to the calling wave (wave_rank64).  Returns (expert, weight) of pick `want`.
+// coop: the four waves of a block all call this (same logits), each counting the keys of one quarter and
+// summing the quarters over part (4 x 64 ints, one block barrier).  At one page every routed wave ranks
+// the same 64 scores, 28 waves per CU at once: the whole-rank form is bound by the CU's LDS read rate
+// (32 broadcast 16-byte reads per wave), the quarter form reads a quarter of that.
 __device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int softmax_scoring, int norm_topk,
-                                               float scaling, int want, float* lds, int& e_out, float& w_out) {
+                                               float scaling, int want, float* lds, int* part, bool coop,
+                                               int& e_out, float& w_out) {
     const int lane = threadIdx.x & 63;
     float sc;
     if (softmax_scoring) {
@@ -2226,33 +2195,41 @@ __device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int so
     } else {
         sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
     }
-    lds[lane] = sc;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    int rank = 0;
+    int rank;
+    if (coop) {
+        const int wave = threadIdx.x >> 6;
+        const unsigned long long key = ((unsigned long long)fkey(sc) << 32) | (unsigned)(63 - lane);
+        unsigned long long* kl = reinterpret_cast<unsigned long long*>(lds);
+        kl[lane] = key;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        int r0 = 0, r1 = 0;
 #pragma unroll
-    for (int j4 = 0; j4 < 16; ++j4) {
-        const float4 o = reinterpret_cast<const float4*>(lds)[j4];
-        const float oj[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = j4 * 4 + q;
-            rank += (oj[q] > sc || (oj[q] == sc && j < lane)) ? 1 : 0;
+        for (int j2 = 0; j2 < 8; ++j2) {
+            const ulonglong2 o = reinterpret_cast<const ulonglong2*>(kl)[8 * wave + j2];
+            r0 += o.x > key ? 1 : 0;
+            r1 += o.y > key ? 1 : 0;
         }
+        part[wave * 64 + lane] = r0 + r1;
+        __syncthreads();
+        rank = part[lane] + part[64 + lane] + part[128 + lane] + part[192 + lane];
+    } else {
+        rank = wave_rank64(sc, lds);
     }
     if (lane >= E) rank = 1 << 20;
-    // sum of the top-k scores in pick order (topk_select adds them in rank order)
+    // sum of the top-k scores in pick order (topk_select adds them in rank order); the pick's lane is uniform,
+    // so its score comes over with a lane read, not an LDS permute
     float wsum = 0.f;
     if (K > 1 && norm_topk) {
         for (int k = 0; k < K; ++k) {
             const unsigned long long bm = __ballot(rank == k);
             const int e = __builtin_ctzll(bm);
-            wsum += __shfl(sc, e);
+            wsum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), e));
         }
     }
     const unsigned long long bm = __ballot(rank == want);
     const int e = __builtin_ctzll(bm);
-    float v = __shfl(sc, e);
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), e));
     if (K > 1 && norm_topk) v = v / (wsum + 1e-20f);
     if (scaling != 1.0f) v = v * scaling;
     e_out = e;
@@ -2263,7 +2240,8 @@ template <typename WT>
 __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn, int routed_first) {
     constexpr int RB = 1;  // one gate + up row pair per wave (66 VGPRs: the 1792-block grid is resident at once)
     WaveSpan span_(a.span);
-    __shared__ __attribute__((aligned(16))) float rank_lds[4][64];
+    __shared__ __attribute__((aligned(16))) float rank_lds[4][128];
+    __shared__ int part_s[4 * 64];
     constexpr int U = 3;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x;
@@ -2309,11 +2287,17 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
         issue(Wg, Wg + (long)a.Is * a.K, a.Is);
         load_x();
     } else {
+        // the token row goes out behind the pick's weight rows: its L2 latency hides under theirs, and the pick
+        // runs with no row registers live (the 1792-block grid's residency is set by this kernel's VGPRs)
         const float lg = a.logits[min(lane, a.E - 1)];
-        load_x();
-        topk_rank_pick(lg, a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, sl, rank_lds[wave], e, wk);
+        // a whole routed block (routed_first: blocks < n_rt / 4 hold four routed waves, none returned) ranks
+        // cooperatively; any other routed wave alone
+        const bool coop = routed_first && b < (n_rt >> 2);
+        topk_rank_pick(lg, a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, sl, rank_lds[wave], part_s, coop, e,
+                       wk);
         const WT* Wg = reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
         issue(Wg, Wg + (long)a.I * a.K, a.I);
+        load_x();
         if (i0 == 0 && lane == 0) { a.ids_out[sl] = e; a.w_out[sl] = wk; }
     }
     const int rows = shared ? a.Is : a.I;

@@ -420,8 +420,8 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
     // waited on with vmcnt, i.e. behind every weight load in flight (the double-buffered stream drained at each
     // unit: measured in the round-4 kernel's ISA, `s_waitcnt vmcnt(0)` after each record load).
     __shared__ __attribute__((aligned(16))) int grp_s[GREC];
-    __shared__ int ids_s[ROUTE ? 64 : 1];
-    __shared__ float w_s[ROUTE ? 64 : 1];
+    __shared__ __attribute__((aligned(16))) int ids_s[ROUTE ? 64 : 4];
+    __shared__ float w_s[ROUTE ? 64 : 1];  // ROUTE: [8 tokens][8 picks], like ids_s
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the hand-off branches are scalar
     const int col = lane & 15, g = lane >> 4;
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         // staged as the B planes (the gate/up below uses the same rows); the 64 x K router matrix from L2 as MFMA
         // A fragments (wave w: rows 16 (w & 3) .., k-steps of half w >> 2), halves met in LDS; top-k per token
         // (topk_wave64) and the expert records (wave 0), so no router launch runs before this one
-        constexpr int RB = 10;  // router k-steps per register batch
+        constexpr int RB = 10;  // router k-steps per register batch (the router_ok range: two batches per half)
         const int half = steps >> 1, nrb = half / RB;
         const int tile = wave & 3, kh = wave >> 2;
         const WT* R = reinterpret_cast<const WT*>(a.router) + (long)min(16 * tile + col, a.E - 1) * a.K + 8 * g +
@@ -455,9 +455,12 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
                 __builtin_memcpy(&f[i], &q, 16);
             }
         };
+        // both router batches go out first (L2-resident after the first blocks of an XCD touch them), then the
+        // token rows; the staging barrier below waits for all of them, so the MFMAs run without a load wait
+        rload(ra, 0);
+        if (nrb > 1) rload(rb, 1);
         MmRow xr;
         if (wave < a.T) mm_row_load<true>(xr, a.x + (long)wave * a.K, a.K, a.norm_w);
-        rload(ra, 0);
         if (wave < a.T) mm_row_store<WT, true, 3, true>(xr, a.K, a.eps, xp, KP, scl, wave);
         if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
         __syncthreads();
@@ -475,16 +478,16 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             }
         };
         for (int bi = 0; bi < nrb; bi += 2) {
-            if (bi + 1 < nrb) rload(rb, bi + 1);
             rcompute(ra, bi);
-            if (bi + 1 >= nrb) break;
             if (bi + 2 < nrb) rload(ra, bi + 2);
+            if (bi + 1 >= nrb) break;
             rcompute(rb, bi + 1);
+            if (bi + 3 < nrb) rload(rb, bi + 3);
         }
         GU_STAMP(2);
         f32x4* rpart = reinterpret_cast<f32x4*>(scr);  // [4 tiles][64 lanes]
         float* lg_s = scr + 1024;                       // [8 tokens][64 experts]
-        float* rank_s = scr + 1536;                     // [8][64]
+        float* rank_s = scr;                            // [8][128] (64-bit keys; the halves are read by then)
         if (kh == 1) rpart[tile * 64 + lane] = racc;
         __syncthreads();
         if (kh == 0) {
@@ -498,51 +501,23 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         }
         __syncthreads();
         if (wave < a.T)
-            topk_wave64(lg_s[wave * 64 + lane], a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, rank_s + wave * 64,
-                        ids_s + wave * a.topk, w_s + wave * a.topk);
+            topk_wave64(lg_s[wave * 64 + lane], a.E, a.topk, a.softmax_scoring, a.norm_topk, a.scaling, rank_s + wave * 128,
+                        ids_s + wave * 8, w_s + wave * 8);  // token t's picks at 8 t ..
         __syncthreads();
         GU_STAMP(3);
         // wave 0, lane e: the tokens that picked expert e (a token's picks are distinct), in increasing token
         // order -> record sidx = number of picked experts below e (dec_route_grp's records); block 0 also writes
         // them, the picks and the logits to global memory (for the down launch and the tools), after its last
         // barrier
-        if (wave == 0) {
-            const int K = a.topk;
-            int hit[MM_MT];
-            int cnt = 0;
-#pragma unroll
-            for (int t = 0; t < MM_MT; ++t) {
-                hit[t] = -1;
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (k < K && t < a.T && ids_s[min(t * K + k, 63)] == lane) hit[t] = t * K + k;
-                cnt += hit[t] >= 0 ? 1 : 0;
-            }
-            const bool act = cnt > 0 && lane < a.E;
-            const unsigned long long bm = __ballot(act);
-            const int sidx = __popcll(bm & ((1ull << lane) - 1ull));
-            if (act) {
-                int* rl = grp_s + MOE_GRP_REC * (1 + sidx);
-                rl[0] = lane;
-                rl[1] = cnt;
-                int q = 0;
-#pragma unroll
-                for (int t = 0; t < MM_MT; ++t)
-                    if (hit[t] >= 0) {
-                        rl[2 + q] = hit[t];
-                        rl[10 + q] = __float_as_int(w_s[hit[t]]);
-                        ++q;
-                    }
-            }
-            if (lane == 0) grp_s[0] = __popcll(bm);
-        }
+        if (wave == 0) group_picks_wave64<8>(ids_s, w_s, a.T, a.topk, a.E, grp_s, reinterpret_cast<int*>(rank_s));
         __syncthreads();
         GU_STAMP(4);
         if (blockIdx.x == 0) {
             const int TK = a.T * a.topk;
             if (tid < TK) {
-                a.ids_out[tid] = ids_s[tid];
-                a.w_out[tid] = w_s[tid];
+                const int t = tid / a.topk, l = 8 * t + tid - t * a.topk;
+                a.ids_out[tid] = ids_s[l];
+                a.w_out[tid] = w_s[l];
             }
             if (a.logits && (tid >> 6) < a.T && (tid & 63) < a.E)
                 const_cast<float*>(a.logits)[(tid >> 6) * a.E + (tid & 63)] = lg_s[(tid >> 6) * 64 + (tid & 63)];

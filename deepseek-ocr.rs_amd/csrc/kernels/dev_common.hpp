@@ -167,10 +167,43 @@ struct WaveSpan {
     }
 };
 
+// order-preserving float <-> unsigned key (atomicMax over floats); key 0 sorts below every
+// float and decodes to -inf
+__device__ __forceinline__ unsigned fkey(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_dec(unsigned k) {
+    if (k == 0u) return -INFINITY;
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Rank of the lane's score among the wave's 64, descending, ties -> lower lane: #{j : s_j > s_e or (s_j == s_e and
+// j < e)}.  Each score becomes a 64-bit key (order-preserving score bits, then 63 - lane), so the rank is a count of
+// keys above the lane's own: one 64-bit vector compare and one carry-add per key, from a 64-key LDS copy (32
+// broadcast 16-byte reads).  The float-compare form (a > b || (a == b && j < e)) compiles to scalar mask
+// arithmetic between vector compares and measured 1.9 us per call on gfx950 (tools/mb_topk.hip).  Same order for
+// the scores top-k sees (no NaN; -inf pads lanes >= E; +0 only).  lds: 128 floats (64 keys) private to the wave.
+__device__ __forceinline__ int wave_rank64(float sc, float* lds) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long key = ((unsigned long long)fkey(sc) << 32) | (unsigned)(63 - lane);
+    unsigned long long* kl = reinterpret_cast<unsigned long long*>(lds);
+    kl[lane] = key;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    int r0 = 0, r1 = 0;
+#pragma unroll
+    for (int j2 = 0; j2 < 32; ++j2) {
+        const ulonglong2 o = reinterpret_cast<const ulonglong2*>(kl)[j2];
+        r0 += o.x > key ? 1 : 0;
+        r1 += o.y > key ? 1 : 0;
+    }
+    return r0 + r1;
+}
+
 // Greedy top-k of one token by one wave, lane e holding expert e's logit (E <= 64): the picks of
 // topk_write (softmax / sigmoid scores, descending, ties -> lower expert id, weights summed in
-// pick order, optional renormalise + scaling), by rank: every lane counts the scores that beat its
-// own from a 64-float LDS copy (16 broadcast reads).  lds: 64 floats private to the wave.  Lane 0
+// pick order, optional renormalise + scaling), by rank (wave_rank64).  lds: 128 floats private to the wave.  Lane 0
 // writes ids[k], w[k].
 __device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softmax_scoring, int norm_topk, float scaling,
                                             float* lds, int* ids, float* w) {
@@ -185,20 +218,7 @@ __device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softm
     } else {
         sc = lane < E ? 1.0f / (1.0f + expf(-logit)) : -INFINITY;
     }
-    lds[lane] = sc;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    int rank = 0;
-#pragma unroll
-    for (int j4 = 0; j4 < 16; ++j4) {
-        const float4 o = reinterpret_cast<const float4*>(lds)[j4];
-        const float oj[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = j4 * 4 + q;
-            rank += (oj[q] > sc || (oj[q] == sc && j < lane)) ? 1 : 0;
-        }
-    }
+    int rank = wave_rank64(sc, lds);
     if (lane >= E) rank = 1 << 20;
     float wsum = 0.f;
     int pe[8];
@@ -227,15 +247,55 @@ __device__ __forceinline__ void topk_wave64(float logit, int E, int K, int softm
     }
 }
 
-// order-preserving float <-> unsigned key (atomicMax over floats); key 0 sorts below every
-// float and decodes to -inf
-__device__ __forceinline__ unsigned fkey(float f) {
-    const unsigned u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+// The expert records of one step's picks (MOE_GRP_* layout, kernels.hpp) on one wave: lane e collects the tokens
+// that picked expert e (a token's picks are distinct, so at most one per token) in increasing token order; record
+// s = the number of picked experts below e.  ids / w: token t's picks at P t + k, P = PITCH (0: topk), T <= 8,
+// P t + k < 64.  Scatter, not search: lane P t + k ORs bit t into its expert's token mask and notes k (LDS, tmp:
+// 576 ints private to the wave), then lane e reads its mask and its 8 slots back — a few dozen instructions where
+// comparing every lane with all 64 picks costs ~200 (measured 1.5 us, tools/mb_topk.hip).  grp[0] = record count.
+template <int PITCH>
+__device__ __forceinline__ void group_picks_wave64(const int* ids, const float* w, int T, int K, int E, int* grp,
+                                                   int* tmp) {
+    const int lane = threadIdx.x & 63;
+    const int P = PITCH ? PITCH : K;
+    int* tok = tmp;       // [64 experts] token bit masks
+    int* kof = tmp + 64;  // [64 experts][8 tokens] the pick's k
+    tok[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int t = lane / P, k = lane - t * P;
+    const int v = ids[lane];
+    if (t < T && k < K && v >= 0 && v < 64) {
+        __hip_atomic_fetch_or(tok + v, 1 << t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        kof[v * 8 + t] = k;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const int msk = tok[lane];
+    const int4 ka = reinterpret_cast<const int4*>(kof + lane * 8)[0], kb = reinterpret_cast<const int4*>(kof + lane * 8)[1];
+    const int kk[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+    float hw[8];  // read for every token (stale slots clamped in range), used for the hits only
+#pragma unroll
+    for (int u = 0; u < 8; ++u) hw[u] = w[min(P * u + (kk[u] & 7), 63)];
+    const int cnt = __popc(msk);
+    const bool act = cnt > 0 && lane < E;
+    const unsigned long long bm = __ballot(act);
+    const int sidx = __popcll(bm & ((1ull << lane) - 1ull));
+    if (act) {
+        int* rec = grp + MOE_GRP_REC * (1 + sidx);
+        rec[0] = lane;
+        rec[1] = cnt;
+        int q = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if ((msk >> u) & 1) {
+                rec[2 + q] = u * K + kk[u];
+                rec[10 + q] = __float_as_int(hw[u]);
+                ++q;
+            }
+    }
+    if (lane == 0) grp[0] = __popcll(bm);
 }
-__device__ __forceinline__ float fkey_dec(unsigned k) {
-    if (k == 0u) return -INFINITY;
-    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
+
 
 }  // namespace dsocr
