@@ -2796,14 +2796,16 @@ struct MoePlan {
     bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
     bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
     bool route_in_gu = false;  // grouped mode: the routing runs inside the gate/up launch (no router launch)
+    bool route_one = false;    // grouped mode: that routing as a one-block launch of the same kernel (route only)
     MoeDec2Args mr;            // ... its arguments
 };
 
 // DSOCR_ROUTE_FUSED (A/B switch, read at every plan): 1 (default) = at 3..8 tokens the router runs inside the
-// matrix-core gate/up launch (moe_gateup_mm_route_ok); 0 = dec_route_grp launch + gate/up
-static bool route_fused_on() {
+// matrix-core gate/up launch (moe_gateup_mm_route_ok); 2 = the same routing as a one-block launch (route only)
+// before a plain gate/up; 0 = dec_route_grp launch + gate/up
+static int route_fused_mode() {
     const char* e = getenv("DSOCR_ROUTE_FUSED");
-    return !e || atoi(e) != 0;
+    return e ? atoi(e) : 1;
 }
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
@@ -2833,13 +2835,19 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
         p.route1 = dec_route_grp_ok(T, E, a.H, K);
         p.gu_mm = moe_gateup_mm_ok(m);
         p.dn_mm = moe_down_mm_ok(m);
-        if (p.route1 && p.gu_mm && a.norm_w && a.router_wdt == a.wdtype && route_fused_on()) {
+        const int rmode = route_fused_mode();
+        if (p.route1 && p.gu_mm && a.norm_w && a.router_wdt == a.wdtype && rmode != 0) {
             MoeDec2Args r = m;
             r.x = a.x; r.norm_w = a.norm_w; r.eps = a.eps;
             r.router = a.router; r.router_bias = a.router_bias;
             r.softmax_scoring = a.softmax_scoring; r.norm_topk = a.norm_topk; r.scaling = a.scaling;
             r.ids_out = a.ids; r.w_out = a.wts; r.logits = a.logits;  // (block 0 also writes the logits)
-            if (moe_gateup_mm_route_ok(r)) { p.route_in_gu = true; p.mr = r; }
+            if (rmode == 2) r.xn_out = a.xn;  // the plain gate/up reads the normalised rows (m.x == a.xn)
+            if (moe_gateup_mm_route_ok(r)) {
+                p.mr = r;
+                if (rmode == 2) p.route_one = true;
+                else p.route_in_gu = true;
+            }
         }
     } else if (T <= 8) {
         // every gate/up block routes itself from the router logits (rank / serial greedy top-k)
@@ -2881,6 +2889,8 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     const MoeDec2Args& m = p.m;
     if ((parts & MOE_ROUTE) && p.route_in_gu) {
         // (the gate/up launch routes)
+    } else if ((parts & MOE_ROUTE) && p.route_one) {
+        launch_moe_gateup_mm(p.mr, s);  // one block: norm + router + top-k + records, no expert
     } else if ((parts & MOE_ROUTE) && p.route1) {
         // norm + logits + top-k + records in one block (the grouped kernels read a.xn)
         DecGemvArgs g = p.router;

@@ -334,6 +334,9 @@ struct MoeDec2Args {
     // grouped gate/up with the routing inside (moe_gateup_mm_route_ok): the router rows [E][K] (wdtype), an
     // optional logit bias; x is then the raw residual stream, normalised with norm_w in every block
     const void* router = nullptr; const float* router_bias = nullptr;
+    // ... route only: one block runs that routing, writes the normalised rows here (f32 [T][K]) with the picks and
+    // records, and streams no expert (a plain gate/up launch follows)
+    float* xn_out = nullptr;
     unsigned long long* stamps = nullptr;  // dev (tools/kbench moe8): per block 8 words of s_memrealtime at phase points
 };
 // Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams
