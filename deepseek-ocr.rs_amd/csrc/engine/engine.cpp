@@ -991,6 +991,13 @@ void Engine::layer_forward_prefill(int l, int T, int B, const int* row_page, con
     launch_moe_combine(Y, APOS, WTS, YS, T, K, H, X, 1, st);
 }
 
+// DSOCR_ROUTER_SWZ=0 (A/B switch, read at every MoE argument build, i.e. per capture): the routing inside gate/up
+// reads the row-major router rows instead of their fragment-ordered copy
+static bool router_swz_off() {
+    const char* e = getenv("DSOCR_ROUTER_SWZ");
+    return e && atoi(e) == 0;
+}
+
 // Decode MoE arguments of layer l for B pages (shared by decode_step and profile_decode): the
 // layer's weights and the named workspaces; launch_moe_decode (decode.hip) picks the kernels.
 MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
@@ -1020,6 +1027,7 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     }
     if (B <= 8 && d.e_gu_swz && (!d.has_shared || d.s_gu_swz)) {  // fragment-ordered experts
         a.Wgu_swz = d.e_gu_swz; a.Wd_swz = d.e_d_swz; a.sWgu_swz = d.s_gu_swz; a.sWd_swz = d.s_d_swz;
+        if (!router_swz_off()) a.router_swz = d.router_swz;
     }
     if (B > 8) {
         a.eoff = wsi("s_eoff", E + 1); a.arow = wsi("s_arow", TK); a.apos = wsi("s_apos", TK);
@@ -1234,6 +1242,10 @@ void Engine::ensure_mm_weights(int B) {
             launch_mm_swizzle(d.s_gu.W, 2 * Is, H, d.s_gu_swz, stream_);
             d.s_d_swz = dev_alloc(mm_swizzle_elems(H, Is) * 2);
             launch_mm_swizzle(d.s_d.W, H, Is, d.s_d_swz, stream_);
+        }
+        if (d.router.W && d.router.wdt == WDT_F16 && E % 16 == 0) {
+            d.router_swz = dev_alloc(mm_swizzle_elems(E, H) * 2);
+            launch_mm_swizzle(d.router.W, E, H, d.router_swz, stream_);
         }
     }
     HIP_CHECK(hipStreamSynchronize(stream_));

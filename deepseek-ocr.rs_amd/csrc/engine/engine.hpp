@@ -79,6 +79,7 @@ struct DecLayer {
     Lin s_gu, s_d;                // [2Is][H], [H][Is]
     // fragment-ordered copies for the 3..8-page matrix-core kernels (Engine::ensure_mm_weights)
     void* e_gu_swz = nullptr; void* e_d_swz = nullptr; void* s_gu_swz = nullptr; void* s_d_swz = nullptr;
+    void* router_swz = nullptr;  // fragment-ordered router rows (3..8 pages: the routing inside gate/up)
 };
 
 struct PagePixels {

@@ -2839,7 +2839,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
         if (p.route1 && p.gu_mm && a.norm_w && a.router_wdt == a.wdtype && rmode != 0) {
             MoeDec2Args r = m;
             r.x = a.x; r.norm_w = a.norm_w; r.eps = a.eps;
-            r.router = a.router; r.router_bias = a.router_bias;
+            r.router = a.router; r.router_bias = a.router_bias; r.router_swz = a.router_swz;
             r.softmax_scoring = a.softmax_scoring; r.norm_topk = a.norm_topk; r.scaling = a.scaling;
             r.ids_out = a.ids; r.w_out = a.wts; r.logits = a.logits;  // (block 0 also writes the logits)
             if (rmode == 2) r.xn_out = a.xn;  // the plain gate/up reads the normalised rows (m.x == a.xn)

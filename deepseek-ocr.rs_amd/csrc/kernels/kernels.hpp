@@ -334,6 +334,7 @@ struct MoeDec2Args {
     // grouped gate/up with the routing inside (moe_gateup_mm_route_ok): the router rows [E][K] (wdtype), an
     // optional logit bias; x is then the raw residual stream, normalised with norm_w in every block
     const void* router = nullptr; const float* router_bias = nullptr;
+    const void* router_swz = nullptr;  // ... optional fragment-ordered copy of the router rows (launch_mm_swizzle)
     // ... route only: one block runs that routing, writes the normalised rows here (f32 [T][K]) with the picks and
     // records, and streams no expert (a plain gate/up launch follows)
     float* xn_out = nullptr;
@@ -380,6 +381,7 @@ struct MoeDecodeArgs {
     const void* sWgu = nullptr; const void* sWd = nullptr;  // [2Is][H], [H][Is] (or null)
     const void* Wgu_swz = nullptr; const void* sWgu_swz = nullptr;  // optional fragment-ordered copies
     const void* Wd_swz = nullptr; const void* sWd_swz = nullptr;
+    const void* router_swz = nullptr;  // optional fragment-ordered router rows (the routing inside gate/up)
     int wdtype = WDT_F16;
     int softmax_scoring = 1, norm_topk = 0; float scaling = 1.f;
     float* out = nullptr;

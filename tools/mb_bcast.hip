@@ -3,7 +3,8 @@
 // lane loads), all issued before one wait.  Per launch: median over blocks of (all loads back - entry), in
 // s_memrealtime ticks (10 ns).  Variants: 0 same order in every block; 1 the wave -> (tile, half) map rotated by
 // block; 2 the k-step issue order rotated by block; 3 a single block (no sharing); 4 every block its own copy
-// (no sharing, same bytes).
+// (no sharing, same bytes); 5 a fragment-ordered copy (each wave's 20 fragments contiguous: 1 KB per load
+// instruction); 6 the same, a single block.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_bcast.hip -o tools/mb_bcast
 #include <hip/hip_runtime.h>
 
@@ -24,13 +25,15 @@ __global__ __launch_bounds__(512) void k(const uint16_t* R, long copy_stride, in
     if (mode == 1) { tile = (wave + b) & 3; kh = ((wave >> 2) + (b >> 2)) & 1; }
     const uint16_t* base = R + (mode == 4 ? (long)b * copy_stride : 0) + (long)(16 * tile + col) * K + 8 * g +
                            32L * kh * HALF;
+    // fragment-ordered copy: wave w's 20 fragments are 20 KB contiguous, lane l's 16 bytes at 1 KB step + 16 l
+    if (mode >= 5) base = R + (long)wave * (HALF * 512) + 8 * lane - 32L * 0;
     uint4 q[HALF];
     const int rot = mode == 2 ? (b % HALF) : 0;
 #pragma unroll
     for (int i = 0; i < HALF; ++i) {
         int s = i + rot;
         s = s >= HALF ? s - HALF : s;
-        q[i] = *reinterpret_cast<const uint4*>(base + 32L * s);
+        q[i] = *reinterpret_cast<const uint4*>(base + (mode >= 5 ? 512L : 32L) * s);
     }
     unsigned acc = 0;
 #pragma unroll
@@ -52,9 +55,10 @@ int main() {
     CK(hipMemset(R, 1, copy * grid * 2));
     CK(hipMalloc(&out, grid * 8));
     CK(hipMalloc(&sink, grid * 4));
-    const char* names[5] = {"same order", "tile/half rotated", "k-steps rotated", "one block", "private copies"};
-    for (int mode = 0; mode < 5; ++mode) {
-        const int gr = mode == 3 ? 1 : grid;
+    const char* names[7] = {"same order", "tile/half rotated", "k-steps rotated", "one block", "private copies",
+                            "fragment order", "fragment, 1 block"};
+    for (int mode = 0; mode < 7; ++mode) {
+        const int gr = (mode == 3 || mode == 6) ? 1 : grid;
         for (int rep = 0; rep < 6; ++rep) {
             // a fresh buffer touch pattern per launch is not needed: the matrix is L2/MALL-resident after the first
             hipLaunchKernelGGL(k, dim3(gr), dim3(512), 0, 0, R, copy, mode, out, sink);
