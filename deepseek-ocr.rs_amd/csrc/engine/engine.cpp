@@ -997,6 +997,11 @@ static bool router_swz_off() {
     const char* e = getenv("DSOCR_ROUTER_SWZ");
     return e && atoi(e) == 0;
 }
+// DSOCR_MM_SWZ=0 (A/B switch, per capture): 3..8 pages' q/k/v, o_proj and dense gate|up read row-major weights
+static bool mm_swz_off() {
+    const char* e = getenv("DSOCR_MM_SWZ");
+    return e && atoi(e) == 0;
+}
 
 // Decode MoE arguments of layer l for B pages (shared by decode_step and profile_decode): the
 // layer's weights and the named workspaces; launch_moe_decode (decode.hip) picks the kernels.
@@ -1120,6 +1125,7 @@ void Engine::decode_step(int B, int Lmax) {
                 launch_dec_qkv_rope(g, re, st);
             }
         } else if (B <= 8) {
+            if (B >= 3 && !mm_swz_off()) g.w_swz = d.qkv_swz;
             launch_dec_gemv(g, st);
         } else {
             launch_rmsnorm(X, H, XN, H, B, H, d.in_norm.w, L.rms_eps, st);
@@ -1131,6 +1137,7 @@ void Engine::decode_step(int B, int Lmax) {
         DecGemvArgs go;
         go.M = B; go.N = H; go.K = L.heads * hd; go.x = CTX; go.ldx = H; go.W = d.o.W; go.ldw = go.K;
         go.wdtype = d.o.wdt; go.bias = d.o.b; go.y = X; go.ldy = H; go.accumulate = 1; go.span = chain_slots(l, SPAN_OPROJ);
+        if (B >= 3 && B <= 8 && !mm_swz_off()) go.w_swz = d.o_swz;
         launch_dec_gemv(go, st);
         // MLP / MoE
         if (!d.moe && B >= 3 && B <= 8 && dense_mm_ok(d, B)) {
@@ -1142,6 +1149,7 @@ void Engine::decode_step(int B, int Lmax) {
             DecGemvArgs g1;
             g1.M = B; g1.N = 2 * I; g1.K = H; g1.x = X; g1.ldx = H; g1.norm_w = d.post_norm.w; g1.eps = L.rms_eps;
             g1.W = d.gu.W; g1.ldw = H; g1.wdtype = d.gu.wdt; g1.bias = d.gu.b; g1.y = G; g1.ldy = 2 * I;
+            if (!mm_swz_off()) g1.w_swz = d.gu_swz;
             launch_dec_gemv(g1, st);
             launch_silu_mul(G, 2 * I, I, B, HH, I, st);
             DecGemvArgs g2;
@@ -1230,6 +1238,20 @@ void Engine::ensure_mm_weights(int B) {
     // grouped matrix-core kernels stream them (3..8 pages)
     const int H = L.hidden, E = L.n_routed, I = L.moe_inter;
     if (B < 3) return;
+    // q/k/v, o_proj and the dense gate|up for dec_mm (each wave load one contiguous 1 KiB instead of 64 bytes of
+    // 16 rows: tools/mb_bcast.hip)
+    auto swz = [&](const Lin& w, void*& out) {
+        DecGemvArgs g;
+        g.M = B; g.N = w.N; g.K = w.K; g.ldw = w.K;
+        if (out || !w.W || (w.wdt != WDT_F16 && w.wdt != WDT_BF16) || !dec_mm_ok(g)) return;
+        out = dev_alloc(mm_swizzle_elems(w.N, w.K) * 2);
+        launch_mm_swizzle(w.W, w.N, w.K, out, stream_);
+    };
+    for (DecLayer& d : layers_) {
+        swz(d.qkv, d.qkv_swz);
+        swz(d.o, d.o_swz);
+        if (!d.moe) swz(d.gu, d.gu_swz);
+    }
     for (DecLayer& d : layers_) {
         if (!d.moe || d.e_gu_swz || d.e_wdt != WDT_F16 || H % 32 || I % 32) continue;
         d.e_gu_swz = dev_alloc(mm_swizzle_elems(E * 2 * I, H) * 2);

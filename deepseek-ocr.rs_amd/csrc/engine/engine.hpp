@@ -80,6 +80,7 @@ struct DecLayer {
     // fragment-ordered copies for the 3..8-page matrix-core kernels (Engine::ensure_mm_weights)
     void* e_gu_swz = nullptr; void* e_d_swz = nullptr; void* s_gu_swz = nullptr; void* s_d_swz = nullptr;
     void* router_swz = nullptr;  // fragment-ordered router rows (3..8 pages: the routing inside gate/up)
+    void* qkv_swz = nullptr; void* o_swz = nullptr; void* gu_swz = nullptr;  // ... q/k/v, o_proj, dense gate|up
 };
 
 struct PagePixels {

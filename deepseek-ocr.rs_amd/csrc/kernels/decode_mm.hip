@@ -350,10 +350,11 @@ static void mm_launch(const DecGemvArgs& a, hipStream_t s) {
 // fragment order were slower)
 template <typename WT, bool NORM>
 static void mm_dispatch(const DecGemvArgs& a, hipStream_t s) {
-    if (a.w_swz) {  // fragment-ordered weights (the lm_head's B > 2 copy)
+    if (a.w_swz) {  // fragment-ordered weights (3..8 pages: the lm_head's copy, q/k/v, o_proj, dense gate|up)
         DecGemvArgs b = a;
         b.W = a.w_swz;
-        mm_launch<WT, 8, 1, 10, 1, NORM, true>(b, s);
+        if (a.N >= 16384) mm_launch<WT, 8, 1, 10, 1, NORM, true>(b, s);
+        else mm_launch<WT, 1, 8, 5, 1, NORM, true>(b, s);
         return;
     }
     if (a.N >= 16384) mm_launch<WT, 8, 1, 10, 1, NORM>(a, s);

@@ -125,6 +125,7 @@ constexpr int NL = 11;  // MoE layers
 struct MoeLayerW {
     uint16_t *router, *gu, *d, *sgu, *sd;
     uint16_t *gu_s = nullptr, *sgu_s = nullptr, *d_s = nullptr, *sd_s = nullptr;  // fragment-ordered copies
+    uint16_t* router_s = nullptr;
     float* norm;
 };
 static bool g_swz = getenv("KB_SWZ") && atoi(getenv("KB_SWZ")) != 0;
@@ -149,6 +150,8 @@ static void moe_weights() {
             launch_mm_swizzle(w.d, E * H, I, w.d_s, nullptr);
             w.sd_s = (uint16_t*)dalloc(mm_swizzle_elems(H, IS) * 2);
             launch_mm_swizzle(w.sd, H, IS, w.sd_s, nullptr);
+            w.router_s = (uint16_t*)dalloc(mm_swizzle_elems(E, H) * 2);
+            launch_mm_swizzle(w.router, E, H, w.router_s, nullptr);
         }
         g_moe.push_back(w);
     }
@@ -178,7 +181,7 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
     auto set = [&](int l) {
         const MoeLayerW& w = g_moe[l % NL];
         a.norm_w = w.norm; a.router = w.router; a.Wgu = w.gu; a.Wd = w.d; a.sWgu = w.sgu; a.sWd = w.sd;
-        a.Wgu_swz = w.gu_s; a.sWgu_swz = w.sgu_s; a.Wd_swz = w.d_s; a.sWd_swz = w.sd_s;
+        a.Wgu_swz = w.gu_s; a.sWgu_swz = w.sgu_s; a.Wd_swz = w.d_s; a.sWd_swz = w.sd_s; a.router_swz = w.router_s;
     };
     const int n = 4 * NL;
     CK(hipDeviceSynchronize());  // the fills ran on the null stream; s does not wait for it
