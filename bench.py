@@ -305,6 +305,8 @@ def run_dots(args, rank, world, local, dist):
     gemm_f, attn_f, other_f = dots_flops(cfg, N)
     attn_layer_ms = tm["attention_ms"] / 4
     attn_tf = (attn_f / cfg["num_hidden_layers"]) / (attn_layer_ms * 1e-3) / 1e12
+    planes = 3 if os.environ.get("DSOCR_DOTS_PV_PLANES") == "3" else 2
+    issue = (1 + planes) / 2.0
     page_ms = elapsed / (args.steps * ppg) * 1e3
     return {
         "metric": "pages/sec, dots.ocr bf16 vision tower, 2048px page (BASELINE configs[3])",
@@ -319,14 +321,15 @@ def run_dots(args, rank, world, local, dist):
         "stage_ms": {"page_ms": round(page_ms, 2), "blocks_ms": round(tm["blocks_ms"], 2),
                      "patch_ms": round(tm["patch_ms"], 2), "merger_ms": round(tm["merger_ms"], 2)},
         # achieved = the reference's attention FLOPs (QK^T + P.V, f32 math) / the kernel's time; the kernel
-        # runs them on the bf16 matrix cores (exact: 1 pass for QK^T, 3 bf16 planes of P for P.V), so the
-        # peak is the dense bf16 MFMA rate and the issued MFMA work is 2x the algorithmic FLOPs
+        # runs them on the bf16 matrix cores (1 exact pass for QK^T; P.V on 2 bf16 planes of P — 16 significant
+        # bits, DSOCR_DOTS_PV_PLANES=3 for the exact 3), so the peak is the dense bf16 MFMA rate and the issued
+        # MFMA work is (1 + planes) / 2 x the algorithmic FLOPs
         "roofline": {"bound": "mfma", "achieved": round(attn_tf, 2), "peak": 2500.0, "unit": "TFLOP/s",
                      "frac": round(attn_tf / 2500.0, 4), "traffic": pmc_traffic("attention_bf16_tr_kernel")[0],
-                     "mfma_issued_tflops": round(2.0 * attn_tf, 2), "mfma_issued_frac": round(2.0 * attn_tf / 2500.0, 4),
-                     "kernel": "attention_bf16_tr_kernel<128> (bidirectional flash attention over the page's 21316 tokens "
-                               "on v_mfma_f32_32x32x16_bf16 with the reference's f32 math: exact bf16 q.k products, "
-                               "P split into 3 exact bf16 planes for P.V)",
+                     "mfma_issued_tflops": round(issue * attn_tf, 2), "mfma_issued_frac": round(issue * attn_tf / 2500.0, 4),
+                     "kernel": f"attention_bf16_tr_kernel<128, {planes}> (bidirectional flash attention over the page's "
+                               f"21316 tokens on v_mfma_f32_32x32x16_bf16 with the reference's f32 math: exact bf16 q.k "
+                               f"products, P split into {planes} bf16 planes for P.V)",
                      "avg_launch_us": round(attn_layer_ms * 1e3, 1),
                      "flops_per_launch": attn_f / cfg["num_hidden_layers"],
                      "tower_tflops_total": round((gemm_f + attn_f + other_f) / 1e12, 2),

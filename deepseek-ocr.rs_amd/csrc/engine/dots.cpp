@@ -134,6 +134,12 @@ DotsPatches dots_preprocess(const DotsConfig& c, const uint8_t* rgb, int w, int 
 }
 
 namespace {
+// DSOCR_DOTS_PV_PLANES (A/B switch, read per layer): the attention's P.V in 2 bf16 planes of p (default: 16
+// significant bits, <= 2^-17 relative per probability, 2^-8 below the block output's bf16 rounding) or 3 (exact)
+int dots_pv_planes() {
+    const char* e = getenv("DSOCR_DOTS_PV_PLANES");
+    return (e && atoi(e) == 3) ? 3 : 2;
+}
 std::string read_text(const std::string& p) {
     std::ifstream f(p);
     if (!f) throw std::runtime_error("ENOENT: cannot read config " + p);
@@ -286,29 +292,35 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
     if (gh % M || gw % M) throw std::runtime_error("EINVAL: grid not divisible by the merge size");
     const long per = (long)gh * gw, N = (long)gt * per, groups = N / (M * M);
     // rotary table (VisionRotaryEmbedding::build_embeddings, dots_vit.rs:717-735): per token
-    // [h * inv_freq | w * inv_freq] (f32), cos / sin correctly rounded, duplicated to [t | t]
+    // [h * inv_freq | w * inv_freq] (f32), cos / sin correctly rounded, duplicated to [t | t].  A function of
+    // the grid alone: built on the host once per grid shape and kept on the device (2.7 M double cos / sin
+    // per 2044 px page took ~30 ms of host time ahead of the page's first kernel)
     const int rope = hd / 2, axis = rope / 2;
-    std::vector<float> inv(axis);
-    for (int i = 0; i < axis; ++i) inv[i] = 1.0f / std::pow(10000.0f, (float)(2 * i) / (float)rope);
-    std::vector<float> cs((size_t)N * hd), sn((size_t)N * hd);
-    long n = 0;
-    for (int f = 0; f < gt; ++f)
-        for (int bh = 0; bh < gh / M; ++bh)
-            for (int bw = 0; bw < gw / M; ++bw)
-                for (int ih = 0; ih < M; ++ih)
-                    for (int iw = 0; iw < M; ++iw, ++n) {
-                        const float hp = (float)(bh * M + ih), wp = (float)(bw * M + iw);
-                        for (int j = 0; j < rope; ++j) {
-                            const float a = j < axis ? hp * inv[j] : wp * inv[j - axis];
-                            const float c = (float)std::cos((double)a), s = (float)std::sin((double)a);
-                            cs[n * hd + j] = cs[n * hd + rope + j] = c;
-                            sn[n * hd + j] = sn[n * hd + rope + j] = s;
+    float* d_cos = (float*)ws("d_cos", (size_t)N * hd * 4);
+    float* d_sin = (float*)ws("d_sin", (size_t)N * hd * 4);
+    if (rope_key_[0] != gt || rope_key_[1] != gh || rope_key_[2] != gw) {
+        std::vector<float> inv(axis);
+        for (int i = 0; i < axis; ++i) inv[i] = 1.0f / std::pow(10000.0f, (float)(2 * i) / (float)rope);
+        std::vector<float> cs((size_t)N * hd), sn((size_t)N * hd);
+        long n = 0;
+        for (int f = 0; f < gt; ++f)
+            for (int bh = 0; bh < gh / M; ++bh)
+                for (int bw = 0; bw < gw / M; ++bw)
+                    for (int ih = 0; ih < M; ++ih)
+                        for (int iw = 0; iw < M; ++iw, ++n) {
+                            const float hp = (float)(bh * M + ih), wp = (float)(bw * M + iw);
+                            for (int j = 0; j < rope; ++j) {
+                                const float a = j < axis ? hp * inv[j] : wp * inv[j - axis];
+                                const float c = (float)std::cos((double)a), s = (float)std::sin((double)a);
+                                cs[n * hd + j] = cs[n * hd + rope + j] = c;
+                                sn[n * hd + j] = sn[n * hd + rope + j] = s;
+                            }
                         }
-                    }
-    float* d_cos = (float*)ws("d_cos", cs.size() * 4);
-    float* d_sin = (float*)ws("d_sin", sn.size() * 4);
-    HIP_CHECK(hipMemcpyAsync(d_cos, cs.data(), cs.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(d_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d_cos, cs.data(), cs.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));  // the host vectors go out of scope
+        rope_key_[0] = gt; rope_key_[1] = gh; rope_key_[2] = gw;
+    }
 
     void* X = ws("d_x", (size_t)N * D * 2);
     void* XN = ws("d_xn", (size_t)N * D * 2);
@@ -364,6 +376,7 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
             a.q_rs = a.k_rs = a.v_rs = 3L * D; a.q_hs = a.k_hs = a.v_hs = hd;
             a.o = CTXb; a.o_rs = D; a.o_hs = hd; a.o_bf16 = 1;
             a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
+            a.pv_planes = dots_pv_planes();
             if (timed) prof_events() = ProfEvents{a0, a1};  // the launch's own dispatch timestamps
             launch_attention_bf16(a, st);
         }

@@ -78,6 +78,7 @@ class DotsVision {
     hipStream_t stream_ = nullptr;
     std::vector<void*> allocs_;
     std::map<std::string, std::pair<void*, size_t>> ws_;
+    long rope_key_[3] = {-1, -1, -1};  // (gt, gh, gw) of the rotary table now in d_cos / d_sin
     void* patch_w_ = nullptr;  // bf16 [D][Kp] (K = 3 p p zero-padded to a multiple of 64)
     int patch_k_ = 0, patch_kp_ = 0;
     float* patch_b_ = nullptr;

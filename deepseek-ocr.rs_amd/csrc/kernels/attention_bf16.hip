@@ -49,7 +49,7 @@ __device__ __forceinline__ uint16_t bf_bits(float v) {
 typedef short v4i16_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16_t lds_v4i16;
 
-template <int HD>
+template <int HD, int PL>
 __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args a) {
     constexpr int KP = HD + 8, VP = HD + 32;      // LDS row pitches (bf16 elements)
     constexpr int C8 = HD / 8;                    // 16-byte chunks per row
@@ -172,13 +172,25 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float p0 = sc[u][8 * t + 2 * q], p1 = sc[u][8 * t + 2 * q + 1];
-                    const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
-                    const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
-                    const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
-                    const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
-                    ph[q] = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
-                    pm[q] = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
-                    pl[q] = __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u);
+                    if constexpr (PL == 3) {
+                        const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
+                        const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
+                        const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+                        const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+                        ph[q] = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+                        pm[q] = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
+                        pl[q] = __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u);
+                    } else {
+                        // hi = RNE(p), its residual exact in f32, mid = RNE(residual): p to 16 significant bits
+                        const __bf16 h0 = (__bf16)p0, h1 = (__bf16)p1;
+                        const __bf16 m0 = (__bf16)(p0 - (float)h0), m1 = (__bf16)(p1 - (float)h1);
+                        uint16_t x0, x1, y0, y1;
+                        __builtin_memcpy(&x0, &h0, 2); __builtin_memcpy(&x1, &h1, 2);
+                        __builtin_memcpy(&y0, &m0, 2); __builtin_memcpy(&y1, &m1, 2);
+                        ph[q] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+                        pm[q] = (uint32_t)y0 | ((uint32_t)y1 << 16);
+                        pl[q] = 0u;
+                    }
                 }
                 const bf16x8_t fh = __builtin_bit_cast(bf16x8_t, ph), fm = __builtin_bit_cast(bf16x8_t, pm),
                                fl = __builtin_bit_cast(bf16x8_t, pl);
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
                     bf16x8_t vf;
                     __builtin_memcpy(&vf, &lo, 8);
                     __builtin_memcpy(reinterpret_cast<char*>(&vf) + 8, &hi, 8);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fl, o[c], 0, 0, 0);
+                    if constexpr (PL == 3) o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fl, o[c], 0, 0, 0);
                     o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fm, o[c], 0, 0, 0);
                     o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fh, o[c], 0, 0, 0);
                 }
@@ -226,9 +238,15 @@ void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s) {
         throw std::runtime_error("EINVAL: attention_bf16 needs 16-byte aligned rows");
     if ((long)(a.L + AB_KT) * std::max(a.k_rs, a.v_rs) * 2 >= (1L << 31))
         throw std::runtime_error("EINVAL: attention_bf16 sequence slice beyond 32-bit buffer offsets");
+    if (a.pv_planes != 2 && a.pv_planes != 3) throw std::runtime_error("EINVAL: attention_bf16 pv_planes is 2 or 3");
     dim3 grid((a.L + 4 * AB_Q - 1) / (4 * AB_Q), a.heads, a.n_seq);
-    if (a.hd == 128) DSOCR_LAUNCH(attention_bf16_tr_kernel<128>, grid, dim3(256), 0, s, a);
-    else DSOCR_LAUNCH(attention_bf16_tr_kernel<64>, grid, dim3(256), 0, s, a);
+    if (a.pv_planes == 2) {
+        if (a.hd == 128) DSOCR_LAUNCH((attention_bf16_tr_kernel<128, 2>), grid, dim3(256), 0, s, a);
+        else DSOCR_LAUNCH((attention_bf16_tr_kernel<64, 2>), grid, dim3(256), 0, s, a);
+    } else {
+        if (a.hd == 128) DSOCR_LAUNCH((attention_bf16_tr_kernel<128, 3>), grid, dim3(256), 0, s, a);
+        else DSOCR_LAUNCH((attention_bf16_tr_kernel<64, 3>), grid, dim3(256), 0, s, a);
+    }
 }
 
 }  // namespace dsocr

@@ -139,6 +139,9 @@ struct AttnBf16Args {
     void* o = nullptr; long o_rs = 0, o_hs = 0; int o_bf16 = 0;
     int n_seq = 0, L = 0, heads = 0, kv_heads = 0, hd = 0;
     float scale = 1.f;
+    // P.V passes: 3 = p split exactly into three bf16 planes (f32 products); 2 = hi + mid planes, p to 16
+    // significant bits (each plane round-to-nearest: relative error <= 2^-17 per probability)
+    int pv_planes = 3;
 };
 void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s);
 // SAM decomposed rel-pos: out[s][h][q][kh] = q . Rh[qh-kh+gh-1], out[..][gh+kw] = q . Rw[qw-kw+gw-1]
