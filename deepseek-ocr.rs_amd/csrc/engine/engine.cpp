@@ -1026,6 +1026,12 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     a.h = wsf("s_ehh", (size_t)TK * I);
     a.grp = wsi("s_grp", moe_grp_ints(E, B, K));
     a.route_cnt = wsi("s_route_cnt", 16);
+    if (B == 1) {  // the router inside the one-token gate/up launch: tagged logits, tag = decode position * 64 + layer
+        a.lg_tag = reinterpret_cast<unsigned long long*>(wsi("s_lgtag", 128));
+        a.tag_pos = wsi("s_kvpos", B);
+        a.layer = l;
+        a.err = wsi("s_err", 4);
+    }
     if (B >= 3 && B <= 8) {  // matrix-core grouped kernels: down partials + tickets
         a.dn_part = wsf("s_dnpart", moe_down_mm_part_floats(E, B, K, I, a.Is, H));
         a.dn_tick = wsi("s_dntick", (size_t)H / 64 + 1);  // one ticket per 64-row tile
@@ -1576,6 +1582,8 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
+    // the one-token gate/up's tagged router logits: no tag of an earlier generate may match this one's
+    HIP_CHECK(hipMemsetAsync(wsi("s_lgtag", 128), 0xff, sizeof(int) * 128, st));
     const int QKVN = layers_[0].qkv.N;
     float* SX = wsf("s_x", (size_t)B * H);
     float* SXN = wsf("s_xn", (size_t)B * H);
@@ -1814,6 +1822,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
+    HIP_CHECK(hipMemsetAsync(wsi("s_lgtag", 128), 0xff, sizeof(int) * 128, st));  // the dry step's tags
     if (chain_active_) {  // the dry step's stamps must not join step 1's: clear the regions and the marks
         HIP_CHECK(hipMemsetAsync(span_chain_, 0, (size_t)L.layers * SPAN_KINDS_CHAIN * SPAN_SLOTS * 16, st));
         HIP_CHECK(hipMemsetAsync(span_tmark_, 0, 16, st));

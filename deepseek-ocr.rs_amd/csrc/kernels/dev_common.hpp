@@ -184,6 +184,7 @@ __device__ __forceinline__ float fkey_dec(unsigned k) {
 // broadcast 16-byte reads).  The float-compare form (a > b || (a == b && j < e)) compiles to scalar mask
 // arithmetic between vector compares and measured 1.9 us per call on gfx950 (tools/mb_topk.hip).  Same order for
 // the scores top-k sees (no NaN; -inf pads lanes >= E; +0 only).  lds: 128 floats (64 keys) private to the wave.
+template <bool LOWREG = false>
 __device__ __forceinline__ int wave_rank64(float sc, float* lds) {
     const int lane = threadIdx.x & 63;
     const unsigned long long key = ((unsigned long long)fkey(sc) << 32) | (unsigned)(63 - lane);
@@ -192,11 +193,24 @@ __device__ __forceinline__ int wave_rank64(float sc, float* lds) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     int r0 = 0, r1 = 0;
+    if constexpr (LOWREG) {
+        // four passes of 16 keys (32 VGPRs of keys in flight, not 128: for callers that keep a token row live)
+#pragma unroll 1
+        for (int g = 0; g < 4; ++g) {
 #pragma unroll
-    for (int j2 = 0; j2 < 32; ++j2) {
-        const ulonglong2 o = reinterpret_cast<const ulonglong2*>(kl)[j2];
-        r0 += o.x > key ? 1 : 0;
-        r1 += o.y > key ? 1 : 0;
+            for (int j2 = 0; j2 < 8; ++j2) {
+                const ulonglong2 o = reinterpret_cast<const ulonglong2*>(kl)[8 * g + j2];
+                r0 += o.x > key ? 1 : 0;
+                r1 += o.y > key ? 1 : 0;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j2 = 0; j2 < 32; ++j2) {
+            const ulonglong2 o = reinterpret_cast<const ulonglong2*>(kl)[j2];
+            r0 += o.x > key ? 1 : 0;
+            r1 += o.y > key ? 1 : 0;
+        }
     }
     return r0 + r1;
 }
