@@ -2278,7 +2278,7 @@ __device__ __forceinline__ void mix_router_block(const MoeDec2Args& a, int rb, f
     }
 }
 
-template <typename WT>
+template <typename WT, bool ROUTE>
 __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn, int routed_first) {
     constexpr int RB = 1;  // one gate + up row pair per wave (66 VGPRs: the 1792-block grid is resident at once)
     WaveSpan span_(a.span);
@@ -2288,8 +2288,11 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
     constexpr int U = 3;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int b = blockIdx.x;
+    // ROUTE = false compiles the plain launch (66 VGPRs); ROUTE = true keeps the routing a runtime branch, the form
+    // measured (72 VGPRs, seven blocks per CU: specialised, the compiler hoisted the row loads into 108 VGPRs)
+    const bool route = ROUTE && a.route_blocks != 0;
     unsigned tag = 0;
-    if (a.route_blocks) {
+    if (route) {
         __shared__ __attribute__((aligned(16))) float rsm[XS_RED + 64 * U * 8];  // the router blocks' xstage
         tag = (unsigned)(*a.tag_pos * 64 + a.layer);
         if (b < a.route_blocks) {
@@ -2328,7 +2331,7 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
         }
     };
     auto load_x = [&]() {
-        if (a.route_blocks) {
+        if (route) {
             // no router launch hands over the normalised row: every wave normalises x itself (the grouped
             // router's form: its chunks' squares u-major then j, one wave sum, x / den * w)
 #pragma unroll
@@ -2360,14 +2363,14 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
         // the wave's own normalisation — off the critical path, and the row and the norm weights are not live
         // beside the weight registers)
         const WT* Wg = reinterpret_cast<const WT*>(a.sWgu);
-        if (a.route_blocks) load_x();
+        if (route) load_x();
         issue(Wg, Wg + (long)a.Is * a.K, a.Is);
-        if (!a.route_blocks) load_x();
+        if (!route) load_x();
     } else {
         // the token row goes out behind the pick's weight rows: its L2 latency hides under theirs, and the pick
         // runs with no row registers live (the 1792-block grid's residency is set by this kernel's VGPRs)
         float lg;
-        if (a.route_blocks) {
+        if (route) {
             load_x();  // normalised while the router blocks work
             // poll this (step, layer)'s logits: every lane one tagged word, until none is stale (bounded spin).
             // poll_mode 1 / 2: in a whole routed block only wave 0 polls and hands the logits over in LDS (a
@@ -2404,7 +2407,7 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
                        wk);
         const WT* Wg = reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
         issue(Wg, Wg + (long)a.I * a.K, a.I);
-        if (!a.route_blocks) load_x();
+        if (!route) load_x();
         if (i0 == 0 && lane == 0) { a.ids_out[sl] = e; a.w_out[sl] = wk; }
     }
     const int rows = shared ? a.Is : a.I;
@@ -2549,7 +2552,7 @@ namespace {
 int mix_blocks_per_cu(int wdtype) {
     static int bf = -1, f16 = -1;
     int& v = wdtype == WDT_BF16 ? bf : f16;
-    if (v < 0) v = wdtype == WDT_BF16 ? blocks_per_cu(moe_gateup_mix_kernel<bf16_t>, 0) : blocks_per_cu(moe_gateup_mix_kernel<f16_t>, 0);
+    if (v < 0) v = wdtype == WDT_BF16 ? blocks_per_cu(moe_gateup_mix_kernel<bf16_t, true>, 0) : blocks_per_cu(moe_gateup_mix_kernel<f16_t, true>, 0);
     return v;
 }
 }  // namespace
@@ -2565,8 +2568,13 @@ void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s)
     if (a.route_blocks && (!rf || !poll_wait_fits((n_rt + 3) / 4, mix_blocks_per_cu(a.wdtype), device_cus())))
         throw std::runtime_error("EINVAL: moe_gateup_mix routing inside needs routed-first order and resident waiters");
     dim3 grid(a.route_blocks + (rf ? (n_rt + 3) / 4 + (n_sh + 3) / 4 : std::max(n_sh, (n_rt + 2) / 3)));
-    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t>), grid, dim3(256), 0, s, a, xn, rf);
-    else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t>), grid, dim3(256), 0, s, a, xn, rf);
+    if (a.route_blocks) {
+        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t, true>), grid, dim3(256), 0, s, a, xn, rf);
+        else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t, true>), grid, dim3(256), 0, s, a, xn, rf);
+    } else {
+        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t, false>), grid, dim3(256), 0, s, a, xn, rf);
+        else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t, false>), grid, dim3(256), 0, s, a, xn, rf);
+    }
 }
 
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
