@@ -70,6 +70,8 @@ for step in "$@"; do
     pmc8t_write) DSOCR_NO_GRAPH=1 run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc8t_write -o pmc --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 16 --no-cpu-baseline --roofline-iters 2 > gpurun_out/pmc8t_write.log 2>&1 ;;
     gprof8t_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gprof8t_nopc -o g --output-format csv -- python bench.py --pages-per-gpu 8 --text-pages --steps 1 --warmup 0 --max-new-tokens 64 --no-cpu-baseline --roofline-iters 4 > gpurun_out/gprof8t_nopc.log 2>&1 ;;
     pmcdots_fetch) run 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcdots_fetch -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmcdots_fetch.log 2>&1 ;;
+    # MFMA busy per kernel over one dots page (tools/pmc_mfma.py reads the csv)
+    pmc_mfma_dots) run 900 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/pmc_mfma_dots -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmc_mfma_dots.log 2>&1 ;;
     pmcdots_write) run 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcdots_write -o pmc --output-format csv -- python bench.py --workload dots2048 --steps 1 --warmup 0 > gpurun_out/pmcdots_write.log 2>&1 ;;
     # round 5
     counters) run 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1 ;;
