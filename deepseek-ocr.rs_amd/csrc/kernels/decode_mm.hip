@@ -805,6 +805,14 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rw = wave % NWV, piece = wave / NWV;
     const int col = lane & 15, g = lane >> 4;
+    // phase clocks (dev, tools/kbench moe8 KB_STAMPS): kept in LDS, written at the block's exit
+    __shared__ unsigned long long dst_s[8];
+#define DN_STAMP(i) \
+    if (a.stamps && tid == 0) dst_s[i] = __builtin_amdgcn_s_memrealtime();
+#define DN_FLUSH(n)                                                                             \
+    if (a.stamps && tid == 0)                                                                   \
+        for (int i_ = 0; i_ < (n); ++i_) a.stamps[(long)blockIdx.x * 8 + i_] = dst_s[i_];
+    DN_STAMP(0);
     const int n_sh = a.sWd ? a.Is / a.I : 0;
     const int tiles = a.Hout / RT;
     const int unit = blockIdx.x;
@@ -888,6 +896,7 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         mm_row_store<WT, false, U>(xr[q], a.I, 0.f, xp, KP, scl, wave + q * NW);
     }
     __syncthreads();
+    DN_STAMP(1);
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const frag(&f)[PF], int c) {
@@ -908,6 +917,7 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         if (c + 2 < nch) load(fa, c0 + c + 2);
         compute(fb, c0 + c + 1);
     }
+    DN_STAMP(2);
     if (KS > 1) {  // the pieces of a row tile meet in LDS, summed in piece order by piece 0
         __shared__ f32x4 red[KS > 1 ? KS - 1 : 1][NWV][64];
         if (piece > 0) red[piece - 1][rw][lane] = acc;
@@ -939,7 +949,11 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         last_s = last;
     }
     __syncthreads();
-    if (!last_s) return;
+    DN_STAMP(3);
+    if (!last_s) {
+        DN_FLUSH(4);
+        return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
     // the last arriver: the ordered sum over segments.  A token's column of a segment it does not
     // belong to was computed from a zero B column, so it holds exact zeros and adding it leaves every
@@ -990,6 +1004,10 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         o.w = o.w + (v.w + u.w);
         *op = o;
     }
+    DN_STAMP(4);
+    DN_FLUSH(5);
+#undef DN_STAMP
+#undef DN_FLUSH
 }
 
 bool moe_down_mm_ok(const MoeDec2Args& a) {

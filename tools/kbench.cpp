@@ -266,6 +266,34 @@ static void case_moe(int T, hipStream_t s, bool route_only) {
             printf("\n");
         }
     }
+    if (T >= 3) {
+        // phase clocks of the grouped down (per block: entry, staged, streamed, ticket taken, last arriver done)
+        auto* st = (unsigned long long*)dalloc(2048 * 8 * 8);
+        for (int it = 0; it < 3; ++it) {
+            CK(hipMemset(st, 0, 2048 * 64));
+            set(it + 1);
+            launch_moe_decode(a, s, MOE_ROUTE);
+            launch_moe_decode(a, s, MOE_GATEUP);
+            a.stamps = st;
+            launch_moe_decode(a, s, MOE_DOWN);
+            a.stamps = nullptr;
+            CK(hipStreamSynchronize(s));
+            std::vector<unsigned long long> h(2048 * 8);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            int nb = 0;
+            for (int b = 0; b < 2048; ++b) if (h[b * 8]) { ++nb; if (h[b * 8] < t0) t0 = h[b * 8]; }
+            printf("down%d stamps, %d blocks (us; min/med/max):", T, nb);
+            for (int i = 0; i < 5; ++i) {
+                std::vector<double> v;
+                for (int b = 0; b < 2048; ++b) if (h[b * 8 + i]) v.push_back(((long long)h[b * 8 + i] - (long long)t0) / 100.0);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                printf(" %d:%.2f/%.2f/%.2f(n%zu)", i, v.front(), v[v.size() / 2], v.back(), v.size());
+            }
+            printf("\n");
+        }
+    }
     if (T != 1 || !getenv("KB_WAVES")) return;
     // per-wave entry / exit clocks (WaveSpan slots) of single gate/up and down launches after a fresh route,
     // by role: the gate/up's shared-expert and routed waves, the down's routed and shared waves
