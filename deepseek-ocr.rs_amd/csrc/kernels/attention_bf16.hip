@@ -38,7 +38,7 @@ __device__ __forceinline__ uint16_t bf_bits(float v) {
 #define AB_EXP(x) __expf(x)
 #endif
 #ifndef AB_PRIO
-#define AB_PRIO 1
+#define AB_PRIO 2  // bit 0: raised wave priority over the QK^T burst, bit 1: over the P.V burst (P.V only: 4.07 vs 4.03 both, 3.92 QK only; profiles/r05_dots/ab_setprio_placement)
 #endif
 
 // V is staged ROW-major (16-byte writes, as loaded) and read as the V^T MFMA operand through
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
     for (int k0 = 0; k0 < len; k0 += AB_KT, buf ^= 1) {
         AB_GLOAD(rk, a.k_rs, ko, k0 + AB_KT);  // in flight under QK^T and the softmax
         f32x16 sc[2];
-        if (AB_PRIO) __builtin_amdgcn_s_setprio(1);  // the matrix-core burst first, the other wave's VALU in its shadow
+        if (AB_PRIO & 1) __builtin_amdgcn_s_setprio(1);  // the matrix-core burst first, the other wave's VALU in its shadow
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
                 sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qreg[st], sc[u], 0, 0, 0);
             }
         }
-        if (AB_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (AB_PRIO & 1) __builtin_amdgcn_s_setprio(0);
         if (k0 + AB_KT > len) {  // the last, partial tile: keys past the end score -inf
 #pragma unroll
             for (int u = 0; u < 2; ++u)
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
         }
         AB_LSTORE(Ks[buf ^ 1]);                // the other buffer's last readers passed the previous barrier
         AB_GLOAD(rv, a.v_rs, vo, k0 + AB_KT);   // in flight under P.V
-        if (AB_PRIO) __builtin_amdgcn_s_setprio(1);
+        if (AB_PRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
                 }
             }
         }
-        if (AB_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (AB_PRIO & 2) __builtin_amdgcn_s_setprio(0);
         // the next tile into the other buffer (its last readers passed the previous barrier), then one
         // barrier: the tile is visible and every wave is done with this buffer before it is refilled
         AB_LSTORE(Vs[buf ^ 1]);
