@@ -263,6 +263,242 @@ static void launch_splitk_reduce(const GemmBf16Args& g, hipStream_t s) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
 }
 
+// ---------------------------------------------------------------------------------------
+// Ping-pong form for the large bf16-output linears (the dots.ocr tower: 21316 rows x 1536 / 4608 / 8448
+// columns).  256 x 256 tiles, 32 k per LDS stage, four stages (128 KiB, one block per CU), 8 waves as
+// 2 (M) x 4 (N) of 128 x 64 (4 x 2 tiles of v_mfma_f32_32x32x16_bf16).  The two wave rows run one
+// barrier apart: in every interval between two workgroup barriers one row issues its LDS DMAs and reads
+// its fragments (12 ds_read_b128) while the other runs its 16 MFMAs, and the two waves sharing a SIMD
+// (w and w + 4) belong to different rows, so the matrix core always has a wave to run.  Stage use, with
+// interval I_j ending at barrier b_j, row g loading k-tile t in I_{2t+g} and multiplying in I_{2t+g+1}:
+//  - at the start of its load interval for k-tile t a row issues the DMAs of k-tile t + 3 (its share:
+//    its own 128 A rows, 128 of the 256 W rows) into stage (t + 3) & 3 = (t - 1) & 3, whose last
+//    reads (k-tile t - 1) both rows finished (lgkmcnt(0)) before b_{2t-1};
+//  - k-tile u + 1 is waited for (counted vmcnt: the DMAs of the k-tiles after it stay in flight) by row
+//    1 at the end of its load interval for u and by row 0 at the end of its multiply interval for u, both
+//    before b_{2u+1}; it is read in I_{2u+2} and I_{2u+3}, after that barrier.
+// Row 1 takes one extra barrier before its first k-tile, row 0 one after its last, so both rows pass the
+// same number.  The DMA images are lane-linear per instruction (16 rows of 64 B) with the 16-byte chunk
+// XOR-swizzled by the SOURCE address (chunk ^ ((row >> 2) & 3)), which puts every ds_read_b128 lane group
+// on 16 distinct slots of the 256-byte bank row.  Every output element sees the same MFMA sequence as
+// gemm_bf16_nt_kernel (k ascending, 16 per instruction), so the results are bitwise equal to it
+// (tools/kbench dgemm compares them).
+constexpr int PP_M = 256, PP_N = 256, PP_K = 32, PP_NST = 4;
+constexpr int PP_STAGE = (PP_M + PP_N) * PP_K;  // bf16 elements per stage (32 KiB)
+constexpr int PP_LDS = PP_NST * PP_STAGE * 2;    // bytes
+
+__device__ __forceinline__ bf16x8_v pp_frag(const uint16_t* lds, int r, int kc) {
+    return *reinterpret_cast<const bf16x8_v*>(lds + r * PP_K + ((kc ^ ((r >> 2) & 3)) * 8));
+}
+
+// row g's share of k-tile kt: 128 A rows (g * 128 + ...) and 128 W rows, 2 + 2 DMAs of 16 rows per wave;
+// piece p: rows (wg * 2 + (p >> 1)) * 16 of A (p even) or W (p odd)
+__device__ __forceinline__ void pp_issue(int p, const uint16_t* A, long lda, int m0, int mmax, const uint16_t* W,
+                                         long ldw, int n0, int nmax, int k0, uint16_t* st, int grp, int wg, int lane) {
+    const int R = grp * 128 + (wg * 2 + (p >> 1)) * 16;
+    const int r = R + (lane >> 2);
+    const int j = (lane & 3) ^ ((r >> 2) & 3);
+    if ((p & 1) == 0) {
+        const long ra = min(m0 + r, mmax);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(A + ra * lda + k0 + j * 8),
+                                         (lds_void*)(st + R * PP_K), 16, 0, 0);
+    } else {
+        const long rw = min(n0 + r, nmax);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(W + rw * ldw + k0 + j * 8),
+                                         (lds_void*)(st + PP_M * PP_K + R * PP_K), 16, 0, 0);
+    }
+}
+
+// k-tile `ready` landed: the DMAs of the k-tiles after it (up to last, 4 per k-tile) stay in flight
+__device__ __forceinline__ void pp_wait(int ready, int last) {
+    const int ahead = last - ready;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void pp_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// diagnostic stamp (separate instantiation; read shares, not the run time): s_memtime with its own wait
+#define PP_STAMP(var)                                                                           \
+    if (STAMPS) {                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+    }
+
+template <bool STAMPS>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t pp_smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 2, wc = wave & 3;  // wave row = staggered group, wave column
+    const int ntn = (g.N + PP_N - 1) / PP_N;
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    int bm, bn;
+    tile_coords(tile, (g.M + PP_M - 1) / PP_M, ntn, g.group_m, bm, bn);
+    const int m0 = bm * PP_M, n0 = bn * PP_N;
+    const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A);
+    const uint16_t* W = reinterpret_cast<const uint16_t*>(g.W);
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nk = g.K / PP_K;
+    auto issue = [&](int p, int kt) {
+        pp_issue(p, A, g.lda, m0, g.M - 1, W, g.ldw, n0, g.N - 1, kt * PP_K, pp_smem + (kt & 3) * PP_STAGE, wr, wc, lane);
+    };
+    // prologue: k-tiles 0..2 in flight, k-tile 0 landed everywhere before the first barrier
+    unsigned long long p0 = 0, rt0 = 0;
+    if (STAMPS) {
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(p0)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt0)::"memory");
+    }
+    for (int kt = 0; kt < 3 && kt < nk; ++kt)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) issue(p, kt);
+    pp_wait(0, min(2, nk - 1));
+    pp_barrier();
+    if (wr == 1) pp_barrier();
+    unsigned long long seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sa = 0, sb = 0, sc = 0, sd = 0, se = 0, sf = 0, sh = 0, si = 0, s0 = 0;
+    PP_STAMP(s0);
+    for (int t = 0; t < nk; ++t) {
+        // load interval: this wave's fragments of k-tile t
+        PP_STAMP(sa);
+        PP_STAMP(sb);
+        const uint16_t* As = pp_smem + (t & 3) * PP_STAGE;
+        const uint16_t* Bs = As + PP_M * PP_K;
+        bf16x8_v af[2][4], bfv[2][2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int kc = ks * 2 + (lane >> 5);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bfv[ks][j] = pp_frag(Bs, wc * 64 + j * 32 + (lane & 31), kc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[ks][i] = pp_frag(As, wr * 128 + i * 32 + (lane & 31), kc);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PP_STAMP(sc);
+        if (wr == 1 && t + 1 < nk) pp_wait(t + 1, min(t + 2, nk - 1));
+        PP_STAMP(sd);
+        pp_barrier();
+        PP_STAMP(se);
+        // multiply interval, the DMAs of k-tile t + 3 one after every 4 MFMAs (their issue cost, ~100 cycles
+        // each, runs in the MFMA shadow instead of lengthening the load interval)
+        const bool more = t + 3 < nk;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfv[ks][j], acc[i][j], 0, 0, 0);
+                if (i & 1) {
+                    if (more) issue(ks * 2 + (i >> 1), t + 3);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        __builtin_amdgcn_s_setprio(0);
+        PP_STAMP(sf);
+        if (wr == 0 && t + 1 < nk) pp_wait(t + 1, min(t + 3, nk - 1));
+        PP_STAMP(sh);
+        pp_barrier();
+        PP_STAMP(si);
+        if (STAMPS) {
+            seg[0] += sb - sa; seg[1] += sc - sb; seg[2] += sd - sc; seg[3] += se - sd;
+            seg[4] += sf - se; seg[5] += sh - sf; seg[6] += si - sh;
+        }
+    }
+    if (wr == 0) pp_barrier();
+    // epilogue (bf16 out, no activation, no row scatter, 16-byte aligned C rows: the launch checks).  The
+    // wave's 128 x 64 result goes through its own 16 KiB of the (now idle) staging LDS: the D layout
+    // (col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) is written as bf16 rnd(rnd(acc) + b)
+    // with ds_write_b16 (16-byte chunk ^ 4 on rows with bit 2 set: the two half-waves on distinct banks),
+    // read back as 16-byte row chunks and stored with one global_store_dwordx4 per lane (128-byte rows per
+    // 8 lanes) -- the 2-byte scattered stores took ~55k cycles per block, a third of the kernel
+    const int half = lane >> 5, l32 = lane & 31;
+    uint16_t* ep = pp_smem + wave * (128 * 64);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wc * 64 + j * 32 + l32;
+        const float bv = (g.bias && col < g.N) ? g.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                float v = rnd_bf16(acc[i][j][r]);
+                if (g.bias) v = rnd_bf16(v + bv);
+                const int c = j * 32 + l32;
+                const int cs = (((c >> 3) ^ (((row >> 2) & 1) << 2)) << 3) | (c & 7);
+                const __bf16 hv = (__bf16)v;
+                ep[row * 64 + cs] = *reinterpret_cast<const uint16_t*>(&hv);
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    __bf16* C = reinterpret_cast<__bf16*>(g.C);
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int row = it * 8 + (lane >> 3), ch = lane & 7;
+        const u32x4 q = *reinterpret_cast<const u32x4*>(ep + row * 64 + ((ch ^ (((row >> 2) & 1) << 2)) << 3));
+        const int grow = m0 + wr * 128 + row, gcol = n0 + wc * 64 + ch * 8;
+        if (grow >= g.M || gcol >= g.N) continue;
+        __bf16* cp = C + (long)grow * g.ldc + gcol;
+        const uint16_t* qv = reinterpret_cast<const uint16_t*>(&q);
+        if (gcol + 8 <= g.N && !g.accumulate) {
+            *reinterpret_cast<u32x4*>(cp) = q;
+            continue;
+        }
+        u32x4 cv = gcol + 8 <= g.N ? *reinterpret_cast<const u32x4*>(cp) : u32x4{0, 0, 0, 0};
+        uint16_t* cw = reinterpret_cast<uint16_t*>(&cv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (gcol + e >= g.N) break;
+            float v = __uint_as_float((uint32_t)qv[e] << 16);
+            if (g.accumulate) {
+                const float cold = gcol + 8 <= g.N ? __uint_as_float((uint32_t)cw[e] << 16) : (float)cp[e];
+                v = rnd_bf16(cold + v);
+            }
+            const __bf16 hv = (__bf16)v;
+            cw[e] = *reinterpret_cast<const uint16_t*>(&hv);
+        }
+        if (gcol + 8 <= g.N) *reinterpret_cast<u32x4*>(cp) = cv;
+        else
+            for (int e = 0; e < 8 && gcol + e < g.N; ++e) reinterpret_cast<uint16_t*>(cp)[e] = cw[e];
+    }
+    if (STAMPS) {
+        unsigned long long e1 = 0, rt1 = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(e1)::"memory");
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt1)::"memory");
+        if (lane == 0 && blockIdx.x < 64) {
+            seg[7] = si - s0;
+            unsigned long long* o = g.stamps + ((long)blockIdx.x * 8 + wave) * 12;
+            for (int k = 0; k < 8; ++k) o[k] = seg[k];
+            o[8] = s0 - p0; o[9] = e1 - si; o[10] = e1 - p0; o[11] = rt1 - rt0;
+        }
+    }
+}
+
+// DSOCR_GEMM_PP=0 keeps the 128 x 128 one-stage kernel for the large linears (A/B)
+static bool gemm_pp_on() {
+    static const int v = getenv("DSOCR_GEMM_PP") ? atoi(getenv("DSOCR_GEMM_PP")) : 1;
+    return v != 0;
+}
+
 int gemm_bf16_splits(int M, int N, int K) {
     const int tiles = ((M + TB_M - 1) / TB_M) * ((N + TB_N - 1) / TB_N);
     const int nk = K / TB_K;
@@ -280,6 +516,24 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
         throw std::runtime_error("EINVAL: gemm_bf16 needs K % 64 == 0 and 16-byte aligned rows");
     if (g.splits < 1 || !g.part) g.splits = 1;
     g.group_m = gemm_group_m(g.group_m);
+    // ping-pong 256 x 256 kernel: variant 3, or by default for one-slice problems of >= 256 such tiles
+    const long pp_tiles = (long)((g.M + PP_M - 1) / PP_M) * ((g.N + PP_N - 1) / PP_N);
+    if (g.splits == 1 && g.K % PP_K == 0 && g.out_bf16 && !g.act && !g.c_rows && g.ldc % 8 == 0 &&
+        (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
+        (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256))) {
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess ||
+                hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess)
+                throw std::runtime_error("gemm_bf16_pp: cannot reserve 128 KiB of LDS");
+            attr = true;
+        }
+        if (g.stamps) hipLaunchKernelGGL(gemm_bf16_pp_kernel<true>, dim3((unsigned)pp_tiles), dim3(512), PP_LDS, s, g);
+        else hipLaunchKernelGGL(gemm_bf16_pp_kernel<false>, dim3((unsigned)pp_tiles), dim3(512), PP_LDS, s, g);
+        return;
+    }
     const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);
     // one LDS stage unless variant 2 (tools/kbench dgemm A/B: 1.2-1.4x on the dots.ocr linears,
     // profiles/r03_kbench_dgemm.log; bitwise equal results)

@@ -52,6 +52,7 @@ struct GemmBf16Args {
     // k-slices in the XCD's L2); 1 = one band across all N tiles (the round-3 order); -1 = the default
     // (DSOCR_GEMM_GROUP_M, else 8)
     int group_m = -1;
+    unsigned long long* stamps = nullptr;  // ping-pong kernel diagnostic build: per-wave segment cycle sums (tools/kbench)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
 int gemm_bf16_splits(int M, int N, int K);  // K slices that fill the chip (>= 8 K steps each)

@@ -591,19 +591,25 @@ static void case_dgemm(hipStream_t s) {
     struct Shape { int M, N, K; const char* what; };
     const Shape shapes[] = {{21316, 4608, 1536, "qkv"}, {21316, 1536, 1536, "proj"}, {21316, 8448, 1536, "fc1|fc3"},
                             {21316, 1536, 4224, "fc2"}};
-    const int vars[2] = {1, 2};
+    const int vars[2] = {1, getenv("KB_DGEMM_V") ? atoi(getenv("KB_DGEMM_V")) : 3};
     for (const Shape& sh : shapes) {
         uint16_t* A = rand_f16((size_t)sh.M * sh.K, 0.5f);
         uint16_t* W = rand_f16((size_t)sh.N * sh.K, 0.05f);
         float* bias = rand_f32(sh.N, 0.1f);
         uint16_t* C[2] = {(uint16_t*)dalloc((size_t)sh.M * sh.N * 2), (uint16_t*)dalloc((size_t)sh.M * sh.N * 2)};
+        const int acc_mode = getenv("KB_DGEMM_ACC") ? 1 : 0;  // C += A W^T + b (the residual linears), same start
+        if (acc_mode) {
+            uint16_t* c0 = rand_f16((size_t)sh.M * sh.N, 1.0f);
+            for (auto* c : C) CK(hipMemcpy(c, c0, (size_t)sh.M * sh.N * 2, hipMemcpyDeviceToDevice));
+            (void)hipFree(c0);
+        }
         std::vector<double> us[2];
         const double flop = 2.0 * sh.M * sh.N * sh.K;
         for (int round = 0; round < 3; ++round)
             for (int v = 0; v < 2; ++v) {
                 GemmBf16Args g;
                 g.M = sh.M; g.N = sh.N; g.K = sh.K; g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.bias = bias;
-                g.C = reinterpret_cast<float*>(C[v]); g.ldc = sh.N; g.out_bf16 = 1; g.variant = vars[v];
+                g.C = reinterpret_cast<float*>(C[v]); g.ldc = sh.N; g.out_bf16 = 1; g.variant = vars[v]; g.accumulate = acc_mode;
                 us[v].push_back(time_plain(4, [&] { launch_gemm_bf16(g, s); }, s));
             }
         std::vector<uint16_t> r1((size_t)sh.M * sh.N), r2(r1.size());
@@ -614,8 +620,32 @@ static void case_dgemm(hipStream_t s) {
             std::sort(us[v].begin(), us[v].end());
             printf("  v%d %8.1f us %5.0f TF", vars[v], us[v][1], flop / us[v][1] / 1e6);
         }
-        printf("  v1==v2 %s\n", memcmp(r1.data(), r2.data(), r1.size() * 2) ? "NO" : "yes");
+        printf("  v%d==v%d %s\n", vars[0], vars[1], memcmp(r1.data(), r2.data(), r1.size() * 2) ? "NO" : "yes");
         fflush(stdout);
+        if (getenv("KB_STAMPS")) {  // ping-pong diagnostic build: per-wave segment shares (row 0 = waves 0-3, row 1 = 4-7)
+            unsigned long long* st = (unsigned long long*)dalloc(64 * 8 * 12 * 8);
+            CK(hipMemset(st, 0, 64 * 8 * 12 * 8));
+            GemmBf16Args g;
+            g.M = sh.M; g.N = sh.N; g.K = sh.K; g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.bias = bias;
+            g.C = reinterpret_cast<float*>(C[1]); g.ldc = sh.N; g.out_bf16 = 1; g.variant = 3; g.stamps = st;
+            launch_gemm_bf16(g, s);
+            CK(hipStreamSynchronize(s));
+            std::vector<unsigned long long> h(64 * 8 * 12);
+            CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            const char* nm[8] = {"issue", "reads", "vm_r1", "bar1", "mfma", "vm_r0", "bar2", "total"};
+            for (int row = 0; row < 2; ++row) {
+                double sum[12] = {0};
+                for (int b = 0; b < 64; ++b)
+                    for (int w = row * 4; w < row * 4 + 4; ++w)
+                        for (int k = 0; k < 12; ++k) sum[k] += (double)h[((size_t)b * 8 + w) * 12 + k];
+                printf("  stamps row %d (cycles per k-tile):", row);
+                const double nk = (double)(sh.K / 32) * 64 * 4;
+                for (int k = 0; k < 8; ++k) printf(" %s %.0f", nm[k], sum[k] / nk);
+                printf(" | per block: prologue %.0f epilogue %.0f kernel %.0f cycles, %.2f us (%.2f GHz)\n", sum[8] / 256,
+                       sum[9] / 256, sum[10] / 256, sum[11] / 256 / 100.0, sum[10] / sum[11] / 10.0);
+            }
+            (void)hipFree(st);
+        }
         for (auto* c : C) (void)hipFree(c);
         (void)hipFree(A); (void)hipFree(W); (void)hipFree(bias);
     }
