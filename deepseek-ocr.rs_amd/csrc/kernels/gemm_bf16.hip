@@ -309,11 +309,12 @@ __device__ __forceinline__ void pp_issue(int p, const uint16_t* A, long lda, int
     }
 }
 
-// k-tile `ready` landed: the DMAs of the k-tiles after it (up to last, 4 per k-tile) stay in flight
-__device__ __forceinline__ void pp_wait(int ready, int last) {
-    const int ahead = last - ready;
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+// a k-tile landed: the n DMAs issued after its last one stay in flight (n is 0..8, even)
+__device__ __forceinline__ void pp_wait_n(int n) {
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -332,7 +333,9 @@ __device__ __forceinline__ void pp_barrier() {
         __builtin_amdgcn_sched_barrier(0);                                                      \
     }
 
-template <bool STAMPS>
+// LP: DMA pieces of k-tile t + 3 issued at the start of the load interval (the other 4 - LP one after every
+// few MFMAs of the multiply interval): the load interval has slack while the partner row multiplies
+template <bool STAMPS, int LP>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     extern __shared__ __attribute__((aligned(16))) uint16_t pp_smem[];
     const int lane = threadIdx.x & 63;
@@ -367,14 +370,18 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     for (int kt = 0; kt < 3 && kt < nk; ++kt)
 #pragma unroll
         for (int p = 0; p < 4; ++p) issue(p, kt);
-    pp_wait(0, min(2, nk - 1));
+    pp_wait_n(4 * min(2, nk - 1));
     pp_barrier();
     if (wr == 1) pp_barrier();
     unsigned long long seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sa = 0, sb = 0, sc = 0, sd = 0, se = 0, sf = 0, sh = 0, si = 0, s0 = 0;
     PP_STAMP(s0);
     for (int t = 0; t < nk; ++t) {
-        // load interval: this wave's fragments of k-tile t
+        // load interval: LP DMA pieces of k-tile t + 3, this wave's fragments of k-tile t
+        const bool more = t + 3 < nk;
         PP_STAMP(sa);
+        if (more)
+#pragma unroll
+            for (int p = 0; p < LP; ++p) issue(p, t + 3);
         PP_STAMP(sb);
         const uint16_t* As = pp_smem + (t & 3) * PP_STAGE;
         const uint16_t* Bs = As + PP_M * PP_K;
@@ -389,13 +396,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PP_STAMP(sc);
-        if (wr == 1 && t + 1 < nk) pp_wait(t + 1, min(t + 2, nk - 1));
+        // DMAs issued after k-tile t + 1's: k-tile t + 2's four, k-tile t + 3's first LP
+        if (wr == 1 && t + 1 < nk) pp_wait_n((t + 2 < nk ? 4 : 0) + (more ? LP : 0));
         PP_STAMP(sd);
         pp_barrier();
         PP_STAMP(se);
         // multiply interval, the DMAs of k-tile t + 3 one after every 4 MFMAs (their issue cost, ~100 cycles
         // each, runs in the MFMA shadow instead of lengthening the load interval)
-        const bool more = t + 3 < nk;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
@@ -404,14 +411,17 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfv[ks][j], acc[i][j], 0, 0, 0);
-                if (i & 1) {
-                    if (more) issue(ks * 2 + (i >> 1), t + 3);
+                // MFMA group m = ks * 4 + i (2 MFMAs each): the 4 - LP remaining pieces spread over the 8 groups
+                constexpr int MP = 4 - LP;
+                const int m = ks * 4 + i;
+                if (MP > 0 && (m % (8 / (MP > 0 ? MP : 1))) == (8 / (MP > 0 ? MP : 1)) - 1) {
+                    if (more) issue(LP + m / (8 / (MP > 0 ? MP : 1)), t + 3);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
         __builtin_amdgcn_s_setprio(0);
         PP_STAMP(sf);
-        if (wr == 0 && t + 1 < nk) pp_wait(t + 1, min(t + 3, nk - 1));
+        if (wr == 0 && t + 1 < nk) pp_wait_n((t + 2 < nk ? 4 : 0) + (more ? 4 : 0));
         PP_STAMP(sh);
         pp_barrier();
         PP_STAMP(si);
@@ -498,6 +508,13 @@ static bool gemm_pp_on() {
     static const int v = getenv("DSOCR_GEMM_PP") ? atoi(getenv("DSOCR_GEMM_PP")) : 1;
     return v != 0;
 }
+// DMA pieces per k-tile issued in the load interval (0 or 2; DSOCR_GEMM_PP_LP).  2 measured slower: a DMA
+// issued beside the load interval's ds_reads cost ~180 cycles vs ~25-65 between MFMAs (qkv 406 vs 313 us,
+// profiles/r05_dots/gemm_pp/kb_dgemm_lp{0,2}.log)
+static int gemm_pp_lpieces() {
+    static const int v = getenv("DSOCR_GEMM_PP_LP") ? atoi(getenv("DSOCR_GEMM_PP_LP")) : 0;
+    return v == 2 ? 2 : 0;
+}
 
 int gemm_bf16_splits(int M, int N, int K) {
     const int tiles = ((M + TB_M - 1) / TB_M) * ((N + TB_N - 1) / TB_N);
@@ -523,15 +540,23 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
         (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256))) {
         static bool attr = false;
         if (!attr) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess ||
-                hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess)
-                throw std::runtime_error("gemm_bf16_pp: cannot reserve 128 KiB of LDS");
+            const void* fns[4] = {reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 0>),
+                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 0>),
+                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 2>),
+                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 2>)};
+            for (const void* f : fns)
+                if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess)
+                    throw std::runtime_error("gemm_bf16_pp: cannot reserve 128 KiB of LDS");
             attr = true;
         }
-        if (g.stamps) hipLaunchKernelGGL(gemm_bf16_pp_kernel<true>, dim3((unsigned)pp_tiles), dim3(512), PP_LDS, s, g);
-        else hipLaunchKernelGGL(gemm_bf16_pp_kernel<false>, dim3((unsigned)pp_tiles), dim3(512), PP_LDS, s, g);
+        const dim3 grid((unsigned)pp_tiles), blk(512);
+        if (gemm_pp_lpieces() == 2) {
+            if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 2>), grid, blk, PP_LDS, s, g);
+            else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 2>), grid, blk, PP_LDS, s, g);
+        } else {
+            if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 0>), grid, blk, PP_LDS, s, g);
+            else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 0>), grid, blk, PP_LDS, s, g);
+        }
         return;
     }
     const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);
