@@ -3,7 +3,9 @@
 // vision/preprocess.rs (preprocess_image 103-145, smart_resize 244-279).
 #include "dots.hpp"
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -229,6 +231,21 @@ DotsVision::DotsVision(const std::string& config_path, const std::string& weight
         if (has("patch_embed.patchifier.proj.bias")) patch_b_ = upf("patch_embed.patchifier.proj.bias", D);
         patch_norm_ = upf("patch_embed.patchifier.norm.weight", D);
     }
+    {
+        const char* e = getenv("DSOCR_DOTS_SWIGLU_FUSE");
+        swiglu_fused_ = (!e || atoi(e) != 0) && I % 32 == 0 && D % 32 == 0;
+    }
+    // [fc1 | fc3] rows (or bias entries) -> per 32: fc1 32b..32b+31, fc3 32b..32b+31 (the fused epilogue's pairs)
+    auto pair32 = [&](std::vector<uint16_t>& v, size_t row) {
+        if (!swiglu_fused_) return;
+        std::vector<uint16_t> o(v.size());
+        for (int b = 0; b < I / 32; ++b)
+            for (int k = 0; k < 32; ++k) {
+                std::copy_n(v.begin() + (size_t)(32 * b + k) * row, row, o.begin() + (size_t)(64 * b + k) * row);
+                std::copy_n(v.begin() + (size_t)(I + 32 * b + k) * row, row, o.begin() + (size_t)(64 * b + 32 + k) * row);
+            }
+        v.swap(o);
+    };
     for (int l = 0; l < c_.layers; ++l) {
         Block b;
         const std::string bp = "blocks." + std::to_string(l) + ".";
@@ -239,6 +256,7 @@ DotsVision::DotsVision(const std::string& config_path, const std::string& weight
         std::vector<uint16_t> f13 = bits(bp + "mlp.fc1.weight", (size_t)I * D);
         std::vector<uint16_t> f3 = bits(bp + "mlp.fc3.weight", (size_t)I * D);
         f13.insert(f13.end(), f3.begin(), f3.end());
+        pair32(f13, (size_t)D);
         b.fc13 = up16(f13);
         b.fc2 = up16(bits(bp + "mlp.fc2.weight", (size_t)D * I));
         if (c_.use_bias) {
@@ -249,6 +267,7 @@ DotsVision::DotsVision(const std::string& config_path, const std::string& weight
             if (has(bp + "mlp.fc1.bias")) {
                 std::vector<uint16_t> a = bits(bp + "mlp.fc1.bias", I), c3 = bits(bp + "mlp.fc3.bias", I);
                 a.insert(a.end(), c3.begin(), c3.end());
+                pair32(a, 1);
                 std::vector<float> f(a.size());
                 for (size_t i = 0; i < a.size(); ++i) f[i] = bf16_to_f32(a[i]);
                 b.b_fc13 = (float*)dev_alloc(f.size() * 4);
@@ -277,10 +296,10 @@ DotsVision::~DotsVision() {
 }
 
 void DotsVision::gemm(const void* A, long lda, int M, int N, int K, const void* W, const float* bias, void* C, long ldc,
-                      int accumulate) {
+                      int accumulate, int swiglu) {
     GemmBf16Args g;
     g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.bias = bias;
-    g.C = reinterpret_cast<float*>(C); g.ldc = ldc; g.accumulate = accumulate; g.out_bf16 = 1;
+    g.C = reinterpret_cast<float*>(C); g.ldc = ldc; g.accumulate = accumulate; g.out_bf16 = 1; g.swiglu = swiglu;
     launch_gemm_bf16(g, stream_);
 }
 
@@ -331,7 +350,7 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
     float* CTX = attn_f32 ? (float*)ws("d_ctx", (size_t)N * D * 4) : nullptr;
     void* QKVr = attn_f32 ? nullptr : ws("d_qkvr", (size_t)N * 3 * D * 2);
     void* CTXb = ws("d_ctxb", (size_t)N * D * 2);
-    void* GU = ws("d_gu", (size_t)N * 2 * I * 2);
+    void* GU = swiglu_fused_ ? nullptr : ws("d_gu", (size_t)N * 2 * I * 2);
     void* HB = ws("d_h", (size_t)N * I * 2);
     void* PB = ws("d_pb", (size_t)N * patch_kp_ * 2);
     hipEvent_t ev[4];
@@ -388,8 +407,12 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
         }
         gemm(CTXb, D, (int)N, D, D, b.proj, b.b_proj, X, D, 1);
         launch_dots_rmsnorm(X, 0, N, D, b.n2, (float)c_.eps, XN, st);
-        gemm(XN, D, (int)N, 2 * I, D, b.fc13, b.b_fc13, GU, 2 * I, 0);
-        launch_dots_swiglu(GU, N, I, HB, st);
+        if (swiglu_fused_) {  // h straight from the GEMM epilogue (bitwise the same as the two launches)
+            gemm(XN, D, (int)N, 2 * I, D, b.fc13, b.b_fc13, HB, I, 0, 1);
+        } else {
+            gemm(XN, D, (int)N, 2 * I, D, b.fc13, b.b_fc13, GU, 2 * I, 0);
+            launch_dots_swiglu(GU, N, I, HB, st);
+        }
         gemm(HB, I, (int)N, D, I, b.fc2, b.b_fc2, X, D, 1);
     }
     HIP_CHECK(hipEventRecord(ev[2], st));

@@ -64,14 +64,16 @@ class DotsVision {
         float* n2 = nullptr;
         void* qkv = nullptr;   // bf16 [3D][D]
         void* proj = nullptr;  // bf16 [D][D]
-        void* fc13 = nullptr;  // bf16 [2I][D] = [fc1 | fc3]
+        void* fc13 = nullptr;  // bf16 [2I][D] = [fc1 | fc3], or per 32 rows [fc1 32 | fc3 32] when swiglu_fused_
         void* fc2 = nullptr;   // bf16 [D][I]
         float *b_qkv = nullptr, *b_proj = nullptr, *b_fc13 = nullptr, *b_fc2 = nullptr;
     };
     void* ws(const std::string& name, size_t bytes);
     void* dev_alloc(size_t bytes);
     void gemm(const void* A, long lda, int M, int N, int K, const void* W, const float* bias, void* C, long ldc,
-              int accumulate);
+              int accumulate, int swiglu = 0);
+    // fc1|fc3 GEMM with the SwiGLU in its epilogue (DSOCR_DOTS_SWIGLU_FUSE, default on; needs I % 32, D % 32)
+    bool swiglu_fused_ = false;
 
     DotsConfig c_;
     int device_ = 0;

@@ -439,6 +439,43 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     // 8 lanes) -- the 2-byte scattered stores took ~55k cycles per block, a third of the kernel
     const int half = lane >> 5, l32 = lane & 31;
     uint16_t* ep = pp_smem + wave * (128 * 64);
+    if (g.swiglu) {
+        // SwiGLU pair: this wave's 64 columns are fc1 (j = 0) and fc3 (j = 1) of the same 32 h columns, lane
+        // for lane; h = rnd(rnd(g / rnd(1 + rnd(exp(-g)))) * u) as dots_swiglu8_kernel, g and u each
+        // rnd(rnd(acc) + b) as the separate GEMM stored them.  Staged as [128][32] bf16 (64-byte rows), stored
+        // as 16-byte row chunks (4 lanes per row)
+        if (n0 + wc * 64 >= g.N) return;
+        const int gc = n0 + wc * 64 + l32, uc = gc + 32;
+        const float bg = g.bias ? g.bias[gc] : 0.f, bu = g.bias ? g.bias[uc] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                float gv = rnd_bf16(acc[i][0][r]), uv = rnd_bf16(acc[i][1][r]);
+                if (g.bias) {
+                    gv = rnd_bf16(gv + bg);
+                    uv = rnd_bf16(uv + bu);
+                }
+                const float ex = rnd_bf16(expf(-gv));
+                const float sv = rnd_bf16(gv / rnd_bf16(1.0f + ex));
+                const __bf16 hv = (__bf16)(sv * uv);
+                ep[row * 32 + l32] = *reinterpret_cast<const uint16_t*>(&hv);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        __bf16* H = reinterpret_cast<__bf16*>(g.C);
+        const int hc = (n0 + wc * 64) / 2;
+#pragma unroll 4
+        for (int it = 0; it < 8; ++it) {
+            const int row = it * 16 + (lane >> 2), ch = lane & 3;
+            const int grow = m0 + wr * 128 + row;
+            const u32x4 q = *reinterpret_cast<const u32x4*>(ep + row * 32 + ch * 8);
+            if (grow < g.M) *reinterpret_cast<u32x4*>(H + (long)grow * g.ldc + hc + ch * 8) = q;
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int col = n0 + wc * 64 + j * 32 + l32;
@@ -535,9 +572,12 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
     g.group_m = gemm_group_m(g.group_m);
     // ping-pong 256 x 256 kernel: variant 3, or by default for one-slice problems of >= 256 such tiles
     const long pp_tiles = (long)((g.M + PP_M - 1) / PP_M) * ((g.N + PP_N - 1) / PP_N);
-    if (g.splits == 1 && g.K % PP_K == 0 && g.out_bf16 && !g.act && !g.c_rows && g.ldc % 8 == 0 &&
-        (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
-        (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256))) {
+    if (g.swiglu && (g.splits != 1 || g.K % PP_K || !g.out_bf16 || g.act || g.c_rows || g.accumulate || g.N % 64 ||
+                     g.ldc % 8 || (reinterpret_cast<uintptr_t>(g.C) & 15)))
+        throw std::runtime_error("EINVAL: the SwiGLU-pair GEMM needs one K slice, K % 32, N % 64, bf16 out, 16-byte rows");
+    if (g.swiglu || (g.splits == 1 && g.K % PP_K == 0 && g.out_bf16 && !g.act && !g.c_rows && g.ldc % 8 == 0 &&
+                     (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
+                     (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256)))) {
         static bool attr = false;
         if (!attr) {
             const void* fns[4] = {reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 0>),

@@ -52,6 +52,9 @@ struct GemmBf16Args {
     // k-slices in the XCD's L2); 1 = one band across all N tiles (the round-3 order); -1 = the default
     // (DSOCR_GEMM_GROUP_M, else 8)
     int group_m = -1;
+    // SwiGLU pair epilogue (dots.ocr fc1|fc3, ping-pong kernel only): W rows interleaved per 32 (fc1 rows
+    // 32b..32b+31, then fc3 rows 32b..32b+31), N = 2I; C is bf16 [M][ldc] of h = rnd(silu(g) * u), I columns
+    int swiglu = 0;
     unsigned long long* stamps = nullptr;  // ping-pong kernel diagnostic build: per-wave segment cycle sums (tools/kbench)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);

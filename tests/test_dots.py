@@ -179,3 +179,30 @@ def test_dots_one_block_full_width_tight(gpu, tmp_path):
     mism = float(np.mean(got != ref))
     print(json.dumps({"one_block_rel_err": err, "values_not_bit_equal": mism}))
     assert tuple(grid) == tuple(g) and err <= DOTS_ONE_BLOCK_REL, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["tiny", "one_block"])
+def test_dots_swiglu_fused_gemm_bitwise(gpu, tmp_path, monkeypatch, which):
+    """The fc1|fc3 GEMM with the SwiGLU in its epilogue (interleaved weight rows, DSOCR_DOTS_SWIGLU_FUSE=1,
+    the default) against the separate GEMM + dots_swiglu8 launch: the tower outputs are bitwise equal."""
+    from dsocr.dots import DotsVision
+    from dsocr.synth import synthetic_page
+    if which == "tiny":
+        cfg, img, seed = TINY, synthetic_page(3, 280, 224), 11
+    else:
+        full = json.load(open(FULL))
+        full["vision_config"]["num_hidden_layers"] = 1
+        path = tmp_path / "dots-1block.json"
+        path.write_text(json.dumps(full))
+        cfg, img, seed = str(path), synthetic_page(0, 448, 448), 3
+    outs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("DSOCR_DOTS_SWIGLU_FUSE", fuse)
+        eng = DotsVision(cfg, synthetic_seed=seed)
+        try:
+            outs.append(eng.embed(img)[0])
+        finally:
+            eng.close()
+    assert outs[0].shape == outs[1].shape
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32)), float(np.mean(outs[0] != outs[1]))
