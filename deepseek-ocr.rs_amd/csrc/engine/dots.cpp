@@ -234,6 +234,8 @@ DotsVision::DotsVision(const std::string& config_path, const std::string& weight
     {
         const char* e = getenv("DSOCR_DOTS_SWIGLU_FUSE");
         swiglu_fused_ = (!e || atoi(e) != 0) && I % 32 == 0 && D % 32 == 0;
+        const char* r = getenv("DSOCR_DOTS_ROPE_FUSE");
+        rope_fused_ = (!r || atoi(r) != 0) && D % c_.heads == 0 && D / c_.heads == 128 && D % 128 == 0 && D % 32 == 0;
     }
     // [fc1 | fc3] rows (or bias entries) -> per 32: fc1 32b..32b+31, fc3 32b..32b+31 (the fused epilogue's pairs)
     auto pair32 = [&](std::vector<uint16_t>& v, size_t row) {
@@ -348,7 +350,7 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
     const bool attn_f32 = getenv("DSOCR_DOTS_ATTN") && std::string(getenv("DSOCR_DOTS_ATTN")) == "f32";
     float* QKVf = attn_f32 ? (float*)ws("d_qkvf", (size_t)N * 3 * D * 4) : nullptr;
     float* CTX = attn_f32 ? (float*)ws("d_ctx", (size_t)N * D * 4) : nullptr;
-    void* QKVr = attn_f32 ? nullptr : ws("d_qkvr", (size_t)N * 3 * D * 2);
+    void* QKVr = (attn_f32 || rope_fused_) ? nullptr : ws("d_qkvr", (size_t)N * 3 * D * 2);
     void* CTXb = ws("d_ctxb", (size_t)N * D * 2);
     void* GU = swiglu_fused_ ? nullptr : ws("d_gu", (size_t)N * 2 * I * 2);
     void* HB = ws("d_h", (size_t)N * I * 2);
@@ -369,7 +371,17 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
         const Block& b = blocks_[l];
         // DotsVisionBlock::forward (305-315) / VisionAttention::forward (364-431)
         launch_dots_rmsnorm(X, 0, N, D, b.n1, (float)c_.eps, XN, st);
-        gemm(XN, D, (int)N, 3 * D, D, b.qkv, b.b_qkv, QKV, 3 * D, 0);
+        // the rotary of q / k in the q|k|v GEMM's epilogue (rope_fused_) or by dots_rope8 into QKVr below
+        const bool rope_in_gemm = rope_fused_ && !attn_f32;
+        if (rope_in_gemm) {
+            GemmBf16Args g;
+            g.M = (int)N; g.N = 3 * D; g.K = D; g.A = XN; g.lda = D; g.W = b.qkv; g.ldw = D; g.bias = b.b_qkv;
+            g.C = reinterpret_cast<float*>(QKV); g.ldc = 3 * D; g.out_bf16 = 1;
+            g.rope_cos = d_cos; g.rope_sin = d_sin; g.rope_cols = 2 * D;
+            launch_gemm_bf16(g, st);
+        } else {
+            gemm(XN, D, (int)N, 3 * D, D, b.qkv, b.b_qkv, QKV, 3 * D, 0);
+        }
         const bool timed = l < time_layers;
         const float scale = (float)(1.0 / std::sqrt((double)hd));
         if (attn_f32) {
@@ -389,9 +401,10 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
             // bf16 matrix cores with the same f32 math (attention_bf16.hip): rotated q / k stay bf16
             // (exactly the reference's rounding), the context is written as the bf16 tensor it becomes
             // rotated q / k into QKVr; v is read where the qkv GEMM wrote it
-            launch_dots_rope_qk(QKV, N, H, hd, d_cos, d_sin, QKVr, st);
+            if (!rope_in_gemm) launch_dots_rope_qk(QKV, N, H, hd, d_cos, d_sin, QKVr, st);
+            const uint16_t* QK = (const uint16_t*)(rope_in_gemm ? QKV : QKVr);
             AttnBf16Args a;
-            a.q = (const uint16_t*)QKVr; a.k = (const uint16_t*)QKVr + D; a.v = (const uint16_t*)QKV + 2 * D;
+            a.q = QK; a.k = QK + D; a.v = (const uint16_t*)QKV + 2 * D;
             a.q_rs = a.k_rs = a.v_rs = 3L * D; a.q_hs = a.k_hs = a.v_hs = hd;
             a.o = CTXb; a.o_rs = D; a.o_hs = hd; a.o_bf16 = 1;
             a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;

@@ -74,6 +74,8 @@ class DotsVision {
               int accumulate, int swiglu = 0);
     // fc1|fc3 GEMM with the SwiGLU in its epilogue (DSOCR_DOTS_SWIGLU_FUSE, default on; needs I % 32, D % 32)
     bool swiglu_fused_ = false;
+    // q / k rotary in the q|k|v GEMM's epilogue (DSOCR_DOTS_ROPE_FUSE, default on; needs 128-dim heads)
+    bool rope_fused_ = false;
 
     DotsConfig c_;
     int device_ = 0;

@@ -335,6 +335,15 @@ __device__ __forceinline__ void pp_barrier() {
 
 // LP: DMA pieces of k-tile t + 3 issued at the start of the load interval (the other 4 - LP one after every
 // few MFMAs of the multiply interval): the load interval has slack while the partner row multiplies
+// rotary element as dots_rope8_kernel: x cos + rot sin, no contraction (rot = -partner on the low half)
+__device__ __forceinline__ float pp_rope(float x, float pt, float cs, float sn, bool lo) {
+#pragma clang fp contract(off)
+    const float rot = lo ? -pt : pt;
+    const float a = x * cs;
+    const float b = rot * sn;
+    return a + b;
+}
+
 template <bool STAMPS, int LP>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     extern __shared__ __attribute__((aligned(16))) uint16_t pp_smem[];
@@ -497,6 +506,43 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     __bf16* C = reinterpret_cast<__bf16*>(g.C);
+    if (g.rope_cos && n0 < g.rope_cols) {
+        // q / k tile (two heads of 128): the partner half-head (dims d +- 64) is wave wc ^ 1's LDS region, same
+        // rows and chunk; every wave wrote its region before this barrier
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const uint16_t* pe = pp_smem + (wr * 4 + (wc ^ 1)) * (128 * 64);
+        const int d0 = (wc & 1) * 64;
+#pragma unroll 2
+        for (int it = 0; it < 16; ++it) {
+            const int row = it * 8 + (lane >> 3), ch = lane & 7;
+            const int off = row * 64 + ((ch ^ (((row >> 2) & 1) << 2)) << 3);
+            const u32x4 q = *reinterpret_cast<const u32x4*>(ep + off);
+            const u32x4 pq = *reinterpret_cast<const u32x4*>(pe + off);
+            const int grow = m0 + wr * 128 + row;
+            if (grow >= g.M) continue;
+            const float* ct = g.rope_cos + (long)grow * 128 + d0 + ch * 8;
+            const float* st = g.rope_sin + (long)grow * 128 + d0 + ch * 8;
+            const float4 c0 = *reinterpret_cast<const float4*>(ct), c1 = *reinterpret_cast<const float4*>(ct + 4);
+            const float4 s0 = *reinterpret_cast<const float4*>(st), s1 = *reinterpret_cast<const float4*>(st + 4);
+            const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const uint16_t* xv = reinterpret_cast<const uint16_t*>(&q);
+            const uint16_t* pv = reinterpret_cast<const uint16_t*>(&pq);
+            u32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a0 = pp_rope(__uint_as_float((uint32_t)xv[2 * e] << 16), __uint_as_float((uint32_t)pv[2 * e] << 16),
+                                         cs[2 * e], sn[2 * e], d0 == 0);
+                const float a1 = pp_rope(__uint_as_float((uint32_t)xv[2 * e + 1] << 16),
+                                         __uint_as_float((uint32_t)pv[2 * e + 1] << 16), cs[2 * e + 1], sn[2 * e + 1], d0 == 0);
+                const __bf16 h0 = (__bf16)a0, h1 = (__bf16)a1;
+                o[e] = (uint32_t)*reinterpret_cast<const uint16_t*>(&h0) | ((uint32_t)*reinterpret_cast<const uint16_t*>(&h1) << 16);
+            }
+            *reinterpret_cast<u32x4*>(C + (long)grow * g.ldc + n0 + wc * 64 + ch * 8) = o;
+        }
+        return;
+    }
 #pragma unroll 4
     for (int it = 0; it < 16; ++it) {
         const int row = it * 8 + (lane >> 3), ch = lane & 7;
@@ -575,7 +621,12 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
     if (g.swiglu && (g.splits != 1 || g.K % PP_K || !g.out_bf16 || g.act || g.c_rows || g.accumulate || g.N % 64 ||
                      g.ldc % 8 || (reinterpret_cast<uintptr_t>(g.C) & 15)))
         throw std::runtime_error("EINVAL: the SwiGLU-pair GEMM needs one K slice, K % 32, N % 64, bf16 out, 16-byte rows");
-    if (g.swiglu || (g.splits == 1 && g.K % PP_K == 0 && g.out_bf16 && !g.act && !g.c_rows && g.ldc % 8 == 0 &&
+    if (g.rope_cos && (g.swiglu || g.splits != 1 || g.K % PP_K || !g.out_bf16 || g.act || g.c_rows || g.accumulate ||
+                       g.rope_cols % PP_N || g.rope_cols > g.N || g.ldc % 8 || (reinterpret_cast<uintptr_t>(g.C) & 15) ||
+                       !g.rope_sin))
+        throw std::runtime_error("EINVAL: the rotary GEMM epilogue needs one K slice, K % 32, bf16 out, q|k columns "
+                                 "in whole 256-column tiles, 16-byte rows");
+    if (g.swiglu || g.rope_cos || (g.splits == 1 && g.K % PP_K == 0 && g.out_bf16 && !g.act && !g.c_rows && g.ldc % 8 == 0 &&
                      (reinterpret_cast<uintptr_t>(g.C) & 15) == 0 &&
                      (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256)))) {
         static bool attr = false;

@@ -55,6 +55,12 @@ struct GemmBf16Args {
     // SwiGLU pair epilogue (dots.ocr fc1|fc3, ping-pong kernel only): W rows interleaved per 32 (fc1 rows
     // 32b..32b+31, then fc3 rows 32b..32b+31), N = 2I; C is bf16 [M][ldc] of h = rnd(silu(g) * u), I columns
     int swiglu = 0;
+    // 2-D rotary of the q / k columns in the epilogue (dots.ocr q|k|v GEMM, ping-pong kernel only): columns
+    // below rope_cols (a multiple of 256) are heads of 128 dims rotated with the [M][128] f32 cos / sin tables
+    // exactly as dots_rope8_kernel does
+    const float* rope_cos = nullptr;
+    const float* rope_sin = nullptr;
+    int rope_cols = 0;
     unsigned long long* stamps = nullptr;  // ping-pong kernel diagnostic build: per-wave segment cycle sums (tools/kbench)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);

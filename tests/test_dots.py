@@ -184,8 +184,10 @@ def test_dots_one_block_full_width_tight(gpu, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("which", ["tiny", "one_block"])
 def test_dots_swiglu_fused_gemm_bitwise(gpu, tmp_path, monkeypatch, which):
-    """The fc1|fc3 GEMM with the SwiGLU in its epilogue (interleaved weight rows, DSOCR_DOTS_SWIGLU_FUSE=1,
-    the default) against the separate GEMM + dots_swiglu8 launch: the tower outputs are bitwise equal."""
+    """The fc1|fc3 GEMM with the SwiGLU in its epilogue (interleaved weight rows, DSOCR_DOTS_SWIGLU_FUSE=1)
+    and the q|k|v GEMM with the rotary in its epilogue (DSOCR_DOTS_ROPE_FUSE=1; 128-dim heads, so the
+    one-block case), both defaults, against the separate GEMM + dots_swiglu8 / dots_rope8 launches: the
+    tower outputs are bitwise equal."""
     from dsocr.dots import DotsVision
     from dsocr.synth import synthetic_page
     if which == "tiny":
@@ -199,6 +201,7 @@ def test_dots_swiglu_fused_gemm_bitwise(gpu, tmp_path, monkeypatch, which):
     outs = []
     for fuse in ("0", "1"):
         monkeypatch.setenv("DSOCR_DOTS_SWIGLU_FUSE", fuse)
+        monkeypatch.setenv("DSOCR_DOTS_ROPE_FUSE", fuse)
         eng = DotsVision(cfg, synthetic_seed=seed)
         try:
             outs.append(eng.embed(img)[0])
