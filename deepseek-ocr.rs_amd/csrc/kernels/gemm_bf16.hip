@@ -390,7 +390,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
         PP_STAMP(sa);
         if (more)
 #pragma unroll
-            for (int p = 0; p < LP; ++p) issue(p, t + 3);
+            for (int p = 0; p < (LP == 2 ? 2 : 0); ++p) issue(p, t + 3);
         PP_STAMP(sb);
         const uint16_t* As = pp_smem + (t & 3) * PP_STAGE;
         const uint16_t* Bs = As + PP_M * PP_K;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PP_STAMP(sc);
         // DMAs issued after k-tile t + 1's: k-tile t + 2's four, k-tile t + 3's first LP
-        if (wr == 1 && t + 1 < nk) pp_wait_n((t + 2 < nk ? 4 : 0) + (more ? LP : 0));
+        if (wr == 1 && t + 1 < nk) pp_wait_n((t + 2 < nk ? 4 : 0) + (more ? (LP == 2 ? 2 : 0) : 0));
         PP_STAMP(sd);
         pp_barrier();
         PP_STAMP(se);
@@ -421,10 +421,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfv[ks][j], acc[i][j], 0, 0, 0);
                 // MFMA group m = ks * 4 + i (2 MFMAs each): the 4 - LP remaining pieces spread over the 8 groups
-                constexpr int MP = 4 - LP;
+                // (LP 0: after groups 1, 3, 5, 7; LP 1: after groups 0, 2, 4, 6, so MFMAs follow the last DMA;
+                // LP 2: pieces 2, 3 after groups 3, 7)
                 const int m = ks * 4 + i;
-                if (MP > 0 && (m % (8 / (MP > 0 ? MP : 1))) == (8 / (MP > 0 ? MP : 1)) - 1) {
-                    if (more) issue(LP + m / (8 / (MP > 0 ? MP : 1)), t + 3);
+                const int per = LP == 2 ? 4 : 2, ph = LP == 1 ? 0 : per - 1;
+                if (m % per == ph) {
+                    if (more) issue((LP == 2 ? 2 : 0) + m / per, t + 3);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -596,7 +598,7 @@ static bool gemm_pp_on() {
 // profiles/r05_dots/gemm_pp/kb_dgemm_lp{0,2}.log)
 static int gemm_pp_lpieces() {
     static const int v = getenv("DSOCR_GEMM_PP_LP") ? atoi(getenv("DSOCR_GEMM_PP_LP")) : 0;
-    return v == 2 ? 2 : 0;
+    return (v == 1 || v == 2) ? v : 0;
 }
 
 int gemm_bf16_splits(int M, int N, int K) {
@@ -631,8 +633,10 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
                      (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256)))) {
         static bool attr = false;
         if (!attr) {
-            const void* fns[4] = {reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 0>),
+            const void* fns[6] = {reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 0>),
                                   reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 0>),
+                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 1>),
+                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 1>),
                                   reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 2>),
                                   reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 2>)};
             for (const void* f : fns)
@@ -641,7 +645,10 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
             attr = true;
         }
         const dim3 grid((unsigned)pp_tiles), blk(512);
-        if (gemm_pp_lpieces() == 2) {
+        if (gemm_pp_lpieces() == 1) {
+            if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 1>), grid, blk, PP_LDS, s, g);
+            else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 1>), grid, blk, PP_LDS, s, g);
+        } else if (gemm_pp_lpieces() == 2) {
             if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 2>), grid, blk, PP_LDS, s, g);
             else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 2>), grid, blk, PP_LDS, s, g);
         } else {
