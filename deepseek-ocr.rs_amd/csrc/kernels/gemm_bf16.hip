@@ -412,7 +412,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
         PP_STAMP(se);
         // multiply interval, the DMAs of k-tile t + 3 one after every 4 MFMAs (their issue cost, ~100 cycles
         // each, runs in the MFMA shadow instead of lengthening the load interval)
-        __builtin_amdgcn_s_setprio(1);
+        if (g.pp_prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -643,6 +643,10 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
                 if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess)
                     throw std::runtime_error("gemm_bf16_pp: cannot reserve 128 KiB of LDS");
             attr = true;
+        }
+        if (g.pp_prio < 0) {
+            static const int pr = getenv("DSOCR_GEMM_PP_PRIO") ? atoi(getenv("DSOCR_GEMM_PP_PRIO")) : 1;
+            g.pp_prio = pr;
         }
         const dim3 grid((unsigned)pp_tiles), blk(512);
         if (gemm_pp_lpieces() == 1) {

@@ -61,6 +61,7 @@ struct GemmBf16Args {
     const float* rope_cos = nullptr;
     const float* rope_sin = nullptr;
     int rope_cols = 0;
+    int pp_prio = -1;  // ping-pong kernel: raised wave priority over the MFMA interval (1) or not (0); -1 = DSOCR_GEMM_PP_PRIO, else 1
     unsigned long long* stamps = nullptr;  // ping-pong kernel diagnostic build: per-wave segment cycle sums (tools/kbench)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
