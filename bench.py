@@ -146,31 +146,49 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
     allowed = len(os.sched_getaffinity(0))
     threads = int(os.environ.get("OMP_NUM_THREADS") or allowed)
     cfg = json.load(open(dsocr.FULL_CONFIG))
+    # the same page at two thread counts: the job's share (OMP_NUM_THREADS, 16 on the GPU box) and every CPU the
+    # process may run on (allowed_cpus), each timed whole; the first is `value`, the second `cores_all`
+    counts = [threads] + ([allowed] if allowed != threads and not os.environ.get("DSOCR_CPU_ONE_COUNT") else [])
     t = time.time()
     cv = cpu_ref.CpuVision(cfg, Weights(seed=0, dtype="f16"), threads=threads)
     log(f"[cpu] C++ vision tower loaded in {time.time() - t:.1f}s ({threads} threads)")
-    t0 = time.time()
-    emb, _ = cv.embeddings(pages[0])
-    vision_s = time.time() - t0
-    vis_ms = dict(cv.last_ms)
+    vis = []
+    for n in counts:
+        cpu_ref.set_threads(n)
+        t0 = time.time()
+        emb, _ = cv.embeddings(pages[0])
+        vis.append((time.time() - t0, dict(cv.last_ms)))
     del cv
     t = time.time()
+    cpu_ref.set_threads(threads)
     cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
     log(f"[cpu] C++ decoder loaded in {time.time() - t:.1f}s ({threads} threads)")
-    ids, ms = cr.generate(np.asarray(tok_ids, np.int64), np.asarray(mask, np.uint8), emb, max_new, ngram=20)
+    runs = []
+    for i, n in enumerate(counts):
+        cpu_ref.set_threads(n)
+        ids, ms = cr.generate(np.asarray(tok_ids, np.int64), np.asarray(mask, np.uint8), emb, max_new, ngram=20)
+        vision_s, vis_ms = vis[i]
+        prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3
+        page_s = vision_s + prefill_s + decode_s
+        log(f"[cpu] {n} threads: vision {vision_s:.2f}s prefill {prefill_s:.2f}s decode {decode_s:.2f}s")
+        runs.append({"value": 1.0 / page_s, "unit": "pages/s", "cores": n,
+                     "decode_tok_s": (max_new - 1) / decode_s,
+                     "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
+                     "vision_ms": {k: round(v, 1) for k, v in vis_ms.items()},
+                     "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (C++, incl. numpy preprocessing) + "
+                               f"prefill {prefill_s:.2f}s ({len(tok_ids)} tok, C++) + {max_new - 1} decode steps "
+                               f"{decode_s:.2f}s (C++, {decode_s / max(1, max_new - 1) * 1e3:.1f} ms/step), {n} threads; "
+                               f"first ids {ids[:4]}"})
     cr.close()
-    prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3
-    page_s = vision_s + prefill_s + decode_s
-    return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads, "kind": "cpp",
-            "port": "oracle/cpu_ref.cpp: C++ / OpenMP restatement of the whole page path (vision tower + decoder, "
-                    "AVX-512 micro-kernels, f32 math); the Rust reference cannot be built here",
-            "decode_tok_s": (max_new - 1) / decode_s, "host_cpus": os.cpu_count(),
-            "allowed_cpus": allowed, "cpu_model": cpu_model(),
-            "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
-            "vision_ms": {k: round(v, 1) for k, v in vis_ms.items()},
-            "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (C++, incl. numpy preprocessing) + prefill "
-                      f"{prefill_s:.2f}s ({len(tok_ids)} tok, C++) + {max_new - 1} decode steps {decode_s:.2f}s (C++, "
-                      f"{decode_s / max(1, max_new - 1) * 1e3:.1f} ms/step), {threads} threads; first ids {ids[:4]}"}
+    out = dict(runs[0])
+    out.update({"kind": "cpp",
+                "port": "oracle/cpu_ref.cpp: C++ / OpenMP restatement of the whole page path (vision tower + decoder, "
+                        "AVX-512 micro-kernels, f32 math); the Rust reference cannot be built here",
+                "host_cpus": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model(),
+                "threads_note": "value: the job's CPU share (OMP_NUM_THREADS); cores_all: every allowed CPU"})
+    if len(runs) > 1:
+        out["cores_all"] = runs[1]
+    return out
 
 
 SPAN_HZ = 100e6  # s_memrealtime
@@ -305,14 +323,18 @@ def run_dots(args, rank, world, local, dist):
     gemm_f, attn_f, other_f = dots_flops(cfg, N)
     attn_layer_ms = tm["attention_ms"] / 4
     attn_tf = (attn_f / cfg["num_hidden_layers"]) / (attn_layer_ms * 1e-3) / 1e12
-    planes = 3 if os.environ.get("DSOCR_DOTS_PV_PLANES") == "3" else 2
+    planes = 2 if os.environ.get("DSOCR_DOTS_PV_PLANES") == "2" else 3
     issue = (1 + planes) / 2.0
     page_ms = elapsed / (args.steps * ppg) * 1e3
     return {
         "metric": "pages/sec, dots.ocr bf16 vision tower, 2048px page (BASELINE configs[3])",
         "value": round(value, 4), "unit": "pages/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16 (reference semantics: bf16 tensors between ops; f32 attention math)",
+        "vs_baseline": None,
+        "dtype": ("bf16 (reference semantics: bf16 tensors between ops; f32 attention math, P.V with f32 P: "
+                  "exact 3-plane)" if planes == 3 else
+                  "bf16 (bf16 tensors between ops; f32 scores/softmax; P.V on 2 bf16 planes of P, 16 significant "
+                  "bits: DSOCR_DOTS_PV_PLANES=2, narrower than the reference)"),
         "data": "synthetic document pages + seeded synthetic weights (no checkpoint offline)",
         "config": {"workload": f"configs[3]: dots.ocr vision tower, {size}x{size} page (resized to "
                                f"{grid[1] * 14}x{grid[2] * 14}), grid {grid[1]}x{grid[2]}, "
@@ -321,8 +343,8 @@ def run_dots(args, rank, world, local, dist):
         "stage_ms": {"page_ms": round(page_ms, 2), "blocks_ms": round(tm["blocks_ms"], 2),
                      "patch_ms": round(tm["patch_ms"], 2), "merger_ms": round(tm["merger_ms"], 2)},
         # achieved = the reference's attention FLOPs (QK^T + P.V, f32 math) / the kernel's time; the kernel
-        # runs them on the bf16 matrix cores (1 exact pass for QK^T; P.V on 2 bf16 planes of P — 16 significant
-        # bits, DSOCR_DOTS_PV_PLANES=3 for the exact 3), so the peak is the dense bf16 MFMA rate and the issued
+        # runs them on the bf16 matrix cores (1 exact pass for QK^T; P.V on 3 bf16 planes of P — exact, the
+        # reference's f32 P; DSOCR_DOTS_PV_PLANES=2 opts into 16 significant bits), so the peak is the dense bf16 MFMA rate and the issued
         # MFMA work is (1 + planes) / 2 x the algorithmic FLOPs
         "roofline": {"bound": "mfma", "achieved": round(attn_tf, 2), "peak": 2500.0, "unit": "TFLOP/s",
                      "frac": round(attn_tf / 2500.0, 4), "traffic": pmc_traffic("attention_bf16_tr_kernel")[0],

@@ -136,11 +136,12 @@ DotsPatches dots_preprocess(const DotsConfig& c, const uint8_t* rgb, int w, int 
 }
 
 namespace {
-// DSOCR_DOTS_PV_PLANES (A/B switch, read per layer): the attention's P.V in 2 bf16 planes of p (default: 16
-// significant bits, <= 2^-17 relative per probability, 2^-8 below the block output's bf16 rounding) or 3 (exact)
+// DSOCR_DOTS_PV_PLANES (A/B switch, read per layer): the attention's P.V on 3 bf16 planes of p (default: every
+// product exact in the f32 accumulator, the reference's f32 probs.matmul(v), dots_vit.rs:402-409 / 584-589) or 2
+// (opt-in: 16 significant bits of p, <= 2^-17 relative per probability, 2^-8 below the block output's bf16 rounding)
 int dots_pv_planes() {
     const char* e = getenv("DSOCR_DOTS_PV_PLANES");
-    return (e && atoi(e) == 3) ? 3 : 2;
+    return (e && atoi(e) == 2) ? 2 : 3;
 }
 std::string read_text(const std::string& p) {
     std::ifstream f(p);

@@ -1026,12 +1026,6 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     a.h = wsf("s_ehh", (size_t)TK * I);
     a.grp = wsi("s_grp", moe_grp_ints(E, B, K));
     a.route_cnt = wsi("s_route_cnt", 16);
-    if (B == 1) {  // the router inside the one-token gate/up launch: tagged logits, tag = decode position * 64 + layer
-        a.lg_tag = reinterpret_cast<unsigned long long*>(wsi("s_lgtag", 128));
-        a.tag_pos = wsi("s_kvpos", B);
-        a.layer = l;
-        a.err = wsi("s_err", 4);
-    }
     if (B >= 3 && B <= 8) {  // matrix-core grouped kernels: down partials + tickets
         a.dn_part = wsf("s_dnpart", moe_down_mm_part_floats(E, B, K, I, a.Is, H));
         a.dn_tick = wsi("s_dntick", (size_t)H / 64 + 1);  // one ticket per 64-row tile
@@ -1582,8 +1576,6 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
-    // the one-token gate/up's tagged router logits: no tag of an earlier generate may match this one's
-    HIP_CHECK(hipMemsetAsync(wsi("s_lgtag", 128), 0xff, sizeof(int) * 128, st));
     const int QKVN = layers_[0].qkv.N;
     float* SX = wsf("s_x", (size_t)B * H);
     float* SXN = wsf("s_xn", (size_t)B * H);
@@ -1822,7 +1814,6 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
-    HIP_CHECK(hipMemsetAsync(wsi("s_lgtag", 128), 0xff, sizeof(int) * 128, st));  // the dry step's tags
     if (chain_active_) {  // the dry step's stamps must not join step 1's: clear the regions and the marks
         HIP_CHECK(hipMemsetAsync(span_chain_, 0, (size_t)L.layers * SPAN_KINDS_CHAIN * SPAN_SLOTS * 16, st));
         HIP_CHECK(hipMemsetAsync(span_tmark_, 0, 16, st));
@@ -1993,7 +1984,16 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
     //    whatever startup the chained dispatch hides).
     auto timed = [&](KernelProfile& kp, int n, const std::function<void(int)>& body) {
         body(0);  // warm (code objects, TLB) and every workspace allocated before capture
-        std::vector<hipEvent_t> ev(2 * n);
+        // the events are destroyed on every exit, the EINTERNAL / HIP-error throws below included
+        struct EventSet {
+            std::vector<hipEvent_t> v;
+            ~EventSet() {
+                for (auto& e : v)
+                    if (e) (void)hipEventDestroy(e);
+            }
+        } evs;
+        evs.v.assign(2 * n, nullptr);
+        std::vector<hipEvent_t>& ev = evs.v;
         for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
         for (int i = 0; i < n; ++i) {
             prof_events() = ProfEvents{ev[2 * i], ev[2 * i + 1]};  // the body's first launch times itself
@@ -2006,7 +2006,6 @@ Engine::DecodeProfile Engine::profile_decode(int iters) {
         HIP_CHECK(hipEventSynchronize(ev[2 * n - 1]));
         double sum = 0;
         for (int i = 0; i < n; ++i) sum += ms_between(ev[2 * i], ev[2 * i + 1]);
-        for (auto& e : ev) (void)hipEventDestroy(e);
         kp.avg_us = 1000.0 * sum / n;
         kp.launches = n;
         if (getenv("DSOCR_NO_GRAPH") && atoi(getenv("DSOCR_NO_GRAPH")) != 0) return;

@@ -2236,71 +2236,15 @@ __device__ __forceinline__ void topk_rank_pick(float logit, int E, int K, int so
     w_out = v;
 }
 
-// The router inside the one-token gate/up launch (route_blocks > 0): block rb computes experts 4 rb + wave exactly
-// as the router launch did (dec_gemv_kernel<WT, 1, 1, 3> with the RMSNorm fused: xload / xstage, lane chunks
-// u-major then j, one wave sum, + bias) and publishes each logit write-through as (tag << 32) | bits.  The routed
-// waves of the same launch poll those 64 words until every one carries this (step, layer)'s tag: the router
-// launch, its boundary and the logits' reload leave the chain.
 template <typename WT>
-__device__ __forceinline__ void mix_router_block(const MoeDec2Args& a, int rb, float* smem, unsigned tag) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = rb * 4 + wave;
-    const WT* W = reinterpret_cast<const WT*>(a.router);
-    const int chunks = a.K >> 3;
-    XRegs<1, 2> xr;
-    xload<1, 2>(xr, a.x, a.K, nullptr, 1, a.K, a.norm_w);
-    uint4 wq[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-        const int c = u * 64 + lane;
-        wq[u] = ldg_nt16(W + (long)min(n0, a.E - 1) * a.K + (min(c, chunks - 1) << 3));
-    }
-    xstage<1, 2>(xr, 1, a.K, a.norm_w != nullptr, a.eps, smem);
-    if (n0 >= a.E) return;
-    const float* xs = smem + XS_RED;
-    float acc = 0.f;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-        const int c = u * 64 + lane;
-        if (c < chunks) {
-            float w8[8], xv[8];
-            unpack8<WT>(wq[u], w8);
-            ld_x8(xs + (c << 3), xv);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], w8[j], acc);
-        }
-    }
-    float v = wave_sum(acc);
-    if (lane == 0) {
-        v = v + (a.router_bias ? a.router_bias[n0] : 0.f);
-        const unsigned long long word = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
-        __hip_atomic_store(a.lg_tag + n0, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-template <typename WT, bool ROUTE>
 __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, const float* xn, int routed_first) {
     constexpr int RB = 1;  // one gate + up row pair per wave (66 VGPRs: the 1792-block grid is resident at once)
     WaveSpan span_(a.span);
     __shared__ __attribute__((aligned(16))) float rank_lds[4][128];
     __shared__ int part_s[4 * 64];
-    __shared__ float lg_sh[64];
     constexpr int U = 3;  // K <= 1536
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int b = blockIdx.x;
-    // ROUTE = false compiles the plain launch (66 VGPRs); ROUTE = true keeps the routing a runtime branch, the form
-    // measured (72 VGPRs, seven blocks per CU: specialised, the compiler hoisted the row loads into 108 VGPRs)
-    const bool route = ROUTE && a.route_blocks != 0;
-    unsigned tag = 0;
-    if (route) {
-        __shared__ __attribute__((aligned(16))) float rsm[XS_RED + 64 * U * 8];  // the router blocks' xstage
-        tag = (unsigned)(*a.tag_pos * 64 + a.layer);
-        if (b < a.route_blocks) {
-            mix_router_block<WT>(a, b, rsm, tag);
-            return;
-        }
-        b -= a.route_blocks;
-    }
+    const int b = blockIdx.x;
     const int wpr = (a.I + RB - 1) / RB;                 // routed waves per pick
     const int n_sh = a.sWgu ? (a.Is + RB - 1) / RB : 0;  // shared waves
     const int n_rt = a.topk * wpr;
@@ -2331,27 +2275,6 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
         }
     };
     auto load_x = [&]() {
-        if (route) {
-            // no router launch hands over the normalised row: every wave normalises x itself (the grouped
-            // router's form: its chunks' squares u-major then j, one wave sum, x / den * w)
-#pragma unroll
-            for (int u = 0; u < U; ++u) ld_x8(a.x + (min(u * 64 + lane, chunks - 1) << 3), xr[u]);
-            float q = 0.f;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (u * 64 + lane < chunks)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) q += xr[u][j] * xr[u][j];
-            const float den = sqrtf(wave_sum(q) / (float)a.K + a.eps);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                float w8[8];
-                ld_x8(a.norm_w + (min(u * 64 + lane, chunks - 1) << 3), w8);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) xr[u][j] = (xr[u][j] / den) * w8[j];
-            }
-            return;
-        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int cc = min(u * 64 + lane, chunks - 1);
@@ -2359,47 +2282,14 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
         }
     };
     if (shared) {
-        // the shared expert needs nothing from this step: its weight stream goes out first (routing inside: after
-        // the wave's own normalisation — off the critical path, and the row and the norm weights are not live
-        // beside the weight registers)
+        // the shared expert needs nothing from this step: its weight stream goes out first
         const WT* Wg = reinterpret_cast<const WT*>(a.sWgu);
-        if (route) load_x();
         issue(Wg, Wg + (long)a.Is * a.K, a.Is);
-        if (!route) load_x();
+        load_x();
     } else {
         // the token row goes out behind the pick's weight rows: its L2 latency hides under theirs, and the pick
         // runs with no row registers live (the 1792-block grid's residency is set by this kernel's VGPRs)
-        float lg;
-        if (route) {
-            load_x();  // normalised while the router blocks work
-            // poll this (step, layer)'s logits: every lane one tagged word, until none is stale (bounded spin).
-            // poll_mode 1 / 2: in a whole routed block only wave 0 polls and hands the logits over in LDS (a
-            // quarter of the pollers on the 64 words); 2 also sleeps 8x longer between polls
-            const bool coop_blk = routed_first && b < (n_rt >> 2);
-            const bool poller = a.poll_mode == 0 || !coop_blk || wave == 0;
-            unsigned long long w = 0;
-            if (poller) {
-                const unsigned long long* lp = a.lg_tag + min(lane, a.E - 1);
-                for (unsigned it = 0;; ++it) {
-                    w = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!__ballot((unsigned)(w >> 32) != tag)) break;
-                    if (it > (1u << 22)) {
-                        if (lane == 0 && a.err) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    if (a.poll_mode == 2) __builtin_amdgcn_s_sleep(8);
-                    else __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            lg = __uint_as_float((unsigned)w);
-            if (a.poll_mode != 0 && coop_blk) {
-                if (wave == 0) lg_sh[lane] = lg;
-                __syncthreads();
-                lg = lg_sh[lane];
-            }
-        } else {
-            lg = a.logits[min(lane, a.E - 1)];
-        }
+        const float lg = a.logits[min(lane, a.E - 1)];
         // a whole routed block (routed_first: blocks < n_rt / 4 hold four routed waves, none returned) ranks
         // cooperatively; any other routed wave alone
         const bool coop = routed_first && b < (n_rt >> 2);
@@ -2407,7 +2297,7 @@ __global__ __launch_bounds__(256) void moe_gateup_mix_kernel(MoeDec2Args a, cons
                        wk);
         const WT* Wg = reinterpret_cast<const WT*>(a.Wgu) + (long)e * 2 * a.I * a.K;
         issue(Wg, Wg + (long)a.I * a.K, a.I);
-        if (!route) load_x();
+        load_x();
         if (i0 == 0 && lane == 0) { a.ids_out[sl] = e; a.w_out[sl] = wk; }
     }
     const int rows = shared ? a.Is : a.I;
@@ -2536,8 +2426,7 @@ void launch_moe_down_mix(const MoeDec2Args& a, hipStream_t s) {
 
 bool moe_gateup_mix_ok(const MoeDec2Args& a) {
     return a.slot_mode && a.logits && a.T == 1 && a.E <= 64 && a.topk <= 8 && a.K % 8 == 0 && a.K <= 64 * 3 * 8 &&
-           a.ids_out && a.w_out && (!a.route_blocks || (a.route_blocks == (a.E + 3) / 4 && a.router && a.lg_tag &&
-                                                        a.tag_pos && a.norm_w));
+           a.ids_out && a.w_out;
 }
 
 // DSOCR_GU_ORDER (A/B switch, read at every launch): 1 (default) = routed blocks first, shared blocks last; 0 = one
@@ -2548,33 +2437,15 @@ static int gu_order() {
     return e ? atoi(e) : 1;
 }
 
-namespace {
-int mix_blocks_per_cu(int wdtype) {
-    static int bf = -1, f16 = -1;
-    int& v = wdtype == WDT_BF16 ? bf : f16;
-    if (v < 0) v = wdtype == WDT_BF16 ? blocks_per_cu(moe_gateup_mix_kernel<bf16_t, true>, 0) : blocks_per_cu(moe_gateup_mix_kernel<f16_t, true>, 0);
-    return v;
-}
-}  // namespace
-
 void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s) {
-    if (!moe_gateup_mix_ok(a) || (!xn && !a.route_blocks)) throw std::runtime_error("EINVAL: moe_gateup_mix outside its range");
+    if (!moe_gateup_mix_ok(a) || !xn) throw std::runtime_error("EINVAL: moe_gateup_mix outside its range");
     // one gate + up row pair per wave: 9.46 -> 8.73 us against two (98 / 90 VGPRs), 3.47 -> 3.55 pages/s
     const int n_sh = a.sWgu ? a.Is : 0;
     const int n_rt = a.topk * a.I;
     const int rf = gu_order();
-    // the router blocks come first (lowest ids); only routed waves wait (on them), so the waiting blocks stay below
-    // the device's slots for this kernel (poll_wait_fits) and every router block finds one
-    if (a.route_blocks && (!rf || !poll_wait_fits((n_rt + 3) / 4, mix_blocks_per_cu(a.wdtype), device_cus())))
-        throw std::runtime_error("EINVAL: moe_gateup_mix routing inside needs routed-first order and resident waiters");
-    dim3 grid(a.route_blocks + (rf ? (n_rt + 3) / 4 + (n_sh + 3) / 4 : std::max(n_sh, (n_rt + 2) / 3)));
-    if (a.route_blocks) {
-        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t, true>), grid, dim3(256), 0, s, a, xn, rf);
-        else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t, true>), grid, dim3(256), 0, s, a, xn, rf);
-    } else {
-        if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t, false>), grid, dim3(256), 0, s, a, xn, rf);
-        else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t, false>), grid, dim3(256), 0, s, a, xn, rf);
-    }
+    dim3 grid(rf ? (n_rt + 3) / 4 + (n_sh + 3) / 4 : std::max(n_sh, (n_rt + 2) / 3));
+    if (a.wdtype == WDT_BF16) DSOCR_LAUNCH((moe_gateup_mix_kernel<bf16_t>), grid, dim3(256), 0, s, a, xn, rf);
+    else DSOCR_LAUNCH((moe_gateup_mix_kernel<f16_t>), grid, dim3(256), 0, s, a, xn, rf);
 }
 
 void launch_moe_gateup2(const MoeDec2Args& a, hipStream_t s) {
@@ -2925,20 +2796,9 @@ struct MoePlan {
     bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
     bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
     bool route_in_gu = false;  // grouped mode: the routing runs inside the gate/up launch (no router launch)
-    bool mix_route = false;    // one token: the router blocks inside the gate/up launch (no router launch)
     bool route_one = false;    // grouped mode: that routing as a one-block launch of the same kernel (route only)
     MoeDec2Args mr;            // ... its arguments
 };
-
-// DSOCR_MIX_ROUTE (A/B switch, read at every plan): 1 = at one token the router runs as the first blocks of the
-// gate/up launch (moe_gateup_mix route_blocks, logits polled by one wave per routed block); 0 (default) = the
-// dec_gemv router launch + gate/up.  Same-process A/B under the kernel trace (profiles/r05_ab_mix_route/): 13.40-13.46
-// us for the fused launch against 4.56 + 8.87 for the two, every routed wave polling 14.85 — the router blocks,
-// sharing the chip with 1792 streaming blocks, take as long as the launch boundary they save
-static bool mix_route_on() {
-    const char* e = getenv("DSOCR_MIX_ROUTE");
-    return e && atoi(e) != 0;
-}
 
 // DSOCR_ROUTE_FUSED (A/B switch, read at every plan): 1 (default) = at 3..8 tokens the router runs inside the
 // matrix-core gate/up launch (moe_gateup_mm_route_ok); 2 = the same routing as a one-block launch (route only)
@@ -2997,14 +2857,6 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
         m.scaling = a.scaling; m.ids_out = a.ids; m.w_out = a.wts;
         p.mode = (fuse_norm && moe_gateup_mix_ok(m) && a.xn_router) ? 0 : 1;
         if (p.mode == 0) gr.xn_out = a.xn_router;  // the router hands its normalised row to gate/up
-        if (p.mode == 0 && T == 1 && mix_route_on() && a.lg_tag && a.tag_pos && a.norm_w && a.router &&
-            a.router_wdt == a.wdtype && gu_order()) {
-            MoeDec2Args r = m;
-            r.route_blocks = (E + 3) / 4; r.router = a.router; r.router_bias = a.router_bias;
-            r.lg_tag = a.lg_tag; r.tag_pos = a.tag_pos; r.layer = a.layer; r.err = a.err;
-            r.poll_mode = getenv("DSOCR_MIX_POLL") ? atoi(getenv("DSOCR_MIX_POLL")) : 1;
-            if (moe_gateup_mix_ok(r)) { p.mix_route = true; m = r; }
-        }
         p.mix_dn = moe_down_mix_ok(m);
     } else {
         p.mode = 3;
@@ -3019,7 +2871,7 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
 
 bool moe_decode_route_launch(const MoeDecodeArgs& a) {
     const MoePlan p = moe_plan(a);
-    return !p.route_in_gu && !p.mix_route;
+    return !p.route_in_gu;
 }
 
 void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const char** down) {
@@ -3038,7 +2890,7 @@ void moe_decode_kernel_names(const MoeDecodeArgs& a, const char** gateup, const 
 void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     const MoePlan p = moe_plan(a);
     const MoeDec2Args& m = p.m;
-    if ((parts & MOE_ROUTE) && (p.route_in_gu || p.mix_route)) {
+    if ((parts & MOE_ROUTE) && p.route_in_gu) {
         // (the gate/up launch routes)
     } else if ((parts & MOE_ROUTE) && p.route_one) {
         launch_moe_gateup_mm(p.mr, s);  // one block: norm + router + top-k + records, no expert

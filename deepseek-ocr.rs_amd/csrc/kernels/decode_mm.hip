@@ -461,7 +461,8 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         // one contiguous 1 KiB per load, 20 KiB per wave (tools/mb_bcast.hip: 160 KiB into one CU in 1.4 vs
         // 3.8 us)
         const WT* R = a.router_swz
-                          ? reinterpret_cast<const WT*>(a.router_swz) + ((long)(tile * steps + kh * half) * 64 + lane) * 8
+                          ? reinterpret_cast<const WT*>(a.router_swz) +
+                                ((long)(min(tile, a.E / 16 - 1) * steps + kh * half) * 64 + lane) * 8  // E % 16 == 0 copy
                           : reinterpret_cast<const WT*>(a.router) + (long)min(16 * tile + col, a.E - 1) * a.K + 8 * g +
                                 32L * kh * half;
         const long RS = a.router_swz ? 512 : 32;  // elements between a lane's consecutive k-steps
@@ -530,6 +531,9 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         // them, the picks and the logits to global memory (for the down launch and the tools), after its last
         // barrier
         if (wave == 0) group_picks_wave64<8>(ids_s, w_s, a.T, a.topk, a.E, grp_s, reinterpret_cast<int*>(rank_s));
+        // block 0's logits copy (for the tools) read before the last prologue barrier: the unit loop's split-K
+        // partials reuse this LDS (scr) without another barrier
+        const float lg_copy = (blockIdx.x == 0 && (tid >> 6) < a.T) ? lg_s[(tid >> 6) * 64 + (tid & 63)] : 0.f;
         __syncthreads();
         GU_STAMP(4);
         if (blockIdx.x == 0) {
@@ -540,7 +544,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
                 a.w_out[tid] = w_s[l];
             }
             if (a.logits && (tid >> 6) < a.T && (tid & 63) < a.E)
-                const_cast<float*>(a.logits)[(tid >> 6) * a.E + (tid & 63)] = lg_s[(tid >> 6) * 64 + (tid & 63)];
+                const_cast<float*>(a.logits)[(tid >> 6) * a.E + (tid & 63)] = lg_copy;
             int* gg = const_cast<int*>(a.grp);
             const int nw = MOE_GRP_REC * (1 + grp_s[0]);
             for (int i = tid; i < nw; i += 512) gg[i] = grp_s[i];
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         if (wave < a.T) mm_row_load<false>(xr, a.x + (long)wave * a.K, a.K, nullptr);
         static_assert(GREC / 4 <= 2 * 512, "two int4 per thread cover the records");
         const int4* gsrc = reinterpret_cast<const int4*>(a.grp);
-        const int n4 = min(GREC / 4, MOE_GRP_REC / 4 * (1 + min(a.slots, 64)));
+        const int n4 = min(GREC / 4, MOE_GRP_REC / 4 * (1 + min(min(a.E, a.slots), 64)));  // moe_grp_ints' records
         const int i0 = tid, i1 = tid + 512;
         int4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
         if (i0 < n4) r0 = gsrc[i0];
@@ -821,7 +825,7 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
     // read as if the segment were routed (in bounds either way) and dropped when it is a shared piece
     int rw_[10];
     {
-        const int* recg = a.grp + MOE_GRP_REC * (1 + min(seg, 64));
+        const int* recg = a.grp + MOE_GRP_REC * (1 + min(seg, min(min(a.E, a.slots), 64) - 1));  // allocated records only
         const int4 q0 = *reinterpret_cast<const int4*>(recg), q1 = *reinterpret_cast<const int4*>(recg + 4);
         const int2 q2 = *reinterpret_cast<const int2*>(recg + 8);
         rw_[0] = q0.x; rw_[1] = q0.y; rw_[2] = q0.z; rw_[3] = q0.w;

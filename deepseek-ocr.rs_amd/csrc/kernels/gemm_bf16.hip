@@ -333,8 +333,6 @@ __device__ __forceinline__ void pp_barrier() {
         __builtin_amdgcn_sched_barrier(0);                                                      \
     }
 
-// LP: DMA pieces of k-tile t + 3 issued at the start of the load interval (the other 4 - LP one after every
-// few MFMAs of the multiply interval): the load interval has slack while the partner row multiplies
 // rotary element as dots_rope8_kernel: x cos + rot sin, no contraction (rot = -partner on the low half)
 __device__ __forceinline__ float pp_rope(float x, float pt, float cs, float sn, bool lo) {
 #pragma clang fp contract(off)
@@ -344,7 +342,7 @@ __device__ __forceinline__ float pp_rope(float x, float pt, float cs, float sn, 
     return a + b;
 }
 
-template <bool STAMPS, int LP>
+template <bool STAMPS>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     extern __shared__ __attribute__((aligned(16))) uint16_t pp_smem[];
     const int lane = threadIdx.x & 63;
@@ -385,12 +383,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
     unsigned long long seg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sa = 0, sb = 0, sc = 0, sd = 0, se = 0, sf = 0, sh = 0, si = 0, s0 = 0;
     PP_STAMP(s0);
     for (int t = 0; t < nk; ++t) {
-        // load interval: LP DMA pieces of k-tile t + 3, this wave's fragments of k-tile t
+        // load interval: this wave's fragments of k-tile t (every DMA of k-tile t + 3 goes out in the multiply
+        // interval: issued beside the ds_reads here a DMA cost ~180 cycles vs ~25-65 between MFMAs, qkv 406 vs
+        // 313 us, profiles/r05_dots/gemm_pp/kb_dgemm_lp{0,2}.log)
         const bool more = t + 3 < nk;
         PP_STAMP(sa);
-        if (more)
-#pragma unroll
-            for (int p = 0; p < (LP == 2 ? 2 : 0); ++p) issue(p, t + 3);
         PP_STAMP(sb);
         const uint16_t* As = pp_smem + (t & 3) * PP_STAGE;
         const uint16_t* Bs = As + PP_M * PP_K;
@@ -405,14 +402,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PP_STAMP(sc);
-        // DMAs issued after k-tile t + 1's: k-tile t + 2's four, k-tile t + 3's first LP
-        if (wr == 1 && t + 1 < nk) pp_wait_n((t + 2 < nk ? 4 : 0) + (more ? (LP == 2 ? 2 : 0) : 0));
+        // DMAs issued after k-tile t + 1's: k-tile t + 2's four
+        if (wr == 1 && t + 1 < nk) pp_wait_n(t + 2 < nk ? 4 : 0);
         PP_STAMP(sd);
         pp_barrier();
         PP_STAMP(se);
         // multiply interval, the DMAs of k-tile t + 3 one after every 4 MFMAs (their issue cost, ~100 cycles
-        // each, runs in the MFMA shadow instead of lengthening the load interval)
-        if (g.pp_prio) __builtin_amdgcn_s_setprio(1);
+        // each, runs in the MFMA shadow instead of lengthening the load interval); raised wave priority over the
+        // interval (measured neutral against none, profiles/r05_dots/gemm_pp, kept as built)
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -420,13 +418,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pp_kernel(GemmBf16Args g) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfv[ks][j], acc[i][j], 0, 0, 0);
-                // MFMA group m = ks * 4 + i (2 MFMAs each): the 4 - LP remaining pieces spread over the 8 groups
-                // (LP 0: after groups 1, 3, 5, 7; LP 1: after groups 0, 2, 4, 6, so MFMAs follow the last DMA;
-                // LP 2: pieces 2, 3 after groups 3, 7)
+                // MFMA group m = ks * 4 + i (2 MFMAs each): the 4 pieces after groups 1, 3, 5, 7
                 const int m = ks * 4 + i;
-                const int per = LP == 2 ? 4 : 2, ph = LP == 1 ? 0 : per - 1;
-                if (m % per == ph) {
-                    if (more) issue((LP == 2 ? 2 : 0) + m / per, t + 3);
+                if (m % 2 == 1) {
+                    if (more) issue(m / 2, t + 3);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -593,13 +588,6 @@ static bool gemm_pp_on() {
     static const int v = getenv("DSOCR_GEMM_PP") ? atoi(getenv("DSOCR_GEMM_PP")) : 1;
     return v != 0;
 }
-// DMA pieces per k-tile issued in the load interval (0 or 2; DSOCR_GEMM_PP_LP).  2 measured slower: a DMA
-// issued beside the load interval's ds_reads cost ~180 cycles vs ~25-65 between MFMAs (qkv 406 vs 313 us,
-// profiles/r05_dots/gemm_pp/kb_dgemm_lp{0,2}.log)
-static int gemm_pp_lpieces() {
-    static const int v = getenv("DSOCR_GEMM_PP_LP") ? atoi(getenv("DSOCR_GEMM_PP_LP")) : 0;
-    return (v == 1 || v == 2) ? v : 0;
-}
 
 int gemm_bf16_splits(int M, int N, int K) {
     const int tiles = ((M + TB_M - 1) / TB_M) * ((N + TB_N - 1) / TB_N);
@@ -633,32 +621,16 @@ void launch_gemm_bf16(const GemmBf16Args& g0, hipStream_t s) {
                      (g.variant == 3 || (g.variant == 0 && gemm_pp_on() && pp_tiles >= 256)))) {
         static bool attr = false;
         if (!attr) {
-            const void* fns[6] = {reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 0>),
-                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 0>),
-                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 1>),
-                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 1>),
-                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false, 2>),
-                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true, 2>)};
+            const void* fns[2] = {reinterpret_cast<const void*>(gemm_bf16_pp_kernel<false>),
+                                  reinterpret_cast<const void*>(gemm_bf16_pp_kernel<true>)};
             for (const void* f : fns)
                 if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS) != hipSuccess)
                     throw std::runtime_error("gemm_bf16_pp: cannot reserve 128 KiB of LDS");
             attr = true;
         }
-        if (g.pp_prio < 0) {
-            static const int pr = getenv("DSOCR_GEMM_PP_PRIO") ? atoi(getenv("DSOCR_GEMM_PP_PRIO")) : 1;
-            g.pp_prio = pr;
-        }
         const dim3 grid((unsigned)pp_tiles), blk(512);
-        if (gemm_pp_lpieces() == 1) {
-            if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 1>), grid, blk, PP_LDS, s, g);
-            else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 1>), grid, blk, PP_LDS, s, g);
-        } else if (gemm_pp_lpieces() == 2) {
-            if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 2>), grid, blk, PP_LDS, s, g);
-            else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 2>), grid, blk, PP_LDS, s, g);
-        } else {
-            if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true, 0>), grid, blk, PP_LDS, s, g);
-            else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false, 0>), grid, blk, PP_LDS, s, g);
-        }
+        if (g.stamps) hipLaunchKernelGGL((gemm_bf16_pp_kernel<true>), grid, blk, PP_LDS, s, g);
+        else hipLaunchKernelGGL((gemm_bf16_pp_kernel<false>), grid, blk, PP_LDS, s, g);
         return;
     }
     const int tiles = ((g.M + TB_M - 1) / TB_M) * ((g.N + TB_N - 1) / TB_N);

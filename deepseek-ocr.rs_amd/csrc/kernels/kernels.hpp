@@ -61,7 +61,6 @@ struct GemmBf16Args {
     const float* rope_cos = nullptr;
     const float* rope_sin = nullptr;
     int rope_cols = 0;
-    int pp_prio = -1;  // ping-pong kernel: raised wave priority over the MFMA interval (1) or not (0); -1 = DSOCR_GEMM_PP_PRIO, else 1
     unsigned long long* stamps = nullptr;  // ping-pong kernel diagnostic build: per-wave segment cycle sums (tools/kbench)
 };
 void launch_gemm_bf16(const GemmBf16Args& g, hipStream_t s);
@@ -352,12 +351,6 @@ struct MoeDec2Args {
     // ... route only: one block runs that routing, writes the normalised rows here (f32 [T][K]) with the picks and
     // records, and streams no expert (a plain gate/up launch follows)
     float* xn_out = nullptr;
-    // one token (moe_gateup_mix): route_blocks > 0 = blocks [0, route_blocks) compute the router logits of x
-    // (dec_gemv's arithmetic, 4 experts per block) and publish them as (tag << 32) | bits in lg_tag, tag =
-    // *tag_pos * 64 + layer; the routed waves poll them, every wave normalises x itself (no router launch)
-    int route_blocks = 0; unsigned long long* lg_tag = nullptr; const int* tag_pos = nullptr; int layer = 0;
-    int* err = nullptr;  // ... a poll that gives up sets *err
-    int poll_mode = 1;   // ... 0 every routed wave polls; 1 one wave per whole routed block (LDS hand-over); 2 = 1 + longer sleeps
     unsigned long long* stamps = nullptr;  // dev (tools/kbench moe8): per block 8 words of s_memrealtime at phase points
 };
 // Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams
@@ -421,10 +414,6 @@ struct MoeDecodeArgs {
     unsigned long long* span = nullptr;  // launch-span slots for the gate/up and down launches (or null)
     unsigned long long* route_span = nullptr;  // launch-span slots for the router launch (or null)
     unsigned long long* stamps = nullptr;      // dev: the grouped gate/up's phase clocks (MoeDec2Args::stamps)
-    // one token: the router inside the gate/up launch (MoeDec2Args::route_blocks) — tagged logits [64] and the tag
-    // source (the decode position; tag = *tag_pos * 64 + layer, the buffer reset to ~0 at every generate)
-    unsigned long long* lg_tag = nullptr; const int* tag_pos = nullptr; int layer = 0;
-    int* err = nullptr;  // a give-up of that poll sets *err
 };
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments

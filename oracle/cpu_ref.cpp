@@ -979,6 +979,11 @@ void cr_free() {
 
 int cr_threads() { return omp_get_max_threads(); }
 
+// the OpenMP team size of every later parallel region (the bench times the same page at two thread counts)
+void cr_set_threads(int n) {
+    if (n > 0) omp_set_num_threads(n);
+}
+
 // Y = X . W^T for a tensor set with cr_set (micro-benchmark of the linear kernel)
 int cr_linear(const char* wname, const float* X, int M, int K, float* Y, int N) {
     try {

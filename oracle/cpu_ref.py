@@ -37,6 +37,8 @@ def _lib():
     L.cr_set.argtypes = [C.c_char_p, vp, C.c_long, C.c_long, i32]
     L.cr_generate.argtypes = [vp, vp, i32, vp, i32, i32, i32, vp, vp]
     L.cr_free.restype = None
+    L.cr_set_threads.argtypes = [i32]
+    L.cr_set_threads.restype = None
     L.cv_init.argtypes = [i32, i32, i32, i32, vp, i32, i32, i32, i32, f32, i32, i32, i32, i32, f32, i32, i32, i32]
     L.cv_features.argtypes = [vp, i32, i32, i32, vp, vp, vp]
     return L
@@ -178,3 +180,8 @@ class CpuVision:
             return v.embeddings(glob, patches, crop), crop
         finally:
             v.features = orig
+
+
+def set_threads(n: int) -> None:
+    """OpenMP team size for every later CpuRef / CpuVision call in this process."""
+    _lib().cr_set_threads(int(n))
