@@ -24,7 +24,7 @@ CLANG = os.environ.get("DSOCR_CXX", "/opt/rocm/llvm/bin/clang++")
 ARCH = "gfx950"
 
 KERNELS = ["gemm", "gemm_bf16", "moe", "norm", "attention", "misc", "decode", "lmhead", "dsq", "preprocess", "sampling",
-           "dots_ops", "attention_bf16", "decode_mm"]
+           "dots_ops", "attention_bf16", "decode_mm", "decode_persist"]
 HOST = ["engine", "dots", "capi"]
 
 

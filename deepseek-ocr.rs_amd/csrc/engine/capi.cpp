@@ -411,6 +411,33 @@ dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap
 }
 static_assert(dsocr::Engine::SPAN_FIELDS == 5, "dsocr.h documents 5 fields per span record");
 
+dsocr_status dsocr_engine_set_persist_stamps(dsocr_engine* e, int mode) {
+    return guarded([&] {
+        if (!e) throw std::runtime_error("EINVAL: NULL engine");
+        e->impl->set_persist_stamps(mode);
+    });
+}
+
+dsocr_status dsocr_engine_persist_info(const dsocr_engine* e, int* used, double* durations, size_t cap_d,
+                                       size_t* n_launches, uint64_t* stamps, size_t cap_s, size_t* n_stamps) {
+    return guarded([&] {
+        if (!e) throw std::runtime_error("EINVAL: NULL engine");
+        const auto& d = e->impl->persist_launch_us();
+        const auto& st = e->impl->persist_stamps();
+        if (used) *used = e->impl->persist_used() ? 1 : 0;
+        if (n_launches) *n_launches = d.size();
+        if (n_stamps) *n_stamps = st.size();
+        if (durations) {
+            if (d.size() > cap_d) throw std::runtime_error("EINVAL: duration buffer too small");
+            if (!d.empty()) std::memcpy(durations, d.data(), d.size() * sizeof(double));
+        }
+        if (stamps) {
+            if (st.size() > cap_s) throw std::runtime_error("EINVAL: stamp buffer too small");
+            if (!st.empty()) std::memcpy(stamps, st.data(), st.size() * 8);
+        }
+    });
+}
+
 dsocr_status dsocr_device_count(int* n) {
     return guarded([&] { check_hip(hipGetDeviceCount(n), "hipGetDeviceCount"); });
 }

@@ -1041,6 +1041,80 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
     return a;
 }
 
+bool Engine::persist_ok(int B, int Lmax) {
+    const char* e = getenv("DSOCR_PERSIST");
+    if (e && atoi(e) == 0) return false;
+    const LangConfig& L = cfg_.lang;
+    if (B != 1 || L.use_mla || L.rope_dim != L.head_dim || L.v_head_dim != L.head_dim || L.n_shared <= 0 ||
+        L.topk_method != "greedy" || L.hidden_act != "silu")
+        return false;
+    if (!dec_persist_shape_ok(L.hidden, L.heads, L.kv_heads, L.head_dim, L.n_routed, L.topk, L.moe_inter,
+                              L.n_shared * L.moe_inter, L.inter, Lmax))
+        return false;
+    for (const DecLayer& d : layers_) {
+        if (d.qkv.wdt != WDT_F16 || d.qkv.b || d.o.wdt != WDT_F16 || d.o.b) return false;
+        if (d.moe) {
+            if (!d.router.W || d.router.wdt != WDT_F16 || d.e_wdt != WDT_F16 || !d.has_shared || d.s_gu.wdt != WDT_F16 ||
+                d.s_d.wdt != WDT_F16 || d.s_gu.b || d.s_d.b)
+                return false;
+        } else if (!d.gu.W || d.gu.wdt != WDT_F16 || d.down.wdt != WDT_F16) {
+            return false;
+        }
+    }
+    return dec_persist_resident() != 0;
+}
+
+// the persistent decode's weight table: every down projection transposed to [inter][H] (split-K rows), the
+// per-layer pointer table on the device, the granule buffer (made once, outside any capture)
+void Engine::ensure_persist() {
+    if (persist_lw_ || capturing_) return;
+    const LangConfig& L = cfg_.lang;
+    const int H = L.hidden, E = L.n_routed, I = L.moe_inter;
+    std::vector<PersistLayerW> tab(layers_.size());
+    for (size_t l = 0; l < layers_.size(); ++l) {
+        DecLayer& d = layers_[l];
+        PersistLayerW& w = tab[l];
+        w.qkv = (const uint16_t*)d.qkv.W;
+        w.o = (const uint16_t*)d.o.W;
+        w.in_w = d.in_norm.w;
+        w.post_w = d.post_norm.w;
+        w.moe = d.moe ? 1 : 0;
+        if (d.moe) {
+            if (!d.e_dT) {
+                d.e_dT = dev_alloc((size_t)E * I * H * 2);
+                for (int e = 0; e < E; ++e)
+                    launch_transpose16((const uint16_t*)d.e_d + (size_t)e * H * I, (uint16_t*)d.e_dT + (size_t)e * I * H, H, I,
+                                       stream_);
+            }
+            const int Is = d.s_d.K;
+            if (!d.s_dT) {
+                d.s_dT = dev_alloc((size_t)Is * H * 2);
+                launch_transpose16(d.s_d.W, d.s_dT, H, Is, stream_);
+            }
+            w.router = (const uint16_t*)d.router.W;
+            w.router_bias = d.router.b;
+            w.e_gu = (const uint16_t*)d.e_gu;
+            w.e_dT = (const uint16_t*)d.e_dT;
+            w.s_gu = (const uint16_t*)d.s_gu.W;
+            w.s_dT = (const uint16_t*)d.s_dT;
+            w.inter = Is;
+        } else {
+            if (!d.s_dT) {
+                d.s_dT = dev_alloc((size_t)L.inter * H * 2);
+                launch_transpose16(d.down.W, d.s_dT, H, L.inter, stream_);
+            }
+            w.s_gu = (const uint16_t*)d.gu.W;
+            w.s_dT = (const uint16_t*)d.s_dT;
+            w.inter = L.inter;
+        }
+    }
+    PersistLayerW* dtab = (PersistLayerW*)dev_alloc(tab.size() * sizeof(PersistLayerW));
+    HIP_CHECK(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(PersistLayerW), hipMemcpyHostToDevice, stream_));
+    persist_g_ = (unsigned long long*)dev_alloc(dec_persist_granules(L.layers) * 8);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    persist_lw_ = dtab;
+}
+
 // the dense MLP's matrix-core form at 3..8 pages (decode_mm.hip): q/k/v-sized K for gate|up, K % 64 for down
 bool Engine::dense_mm_ok(const DecLayer& d, int B) const {
     const LangConfig& L = cfg_.lang;
@@ -1065,6 +1139,27 @@ void Engine::decode_step(int B, int Lmax) {
     float* part = wsf("s_part", dec_attn_workspace(B, L.heads, hd, Lmax) / 4 + 16);
     if (L.heads % L.kv_heads) throw std::runtime_error("EINVAL: num_attention_heads must be a multiple of num_key_value_heads");
     int* err = wsi("s_err", 4);
+    if (B == 1 && persist_active_ && !step_skip_ && !span_rec_) {
+        // every layer of the step in one persistent launch (decode_persist.hip)
+        DecPersistArgs pa;
+        pa.layers = L.layers; pa.lw = persist_lw_; pa.x = X; pa.kv_pos = kv_pos;
+        pa.cos = rope_cos_; pa.sin = rope_sin_; pa.kc = kc_; pa.vc = vc_;
+        pa.layer_kv = (long)B * page_stride_; pa.head_stride = head_stride_;
+        pa.scale = (float)(1.0 / std::sqrt((double)hd)); pa.eps = L.rms_eps;
+        pa.softmax_scoring = L.scoring == "softmax"; pa.norm_topk = L.norm_topk; pa.scaling = L.routed_scaling;
+        pa.g = persist_g_; pa.err = err;
+        if (persist_stamp_mode_ && !persist_ev_.empty() && persist_stamps_) {
+            pa.stamps = persist_stamps_;
+            pa.stamp_pos0 = persist_stamp_pos0_;
+            pa.stamp_cap = persist_stamp_cap_;
+            HIP_CHECK(hipEventRecord(persist_ev_[0], st));
+            launch_dec_persist(pa, st);
+            HIP_CHECK(hipEventRecord(persist_ev_[1], st));
+        } else {
+            launch_dec_persist(pa, st);
+        }
+        return;
+    }
     // launch spans (set_spans): HIP events on the stream around the launch (dispatch-level duration,
     // what rocprofv3's kernel trace reports) + the in-kernel wave span folded right after it
     auto stamped = [&](int kind, int l, const std::function<void()>& launch, const int* ids, int n_ids) {
@@ -1576,6 +1671,12 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     HIP_CHECK(hipMemsetAsync(wsi("s_dtick", dec_mm_splitk_ticks(H)), 0, sizeof(int) * dec_mm_splitk_ticks(H), st));
     HIP_CHECK(hipMemsetAsync(wsi("s_err", 4), 0, sizeof(int) * 4, st));  // fused-kernel give-up flag
+    // one page: the persistent decode step (its granules: no tag of an earlier generate may match this one's)
+    persist_active_ = p.use_cache && persist_ok(B, Lmax);
+    if (persist_active_) {
+        ensure_persist();
+        HIP_CHECK(hipMemsetAsync(persist_g_, 0xff, dec_persist_granules(L.layers) * 8, st));
+    }
     const int QKVN = layers_[0].qkv.N;
     float* SX = wsf("s_x", (size_t)B * H);
     float* SXN = wsf("s_xn", (size_t)B * H);
@@ -1814,6 +1915,18 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     // make sure every decode workspace exists before capture: a dry step allocates them
     // (it writes the step-0 K/V slot, which the real step rewrites), then the state is restored
     decode_step(B, Lmax);
+    if (persist_active_) {  // the dry step's granules carry step 1's tags: reset them
+        HIP_CHECK(hipMemsetAsync(persist_g_, 0xff, dec_persist_granules(L.layers) * 8, st));
+        persist_stamps_host_.clear();
+        persist_ev_us_.clear();
+        if (persist_stamp_mode_) {
+            persist_stamp_pos0_ = kvpos[0];
+            persist_stamp_cap_ = (int)p.max_new;
+            const size_t n = (size_t)persist_stamp_cap_ * PK_G * L.layers * PK_STAMPS;
+            persist_stamps_ = (unsigned long long*)ws("p_pk_stamps", n * 8);
+            HIP_CHECK(hipMemsetAsync(persist_stamps_, 0, n * 8, st));
+        }
+    }
     if (chain_active_) {  // the dry step's stamps must not join step 1's: clear the regions and the marks
         HIP_CHECK(hipMemsetAsync(span_chain_, 0, (size_t)L.layers * SPAN_KINDS_CHAIN * SPAN_SLOTS * 16, st));
         HIP_CHECK(hipMemsetAsync(span_tmark_, 0, 16, st));
@@ -1835,6 +1948,11 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
             launch_span_chain_fold(span_chain_, L.layers * SPAN_KINDS_CHAIN, span_chain_rec_, span_step_, span_cap_,
                                    span_tmark_, st);
     };
+    const bool pk_timed = persist_active_ && persist_stamp_mode_ && !span_rec_;
+    if (pk_timed && persist_ev_.empty()) {
+        persist_ev_.resize(2);
+        for (auto& e : persist_ev_) HIP_CHECK(hipEventCreate(&e));
+    }
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
     if (use_graph) {
@@ -1851,6 +1969,12 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
         if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
         else step_body();
         if (span_rec_ && (span_mode_ & SPAN_EVENTS)) read_span_events(i);
+        if (pk_timed) {  // the persistent launch's dispatch duration (events recorded around it in the step)
+            HIP_CHECK(hipEventSynchronize(persist_ev_[1]));
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, persist_ev_[0], persist_ev_[1]));
+            persist_ev_us_.push_back(ms * 1e3);
+        }
         ++steps;
         const bool check = cb != nullptr || (!p.ignore_eos && (i % 8 == 0 || i + 1 == p.max_new));
         if (check) {
@@ -1863,6 +1987,12 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     HIP_CHECK(hipStreamSynchronize(st));
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
+    if (pk_timed) {
+        persist_stamps_host_.resize((size_t)persist_stamp_cap_ * PK_G * L.layers * PK_STAMPS);
+        HIP_CHECK(hipMemcpy(persist_stamps_host_.data(), persist_stamps_, persist_stamps_host_.size() * 8,
+                            hipMemcpyDeviceToHost));
+        persist_stamp_mode_ = 0;
+    }
     if (chain_active_) {
         const size_t nreg = (size_t)L.layers * SPAN_KINDS_CHAIN;
         std::vector<unsigned long long> dev((size_t)span_cap_ * nreg * 4);

@@ -81,6 +81,9 @@ struct DecLayer {
     void* e_gu_swz = nullptr; void* e_d_swz = nullptr; void* s_gu_swz = nullptr; void* s_d_swz = nullptr;
     void* router_swz = nullptr;  // fragment-ordered router rows (3..8 pages: the routing inside gate/up)
     void* qkv_swz = nullptr; void* o_swz = nullptr; void* gu_swz = nullptr;  // ... q/k/v, o_proj, dense gate|up
+    // the persistent one-page decode (decode_persist.hip): down projections transposed to [inter][H] rows
+    void* e_dT = nullptr;         // routed [E][Im][H]
+    void* s_dT = nullptr;         // shared [Is][H] (MoE) / dense [I][H]
 };
 
 struct PagePixels {
@@ -182,6 +185,12 @@ class Engine {
     const std::vector<unsigned long long>& spans() const { return spans_host_; }
     int span_steps() const { return spans_steps_; }  // the steps of spans_host_ (set with it)
     hipStream_t stream() const { return stream_; }
+    // persistent decode diagnostics: mode 1 = the next generate times every persistent launch with HIP events
+    // and records the phase clocks (PK_STAMPS per workgroup and layer) of its decode steps; read them after it
+    void set_persist_stamps(int mode) { persist_stamp_mode_ = mode; }
+    bool persist_used() const { return persist_active_; }
+    const std::vector<unsigned long long>& persist_stamps() const { return persist_stamps_host_; }
+    const std::vector<double>& persist_launch_us() const { return persist_ev_us_; }
     void upload_page(PagePixels& pg);
     void prepare_page_device(const uint8_t* rgb, int w, int h, PagePixels& px);
 
@@ -218,6 +227,10 @@ class Engine {
     float* vision_pass(const float* imgs, int n, int S, const std::string& out);
     void prefill(int B, const std::vector<int>& rows_per_page, const float* x0, int Lmax);
     void decode_step(int B, int Lmax);
+    // one page: every decoder layer of a step as one persistent launch (decode_persist.hip) when the model's
+    // shape and dtypes fit it and all 256 workgroups are resident; DSOCR_PERSIST=0 keeps the launch chain
+    bool persist_ok(int B, int Lmax);
+    void ensure_persist();
     MoeDecodeArgs moe_args(int l, int B, float* X);
     void decode_head(int B, DecSampleArgs& sa, const SampleArgs& pen);
     void reserve_head_ws(int B);
@@ -302,6 +315,15 @@ class Engine {
         return span_rec_ + ((size_t)kind * cfg_.lang.layers + layer) * span_cap_ * 4;
     }
     long trace_steps_ = 0;
+    bool persist_active_ = false;               // this generate's decode steps run dec_persist
+    PersistLayerW* persist_lw_ = nullptr;       // device [layers]
+    unsigned long long* persist_g_ = nullptr;   // granules [dec_persist_granules(layers)]
+    unsigned long long* persist_stamps_ = nullptr;  // device phase clocks of the last stamped step (optional)
+    int persist_stamp_mode_ = 0;                // 1: the next generate records stamps of its decode steps
+    int persist_stamp_pos0_ = 0, persist_stamp_cap_ = 0;
+    std::vector<unsigned long long> persist_stamps_host_;
+    std::vector<hipEvent_t> persist_ev_;        // [steps][2] HIP events around each persistent launch (timing mode)
+    std::vector<double> persist_ev_us_;
 
     void* dev_alloc(size_t bytes);
     void ensure_rope(int len);

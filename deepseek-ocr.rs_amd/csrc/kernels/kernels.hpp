@@ -415,6 +415,53 @@ struct MoeDecodeArgs {
     unsigned long long* route_span = nullptr;  // launch-span slots for the router launch (or null)
     unsigned long long* stamps = nullptr;      // dev: the grouped gate/up's phase clocks (MoeDec2Args::stamps)
 };
+// ---- one-page decode step as ONE persistent launch (decode_persist.hip): every decoder layer inside 256 resident
+// workgroups handing their vectors over as {f32, tag} granules (tag = the decode position; the granule buffer is
+// reset to all-ones before a generate's first step and after the dry step)
+constexpr int PK_G = 256;                 // workgroups, one per CU
+constexpr int PK_CPH = 25;                // attention chunks per head
+constexpr int PK_STAMPS = 9;              // phase clocks per (workgroup, layer) when DecPersistArgs::stamps is set
+constexpr long PK_SPIN_TICKS = 5000000;   // one hand-off gives up after 50 ms (s_memrealtime, 100 MHz): *err = 2
+struct PersistLayerW {
+    const uint16_t* qkv = nullptr;        // f16 [3 heads hd][H] (q | k | v)
+    const uint16_t* o = nullptr;          // f16 [H][heads hd]
+    const float* in_w = nullptr;          // input RMSNorm weight [H]
+    const float* post_w = nullptr;        // post-attention RMSNorm weight [H]
+    const uint16_t* router = nullptr;     // f16 [E][H] (MoE layers)
+    const float* router_bias = nullptr;   // [E] or null
+    const uint16_t* e_gu = nullptr;       // routed f16 [E][2I][H] (gate rows, then up rows)
+    const uint16_t* e_dT = nullptr;       // routed down TRANSPOSED f16 [E][I][H]
+    const uint16_t* s_gu = nullptr;       // shared (MoE) / dense f16 [2 inter][H]
+    const uint16_t* s_dT = nullptr;       // shared / dense down TRANSPOSED f16 [inter][H]
+    int moe = 0;
+    int inter = 0;                        // MoE: shared inter (n_shared * moe_inter); dense: intermediate_size
+};
+struct DecPersistArgs {
+    int layers = 0;
+    const PersistLayerW* lw = nullptr;    // device array [layers]
+    float* x = nullptr;                   // s_x [H]: layer 0's input (plain loads), the last layer's output
+    const int* kv_pos = nullptr;          // decode position (the tag of every granule of this step)
+    const float* cos = nullptr; const float* sin = nullptr;  // rope tables [pos][hd]
+    float* kc = nullptr; float* vc = nullptr;                // f32 cache, + l * layer_kv + head * head_stride + pos * hd
+    long layer_kv = 0, head_stride = 0;
+    float scale = 1.f, eps = 0.f;
+    int softmax_scoring = 1, norm_topk = 0;
+    float scaling = 1.f;
+    unsigned long long* g = nullptr;      // granules [dec_persist_granules(layers)]
+    int* err = nullptr;                   // a hand-off that gave up sets 2
+    unsigned long long* stamps = nullptr; // optional [stamp_cap][PK_G][layers][PK_STAMPS] s_memrealtime phase clocks,
+    int stamp_pos0 = 0, stamp_cap = 0;    // ... of the step at position stamp_pos0 + i, i < stamp_cap
+};
+size_t dec_persist_granules(int layers);
+size_t dec_persist_lds_bytes();
+// the decoder shape the launch is written for (DeepSeek-OCR: H 1280, 10 x 128 MHA, 64 experts top-6 of 896, 2
+// shared, dense 6848), max_len <= 25 chunks x 64 keys
+bool dec_persist_shape_ok(int hidden, int heads, int kv_heads, int head_dim, int n_routed, int topk, int moe_inter,
+                          int shared_inter, int dense_inter, int max_len);
+int dec_persist_resident();  // 1: all PK_G workgroups are resident at once on this device
+void launch_dec_persist(const DecPersistArgs& a, hipStream_t s);
+void launch_transpose16(const void* in, void* out, int N, int K, hipStream_t s);  // out[k][n] = in[n][k], 16-bit
+
 enum MoeParts : int { MOE_ROUTE = 1, MOE_GATEUP = 2, MOE_DOWN = 4, MOE_ALL = 7 };
 // kernel names of the gate/up and down launches the dispatch picks for these arguments
 // false when the routing runs inside the gate/up launch (3..8 tokens, DSOCR_ROUTE_FUSED): MOE_ROUTE launches nothing

@@ -87,6 +87,7 @@ EXPORTS = [
     "dsocr_dots_load", "dsocr_dots_free", "dsocr_dots_info", "dsocr_dots_preprocess", "dsocr_dots_embed",
     "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16", "dsocr_k_gemv_splitk",
     "dsocr_engine_set_spans", "dsocr_engine_spans", "dsocr_k_qkv_attention", "dsocr_k_poll_wait_fits",
+    "dsocr_engine_set_persist_stamps", "dsocr_engine_persist_info",
 ]
 
 _lib = None
@@ -134,6 +135,8 @@ def lib():
     L.dsocr_profile_decode.argtypes = [vp, i32, C.POINTER(DecodeProfileC)]
     L.dsocr_engine_set_spans.argtypes = [vp, i32]
     L.dsocr_engine_spans.argtypes = [vp, vp, sz, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
+    L.dsocr_engine_set_persist_stamps.argtypes = [vp, i32]
+    L.dsocr_engine_persist_info.argtypes = [vp, C.POINTER(i32), vp, sz, C.POINTER(sz), vp, sz, C.POINTER(sz)]
     L.dsocr_device_count.argtypes = [C.POINTER(i32)]
     L.dsocr_dev_alloc.argtypes = [sz, C.POINTER(vp)]
     L.dsocr_dev_free.argtypes = [vp]

@@ -301,6 +301,24 @@ class DeepseekOcrEngine:
         check(lib().dsocr_engine_spans(self._h, buf.ctypes.data_as(C.c_void_p), buf.size, None, None, None))
         return {name: buf[i] for i, name in enumerate(self.SPAN_KINDS[:k.value])}
 
+    def set_persist_stamps(self, mode: int = 1):
+        """The next generate times every persistent decode launch (HIP events) and records its phase clocks."""
+        check(lib().dsocr_engine_set_persist_stamps(self._h, int(mode)))
+
+    def persist_info(self, layers: int = 0) -> dict:
+        """{used, launch_us [steps], stamps [steps][256][layers][9] uint64} of the last generate
+        (dsocr_engine_persist_info)."""
+        used, nd, ns = C.c_int(), C.c_size_t(), C.c_size_t()
+        check(lib().dsocr_engine_persist_info(self._h, C.byref(used), None, 0, C.byref(nd), None, 0, C.byref(ns)))
+        d = np.zeros(nd.value, np.float64)
+        st = np.zeros(ns.value, np.uint64)
+        check(lib().dsocr_engine_persist_info(self._h, None, d.ctypes.data_as(C.c_void_p), d.size, None,
+                                              st.ctypes.data_as(C.c_void_p), st.size, None))
+        out = {"used": bool(used.value), "launch_us": d}
+        if layers and st.size:
+            out["stamps"] = st.reshape(-1, 256, layers, 9)
+        return out
+
     def profile_decode(self, iters: int = 3) -> dict:
         """HIP-event timings + algorithmic bytes of the dominant decode kernels (see dsocr.h)."""
         from ._lib import DecodeProfileC

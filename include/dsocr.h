@@ -225,6 +225,18 @@ dsocr_status dsocr_engine_set_spans(dsocr_engine* e, int mode);
 dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap, size_t* kinds, size_t* layers,
                                 size_t* steps);
 
+/* ---- one-page persistent decode (decode_persist.hip; no reference counterpart: the reference's decode step is
+ * Candle's per-op launches, model/mod.rs:1977-2034).  At B = 1 every decoder layer of a step runs as ONE
+ * persistent launch when the model's shape and dtypes fit it (DSOCR_PERSIST=0 keeps the per-layer launch chain).
+ * dsocr_engine_set_persist_stamps(e, 1): the next generate times each persistent launch with HIP events and
+ * records its phase clocks; dsocr_engine_persist_info then returns whether the last generate used the persistent
+ * launch (*used), the launch durations in us (durations[cap_d], *n_launches) and the phase clocks
+ * [steps][256 workgroups][layers][9] uint64 (s_memrealtime, 100 MHz) of its decode steps (stamps[cap_s],
+ * *n_stamps; step i = position prompt_len + i).  NULL arrays: sizes only. */
+dsocr_status dsocr_engine_set_persist_stamps(dsocr_engine* e, int mode);
+dsocr_status dsocr_engine_persist_info(const dsocr_engine* e, int* used, double* durations, size_t cap_d,
+                                       size_t* n_launches, uint64_t* stamps, size_t cap_s, size_t* n_stamps);
+
 /* ---- device helpers for tests / tooling (plain pointers; no torch) */
 dsocr_status dsocr_device_count(int* n);
 dsocr_status dsocr_dev_alloc(size_t bytes, void** ptr);
