@@ -409,6 +409,73 @@ def chain_roofline(chain, waves, d, B, P):
     return out
 
 
+def persist_bytes(cfg, L_keys):
+    """Algorithmic HBM bytes of one persistent decode launch (every decoder layer of one step, one page): each
+    layer's f16 weights once (q/k/v, o_proj, router, the 6 picked experts' gate/up/down, the shared experts; the
+    dense layer's MLP), its f32 K and V over the L_keys - 1 cached keys read + the new key written, the norm
+    weights; hand-off granules are not algorithmic."""
+    c = cfg.get("language_config", cfg)
+    H, heads = c["hidden_size"], c["num_attention_heads"]
+    hd = H // heads
+    I, E_k, n_sh = c["moe_intermediate_size"], c["num_experts_per_tok"], c.get("n_shared_experts", 0)
+    Is, Id, nl = I * n_sh, c["intermediate_size"], c["num_hidden_layers"]
+    dense = c.get("first_k_dense_replace", 0)
+    attn = 3 * heads * hd * H * 2 + H * heads * hd * 2 + 2 * H * 4
+    moe = c["n_routed_experts"] * H * 2 + 3 * (E_k * I + Is) * H * 2
+    mlp_dense = 3 * Id * H * 2
+    kv = heads * hd * 4 * 2 * (L_keys - 1) + heads * hd * 4 * 2
+    return nl * (attn + kv) + dense * mlp_dense + (nl - dense) * moe, (E_k * I) * H * 2 * 3
+
+
+def persist_roofline(eng, batch, params, ppg, args):
+    """Roofline of the one-page decode as it runs: ONE persistent launch per step (decode_persist.hip) holds every
+    decoder layer, so it is the dominant kernel.  A generate of the first timed batch with HIP events around each
+    persistent launch (the dispatch-level duration rocprofv3 reports for dec_persist_kernel) and the kernel's
+    phase clocks: achieved = algorithmic bytes of each launch (persist_bytes at its step's key count) summed over
+    the generate / the summed launch durations.  `moe_routed`: the routed experts' gate + up + down bytes (6 x 3 x
+    896 x 1280 f16 per layer) over the routed phase of each layer (picks known on the first workgroup -> the last
+    workgroup's split-K partial stored), the window that holds every routed expert byte (the shared expert's rows
+    stream earlier, beside the attention hand-offs)."""
+    import numpy as np
+    import dsocr
+    cfg = json.load(open(dsocr.FULL_CONFIG))
+    nl = cfg.get("language_config", cfg)["num_hidden_layers"]
+    P = len(batch[0][0])
+    eng.set_persist_stamps(1)
+    eng.generate_batch(batch, params, ignore_eos=True)
+    info = eng.persist_info(layers=nl)
+    us = np.asarray(info["launch_us"], np.float64)
+    st = info["stamps"][: len(us)].astype(np.int64)  # [steps][256][layers][9]
+    n = len(us)
+    byts = np.array([persist_bytes(cfg, P + i + 1)[0] for i in range(n)], np.float64)
+    routed_b = persist_bytes(cfg, P)[1]
+    gbs = byts.sum() / (us.sum() * 1e-6) / 1e9
+    # phase windows over the workgroups (s_memrealtime, 100 MHz), per step and layer
+    first = st.min(axis=1)  # [steps][layers][9]
+    last = st.max(axis=1)
+    dense = cfg.get("language_config", cfg).get("first_k_dense_replace", 0)
+    routed_s = (last[:, dense:, 7] - first[:, dense:, 6]) / SPAN_HZ
+    layer_s = (last[:, :, 8] - first[:, :, 0]) / SPAN_HZ
+    phase_names = ("x gathered", "q/k/v published", "attention partials", "merge -> ctx published",
+                   "ctx gathered", "x_new normalised + picks", "split-K partials", "x_{l+1} published")
+    # per phase: mean over steps and layers of (last workgroup at phase k) - (last workgroup at phase k - 1)
+    ph = {phase_names[k - 1]: round(float(np.mean(last[:, :, k] - last[:, :, k - 1]) / SPAN_HZ * 1e6), 2)
+          for k in range(1, 9)}
+    rt_gbs = routed_b * routed_s.size / routed_s.sum() / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("dec_persist_kernel", runs=("b1",))[0],
+            "kernel": "dec_persist_kernel (one decode step: all decoder layers of the page in ONE persistent launch)",
+            "avg_launch_us": round(float(us.mean()), 2), "p50_launch_us": round(float(np.median(us)), 2),
+            "launches": int(n), "bytes_per_launch": round(float(byts.mean())),
+            "timing": "HIP events around every persistent launch inside the replayed step graph",
+            "layer_us": round(float(layer_s.mean() * 1e6), 2),
+            "phase_us": ph,
+            "moe_routed": {"bytes_per_layer": routed_b, "window_us": round(float(routed_s.mean() * 1e6), 2),
+                           "GB/s": round(rt_gbs, 1), "frac": round(rt_gbs / HBM_PEAK_GBS, 4),
+                           "window": "picks known (first workgroup) -> split-K partials stored (last workgroup)"},
+            "kv_len": [P + 1, P + n]}
+
+
 def decode_roofline(eng, batch, params, ppg, args):
     """The roofline object of the decode MoE gate/up (the north-star kernel) at this batch size (rank 0, after the
     timed region, on the first timed batch):
@@ -483,6 +550,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-decode-steps", type=int, default=0, help="(unused: the C++ baseline times every decode step)")
     ap.add_argument("--roofline-iters", type=int, default=20)
+    ap.add_argument("--no-chain-roofline", action="store_true",
+                    help="skip the per-layer launch chain's roofline beside the persistent decode's (one page)")
     ap.add_argument("--trace-only", action="store_true",
                     help="production-only run for a rocprofv3 kernel trace: the timed generates and nothing else "
                          "(no span / event / profile_decode generates, no CPU baseline); roofline is null")
@@ -614,7 +683,18 @@ def main():
 
     result = None
     if rank == 0:
-        roofline = None if args.trace_only else decode_roofline(eng, batches[args.warmup][1], params, ppg, args)
+        log(f"[bench] timed: {value:.4f} pages/s, {tok_s:.1f} decode tok/s, stages "
+            + ", ".join(f"{k} {stage[k]:.2f}" for k in ("vision_compute_ms", "decode_prefill_ms", "decode_iterative_ms")))
+        roofline = None
+        if not args.trace_only:
+            if eng.persist_info()["used"] and ppg == 1:  # the timed generates ran the persistent decode
+                roofline = persist_roofline(eng, batches[args.warmup][1], params, ppg, args)
+                if not args.no_chain_roofline:  # the per-layer launch chain's line, same page (DSOCR_PERSIST=0)
+                    os.environ["DSOCR_PERSIST"] = "0"
+                    roofline["launch_chain"] = decode_roofline(eng, batches[args.warmup][1], params, ppg, args)
+                    os.environ.pop("DSOCR_PERSIST")
+            else:
+                roofline = decode_roofline(eng, batches[args.warmup][1], params, ppg, args)
         cpu = None
         if world == 1 and not (args.no_cpu_baseline or args.trace_only) and not snap and not args.text_pages:
             b = batches[args.warmup]

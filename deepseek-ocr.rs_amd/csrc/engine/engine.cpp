@@ -1042,8 +1042,10 @@ MoeDecodeArgs Engine::moe_args(int l, int B, float* X) {
 }
 
 bool Engine::persist_ok(int B, int Lmax) {
+    // opt-in (DSOCR_PERSIST=1, read per generate): measured slower than the per-layer launch chain on MI355X
+    // (43.5 vs 33.5 us per layer), kept as the A/B of the persistent-layer design
     const char* e = getenv("DSOCR_PERSIST");
-    if (e && atoi(e) == 0) return false;
+    if (!e || atoi(e) == 0) return false;
     const LangConfig& L = cfg_.lang;
     if (B != 1 || L.use_mla || L.rope_dim != L.head_dim || L.v_head_dim != L.head_dim || L.n_shared <= 0 ||
         L.topk_method != "greedy" || L.hidden_act != "silu")
@@ -1152,9 +1154,11 @@ void Engine::decode_step(int B, int Lmax) {
             pa.stamps = persist_stamps_;
             pa.stamp_pos0 = persist_stamp_pos0_;
             pa.stamp_cap = persist_stamp_cap_;
-            HIP_CHECK(hipEventRecord(persist_ev_[0], st));
+            // the launch's own dispatch begin / end (hipExtLaunchKernelGGL events: what rocprofv3's kernel trace
+            // reports); the timed generate runs its steps eagerly (events on a dispatch packet cannot be captured)
+            prof_events() = ProfEvents{persist_ev_[0], persist_ev_[1]};
             launch_dec_persist(pa, st);
-            HIP_CHECK(hipEventRecord(persist_ev_[1], st));
+            prof_events() = ProfEvents();
         } else {
             launch_dec_persist(pa, st);
         }
@@ -1955,7 +1959,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
     }
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    if (use_graph) {
+    if (use_graph && !pk_timed) {
         capturing_ = true;
         HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
         step_body();
@@ -1966,7 +1970,7 @@ std::vector<std::vector<int64_t>> Engine::generate(const std::vector<GenRequest>
 
     HIP_CHECK(hipEventRecord(ev[4], st));
     for (size_t i = 1; i < p.max_new; ++i) {
-        if (use_graph) HIP_CHECK(hipGraphLaunch(gexec, st));
+        if (gexec) HIP_CHECK(hipGraphLaunch(gexec, st));
         else step_body();
         if (span_rec_ && (span_mode_ & SPAN_EVENTS)) read_span_events(i);
         if (pk_timed) {  // the persistent launch's dispatch duration (events recorded around it in the step)

@@ -228,7 +228,7 @@ class Engine {
     void prefill(int B, const std::vector<int>& rows_per_page, const float* x0, int Lmax);
     void decode_step(int B, int Lmax);
     // one page: every decoder layer of a step as one persistent launch (decode_persist.hip) when the model's
-    // shape and dtypes fit it and all 256 workgroups are resident; DSOCR_PERSIST=0 keeps the launch chain
+    // shape and dtypes fit it, all 256 workgroups are resident and DSOCR_PERSIST=1 (opt-in)
     bool persist_ok(int B, int Lmax);
     void ensure_persist();
     MoeDecodeArgs moe_args(int l, int B, float* X);

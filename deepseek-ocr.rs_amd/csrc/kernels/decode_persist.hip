@@ -62,7 +62,7 @@ constexpr int CPH = PK_CPH;               // attention chunks per head
 constexpr int KPW = 8;                    // keys per worker wave
 constexpr int CHMAX = KPW * NWK;          // 56 keys per chunk
 constexpr int PR = 132;                   // partial record granules: m, l, -, -, o[128]
-constexpr int DPR = 6;                    // down partial record per (owner, source): 5 rows + pad
+constexpr int DPR = 6;                    // owner staging per source: the 3 granule pairs that hold its 5 rows
 constexpr int SLOTS = 4;                  // MLP h slots per worker
 static_assert(QR * G == QKVN && OR * G == H && SH_PER * G == IS && RT_PER * G == TOPK * I, "exact split");
 static_assert(SH_PER == NWK && RT_PER == 3 * NWK && QR <= 3 * NWK && OR <= NWK - 2, "worker roles");
@@ -75,7 +75,7 @@ constexpr long O_CTX = O_PART + (long)NH * CPH * PR;
 constexpr long O_XN = O_CTX + H;
 constexpr long O_LG = O_XN + H;
 constexpr long O_DP = O_LG + E;
-constexpr long O_LAYER = O_DP + (long)G * G * DPR;
+constexpr long O_LAYER = O_DP + (long)G * H;  // DP: [source workgroup][H] (contiguous per producer)
 static_assert(O_LAYER % 2 == 0 && O_DP % 2 == 0 && O_PART % 2 == 0 && O_LG % 2 == 0 && PR % 2 == 0, "pairs");
 
 // LDS (floats; every region 16-byte aligned)
@@ -251,7 +251,8 @@ __global__ __launch_bounds__(NT, 1) void dec_persist_kernel(DecPersistArgs a) {
     };
     // poller: pairs lane, lane + 64, ... (< np, at most MAXP per lane) of the granules from gi0 (even) into
     // dst[2 p], dst[2 p + 1]; every load of a pass in flight at once
-    auto gather = [&](auto maxp_tag, long gi0, int np, float* dst) __attribute__((always_inline)) {
+    auto gather = [&](auto maxp_tag, long gi0, int np, float* dst, int pmap = 0) __attribute__((always_inline)) {
+        // pmap = 0: pair p at granule gi0 + 2 p; pmap = 1 (owner reduction): pair p = 3 s + k at gi0 + s H + 2 k
         constexpr int MAXP = decltype(maxp_tag)::value;
         unsigned pend = 0;
 #pragma unroll
@@ -263,7 +264,11 @@ __global__ __launch_bounds__(NT, 1) void dec_persist_kernel(DecPersistArgs a) {
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int k = 0; k < MAXP; ++k)
-                if ((pend >> k) & 1u) v[k] = __builtin_amdgcn_raw_buffer_load_b128(gr, (int)((gi0 + 2 * (lane + 64 * k)) * 8), 0, 16);
+                if ((pend >> k) & 1u) {
+                    const int pp = lane + 64 * k;
+                    const long gi = pmap ? gi0 + (long)(pp / 3) * H + 2 * (pp % 3) : gi0 + 2 * pp;
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(gr, (int)(gi * 8), 0, 16);
+                }
 #pragma unroll
             for (int k = 0; k < MAXP; ++k)
                 if (((pend >> k) & 1u) && v[k].y == tag && v[k].w == tag) {
@@ -452,12 +457,14 @@ __global__ __launch_bounds__(NT, 1) void dec_persist_kernel(DecPersistArgs a) {
             pk_sync();  // #9: the workgroup's partial; ys free
             stamp(7);
             // ======== owner reduction: rows [5 c, 5 c + 5) over the 256 partials, + x_new
-            gather(std::integral_constant<int, 12>(), gl + O_DP + (long)c * G * DPR, G * DPR / 2, ys);
+            // every source's partial is contiguous: rows 5 c .. 5 c + 4 sit in the 3 pairs from granule 5 c & ~1
+            const int odd = (OR * c) & 1;
+            gather(std::integral_constant<int, 12>(), gl + O_DP + ((OR * c) & ~1), G * 3, ys, 1);
             pk_wave_lds();
 #pragma unroll
             for (int r = 0; r < OR; ++r) {
-                float s = ys[lane * DPR + r] + ys[(lane + 64) * DPR + r];
-                s += ys[(lane + 128) * DPR + r] + ys[(lane + 192) * DPR + r];
+                float s = ys[lane * DPR + odd + r] + ys[(lane + 64) * DPR + odd + r];
+                s += ys[(lane + 128) * DPR + odd + r] + ys[(lane + 192) * DPR + odd + r];
                 s = wave_sum(s);
                 const float xo = xnew[r] + s;
                 if (lane == 0) {
@@ -691,13 +698,8 @@ __global__ __launch_bounds__(NT, 1) void dec_persist_kernel(DecPersistArgs a) {
             xb[j] = v;
         }
         pk_sync();  // #9: the workgroup's partial; ys free
-        if (tid < G) {
-            const long rec = gl + O_DP + ((long)tid * G + c) * DPR;
-            const float* yv = xb + OR * tid;
-            put2(rec, yv[0], yv[1]);
-            put2(rec + 2, yv[2], yv[3]);
-            put2(rec + 4, yv[4], 0.f);
-        }
+        // this workgroup's partial of all 1280 outputs, contiguous (coalesced 16-byte write-through stores)
+        for (int pp = tid; pp < H / 2; pp += NWK * 64) put2(gl + O_DP + (long)c * H + 2 * pp, xb[2 * pp], xb[2 * pp + 1]);
         // the next layer's q/k/v rows and K / V chunk stream during the reduction hand-off
         if (l + 1 < a.layers) issue_qkv_kv(l + 1);
     }

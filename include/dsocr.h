@@ -227,7 +227,8 @@ dsocr_status dsocr_engine_spans(const dsocr_engine* e, uint64_t* out, size_t cap
 
 /* ---- one-page persistent decode (decode_persist.hip; no reference counterpart: the reference's decode step is
  * Candle's per-op launches, model/mod.rs:1977-2034).  At B = 1 every decoder layer of a step runs as ONE
- * persistent launch when the model's shape and dtypes fit it (DSOCR_PERSIST=0 keeps the per-layer launch chain).
+ * persistent launch when DSOCR_PERSIST=1 and the model's shape and dtypes fit it (opt-in: measured slower than
+ * the per-layer launch chain).
  * dsocr_engine_set_persist_stamps(e, 1): the next generate times each persistent launch with HIP events and
  * records its phase clocks; dsocr_engine_persist_info then returns whether the last generate used the persistent
  * launch (*used), the launch durations in us (durations[cap_d], *n_launches) and the phase clocks

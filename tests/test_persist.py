@@ -25,9 +25,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def engine(gpu):
+    old = os.environ.get("DSOCR_PERSIST")
+    os.environ["DSOCR_PERSIST"] = "1"  # the persistent step is opt-in (DSOCR_PERSIST=1)
     eng = load_model(ModelLoadArgs(config_path=FULL, synthetic_seed=7, dtype="f16"))
     yield eng
     eng.close()
+    if old is None:
+        os.environ.pop("DSOCR_PERSIST", None)
+    else:
+        os.environ["DSOCR_PERSIST"] = old
 
 
 @pytest.fixture(scope="module")
@@ -46,10 +52,7 @@ def _trace(engine, page, ids, mask, n, persist):
         outs, logits = engine.generate_trace([(ids, mask, page, None)], DecodeParameters(max_new_tokens=n),
                                              ignore_eos=True)
     finally:
-        if old is None:
-            os.environ.pop("DSOCR_PERSIST", None)
-        else:
-            os.environ["DSOCR_PERSIST"] = old
+        os.environ["DSOCR_PERSIST"] = old if old is not None else "1"
     return outs[0], logits[0]
 
 
