@@ -471,6 +471,14 @@ dsocr_status dsocr_resize_bicubic(const uint8_t* src, uint32_t sw, uint32_t sh, 
     });
 }
 
+dsocr_status dsocr_resize_catmull_rom(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw,
+                                      uint32_t dh) {
+    return guarded([&] {
+        if (!src || !dst || !sw || !sh || !dw || !dh) throw std::runtime_error("EINVAL: NULL argument or empty image");
+        dsocr::resize_catmull_rom_fir(src, (int)sw, (int)sh, dst, (int)dw, (int)dh);
+    });
+}
+
 // ---------------------------------------------------------------- kernel-level entry points
 dsocr_status dsocr_k_gemm(int M, int N, int K, const float* A, const void* W, int wdtype, const float* bias, float* C,
                           int act, int accumulate) {

@@ -88,6 +88,7 @@ EXPORTS = [
     "dsocr_dots_embed_device", "dsocr_dots_last_timings", "dsocr_k_attention_bf16", "dsocr_k_gemv_splitk",
     "dsocr_engine_set_spans", "dsocr_engine_spans", "dsocr_k_qkv_attention", "dsocr_k_poll_wait_fits",
     "dsocr_engine_set_persist_stamps", "dsocr_engine_persist_info",
+    "dsocr_resize_catmull_rom",
 ]
 
 _lib = None
@@ -144,6 +145,7 @@ def lib():
     L.dsocr_memcpy_d2h.argtypes = [vp, vp, sz]
     L.dsocr_synth_bf16.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, vp]
     L.dsocr_resize_bicubic.argtypes = [vp, u32, u32, vp, u32, u32]
+    L.dsocr_resize_catmull_rom.argtypes = [vp, u32, u32, vp, u32, u32]
     L.dsocr_k_gemm.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32]
     L.dsocr_k_gemm_f32a.argtypes = [i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32]
     L.dsocr_k_gemm_grouped.argtypes = [i32, i32, i32, vp, i32, vp, vp, i32, C.c_longlong, vp, C.c_longlong, vp, i32, vp, i32,

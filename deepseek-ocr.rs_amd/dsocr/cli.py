@@ -44,7 +44,8 @@ def add_model_args(p: argparse.ArgumentParser) -> None:
     """CommonModelArgs (config/src/args.rs:9-29)."""
     g = p.add_argument_group("Application")
     g.add_argument("--config", metavar="PATH", help="application config (accepted for compatibility; unused)")
-    g.add_argument("--model", metavar="ID", default="deepseek-ocr", help="model id (only deepseek-ocr)")
+    g.add_argument("--model", metavar="ID", default="deepseek-ocr",
+                   help="model id: deepseek-ocr (MI355X engine) or paddleocr-vl (host CPU plumbing path, configs[0])")
     g.add_argument("--model-config", metavar="PATH", help="model config.json (default: bundled DeepSeek-OCR)")
     g.add_argument("--tokenizer", metavar="PATH", help="tokenizer.json (default: synthetic tokenizer)")
     g.add_argument("--weights", metavar="PATH", help="model .safetensors (default: synthetic weights)")
@@ -155,6 +156,8 @@ def run_inference(args, out=sys.stdout, err=sys.stderr) -> int:
             print(msg, file=err, flush=True)
 
     prompt_raw = load_prompt(args)
+    if args.model in PADDLE_IDS:
+        return run_paddle(args, prompt_raw, out, err)
     device = parse_device(args.device)
     if args.model not in ("deepseek-ocr", "deepseek"):
         raise DsocrError(1, f"model `{args.model}` is not served by the MI355X engine (deepseek-ocr only)")
@@ -236,6 +239,57 @@ def run_inference(args, out=sys.stdout, err=sys.stderr) -> int:
                           f"avg={s['avg_ms']:.2f}ms", file=err)
     finally:
         engine.close()
+    return 0
+
+
+PADDLE_IDS = ("paddleocr-vl", "paddleocr", "paddle-ocr-vl")
+
+
+def run_paddle(args, prompt_raw: str, out=sys.stdout, err=sys.stderr) -> int:
+    """ModelKind::PaddleOcrVl on the host CPU (crates/infer-paddleocr model.rs:286-416; BASELINE configs[0]:
+    Candle CPU backend plumbing): dsocr.paddle's numpy restatement with a seeded synthetic checkpoint."""
+    from . import paddle
+
+    def info(msg):
+        if not args.quiet:
+            print(msg, file=err, flush=True)
+
+    if args.device.strip().lower() not in ("cpu", "hip", "cuda") and not args.device.lower().startswith(("hip:", "cuda:")):
+        raise DsocrError(1, f"device {args.device!r} is not supported")
+    if args.weights or args.snapshot:
+        raise DsocrError(1, "the PaddleOCR-VL CPU path runs the seeded synthetic checkpoint only (no weights offline)")
+    t0 = time.perf_counter()
+    engine = paddle.PaddleOcrEngine(args.model_config or paddle.PADDLE_CONFIG, synthetic_seed=args.synthetic_seed)
+    load_ms = (time.perf_counter() - t0) * 1e3
+    info(f"Model ready in {load_ms / 1e3:.2f}s (kind=PaddleOcrVl, device=cpu, weights=synthetic(seed={args.synthetic_seed}))")
+    if args.tokenizer:
+        from tokenizers import Tokenizer
+        tokenizer = Tokenizer.from_file(args.tokenizer)
+    else:
+        tokenizer = paddle.PaddleSyntheticTokenizer(engine.cfg)
+    prompt = render_prompt(args.template, "", prompt_raw)
+    slots = prompt.count("<image>")
+    if slots != len(args.images):
+        raise DsocrError(1, f"prompt includes {slots} <image> tokens but {len(args.images)} image paths were provided")
+    images = [open_image(p) for p in args.images]
+    vision = VisionSettings(args.base_size, args.image_size, args.crop_mode)
+    outcome = engine.decode(tokenizer, prompt, images, vision, decode_params(args))
+    out.write(outcome.text + "\n")
+    info(f"generated {outcome.response_tokens} tokens: {outcome.generated_tokens}")
+    if args.bench or args.bench_output:
+        t = engine.last_timings()
+        events = [_event("model.load", load_ms, model=args.model, kind="PaddleOcrVl", device="cpu"),
+                  _event("vision.compute_embeddings", t["vision_compute_ms"]),
+                  _event("decode.prefill", t["decode_prefill_ms"], tokens=outcome.prompt_tokens),
+                  _event("decode.iterative", t["decode_iterative_ms"], tokens=outcome.response_tokens)]
+        report = stage_report(events)
+        if args.bench_output:
+            with open(args.bench_output, "w") as f:
+                json.dump(report, f, indent=2)
+        if args.bench:
+            for s_ in report["stage_totals"]:
+                print(f"[bench] {s_['stage']:<28} count={s_['count']:<3} total={s_['total_ms']:.2f}ms", file=err)
+    engine.close()
     return 0
 
 

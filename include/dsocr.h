@@ -250,6 +250,10 @@ dsocr_status dsocr_synth_bf16(const char* name, uint64_t seed, uint64_t n, uint1
 /* host: Pillow-exact bicubic resize (vision/resample.rs:101-160), RGB8 HWC */
 dsocr_status dsocr_resize_bicubic(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw,
                                   uint32_t dh);
+/* fast_image_resize Convolution(CatmullRom) on RGB8 HWC (host; the dots.ocr and PaddleOCR-VL preprocessing resize,
+ * crates/infer-paddleocr/src/vision/preprocess.rs:223-243, infer-dots vision/preprocess.rs) */
+dsocr_status dsocr_resize_catmull_rom(const uint8_t* src, uint32_t sw, uint32_t sh, uint8_t* dst, uint32_t dw,
+                                      uint32_t dh);
 
 /* ---- kernel-level entry points (device pointers, default stream) for parity tests */
 /* C[M][N] = act(A[M][K] . W[N][K]^T + bias) (+ C if accumulate); wdtype 0 = bf16, 1 = f16 */
