@@ -130,6 +130,66 @@ def cpu_model():
     return None
 
 
+CORES_ALL_STEPS = 16       # decode forwards timed by the all-CPU leg (scaled to the page's max_new - 1)
+CORES_ALL_DEADLINE_S = 150  # the all-CPU leg's child process is stopped after this
+
+
+def cpu_quota():
+    """CPUs the job's cgroup may use (cpu.max quota / period), or None when unlimited / unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_leg(threads, page, tok_ids, mask, max_new, steps):
+    """One page of the workload on `threads` OpenMP threads of the C++ restatement (oracle/cpu_ref.cpp): the
+    vision tower (cv_features), then the 706-token prefill and (steps - 1) decode forwards (cr_generate with the
+    greedy 20-gram ban), the decode time scaled to the page's (max_new - 1) forwards when steps < max_new."""
+    import numpy as np
+
+    import dsocr
+    from oracle import cpu_ref
+    from oracle.weights import Weights
+    cfg = json.load(open(dsocr.FULL_CONFIG))
+    cpu_ref.set_threads(threads)
+    t = time.time()
+    cv = cpu_ref.CpuVision(cfg, Weights(seed=0, dtype="f16"), threads=threads)
+    log(f"[cpu] {threads} threads: C++ vision tower loaded in {time.time() - t:.1f}s")
+    t0 = time.time()
+    emb, _ = cv.embeddings(page)
+    vision_s, vis_ms = time.time() - t0, dict(cv.last_ms)
+    del cv
+    log(f"[cpu] {threads} threads: vision {vision_s:.2f}s")
+    t = time.time()
+    cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
+    log(f"[cpu] {threads} threads: C++ decoder loaded in {time.time() - t:.1f}s, decoding {steps - 1} steps")
+    ids, ms = cr.generate(np.asarray(tok_ids, np.int64), np.asarray(mask, np.uint8), emb, steps, ngram=20)
+    cr.close()
+    prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3 * (max_new - 1) / max(1, steps - 1)
+    page_s = vision_s + prefill_s + decode_s
+    scaled = "" if steps == max_new else f", scaled from {steps - 1} timed steps"
+    log(f"[cpu] {threads} threads: vision {vision_s:.2f}s prefill {prefill_s:.2f}s decode {decode_s:.2f}s{scaled}")
+    return {"value": 1.0 / page_s, "unit": "pages/s", "cores": threads,
+            "decode_tok_s": (max_new - 1) / decode_s,
+            "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
+            "vision_ms": {k: round(v, 1) for k, v in vis_ms.items()},
+            "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (C++, incl. numpy preprocessing) + "
+                      f"prefill {prefill_s:.2f}s ({len(tok_ids)} tok, C++) + {max_new - 1} decode steps "
+                      f"{decode_s:.2f}s (C++, {decode_s / max(1, max_new - 1) * 1e3:.1f} ms/step{scaled}), "
+                      f"{threads} threads; first ids {[int(i) for i in ids[:4]]}"}
+
+
+def cpu_leg_child(d):
+    """`bench.py --cpu-leg DIR`: the all-CPU leg in its own process (no GPU: nothing here touches HIP), inputs
+    from DIR/leg.npz, the run record to DIR/leg.json."""
+    import numpy as np
+    z = np.load(os.path.join(d, "leg.npz"))
+    run = cpu_leg(int(z["threads"]), z["page"], z["tok_ids"], z["mask"], int(z["max_new"]), int(z["steps"]))
+    json.dump(run, open(os.path.join(d, "leg.json"), "w"))
+
+
 def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
     """The repo's C++ / OpenMP CPU restatement of the page path (oracle/cpu_ref.cpp, test/bench infrastructure)
     timed on rank 0's host cores, one whole page of the workload: the vision tower (cv_features: SAM-ViTDet-B +
@@ -137,57 +197,45 @@ def cpu_baseline(pages, tok_ids, mask, max_new, decode_steps=0):
     the decoder (cr_generate: the 706-token prefill and ALL (max_new - 1) decode forwards with the greedy
     20-gram-ban selection), timed whole (no extrapolation).  Threads: OMP_NUM_THREADS (the job's CPU share: 16 on
     the GPU box).  Stage sums are reported like the reference's bench (crates/cli/src/bench.rs:200-260: vision,
-    prefill, decode); the vision embeddings are checked against the numpy oracle's in tests/test_cpu_ref.py."""
-    import numpy as np
+    prefill, decode); the vision embeddings are checked against the numpy oracle's in tests/test_cpu_ref.py.
+    `cores_all`: the same page on every CPU the process may run on (allowed_cpus), in a child process with
+    OMP_WAIT_POLICY=passive (256 spinning threads against a 16-CPU cgroup quota stall on every barrier), its
+    decode a bounded sample of CORES_ALL_STEPS forwards, stopped after CORES_ALL_DEADLINE_S."""
+    import subprocess
+    import tempfile
 
-    import dsocr
-    from oracle import cpu_ref
-    from oracle.weights import Weights
+    import numpy as np
     allowed = len(os.sched_getaffinity(0))
     threads = int(os.environ.get("OMP_NUM_THREADS") or allowed)
-    cfg = json.load(open(dsocr.FULL_CONFIG))
-    # the same page at two thread counts: the job's share (OMP_NUM_THREADS, 16 on the GPU box) and every CPU the
-    # process may run on (allowed_cpus), each timed whole; the first is `value`, the second `cores_all`
-    counts = [threads] + ([allowed] if allowed != threads and not os.environ.get("DSOCR_CPU_ONE_COUNT") else [])
-    t = time.time()
-    cv = cpu_ref.CpuVision(cfg, Weights(seed=0, dtype="f16"), threads=threads)
-    log(f"[cpu] C++ vision tower loaded in {time.time() - t:.1f}s ({threads} threads)")
-    vis = []
-    for n in counts:
-        cpu_ref.set_threads(n)
-        t0 = time.time()
-        emb, _ = cv.embeddings(pages[0])
-        vis.append((time.time() - t0, dict(cv.last_ms)))
-    del cv
-    t = time.time()
-    cpu_ref.set_threads(threads)
-    cr = cpu_ref.CpuRef(cfg, Weights(seed=0, dtype="f16"), threads=threads)
-    log(f"[cpu] C++ decoder loaded in {time.time() - t:.1f}s ({threads} threads)")
-    runs = []
-    for i, n in enumerate(counts):
-        cpu_ref.set_threads(n)
-        ids, ms = cr.generate(np.asarray(tok_ids, np.int64), np.asarray(mask, np.uint8), emb, max_new, ngram=20)
-        vision_s, vis_ms = vis[i]
-        prefill_s, decode_s = ms["prefill_ms"] / 1e3, ms["decode_ms"] / 1e3
-        page_s = vision_s + prefill_s + decode_s
-        log(f"[cpu] {n} threads: vision {vision_s:.2f}s prefill {prefill_s:.2f}s decode {decode_s:.2f}s")
-        runs.append({"value": 1.0 / page_s, "unit": "pages/s", "cores": n,
-                     "decode_tok_s": (max_new - 1) / decode_s,
-                     "stage_s": {"vision": round(vision_s, 3), "prefill": round(prefill_s, 3), "decode": round(decode_s, 3)},
-                     "vision_ms": {k: round(v, 1) for k, v in vis_ms.items()},
-                     "sample": f"1 synthetic 1024x1024 page: vision {vision_s:.2f}s (C++, incl. numpy preprocessing) + "
-                               f"prefill {prefill_s:.2f}s ({len(tok_ids)} tok, C++) + {max_new - 1} decode steps "
-                               f"{decode_s:.2f}s (C++, {decode_s / max(1, max_new - 1) * 1e3:.1f} ms/step), {n} threads; "
-                               f"first ids {ids[:4]}"})
-    cr.close()
-    out = dict(runs[0])
+    out = cpu_leg(threads, pages[0], tok_ids, mask, max_new, max_new)
     out.update({"kind": "cpp",
                 "port": "oracle/cpu_ref.cpp: C++ / OpenMP restatement of the whole page path (vision tower + decoder, "
                         "AVX-512 micro-kernels, f32 math); the Rust reference cannot be built here",
-                "host_cpus": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model(),
+                "host_cpus": os.cpu_count(), "allowed_cpus": allowed, "cpu_quota_cpus": cpu_quota(),
+                "cpu_model": cpu_model(),
                 "threads_note": "value: the job's CPU share (OMP_NUM_THREADS); cores_all: every allowed CPU"})
-    if len(runs) > 1:
-        out["cores_all"] = runs[1]
+    if allowed == threads or os.environ.get("DSOCR_CPU_ONE_COUNT"):
+        return out
+    with tempfile.TemporaryDirectory() as d:
+        np.savez(os.path.join(d, "leg.npz"), page=np.asarray(pages[0]), tok_ids=np.asarray(tok_ids, np.int64),
+                 mask=np.asarray(mask, np.uint8), threads=allowed, max_new=max_new,
+                 steps=min(max_new, CORES_ALL_STEPS + 1))
+        env = dict(os.environ, OMP_NUM_THREADS=str(allowed), OMP_WAIT_POLICY="passive")
+        log(f"[cpu] {allowed} threads: child process (deadline {CORES_ALL_DEADLINE_S} s)")
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-leg", d], env=env, cwd=ROOT)
+        t0 = time.time()
+        while p.poll() is None and time.time() - t0 < CORES_ALL_DEADLINE_S:
+            time.sleep(1)
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+            log(f"[cpu] {allowed} threads: stopped at the {CORES_ALL_DEADLINE_S} s deadline")
+            out["cores_all"] = {"cores": allowed, "value": None, "status": f"not finished in {CORES_ALL_DEADLINE_S} s "
+                                f"(cgroup quota {cpu_quota()} CPUs)"}
+        elif p.returncode == 0:
+            out["cores_all"] = json.load(open(os.path.join(d, "leg.json")))
+        else:
+            out["cores_all"] = {"cores": allowed, "value": None, "status": f"child exited {p.returncode}"}
     return out
 
 
@@ -511,6 +559,15 @@ def decode_roofline(eng, batch, params, ppg, args):
                 "frac": round(p["bytes"] / (p["ctx_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if p["ctx_us"] > 0 else None,
                 "isolated_us": round(p["avg_us"], 3), "replay_us": round(p["replay_us"], 3)}
     gu = ctx_line("moe_gateup")
+    dn = ctx_line("moe_down")
+    # the whole MoE of a layer as SURVEY 8(d) prices it: gate + up + down bytes over both launches' durations
+    tot_b, tot_us = gu["bytes"] + dn["bytes"], gu["ctx_us"] + dn["ctx_us"]
+    moe_total = {"bytes_per_layer": tot_b, "ctx_us": round(tot_us, 3),
+                 "GB/s": round(tot_b / (tot_us * 1e-6) / 1e9, 1) if tot_us > 0 else None,
+                 "frac": round(tot_b / (tot_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if tot_us > 0 else None}
+    if chain.get("moe_gateup") and chain.get("moe_down"):
+        cu = chain["moe_gateup"]["avg_us"] + chain["moe_down"]["avg_us"]
+        moe_total.update({"chain_us": round(cu, 3), "chain_frac": round(tot_b / (cu * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)})
     runs = ("b1",) if ppg == 1 else (("b8",) if args.text_pages and ppg == 8 else (("b8i",) if ppg == 8 else ()))
     traffic, ratio = pmc_traffic(kernel, runs=runs)
     return {"bound": "hbm", "achieved": gu["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -532,6 +589,7 @@ def decode_roofline(eng, batch, params, ppg, args):
             "in_kernel_waves": waves,
             "down_kernel": prof["moe_down_kernel"],
             "in_context": {k: ctx_line(k) for k in ("moe_gateup", "moe_down", "attention")},
+            "moe_total": moe_total,
             "others": {k: {"avg_us": round(prof[k]["avg_us"], 2), "bytes": prof[k]["bytes"],
                            "GB/s": round(prof[k]["bytes"] / (prof[k]["avg_us"] * 1e-6) / 1e9, 1)}
                        for k in ("lm_head", "lm_head_screened", "qkv", "o_proj", "router")
@@ -541,6 +599,8 @@ def decode_roofline(eng, batch, params, ppg, args):
 
 
 def main():
+    if "--cpu-leg" in sys.argv:  # the all-CPU baseline leg's child process (cpu_baseline)
+        return cpu_leg_child(sys.argv[sys.argv.index("--cpu-leg") + 1])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)

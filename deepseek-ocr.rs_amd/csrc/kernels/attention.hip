@@ -400,6 +400,11 @@ size_t attention_causal_part_floats(int n_seq, int heads, int L, int hd) {
 // read as the V^T operand through ds_read_b64_tr_b16; K / V planes split once per tile at staging
 // (the next tile's f32 loads in registers under the current tile's compute); SAM's decomposed rel-pos
 // bias from the block's table rows in LDS as in attention_fwd2.
+// Eight waves per block, two per SIMD: waves w and w + 4 own the same 32 queries and take the two 32-key
+// halves of every 64-key tile, each with its own running (m, l, O); the pair combines through LDS at the
+// end (flash-decoding combine of two pieces).  One wave's softmax and plane splits then run under the
+// other wave's MFMAs on the same SIMD (the block's LDS — the rel-pos rows of its 128 queries, 66 KB for
+// the 64x64 SAM grid — allows one block per CU, so a second wave per SIMD has to come from the block).
 typedef __bf16 bf16x8s_t __attribute__((ext_vector_type(8)));
 typedef short v4i16s_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16s_t lds_v4i16s;
@@ -411,14 +416,18 @@ __device__ __forceinline__ void split3_bf16(float v, __bf16& h, __bf16& m, __bf1
     l = (__bf16)(r1 - (float)m);
 }
 
+constexpr int AS_NT = 512;
+
 template <bool REL>
-__global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
+__global__ __launch_bounds__(AS_NT, 1) void attention_split_kernel(AttnArgs a) {
     constexpr int HD = 64, KT = 64;
     constexpr int KP = HD + 8, VP = HD + 32;   // plane row pitches (bf16): VP keeps 4 rows on distinct banks
     constexpr int QS = HD / 16, DC = HD / 32;
-    constexpr int F4 = KT * HD / 4 / 256;      // float4 per thread per operand per tile
+    constexpr int F4 = KT * HD / 4 / AS_NT;    // float4 per thread per operand per tile
+    constexpr int OW = DC * 16 + 2;            // floats a key-half wave hands its partner: O, m, l
     __shared__ __attribute__((aligned(16))) uint16_t Kp[3][KT][KP];
     __shared__ __attribute__((aligned(16))) uint16_t Vp[3][KT][VP];
+    static_assert(sizeof(Vp) >= 4 * OW * 64 * sizeof(float), "combine records reuse the V planes");
     __shared__ int rbh[KT], rbw[KT];
     extern __shared__ __attribute__((aligned(16))) float rbs[];
     const int s = blockIdx.z, h = blockIdx.y;
@@ -426,12 +435,13 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
     const int qb0 = blockIdx.x * (4 * AT_Q);
     if (qb0 >= len) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qg = wave & 3, kh = wave >> 2;   // query group, key half of each tile
     const int half = lane >> 5, l32 = lane & 31;
     const int kvh = h / (a.heads / a.kv_heads);
     const float* Q = a.q.ptr + (long)s * a.L * a.q.row_stride + (long)h * a.q.head_stride;
     const float* K = a.k.ptr + (long)s * a.L * a.k.row_stride + (long)kvh * a.k.head_stride;
     const float* V = a.v.ptr + (long)s * a.L * a.v.row_stride + (long)kvh * a.v.head_stride;
-    const int q_lane = qb0 + wave * AT_Q + l32;
+    const int q_lane = qb0 + qg * AT_Q + l32;
     const bool q_valid = q_lane < len;
     // this lane's query as three planes: dims 16 st + 8 half + j
     bf16x8s_t qh[QS], qm[QS], ql[QS];
@@ -454,11 +464,11 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
     const float* rb = nullptr;
     if (REL) {
         const float* tab = a.relbias + (((long)s * a.heads + h) * a.L) * R;
-        for (int i = tid; i < 4 * AT_Q * R; i += 256) {
+        for (int i = tid; i < 4 * AT_Q * R; i += AS_NT) {
             const int qq = i / R, j = i % R;
             rbs[qq * RP + j] = tab[(long)min(qb0 + qq, len - 1) * R + j];
         }
-        rb = rbs + (wave * AT_Q + l32) * RP;
+        rb = rbs + (qg * AT_Q + l32) * RP;
     }
     const int i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3, gd = 16 * ((lane >> 4) & 1);
     // next tile's K / V in registers: buffer loads bounded at the sequence's last key (keys past it read
@@ -470,7 +480,7 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
     const int vo = ((tid / (HD / 4)) * a.v.row_stride + (tid % (HD / 4)) * 4) * 4;
 #define AS_GLOAD(K0)                                                                           \
     _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
-        const int kr_ = (K0) + j * (256 / (HD / 4));                                           \
+        const int kr_ = (K0) + j * (AS_NT / (HD / 4));                                         \
         rk[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsk, ko + kr_ * a.k.row_stride * 4, 0, 0)); \
         rv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsv, vo + kr_ * a.v.row_stride * 4, 0, 0)); \
     }
@@ -491,7 +501,7 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
     }
 #define AS_LSTORE(K0)                                                                          \
     _Pragma("unroll") for (int j = 0; j < F4; ++j) {                                           \
-        const int f = tid + 256 * j;                                                           \
+        const int f = tid + AS_NT * j;                                                         \
         const int kr = f / (HD / 4), c4 = (f % (HD / 4)) * 4;                                  \
         AS_PUT(Kp, kr, c4, rk[j]);                                                             \
         AS_PUT(Vp, kr, c4, rv[j]);                                                             \
@@ -508,64 +518,55 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
         for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
     const float c2 = (REL ? 1.f : a.scale) * 1.4426950408889634f;  // score -> log2 units
     float m_run = -INFINITY, l_run = 0.f;
+    const int u = kh;  // this wave's 32 keys of every tile: 32 u .. 32 u + 31
     AS_GLOAD(0);
     AS_LSTORE(0);
     __syncthreads();
     for (int k0 = 0; k0 < len; k0 += KT) {
         AS_GLOAD(k0 + KT);  // the next tile in flight under this one
-        f32x16 sc[2];
+        f32x16 sc;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sc[u][r] = 0.f;
-#pragma unroll
-            for (int st = 0; st < QS; ++st) {
-                const int kr = u * 32 + l32, kc = 16 * st + 8 * half;
-                const bf16x8s_t kh = *reinterpret_cast<const bf16x8s_t*>(&Kp[0][kr][kc]);
-                const bf16x8s_t km = *reinterpret_cast<const bf16x8s_t*>(&Kp[1][kr][kc]);
-                const bf16x8s_t kl = *reinterpret_cast<const bf16x8s_t*>(&Kp[2][kr][kc]);
-                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[st], sc[u], 0, 0, 0);
-                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(km, qm[st], sc[u], 0, 0, 0);
-                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], sc[u], 0, 0, 0);
-                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(km, qh[st], sc[u], 0, 0, 0);
-                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qm[st], sc[u], 0, 0, 0);
-                sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], sc[u], 0, 0, 0);
-            }
+        for (int st = 0; st < QS; ++st) {
+            const int kr = u * 32 + l32, kc = 16 * st + 8 * half;
+            const bf16x8s_t kh8 = *reinterpret_cast<const bf16x8s_t*>(&Kp[0][kr][kc]);
+            const bf16x8s_t km8 = *reinterpret_cast<const bf16x8s_t*>(&Kp[1][kr][kc]);
+            const bf16x8s_t kl8 = *reinterpret_cast<const bf16x8s_t*>(&Kp[2][kr][kc]);
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl8, qh[st], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(km8, qm[st], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8, ql[st], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(km8, qh[st], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8, qm[st], sc, 0, 0, 0);
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8, qh[st], sc, 0, 0, 0);
         }
-        // softmax in the log2 domain (p = 2^(v c - m), one FMA before the exponential; every tile holds a
-        // valid key, so m is finite after the first tile and alpha = 0 there); SAM adds its rel-pos bias
-        // to the scaled score first, as the reference does
+        // softmax in the log2 domain (p = 2^(v c - m), one FMA before the exponential); SAM adds its rel-pos
+        // bias to the scaled score first, as the reference does.  A key half can be all past the sequence
+        // (the last tile, or every tile when len <= 32): m stays -inf and exponentials are taken against 0.
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int kl = u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                if (REL) sc[u][r] = fmaf(sc[u][r], a.scale, rb[rbh[kl]] + rb[rbw[kl]]);
-            }
+        for (int r = 0; r < 16; ++r) {
+            const int kl = u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            if (REL) sc[r] = fmaf(sc[r], a.scale, rb[rbh[kl]] + rb[rbw[kl]]);
+        }
         if (k0 + KT > len) {  // the last, partial tile
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= len) sc[u][r] = -INFINITY;
+            for (int r = 0; r < 16; ++r)
+                if (k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= len) sc[r] = -INFINITY;
         }
         float tmax = -INFINITY;
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[r]);
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float m_new = fmaxf(m_run, tmax * c2);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        const float m_ref = m_new == -INFINITY ? 0.f : m_new;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_ref);
         float psum = 0.f;
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c2, -m_new));
-                sc[u][r] = p;
-                psum += p;
-            }
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[r], c2, -m_ref));
+            sc[r] = p;
+            psum += p;
+        }
         psum += __shfl_xor(psum, 32, 64);
         l_run = l_run * alpha + psum;
         m_run = m_new;
@@ -575,59 +576,73 @@ __global__ __launch_bounds__(256, 1) void attention_split_kernel(AttnArgs a) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
         }
-        // O^T += V^T . P^T: the lane's P registers 8t .. 8t+7 of half u hold keys 32u + 16t + 4 half +
-        // {0..3, 8..11}; the transposed reads fetch exactly those rows of each V plane
+        // O^T += V^T . P^T: the lane's P registers 8t .. 8t+7 hold keys 32u + 16t + 4 half + {0..3, 8..11};
+        // the transposed reads fetch exactly those rows of each V plane
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int t = 0; t < 2; ++t) {
+            // p = hi + mid + lo exactly by truncation (low 16 bits cleared, twice; the rest has <= 8
+            // significant bits), two bf16 of a plane packed per register by one byte permute
+            f32x4 phv, pmv, plv;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                // p = hi + mid + lo exactly by truncation (low 16 bits cleared, twice; the rest has <= 8
-                // significant bits), two bf16 of a plane packed per register by one byte permute
-                f32x4 phv, pmv, plv;
+            for (int q = 0; q < 4; ++q) {
+                const float p0 = sc[8 * t + 2 * q], p1 = sc[8 * t + 2 * q + 1];
+                const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
+                const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
+                const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+                const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+                phv[q] = __uint_as_float(__builtin_amdgcn_perm(b1, b0, 0x07060302u));
+                pmv[q] = __uint_as_float(__builtin_amdgcn_perm(c1, c0, 0x07060302u));
+                plv[q] = __uint_as_float(__builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u));
+            }
+            const bf16x8s_t ph = __builtin_bit_cast(bf16x8s_t, phv), pm = __builtin_bit_cast(bf16x8s_t, pmv),
+                            pl = __builtin_bit_cast(bf16x8s_t, plv);
+            const int kr0 = u * 32 + 16 * t + 4 * half + tq;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float p0 = sc[u][8 * t + 2 * q], p1 = sc[u][8 * t + 2 * q + 1];
-                    const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
-                    const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
-                    const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
-                    const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
-                    phv[q] = __uint_as_float(__builtin_amdgcn_perm(b1, b0, 0x07060302u));
-                    pmv[q] = __uint_as_float(__builtin_amdgcn_perm(c1, c0, 0x07060302u));
-                    plv[q] = __uint_as_float(__builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u));
+            for (int c = 0; c < DC; ++c) {
+                const int d0 = c * 32 + gd + 4 * tp;
+                bf16x8s_t vf[3];
+#pragma unroll
+                for (int pl_ = 0; pl_ < 3; ++pl_) {
+                    const v4i16s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16s*)&Vp[pl_][kr0][d0]);
+                    const v4i16s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16s*)&Vp[pl_][kr0 + 8][d0]);
+                    __builtin_memcpy(&vf[pl_], &lo, 8);
+                    __builtin_memcpy(reinterpret_cast<char*>(&vf[pl_]) + 8, &hi, 8);
                 }
-                const bf16x8s_t ph = __builtin_bit_cast(bf16x8s_t, phv), pm = __builtin_bit_cast(bf16x8s_t, pmv),
-                                pl = __builtin_bit_cast(bf16x8s_t, plv);
-                const int kr0 = u * 32 + 16 * t + 4 * half + tq;
-#pragma unroll
-                for (int c = 0; c < DC; ++c) {
-                    const int d0 = c * 32 + gd + 4 * tp;
-                    bf16x8s_t vf[3];
-#pragma unroll
-                    for (int pl_ = 0; pl_ < 3; ++pl_) {
-                        const v4i16s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16s*)&Vp[pl_][kr0][d0]);
-                        const v4i16s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16s*)&Vp[pl_][kr0 + 8][d0]);
-                        __builtin_memcpy(&vf[pl_], &lo, 8);
-                        __builtin_memcpy(reinterpret_cast<char*>(&vf[pl_]) + 8, &hi, 8);
-                    }
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2], ph, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1], pm, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], pl, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1], ph, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], pm, o[c], 0, 0, 0);
-                    o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], ph, o[c], 0, 0, 0);
-                }
+                o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2], ph, o[c], 0, 0, 0);
+                o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1], pm, o[c], 0, 0, 0);
+                o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], pl, o[c], 0, 0, 0);
+                o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[1], ph, o[c], 0, 0, 0);
+                o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], pm, o[c], 0, 0, 0);
+                o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[0], ph, o[c], 0, 0, 0);
             }
         }
         __syncthreads();  // every wave is done with the tile before it is refilled
         AS_LSTORE(k0 + KT);
         __syncthreads();
     }
-    if (q_valid) {
+    // combine the two key halves: the second half's waves hand (O, m, l) over through the V planes' LDS
+    // (no wave reads a plane after the loop's last barrier), lane-contiguous records
+    float* rec = reinterpret_cast<float*>(&Vp[0][0][0]) + qg * OW * 64 + lane;
+    if (kh == 1) {
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) rec[(c * 16 + r) * 64] = o[c][r];
+        rec[(DC * 16) * 64] = m_run;
+        rec[(DC * 16 + 1) * 64] = l_run;
+    }
+    __syncthreads();
+    if (kh == 0 && q_valid) {
+        const float m_b = rec[(DC * 16) * 64], l_b = rec[(DC * 16 + 1) * 64];
+        const float m = fmaxf(m_run, m_b);
+        const float a0 = __builtin_amdgcn_exp2f(m_run - m), a1 = __builtin_amdgcn_exp2f(m_b - m);
+        const float inv = 1.f / (l_run * a0 + l_b * a1);
         float* op = a.o + (long)s * a.L * a.o_row_stride + (long)q_lane * a.o_row_stride + (long)h * a.o_head_stride;
 #pragma unroll
         for (int c = 0; c < DC; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) op[c * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = o[c][r] / l_run;
+            for (int r = 0; r < 16; ++r)
+                op[c * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = (o[c][r] * a0 + rec[(c * 16 + r) * 64] * a1) * inv;
     }
 #undef AS_GLOAD
 #undef AS_PUT
@@ -664,8 +679,8 @@ void launch_attention(const AttnArgs& a, hipStream_t s) {
             attr_s = true;
         }
         if (lds <= 90 * 1024) {
-            if (rel) hipLaunchKernelGGL((attention_split_kernel<true>), grid, dim3(256), lds, s, b);
-            else hipLaunchKernelGGL((attention_split_kernel<false>), grid, dim3(256), 0, s, b);
+            if (rel) hipLaunchKernelGGL((attention_split_kernel<true>), grid, dim3(AS_NT), lds, s, b);
+            else hipLaunchKernelGGL((attention_split_kernel<false>), grid, dim3(AS_NT), 0, s, b);
             return;
         }
     }

@@ -193,7 +193,7 @@ def _attn_ref(q, k, v, scale, causal=False, bias=None):
 
 @pytest.mark.parametrize("n_seq,L,heads,hd,causal", [(2, 257, 16, 64, 0), (3, 101, 4, 32, 0), (1, 706, 10, 128, 1),
                                                      (5, 196, 12, 64, 0), (2, 33, 2, 128, 1), (3, 300, 4, 64, 1),
-                                                     (1, 1217, 10, 128, 1)])
+                                                     (1, 1217, 10, 128, 1), (2, 20, 4, 64, 0), (1, 97, 3, 64, 0)])
 def test_attention(gpu, n_seq, L, heads, hd, causal):
     """Flash attention vs f64 math (block.rs:1504-1526 causal prefill; sam.rs / clip.rs bidirectional).  The
     causal cases run the prefill's key-piece form (one block per (128-query block, 128-key piece) + the piece

@@ -36,8 +36,12 @@ def main():
     ap.add_argument("--text-pages", action="store_true")
     ap.add_argument("--variant", action="append", required=True, help="name:ENV=VAL,ENV2=VAL")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ab_order.json"))
+    ap.add_argument("--lib", default=None, help="another libdsocr.so build (A/B of two kernel versions)")
     args = ap.parse_args()
     import dsocr
+    if args.lib:
+        import dsocr._lib
+        dsocr._lib.LIB_PATH = os.path.abspath(args.lib)
     from dsocr import DecodeParameters, ModelLoadArgs, Page, VisionSettings, build_prompt_tokens, load_model
     from dsocr.synth import BENCH_PROMPT, SyntheticTokenizer, synthetic_page, text_page_prompt
     variants = [parse_variant(v) for v in args.variant]

@@ -19,8 +19,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pages", type=int, default=1)
+    ap.add_argument("--lib", default=None, help="another libdsocr.so build (A/B of two kernel versions)")
     a = ap.parse_args()
     import dsocr
+    if a.lib:
+        import dsocr._lib
+        dsocr._lib.LIB_PATH = os.path.abspath(a.lib)
     from dsocr import DecodeParameters, ModelLoadArgs, Page, VisionSettings, build_prompt_tokens, load_model
     from dsocr.synth import BENCH_PROMPT, SyntheticTokenizer, synthetic_page
     eng = load_model(ModelLoadArgs(config_path=dsocr.FULL_CONFIG, synthetic_seed=0, dtype="f16", device=0))
