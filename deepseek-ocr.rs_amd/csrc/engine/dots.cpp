@@ -22,8 +22,6 @@ namespace dsocr {
 void launch_dots_rmsnorm(const void* x, int in_f32, long rows, int D, const float* w, float eps, void* y, hipStream_t s);
 void launch_dots_layernorm(const void* x, long rows, int D, const float* w, const float* b, float eps, void* y,
                            hipStream_t s);
-void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
-                      int out_bf16, hipStream_t s);
 void launch_dots_swiglu(const void* gu, long N, int I, void* h, hipStream_t s);
 void launch_dots_rope_qk(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
                          hipStream_t s);
@@ -347,11 +345,7 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
     void* X = ws("d_x", (size_t)N * D * 2);
     void* XN = ws("d_xn", (size_t)N * D * 2);
     void* QKV = ws("d_qkv", (size_t)N * 3 * D * 2);
-    // DSOCR_DOTS_ATTN=f32 selects the f32-MFMA attention (f32 copies of q / k / v) for comparison
-    const bool attn_f32 = getenv("DSOCR_DOTS_ATTN") && std::string(getenv("DSOCR_DOTS_ATTN")) == "f32";
-    float* QKVf = attn_f32 ? (float*)ws("d_qkvf", (size_t)N * 3 * D * 4) : nullptr;
-    float* CTX = attn_f32 ? (float*)ws("d_ctx", (size_t)N * D * 4) : nullptr;
-    void* QKVr = (attn_f32 || rope_fused_) ? nullptr : ws("d_qkvr", (size_t)N * 3 * D * 2);
+    void* QKVr = rope_fused_ ? nullptr : ws("d_qkvr", (size_t)N * 3 * D * 2);
     void* CTXb = ws("d_ctxb", (size_t)N * D * 2);
     void* GU = swiglu_fused_ ? nullptr : ws("d_gu", (size_t)N * 2 * I * 2);
     void* HB = ws("d_h", (size_t)N * I * 2);
@@ -373,7 +367,7 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
         // DotsVisionBlock::forward (305-315) / VisionAttention::forward (364-431)
         launch_dots_rmsnorm(X, 0, N, D, b.n1, (float)c_.eps, XN, st);
         // the rotary of q / k in the q|k|v GEMM's epilogue (rope_fused_) or by dots_rope8 into QKVr below
-        const bool rope_in_gemm = rope_fused_ && !attn_f32;
+        const bool rope_in_gemm = rope_fused_;
         if (rope_in_gemm) {
             GemmBf16Args g;
             g.M = (int)N; g.N = 3 * D; g.K = D; g.A = XN; g.lda = D; g.W = b.qkv; g.ldw = D; g.bias = b.b_qkv;
@@ -385,34 +379,19 @@ void DotsVision::embed_device(const float* d_patches, int gt, int gh, int gw, fl
         }
         const bool timed = l < time_layers;
         const float scale = (float)(1.0 / std::sqrt((double)hd));
-        if (attn_f32) {
-            // f32 flash attention on f32 copies of the bf16 q / k / v (f32 MFMA; the comparison path)
-            launch_dots_rope(QKV, N, H, hd, d_cos, d_sin, QKVf, 0, st);
-            AttnArgs a;
-            a.q = {QKVf, 3L * D, hd, nullptr};
-            a.k = {QKVf + D, 3L * D, hd, nullptr};
-            a.v = {QKVf + 2 * D, 3L * D, hd, nullptr};
-            a.o = CTX; a.o_row_stride = D; a.o_head_stride = hd;
-            a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
-            if (timed) HIP_CHECK(hipEventRecord(a0, st));
-            launch_attention(a, st);
-            if (timed) HIP_CHECK(hipEventRecord(a1, st));
-            launch_dots_to_bf16(CTX, N, D, D, CTXb, D, st);
-        } else {
-            // bf16 matrix cores with the same f32 math (attention_bf16.hip): rotated q / k stay bf16
-            // (exactly the reference's rounding), the context is written as the bf16 tensor it becomes
-            // rotated q / k into QKVr; v is read where the qkv GEMM wrote it
-            if (!rope_in_gemm) launch_dots_rope_qk(QKV, N, H, hd, d_cos, d_sin, QKVr, st);
-            const uint16_t* QK = (const uint16_t*)(rope_in_gemm ? QKV : QKVr);
-            AttnBf16Args a;
-            a.q = QK; a.k = QK + D; a.v = (const uint16_t*)QKV + 2 * D;
-            a.q_rs = a.k_rs = a.v_rs = 3L * D; a.q_hs = a.k_hs = a.v_hs = hd;
-            a.o = CTXb; a.o_rs = D; a.o_hs = hd; a.o_bf16 = 1;
-            a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
-            a.pv_planes = dots_pv_planes();
-            if (timed) prof_events() = ProfEvents{a0, a1};  // the launch's own dispatch timestamps
-            launch_attention_bf16(a, st);
-        }
+        // bf16 matrix cores with the same f32 math (attention_bf16.hip): rotated q / k stay bf16
+        // (exactly the reference's rounding), the context is written as the bf16 tensor it becomes
+        // rotated q / k into QKVr; v is read where the qkv GEMM wrote it
+        if (!rope_in_gemm) launch_dots_rope_qk(QKV, N, H, hd, d_cos, d_sin, QKVr, st);
+        const uint16_t* QK = (const uint16_t*)(rope_in_gemm ? QKV : QKVr);
+        AttnBf16Args a;
+        a.q = QK; a.k = QK + D; a.v = (const uint16_t*)QKV + 2 * D;
+        a.q_rs = a.k_rs = a.v_rs = 3L * D; a.q_hs = a.k_hs = a.v_hs = hd;
+        a.o = CTXb; a.o_rs = D; a.o_hs = hd; a.o_bf16 = 1;
+        a.n_seq = gt; a.L = (int)per; a.heads = H; a.kv_heads = H; a.hd = hd; a.scale = scale;
+        a.pv_planes = dots_pv_planes();
+        if (timed) prof_events() = ProfEvents{a0, a1};  // the launch's own dispatch timestamps
+        launch_attention_bf16(a, st);
         if (timed) {
             HIP_CHECK(hipEventSynchronize(a1));
             float ms = 0.f;

@@ -2429,12 +2429,14 @@ bool moe_gateup_mix_ok(const MoeDec2Args& a) {
            a.ids_out && a.w_out;
 }
 
-// DSOCR_GU_ORDER (A/B switch, read at every launch): 1 (default) = routed blocks first, shared blocks last; 0 = one
-// shared wave per block.  Same-process A/B under a graph-mode kernel trace (tools/ab_trace.py, 64 tokens x 3
-// rounds): 9.13 -> 8.77 us per launch (profiles/r05_ab_gu_order.txt); the waves' arithmetic is unchanged
+// DSOCR_GU_ORDER (A/B switch, read at every launch): 0 (default since round 6) = one shared wave per block; 1 =
+// routed blocks first, shared blocks last.  Round 5 kept 1 from a same-process A/B under a graph-mode kernel trace
+// (9.13 -> 8.77 us per launch, profiles/r05_ab_gu_order.txt); without the profiler, in separate processes on one
+// box, 0 is the faster: 256-token decode 107.9 vs 109.8 ms (mean of three alternating pairs, never slower,
+// profiles/r06_ab/gu_order_repeat.log).  The waves' arithmetic is unchanged.
 static int gu_order() {
     const char* e = getenv("DSOCR_GU_ORDER");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
 }
 
 void launch_moe_gateup_mix(const MoeDec2Args& a, const float* xn, hipStream_t s) {
@@ -2796,16 +2798,16 @@ struct MoePlan {
     bool gu_mm = false;   // grouped mode: gate/up on the matrix cores (moe_gateup_mm)
     bool dn_mm = false;   // grouped mode: down on the matrix cores (moe_down_mm)
     bool route_in_gu = false;  // grouped mode: the routing runs inside the gate/up launch (no router launch)
-    bool route_one = false;    // grouped mode: that routing as a one-block launch of the same kernel (route only)
     MoeDec2Args mr;            // ... its arguments
 };
 
-// DSOCR_ROUTE_FUSED (A/B switch, read at every plan): 1 (default) = at 3..8 tokens the router runs inside the
-// matrix-core gate/up launch (moe_gateup_mm_route_ok); 2 = the same routing as a one-block launch (route only)
-// before a plain gate/up; 0 = dec_route_grp launch + gate/up
-static int route_fused_mode() {
+// DSOCR_ROUTE_FUSED=0 (A/B switch, read at every plan): at 3..8 tokens the dec_route_grp launch + a plain
+// gate/up instead of the router inside the matrix-core gate/up launch (moe_gateup_mm_route_ok; 141.0 vs 143.9 ms
+// per 128 8-page steps, profiles/r06_ab/decode8_switches.log).  Round 5's third form, the same routing as a
+// one-block launch before a plain gate/up, measured slower than both (144.9) and was removed in round 6.
+static bool route_fused_on() {
     const char* e = getenv("DSOCR_ROUTE_FUSED");
-    return e ? atoi(e) : 1;
+    return !(e && atoi(e) == 0);
 }
 
 MoePlan moe_plan(const MoeDecodeArgs& a) {
@@ -2835,18 +2837,15 @@ MoePlan moe_plan(const MoeDecodeArgs& a) {
         p.route1 = dec_route_grp_ok(T, E, a.H, K);
         p.gu_mm = moe_gateup_mm_ok(m);
         p.dn_mm = moe_down_mm_ok(m);
-        const int rmode = route_fused_mode();
-        if (p.route1 && p.gu_mm && a.norm_w && a.router_wdt == a.wdtype && rmode != 0) {
+        if (p.route1 && p.gu_mm && a.norm_w && a.router_wdt == a.wdtype && route_fused_on()) {
             MoeDec2Args r = m;
             r.x = a.x; r.norm_w = a.norm_w; r.eps = a.eps;
             r.router = a.router; r.router_bias = a.router_bias; r.router_swz = a.router_swz;
             r.softmax_scoring = a.softmax_scoring; r.norm_topk = a.norm_topk; r.scaling = a.scaling;
             r.ids_out = a.ids; r.w_out = a.wts; r.logits = a.logits;  // (block 0 also writes the logits)
-            if (rmode == 2) r.xn_out = a.xn;  // the plain gate/up reads the normalised rows (m.x == a.xn)
             if (moe_gateup_mm_route_ok(r)) {
                 p.mr = r;
-                if (rmode == 2) p.route_one = true;
-                else p.route_in_gu = true;
+                p.route_in_gu = true;
             }
         }
     } else if (T <= 8) {
@@ -2892,8 +2891,6 @@ void launch_moe_decode(const MoeDecodeArgs& a, hipStream_t s, int parts) {
     const MoeDec2Args& m = p.m;
     if ((parts & MOE_ROUTE) && p.route_in_gu) {
         // (the gate/up launch routes)
-    } else if ((parts & MOE_ROUTE) && p.route_one) {
-        launch_moe_gateup_mm(p.mr, s);  // one block: norm + router + top-k + records, no expert
     } else if ((parts & MOE_ROUTE) && p.route1) {
         // norm + logits + top-k + records in one block (the grouped kernels read a.xn)
         DecGemvArgs g = p.router;

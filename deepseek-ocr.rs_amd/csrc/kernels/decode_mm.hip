@@ -102,8 +102,7 @@ __device__ __forceinline__ void mm_row_load(MmRowU<U>& r, const float* xr, int K
 }
 
 template <typename WT, bool NORM, int U = 3, bool DIVNORM = false>
-__device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uint16_t* xp, int KP, float* scl, int m,
-                                             float* xo = nullptr) {
+__device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uint16_t* xp, int KP, float* scl, int m) {
     const int lane = threadIdx.x & 63;
     const int chunks = K >> 3;
     if (NORM) {
@@ -127,16 +126,6 @@ __device__ __forceinline__ void mm_row_store(MmRowU<U>& r, int K, float eps, uin
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) r.v[u][j] = (r.v[u][j] * inv) * r.w[u][j];
-        }
-    }
-    if (xo) {  // the normalised f32 row, before any scaling
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int c = u * 64 + lane;
-            if (c < chunks) {
-                *reinterpret_cast<float4*>(xo + (c << 3)) = make_float4(r.v[u][0], r.v[u][1], r.v[u][2], r.v[u][3]);
-                *reinterpret_cast<float4*>(xo + (c << 3) + 4) = make_float4(r.v[u][4], r.v[u][5], r.v[u][6], r.v[u][7]);
-            }
         }
     }
     float s_inv = 1.f;
@@ -481,8 +470,7 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
         MmRow xr;
         if (wave < a.T) mm_row_load<true>(xr, a.x + (long)wave * a.K, a.K, a.norm_w);
         if (wave < a.T)
-            mm_row_store<WT, true, 3, true>(xr, a.K, a.eps, xp, KP, scl, wave,
-                                            a.xn_out ? a.xn_out + (long)wave * a.K : nullptr);
+            mm_row_store<WT, true, 3, true>(xr, a.K, a.eps, xp, KP, scl, wave);
         if (KS > 1 && tid < 2 * NU) hand[tid] = 0;
         __syncthreads();
         GU_STAMP(1);
@@ -549,7 +537,6 @@ __global__ __launch_bounds__(512, 2) void moe_gateup_mm_kernel(MoeDec2Args a) {
             const int nw = MOE_GRP_REC * (1 + grp_s[0]);
             for (int i = tid; i < nw; i += 512) gg[i] = grp_s[i];
         }
-        if (a.xn_out) return;  // route only (grid 1)
     }
     // ---- the records (ROUTE: in LDS already; else copied from the router's global records once, behind the
     // x loads and ahead of the weight stream) and the first unit's stream
@@ -758,7 +745,7 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                       \
             resident = mm_resident_blocks((const void*)moe_gateup_mm_kernel<WTY, 5, SW, KS, RT>, 512, lds);         \
         }                                                                                                           \
-        const int blocks = a.xn_out ? 1 : std::max(1, std::min(resident, (max_units + 8 / KS - 1) / (8 / KS)));   \
+        const int blocks = std::max(1, std::min(resident, (max_units + 8 / KS - 1) / (8 / KS)));                   \
         DSOCR_LAUNCH((moe_gateup_mm_kernel<WTY, 5, SW, KS, RT>), dim3(blocks), dim3(512), lds, s, a);                \
         static bool checked = false;                                                                                \
         if (!checked) {                                                                                             \

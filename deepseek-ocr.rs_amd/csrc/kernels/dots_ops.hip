@@ -70,35 +70,6 @@ __global__ __launch_bounds__(256) void dots_layernorm_kernel(const uint16_t* x, 
     for (int i = tid; i < D; i += 256) y[(long)r * D + i] = st_bf((ld_bf(xr + i) - mu) / den * w[i] + b[i]);
 }
 
-// 2-D rotary on q / k (apply_rotary, dots_vit.rs:507-574): the bf16 qkv row -> f32 q / k / v rows for
-// the attention: q' = rnd(q*cos + rotate_half(q)*sin) (two products and a sum, no contraction), v widened.
-// cos / sin: [N][hd] (the [t | t] halves already duplicated).  One thread per element pair.
-__global__ __launch_bounds__(256) void dots_rope_kernel(const uint16_t* qkv, long N, int heads, int hd, const float* cos_t,
-                                                        const float* sin_t, void* out, int out_bf16) {
-#pragma clang fp contract(off)
-    const long D = (long)heads * hd;
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= N * 3 * D) return;
-    const long n = i / (3 * D);
-    const int c = (int)(i % (3 * D));
-    const uint16_t* row = qkv + n * 3 * D;
-    const float x = ld_bf(row + c);
-    if (c >= 2 * D) {  // v
-        if (out_bf16) reinterpret_cast<uint16_t*>(out)[i] = row[c];
-        else reinterpret_cast<float*>(out)[i] = x;
-        return;
-    }
-    const int d = c % hd, half = hd / 2;
-    const int base = c - d;
-    const float partner = ld_bf(row + base + (d < half ? d + half : d - half));
-    const float rot = d < half ? -partner : partner;
-    const float cs = cos_t[n * hd + d], sn = sin_t[n * hd + d];
-    const float a = x * cs;
-    const float bb = rot * sn;
-    if (out_bf16) reinterpret_cast<uint16_t*>(out)[i] = st_bf(a + bb);
-    else reinterpret_cast<float*>(out)[i] = rbf(a + bb);
-}
-
 // SwiGLU (DotsSwiGLUFFN::forward, dots_vit.rs:624-630): gu = [fc1 | fc3] bf16 rows [N][2I];
 // h = rnd(silu(g) * u) with candle-kernels' silu_fwd in bf16 ops: rnd(g / rnd(1 + rnd(exp(-g))))
 __global__ __launch_bounds__(256) void dots_swiglu_kernel(const uint16_t* gu, long N, int I, uint16_t* h) {
@@ -266,13 +237,6 @@ void launch_dots_layernorm(const void* x, long rows, int D, const float* w, cons
     if (rows <= 0) return;
     hipLaunchKernelGGL(dots_layernorm_kernel, dim3((unsigned)rows), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(x),
                        D, w, b, eps, reinterpret_cast<uint16_t*>(y));
-}
-void launch_dots_rope(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
-                      int out_bf16, hipStream_t s) {
-    if (N <= 0) return;
-    if (hd % 2) throw std::runtime_error("EINVAL: rotary needs an even head_dim");
-    hipLaunchKernelGGL(dots_rope_kernel, blocks_for(N * 3 * heads * hd), dim3(256), 0, s,
-                       reinterpret_cast<const uint16_t*>(qkv), N, heads, hd, cos_t, sin_t, out, out_bf16);
 }
 void launch_dots_rope_qk(const void* qkv, long N, int heads, int hd, const float* cos_t, const float* sin_t, void* out,
                          hipStream_t s) {

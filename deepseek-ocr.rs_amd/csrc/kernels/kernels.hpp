@@ -348,9 +348,6 @@ struct MoeDec2Args {
     // optional logit bias; x is then the raw residual stream, normalised with norm_w in every block
     const void* router = nullptr; const float* router_bias = nullptr;
     const void* router_swz = nullptr;  // ... optional fragment-ordered copy of the router rows (launch_mm_swizzle)
-    // ... route only: one block runs that routing, writes the normalised rows here (f32 [T][K]) with the picks and
-    // records, and streams no expert (a plain gate/up launch follows)
-    float* xn_out = nullptr;
     unsigned long long* stamps = nullptr;  // dev (tools/kbench moe8): per block 8 words of s_memrealtime at phase points
 };
 // Decode gate/up for one token (T = 1, E <= 64): every wave is independent — 1 of 4 streams

@@ -25,12 +25,14 @@ for step in "$@"; do
     # round-6 switch table: every DSOCR_* switch A/B'd in separate processes on one box
     abv) run 900 tools/env_ab_vision.sh base: attn_fwd2:DSOCR_ATTN_SPLIT=0 one_stream:DSOCR_VIS_STREAMS=0 nst2:DSOCR_GEMM_NST=2 group1:DSOCR_GEMM_GROUP_M=1 no_ksplit:DSOCR_ATTN_KSPLIT=0 > gpurun_out/abv.log 2>&1 ;;
     abd1) AB_TOKENS=256 AB_ROUNDS=2 run 900 tools/env_ab.sh base: qkv_sep:DSOCR_QKV_ATTN=0 screen0:DSOCR_SCREEN=0 gu_order0:DSOCR_GU_ORDER=0 kvdelay0:DSOCR_ATT_KV_DELAY=0 persist:DSOCR_PERSIST=1 no_graph:DSOCR_NO_GRAPH=1 > gpurun_out/abd1.log 2>&1 ;;
-    abd8) AB_TOKENS=128 AB_ROUNDS=2 AB_EXTRA="--pages 8 --text-pages" run 900 tools/env_ab.sh base: route0:DSOCR_ROUTE_FUSED=0 route2:DSOCR_ROUTE_FUSED=2 mmswz0:DSOCR_MM_SWZ=0 routerswz0:DSOCR_ROUTER_SWZ=0 guks1:DSOCR_GU_KS=1 guks4:DSOCR_GU_KS=4 dnks1:DSOCR_DN_KS=1 > gpurun_out/abd8.log 2>&1 ;;
+    abd8) AB_TOKENS=128 AB_ROUNDS=2 AB_EXTRA="--pages 8 --text-pages" run 900 tools/env_ab.sh base: route0:DSOCR_ROUTE_FUSED=0 mmswz0:DSOCR_MM_SWZ=0 routerswz0:DSOCR_ROUTER_SWZ=0 guks1:DSOCR_GU_KS=1 guks4:DSOCR_GU_KS=4 dnks1:DSOCR_DN_KS=1 > gpurun_out/abd8.log 2>&1 ;;
     katt_split) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "test_attention" > gpurun_out/katt_split.log 2>&1 ;;
     # two library builds of the same tree (tools/prof_vision.py --lib), alternating processes
     vab) for i in 1 2; do for L in dsocr_ab_old dsocr; do echo "== $L" >> gpurun_out/vab.log; run 180 python tools/prof_vision.py --reps 4 --lib deepseek-ocr.rs_amd/lib/lib$L.so >> gpurun_out/vab.log 2>&1; done; done ;;
     vprof) run 300 rocprofv3 --kernel-trace --stats -d gpurun_out/vprof -o v --output-format csv -- python tools/prof_vision.py --reps 3 > gpurun_out/vprof.log 2>&1 ;;
     dab) for i in 1 2; do for L in dsocr_ab_old dsocr; do echo "== $L" >> gpurun_out/dab.log; run 180 python tools/ab_trace.py --tokens 256 --rounds 2 --variant "$L:" --out gpurun_out/dab_$L.json --lib deepseek-ocr.rs_amd/lib/lib$L.so ${AB_EXTRA} >> gpurun_out/dab.log 2>&1; done; done ;;
+    gu_ab) AB_TOKENS=256 AB_ROUNDS=2 run 900 tools/env_ab.sh base: gu0:DSOCR_GU_ORDER=0 base: gu0:DSOCR_GU_ORDER=0 base: gu0:DSOCR_GU_ORDER=0 > gpurun_out/gu_ab.log 2>&1 ;;
+    bgu) for i in 1 2; do for o in 1 0; do echo "== GU_ORDER=$o" >> gpurun_out/bgu.log; DSOCR_GU_ORDER=$o run 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-chain-roofline --roofline-iters 4 >> gpurun_out/bgu.log 2>&1; done; done ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
