@@ -632,6 +632,8 @@ dsocr_status dsocr_k_attention_bf16(int n_seq, int L, int heads, int hd, float s
         a.q_rs = a.k_rs = a.v_rs = ld; a.q_hs = a.k_hs = a.v_hs = hd;
         a.o = o; a.o_rs = o_ld; a.o_hs = hd; a.o_bf16 = o_bf16;
         a.n_seq = n_seq; a.L = L; a.heads = heads; a.kv_heads = heads; a.hd = hd; a.scale = scale;
+        const char* pv = getenv("DSOCR_DOTS_PV_PLANES");  // the tower's P.V plane count (3 unless set to 2)
+        a.pv_planes = (pv && atoi(pv) == 2) ? 2 : 3;
         dsocr::launch_attention_bf16(a, nullptr);
         check_hip(hipGetLastError(), "attention_bf16 launch");
         check_hip(hipDeviceSynchronize(), "attention_bf16");

@@ -237,6 +237,229 @@ __global__ __launch_bounds__(256, 2) void attention_bf16_tr_kernel(AttnBf16Args 
 #undef AB_LSTORE
 }
 
+// Ping-pong form (round 6; the dots.ocr tower's 128-dim heads): 8 waves per block as two groups of 4 that
+// run one interval apart, so the two waves sharing a SIMD (w and w + 4, one per group) alternate between the
+// matrix cores and the VALU.  A wave's work per 64-key tile t is an M phase (P.V of tile t - 1, then
+// S^T = K_t . Q^T: 16 + 16 PL MFMAs) and an S phase (mask, online softmax, O rescale, P split into bf16
+// planes: VALU only).  With interval I_j ending at block barrier b_j, group 0 runs M_t in I_{2t} and S_t in
+// I_{2t+1}; group 1 runs M_t in I_{2t+1} and S_t in I_{2t+2}: in every interval one wave of each SIMD issues
+// MFMAs while the other runs its softmax.  The 256 queries of a block (32 per wave) share every K / V tile.
+// Staging: tile u = (K_u, V_u), each group writes its half of the rows during an S phase — group 1 in
+// I_{2u-2}, group 0 in I_{2u-1} — from registers loaded one tile earlier (bounded buffer loads: keys past
+// the sequence read as zeros).  K_u lives in Ks[u & 1] (read in I_{2u}, I_{2u+1}; its previous tile's last
+// read I_{2u-3}), V_u in Vs[u % 3] (read in I_{2u+2}, I_{2u+3}; previous last read I_{2u-3}).  Every product
+// and sum is the 4-wave kernel's (same tiles, same order per query), so the outputs are bitwise equal to it.
+template <int HD, int PL>
+__global__ __launch_bounds__(512, 1) void attention_bf16_pp_kernel(AttnBf16Args a) {
+    constexpr int KP = HD + 8, VP = HD + 32;  // LDS row pitches (bf16 elements)
+    constexpr int C8 = HD / 8;                // 16-byte chunks per row
+    constexpr int HR = AB_KT / 2;             // rows of a tile half (one group's share)
+    constexpr int NCH = HR * C8 / 256;        // chunks per thread per operand per half
+    constexpr int QS = HD / 16, DC = HD / 32;
+    static_assert(NCH >= 1 && HR * C8 % 256 == 0, "tile half split over a group's 256 threads");
+    __shared__ __attribute__((aligned(16))) uint16_t Ks[2][AB_KT][KP];
+    __shared__ __attribute__((aligned(16))) uint16_t Vs[3][AB_KT][VP];
+    const int s = blockIdx.z, h = blockIdx.y;
+    const int len = a.L;
+    const int qb0 = blockIdx.x * (8 * AB_Q);
+    if (qb0 >= len) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = wave >> 2, gt = tid & 255;
+    const int half = lane >> 5, l32 = lane & 31;
+    const int kvh = h / (a.heads / a.kv_heads);
+    const uint16_t* Q = a.q + (long)s * a.L * a.q_rs + (long)h * a.q_hs;
+    const uint16_t* K = a.k + (long)s * a.L * a.k_rs + (long)kvh * a.k_hs;
+    const uint16_t* V = a.v + (long)s * a.L * a.v_rs + (long)kvh * a.v_hs;
+    const int q_lane = qb0 + wave * AB_Q + l32;
+    const bool q_valid = q_lane < len;
+    bf16x8_t qreg[QS];
+    {
+        const uint16_t* qr = Q + (long)(q_valid ? q_lane : 0) * a.q_rs + 8 * half;
+#pragma unroll
+        for (int st = 0; st < QS; ++st) qreg[st] = *reinterpret_cast<const bf16x8_t*>(qr + 16 * st);
+    }
+    const int i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3, gd = 16 * ((lane >> 4) & 1);
+    const int n = (len + AB_KT - 1) / AB_KT;  // key tiles
+    // this group's half of a tile: rows HR grp + gt / C8 (+ 256 / C8 per j), chunk gt % C8
+    u32x4 rk[NCH], rv[NCH];
+    const auto rsk = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(K), (short)0, len * a.k_rs * 2, 0x00020000);
+    const auto rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(V), (short)0, len * a.v_rs * 2, 0x00020000);
+    const int hrow = HR * grp + gt / C8, hch = (gt % C8) * 8;
+    const int ko = (hrow * a.k_rs + hch) * 2, vo = (hrow * a.v_rs + hch) * 2;
+    auto gload = [&](int u) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int r = u * AB_KT + j * (256 / C8);
+            rk[j] = __builtin_amdgcn_raw_buffer_load_b128(rsk, ko + r * a.k_rs * 2, 0, 0);
+            rv[j] = __builtin_amdgcn_raw_buffer_load_b128(rsv, vo + r * a.v_rs * 2, 0, 0);
+        }
+    };
+    auto lstore = [&](int u) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int r = hrow + j * (256 / C8);
+            *reinterpret_cast<u32x4*>(&Ks[u & 1][r][hch]) = rk[j];
+            *reinterpret_cast<u32x4*>(&Vs[u % 3][r][hch]) = rv[j];
+        }
+    };
+    f32x16 o[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[c][r] = 0.f;
+    f32x16 sc[2];
+    u32x4 ph[2][2], pm[2][2], pl[2][2];  // P planes of the last S phase, for the next M phase's P.V
+    const float c2 = a.scale * 1.4426950408889634f;
+    float m_run = -INFINITY, l_run = 0.f;
+    // prologue: tile 0 whole (both halves), the next half of each group in flight
+    gload(0);
+    lstore(0);
+    if (n > 1) gload(1);
+    __syncthreads();
+    for (int j = 0; j < 2 * n + 2; ++j) {
+        const int mj = j - grp;  // this group's own interval index
+        if (mj == -1) {
+            // group 1's first interval: stage its half of tile 1
+            if (n > 1) {
+                lstore(1);
+                if (n > 2) gload(2);
+            }
+        } else if (mj >= 0 && mj <= 2 * n && (mj & 1) == 0) {
+            // M phase of tile t: P.V of tile t - 1, then S^T = K_t . Q^T
+            const int t = mj >> 1;
+            if (AB_PRIO & 2) __builtin_amdgcn_s_setprio(1);
+            if (t > 0) {
+                const int vb = (t - 1) % 3;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int tt = 0; tt < 2; ++tt) {
+                        const bf16x8_t fh = __builtin_bit_cast(bf16x8_t, ph[u][tt]), fm = __builtin_bit_cast(bf16x8_t, pm[u][tt]),
+                                       fl = __builtin_bit_cast(bf16x8_t, pl[u][tt]);
+                        const int kr0 = u * 32 + 16 * tt + 4 * half + tq;
+#pragma unroll
+                        for (int c = 0; c < DC; ++c) {
+                            const int d0 = c * 32 + gd + 4 * tp;
+                            const v4i16_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)&Vs[vb][kr0][d0]);
+                            const v4i16_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)&Vs[vb][kr0 + 8][d0]);
+                            bf16x8_t vf;
+                            __builtin_memcpy(&vf, &lo, 8);
+                            __builtin_memcpy(reinterpret_cast<char*>(&vf) + 8, &hi, 8);
+                            if constexpr (PL == 3) o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fl, o[c], 0, 0, 0);
+                            o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fm, o[c], 0, 0, 0);
+                            o[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, fh, o[c], 0, 0, 0);
+                        }
+                    }
+            }
+            if (t < n) {
+                const int kb = t & 1;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sc[u][r] = 0.f;
+#pragma unroll
+                    for (int st = 0; st < QS; ++st) {
+                        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(&Ks[kb][u * 32 + l32][16 * st + 8 * half]);
+                        sc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qreg[st], sc[u], 0, 0, 0);
+                    }
+                }
+            }
+            if (AB_PRIO & 2) __builtin_amdgcn_s_setprio(0);
+        } else if (mj >= 1 && mj < 2 * n) {
+            // S phase of tile t: the softmax of its scores, the O rescale, P's planes; then this group's staging
+            const int t = mj >> 1;
+            const int k0 = t * AB_KT;
+            if (k0 + AB_KT > len) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (k0 + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= len) sc[u][r] = -INFINITY;
+            }
+            float tmax = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[u][r]);
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+            const float m_new = fmaxf(m_run, tmax * c2);
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            float psum = 0.f;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(fmaf(sc[u][r], c2, -m_new));
+                    sc[u][r] = pv;
+                    psum += pv;
+                }
+            psum += __shfl_xor(psum, 32, 64);
+            l_run = l_run * alpha + psum;
+            m_run = m_new;
+            if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+                for (int c = 0; c < DC; ++c)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[c][r] *= alpha;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float p0 = sc[u][8 * tt + 2 * q], p1 = sc[u][8 * tt + 2 * q + 1];
+                        if constexpr (PL == 3) {
+                            const uint32_t b0 = __float_as_uint(p0), b1 = __float_as_uint(p1);
+                            const float r0 = p0 - __uint_as_float(b0 & 0xffff0000u), r1 = p1 - __uint_as_float(b1 & 0xffff0000u);
+                            const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+                            const float e0 = r0 - __uint_as_float(c0 & 0xffff0000u), e1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+                            ph[u][tt][q] = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+                            pm[u][tt][q] = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
+                            pl[u][tt][q] = __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302u);
+                        } else {
+                            const __bf16 h0 = (__bf16)p0, h1 = (__bf16)p1;
+                            const __bf16 m0 = (__bf16)(p0 - (float)h0), m1 = (__bf16)(p1 - (float)h1);
+                            uint16_t x0, x1, y0, y1;
+                            __builtin_memcpy(&x0, &h0, 2); __builtin_memcpy(&x1, &h1, 2);
+                            __builtin_memcpy(&y0, &m0, 2); __builtin_memcpy(&y1, &m1, 2);
+                            ph[u][tt][q] = (uint32_t)x0 | ((uint32_t)x1 << 16);
+                            pm[u][tt][q] = (uint32_t)y0 | ((uint32_t)y1 << 16);
+                            pl[u][tt][q] = 0u;
+                        }
+                    }
+            // staging: group 0 writes its half of tile t + 1, group 1 of tile t + 2; then the next half's loads
+            const int u = t + 1 + grp;
+            if (u < n) {
+                lstore(u);
+                if (u + 1 < n) gload(u + 1);
+            }
+        }
+        // every wave's staging stores and tile reads of this interval are done before the next one
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+    if (q_valid) {
+        const long orow = (long)s * a.L * a.o_rs + (long)q_lane * a.o_rs + (long)h * a.o_hs;
+#pragma unroll
+        for (int c = 0; c < DC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = c * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const float v = o[c][r] / l_run;
+                if (a.o_bf16) reinterpret_cast<uint16_t*>(a.o)[orow + d] = bf_bits(v);
+                else reinterpret_cast<float*>(a.o)[orow + d] = v;
+            }
+    }
+}
+
+// DSOCR_DOTS_ATTN_PP=0 (A/B switch, read at every launch): the 4-wave kernel for 128-dim heads too
+static bool attn_pp_on() {
+    const char* e = getenv("DSOCR_DOTS_ATTN_PP");
+    return !(e && atoi(e) == 0);
+}
+
 void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s) {
     if (a.n_seq <= 0 || a.L <= 0) return;
     if (a.hd != 64 && a.hd != 128) throw std::runtime_error("EINVAL: attention_bf16 supports head_dim 64 / 128");
@@ -246,6 +469,12 @@ void launch_attention_bf16(const AttnBf16Args& a, hipStream_t s) {
     if ((long)(a.L + AB_KT) * std::max(a.k_rs, a.v_rs) * 2 >= (1L << 31))
         throw std::runtime_error("EINVAL: attention_bf16 sequence slice beyond 32-bit buffer offsets");
     if (a.pv_planes != 2 && a.pv_planes != 3) throw std::runtime_error("EINVAL: attention_bf16 pv_planes is 2 or 3");
+    if (a.hd == 128 && attn_pp_on()) {
+        const dim3 g2((a.L + 8 * AB_Q - 1) / (8 * AB_Q), a.heads, a.n_seq);
+        if (a.pv_planes == 2) DSOCR_LAUNCH((attention_bf16_pp_kernel<128, 2>), g2, dim3(512), 0, s, a);
+        else DSOCR_LAUNCH((attention_bf16_pp_kernel<128, 3>), g2, dim3(512), 0, s, a);
+        return;
+    }
     dim3 grid((a.L + 4 * AB_Q - 1) / (4 * AB_Q), a.heads, a.n_seq);
     if (a.pv_planes == 2) {
         if (a.hd == 128) DSOCR_LAUNCH((attention_bf16_tr_kernel<128, 2>), grid, dim3(256), 0, s, a);

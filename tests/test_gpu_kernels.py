@@ -532,7 +532,29 @@ def test_screened_head_multi_token_random(gpu, B, V):
 
 
 # ---------------------------------------------------------------- bf16-matrix-core attention (dots.ocr ViT)
-@pytest.mark.parametrize("n_seq,L,heads,hd", [(1, 1000, 2, 128), (2, 257, 3, 64), (1, 64, 1, 128), (1, 4133, 2, 128)])
+@pytest.mark.parametrize("L,planes", [(1000, 3), (4133, 3), (130, 3), (20, 3), (1000, 2)])
+def test_attention_bf16_pingpong_bitwise(gpu, monkeypatch, L, planes):
+    """The 8-wave ping-pong kernel (128-dim heads, two wave groups one interval apart) runs the 4-wave kernel's
+    products and sums in the same order per query: bitwise equal outputs (f32 and bf16 out), ragged lengths and
+    fewer keys than one tile included."""
+    rng = np.random.default_rng(L)
+    heads, hd = 2, 128
+    D = heads * hd
+    qkv = rng.standard_normal((L, 3 * D)).astype(np.float32)
+    qkv[:, :D] *= 0.6
+    dq = Dev(bf16_round(qkv))
+    outs = []
+    for pp in ("1", "0"):
+        monkeypatch.setenv("DSOCR_DOTS_ATTN_PP", pp)
+        monkeypatch.setenv("DSOCR_DOTS_PV_PLANES", str(planes))
+        do = Dev.zeros((L, D))
+        check(lib().dsocr_k_attention_bf16(1, L, heads, hd, 1.0 / math.sqrt(hd), dq.ptr, 3 * D, do.ptr, D, 0))
+        outs.append(do.get())
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@pytest.mark.parametrize("n_seq,L,heads,hd", [(1, 1000, 2, 128), (2, 257, 3, 64), (1, 64, 1, 128), (1, 4133, 2, 128),
+                                              (1, 20, 2, 128), (2, 130, 2, 128), (1, 300, 1, 128)])
 def test_attention_bf16_f32_math(gpu, n_seq, L, heads, hd):
     """attention_bf16 (dots_vit.rs:433-498 math: f32 scores / softmax / probs.V on bf16 q, k, v):
     exact bf16 products and a 3-plane exact split of P, so the result is an f32 attention up to

@@ -33,6 +33,8 @@ for step in "$@"; do
     dab) for i in 1 2; do for L in dsocr_ab_old dsocr; do echo "== $L" >> gpurun_out/dab.log; run 180 python tools/ab_trace.py --tokens 256 --rounds 2 --variant "$L:" --out gpurun_out/dab_$L.json --lib deepseek-ocr.rs_amd/lib/lib$L.so ${AB_EXTRA} >> gpurun_out/dab.log 2>&1; done; done ;;
     gu_ab) AB_TOKENS=256 AB_ROUNDS=2 run 900 tools/env_ab.sh base: gu0:DSOCR_GU_ORDER=0 base: gu0:DSOCR_GU_ORDER=0 base: gu0:DSOCR_GU_ORDER=0 > gpurun_out/gu_ab.log 2>&1 ;;
     bgu) for i in 1 2; do for o in 1 0; do echo "== GU_ORDER=$o" >> gpurun_out/bgu.log; DSOCR_GU_ORDER=$o run 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-chain-roofline --roofline-iters 4 >> gpurun_out/bgu.log 2>&1; done; done ;;
+    kdots) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "attention_bf16" > gpurun_out/kdots.log 2>&1 ;;
+    dpp) for i in 1 2; do for v in 0 1; do echo "== DOTS_ATTN_PP=$v" >> gpurun_out/dpp.log; DSOCR_DOTS_ATTN_PP=$v run 300 python bench.py --workload dots2048 --steps 2 --warmup 1 >> gpurun_out/dpp.log 2>&1; done; done ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
