@@ -35,6 +35,10 @@ for step in "$@"; do
     bgu) for i in 1 2; do for o in 1 0; do echo "== GU_ORDER=$o" >> gpurun_out/bgu.log; DSOCR_GU_ORDER=$o run 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-chain-roofline --roofline-iters 4 >> gpurun_out/bgu.log 2>&1; done; done ;;
     kdots) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "attention_bf16" > gpurun_out/kdots.log 2>&1 ;;
     dpp) for i in 1 2; do for v in 0 1; do echo "== DOTS_ATTN_PP=$v" >> gpurun_out/dpp.log; DSOCR_DOTS_ATTN_PP=$v run 300 python bench.py --workload dots2048 --steps 2 --warmup 1 >> gpurun_out/dpp.log 2>&1; done; done ;;
+    rpb_ab) AB_TOKENS=256 AB_ROUNDS=2 run 900 tools/env_ab.sh base: rpb4:DSOCR_DN_RPB=4 rpb1:DSOCR_DN_RPB=1 base: rpb4:DSOCR_DN_RPB=4 rpb1:DSOCR_DN_RPB=1 > gpurun_out/rpb_ab.log 2>&1 ;;
+    bench8t) run 900 python bench.py --pages-per-gpu 8 --text-pages --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench8t.log 2>&1 ;;
+    bench8q) run 900 python bench.py --pages-per-gpu 8 --snapshot q4k --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench8q.log 2>&1 ;;
+    rpb_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant base: --variant rpb4:DSOCR_DN_RPB=4 --variant rpb1:DSOCR_DN_RPB=1 --out gpurun_out/rpb_sp.json > gpurun_out/rpb_sp.log 2>&1 ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
