@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pages", type=int, default=1)
     ap.add_argument("--lib", default=None, help="another libdsocr.so build (A/B of two kernel versions)")
+    ap.add_argument("--variant", action="append", help="name:ENV=VAL,ENV2=VAL (same-process A/B, alternating)")
     a = ap.parse_args()
     import dsocr
     if a.lib:
@@ -36,11 +37,18 @@ def main():
         ids, mask = build_prompt_tokens(tok, BENCH_PROMPT, [page.n_image_tokens])
         reqs.append((ids, mask, page, None))
     params = DecodeParameters(max_new_tokens=2)
+    variants = [v.partition(":") for v in (a.variant or [":"])]
+    eng.generate_batch(reqs, params, ignore_eos=True)  # warm-up
     for r in range(a.reps):
-        eng.generate_batch(reqs, params, ignore_eos=True)
-        t = eng.last_timings()
-        print(json.dumps({"rep": r, "vision_ms": round(t["vision_compute_ms"], 2),
-                          "prefill_ms": round(t["decode_prefill_ms"], 2)}), flush=True)
+        for name, _, env in variants:  # same-process A/B: each variant's environment set before its pass
+            for k, v in (kv.partition("=")[::2] for kv in filter(None, env.split(","))):
+                os.environ[k] = v
+            eng.generate_batch(reqs, params, ignore_eos=True)
+            t = eng.last_timings()
+            print(json.dumps({"rep": r, "variant": name, "vision_ms": round(t["vision_compute_ms"], 2),
+                              "prefill_ms": round(t["decode_prefill_ms"], 2)}), flush=True)
+            for k in (kv.partition("=")[0] for kv in filter(None, env.split(","))):
+                os.environ.pop(k, None)
     eng.close()
 
 
