@@ -45,6 +45,8 @@ for step in "$@"; do
     rbprof) run 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rbprof -o v --output-format csv -- python tools/prof_vision.py --reps 2 --variant rb3: --variant rb2:DSOCR_RELBIAS=2 > gpurun_out/rbprof.log 2>&1 ;;
     kgrp) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm_grouped" > gpurun_out/kgrp.log 2>&1 ;;
     grp_sp) run 600 python tools/prof_vision.py --reps 5 --variant xm1: --variant xm0:DSOCR_GRP_XCD=0 > gpurun_out/grp_sp.log 2>&1 ;;
+    scr_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant pre2: --variant pre1:DSOCR_SCREEN_PRE2=0 --out gpurun_out/scr_sp.json > gpurun_out/scr_sp.log 2>&1 ;;
+    kscr) run 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -q -m gpu -k "screen" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/kscr.log 2>&1 ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
