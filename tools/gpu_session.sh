@@ -47,6 +47,7 @@ for step in "$@"; do
     grp_sp) run 600 python tools/prof_vision.py --reps 5 --variant xm1: --variant xm0:DSOCR_GRP_XCD=0 > gpurun_out/grp_sp.log 2>&1 ;;
     scr_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant pre2: --variant pre1:DSOCR_SCREEN_PRE2=0 --out gpurun_out/scr_sp.json > gpurun_out/scr_sp.log 2>&1 ;;
     kscr) run 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -q -m gpu -k "screen" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/kscr.log 2>&1 ;;
+    fold_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 3 --variant fold: --variant nofold:DSOCR_ROUTER_FOLD=0 --out gpurun_out/fold_sp.json > gpurun_out/fold_sp.log 2>&1 ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
