@@ -49,6 +49,8 @@ for step in "$@"; do
     kscr) run 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -q -m gpu -k "screen" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/kscr.log 2>&1 ;;
     fold_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 3 --variant fold: --variant nofold:DSOCR_ROUTER_FOLD=0 --out gpurun_out/fold_sp.json > gpurun_out/fold_sp.log 2>&1 ;;
     pmc_l2v) run 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2v -o pmc --output-format csv -- python tools/prof_vision.py --reps 1 > gpurun_out/pmc_l2v.log 2>&1 ;;
+    kgemm) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm_f32a" > gpurun_out/kgemm.log 2>&1 ;;
+    adir_sp) run 600 python tools/prof_vision.py --reps 5 --variant adir: --variant lds1:DSOCR_GEMM_ADIR=0 > gpurun_out/adir_sp.log 2>&1 ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) run 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 ;;
