@@ -47,6 +47,7 @@ for step in "$@"; do
     grp_sp) run 600 python tools/prof_vision.py --reps 5 --variant xm1: --variant xm0:DSOCR_GRP_XCD=0 > gpurun_out/grp_sp.log 2>&1 ;;
     scr_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant pre2: --variant pre1:DSOCR_SCREEN_PRE2=0 --out gpurun_out/scr_sp.json > gpurun_out/scr_sp.log 2>&1 ;;
     kscr) run 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -q -m gpu -k "screen" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/kscr.log 2>&1 ;;
+    defer_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant defer: --variant now:DSOCR_ATT_REFILL_DEFER=0 --out gpurun_out/defer_sp.json > gpurun_out/defer_sp.log 2>&1 ;;
     fold_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 3 --variant fold: --variant nofold:DSOCR_ROUTER_FOLD=0 --out gpurun_out/fold_sp.json > gpurun_out/fold_sp.log 2>&1 ;;
     pmc_l2v) run 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2v -o pmc --output-format csv -- python tools/prof_vision.py --reps 1 > gpurun_out/pmc_l2v.log 2>&1 ;;
     kgemm) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm_f32a" > gpurun_out/kgemm.log 2>&1 ;;
