@@ -47,6 +47,10 @@ for step in "$@"; do
     grp_sp) run 600 python tools/prof_vision.py --reps 5 --variant xm1: --variant xm0:DSOCR_GRP_XCD=0 > gpurun_out/grp_sp.log 2>&1 ;;
     scr_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant pre2: --variant pre1:DSOCR_SCREEN_PRE2=0 --out gpurun_out/scr_sp.json > gpurun_out/scr_sp.log 2>&1 ;;
     kscr) run 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -q -m gpu -k "screen" -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/kscr.log 2>&1 ;;
+    tatt) run 300 python tools/time_attn_bf16.py --lib new=deepseek-ocr.rs_amd/lib/libdsocr.so --lib old=deepseek-ocr.rs_amd/lib/libdsocr_ab_old.so > gpurun_out/tatt.log 2>&1 ;;
+    pmclist) run 60 rocprofv3 -L > gpurun_out/pmclist.txt 2>&1 ;;
+    pmcatt1) run 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAIT_INST_LDS -d gpurun_out/pmcatt1 -o pmc --output-format csv -- python3 tools/time_attn_bf16.py --lib ${ATT_LIB:-new=deepseek-ocr.rs_amd/lib/libdsocr.so} --rounds 1 --reps 1 > gpurun_out/pmcatt1.log 2>&1 ;;
+    pmcatt2) run 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/pmcatt2 -o pmc --output-format csv -- python3 tools/time_attn_bf16.py --lib ${ATT_LIB:-new=deepseek-ocr.rs_amd/lib/libdsocr.so} --rounds 1 --reps 1 > gpurun_out/pmcatt2.log 2>&1 ;;
     defer_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 4 --variant defer: --variant now:DSOCR_ATT_REFILL_DEFER=0 --out gpurun_out/defer_sp.json > gpurun_out/defer_sp.log 2>&1 ;;
     fold_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 3 --variant fold: --variant nofold:DSOCR_ROUTER_FOLD=0 --out gpurun_out/fold_sp.json > gpurun_out/fold_sp.log 2>&1 ;;
     pmc_l2v) run 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2v -o pmc --output-format csv -- python tools/prof_vision.py --reps 1 > gpurun_out/pmc_l2v.log 2>&1 ;;
