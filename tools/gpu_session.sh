@@ -55,6 +55,7 @@ for step in "$@"; do
     fold_sp) run 600 python tools/ab_trace.py --tokens 256 --rounds 3 --variant fold: --variant nofold:DSOCR_ROUTER_FOLD=0 --out gpurun_out/fold_sp.json > gpurun_out/fold_sp.log 2>&1 ;;
     pmc_l2v) run 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2v -o pmc --output-format csv -- python tools/prof_vision.py --reps 1 > gpurun_out/pmc_l2v.log 2>&1 ;;
     kgemm) run 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm_f32a" > gpurun_out/kgemm.log 2>&1 ;;
+    skf_sp) run 600 python tools/prof_vision.py --reps 5 --variant fused: --variant two:DSOCR_SPLITK_FUSED=0 > gpurun_out/skf_sp.log 2>&1 ;;
     adir_sp) run 600 python tools/prof_vision.py --reps 5 --variant adir: --variant lds1:DSOCR_GEMM_ADIR=0 > gpurun_out/adir_sp.log 2>&1 ;;
     gpu_all) run 1100 python -u -m pytest tests -q -m gpu -rf -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
