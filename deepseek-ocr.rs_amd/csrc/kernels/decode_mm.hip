@@ -784,7 +784,7 @@ void launch_moe_gateup_mm(const MoeDec2Args& a, hipStream_t s) {
 // then the shared pieces) with sc1 loads and adds to out (split-K seam: MI355X_MICROARCH.md price list
 // 'splitk-seam'; hand-off: the sc1-load table's first row).
 template <typename WT, int PF, bool SWZ, int NWV, int KS>
-__global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Args a) {
+__global__ __launch_bounds__(64 * NWV * KS, KS == 2 ? 6 : 4) void moe_down_mm_kernel(MoeDec2Args a) {
     WaveSpan span_(a.span);
     typedef typename MmT<WT>::frag frag;
     constexpr int RT = 16 * NWV, U = 2;  // rows per unit (16 per wave), chunks per lane (I <= 1024)
@@ -874,7 +874,11 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         if (srcrow[q]) mm_row_load<false, U>(xr[q], srcrow[q], a.I, nullptr);
     }
     load(fa, c0);
-    if (nch > 1) load(fb, c0 + 1);
+    // KS = 2: the second batch goes out after the token planes are staged, so its registers are not live
+    // beside the token rows: 80 VGPRs, 6 waves per SIMD, three 8-wave blocks per CU, and the 640 units of
+    // 30 experts at 8 pages resident in one round (104 VGPRs held two blocks per CU: 128 units started a
+    // second round at ~12 us).  The first batch alone keeps ~29 MB in flight chip-wide.
+    if (KS == 1 && nch > 1) load(fb, c0 + 1);
     const int KP = mm_pitch(a.I);
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
@@ -886,6 +890,7 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
         }
         mm_row_store<WT, false, U>(xr[q], a.I, 0.f, xp, KP, scl, wave + q * NW);
     }
+    if (KS > 1 && nch > 1) load(fb, c0 + 1);
     __syncthreads();
     DN_STAMP(1);
     const uint16_t* bbase = xp + (long)(col & 7) * KP + 8 * g;
@@ -949,23 +954,24 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
     // the last arriver: the ordered sum over segments.  A token's column of a segment it does not
     // belong to was computed from a zero B column, so it holds exact zeros and adding it leaves every
     // partial sum unchanged; all segments are therefore summed unconditionally.  Thread = (4 rows of one
-    // token, half of the segments): 16-byte sc1 loads of every segment of its half issued together (one
-    // L2 round trip; a per-segment test, or batches of scalar loads, made each batch its own round trip),
-    // summed in segment order; the second half's sum joins the first's through LDS:
-    // (s_0 + .. + s_{h-1}) + (s_h + .. + s_{n-1}), a fixed order.
-    static_assert(NWV == 4 && RT * MM_MT / 4 == 128, "tail layout: 128 row quads x 2 halves = 256 threads");
-    __shared__ float4 half_s[128];
-    const int q4 = tid & 127, hf = tid >> 7;  // threads past 256 (KS > 1) take no part
-    const bool tl = tid < 256;
+    // token, one of NQ contiguous segment ranges): 16-byte sc1 loads of every segment of its range issued
+    // together (one L2 round trip; a per-segment test, or batches of scalar loads, made each batch its own
+    // round trip), summed in segment order; the ranges meet through LDS (the staging planes, dead here):
+    // NQ = 2 (256 threads): r_0 + r_1; NQ = 4 (512 threads, KS = 2): (r_0 + r_1) + (r_2 + r_3), a fixed order.
+    // Four ranges at KS = 2 keep the loads in flight per thread at 13 (52 VGPRs; the kernel is held to 80).
+    constexpr int NQ = 64 * NWV * KS / 128;
+    static_assert(NWV == 4 && RT * MM_MT / 4 == 128 && (NQ == 2 || NQ == 4), "tail layout: 128 row quads x NQ ranges");
+    float4* rng_s = reinterpret_cast<float4*>(xp);  // [NQ - 1][128]
+    const int q4 = tid & 127, hf = tid >> 7;
     const int t = q4 / (RT / 4), j = tile * RT + (q4 % (RT / 4)) * 4;
-    const int nh = (n_seg + 1) >> 1;
-    const int sb = hf ? nh : 0, se = hf ? n_seg : nh;
+    const int nh = (n_seg + NQ - 1) / NQ;
+    const int sb = min(hf * nh, n_seg), se = min(sb + nh, n_seg);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    // the residual quad, loaded with the segments (not after the halves meet: one round trip fewer)
+    // the residual quad, loaded with the segments (not after the ranges meet: one round trip fewer)
     float4* op = reinterpret_cast<float4*>(a.out + (long)min(t, a.T - 1) * a.Hout + j);
     const float4 o_in = hf ? make_float4(0.f, 0.f, 0.f, 0.f) : *op;
-    if (tl && t < a.T) {
-        constexpr int SB = 18;  // segments in flight per batch (n_seg <= 72: at most 2 batches per half)
+    if (t < a.T) {
+        constexpr int SB = NQ == 4 ? 13 : 18;  // segments in flight per batch (n_seg <= 50 at 8 pages: one batch)
         const long sstride = (long)MM_MT * a.Hout * 4;
         const int base = (int)(((long)t * a.Hout + j) * 4);
         for (int s0 = sb; s0 < se; s0 += SB) {
@@ -984,15 +990,20 @@ __global__ __launch_bounds__(64 * NWV * KS, 4) void moe_down_mm_kernel(MoeDec2Ar
             }
         }
     }
-    if (hf == 1) half_s[q4] = v;
+    if (hf > 0) rng_s[(hf - 1) * 128 + q4] = v;
     __syncthreads();
     if (!hf && t < a.T) {
-        const float4 u = half_s[q4];
+        float4 u = rng_s[q4];
+        float4 s = make_float4(v.x + u.x, v.y + u.y, v.z + u.z, v.w + u.w);
+        if (NQ == 4) {
+            const float4 u2 = rng_s[128 + q4], u3 = rng_s[256 + q4];
+            s = make_float4(s.x + (u2.x + u3.x), s.y + (u2.y + u3.y), s.z + (u2.z + u3.z), s.w + (u2.w + u3.w));
+        }
         float4 o = o_in;
-        o.x = o.x + (v.x + u.x);
-        o.y = o.y + (v.y + u.y);
-        o.z = o.z + (v.z + u.z);
-        o.w = o.w + (v.w + u.w);
+        o.x = o.x + s.x;
+        o.y = o.y + s.y;
+        o.z = o.z + s.z;
+        o.w = o.w + s.w;
         *op = o;
     }
     DN_STAMP(4);
