@@ -152,10 +152,12 @@ def test_full_text_batch8_equals_oracle(engine):
     assert len({t for g in got for t in g}) > 64  # distinct streams, not one repeated token
 
 
-def test_full_screened_head_equals_traced_ids(engine):
-    """The bench path (screened lm_head + hipGraph loop) gives the traced (exact head) ids on page 0."""
-    fx = fixture("synthetic0")
-    page = Page(page_image("synthetic0"), VisionSettings(), engine)
+@pytest.mark.parametrize("name", ["synthetic0", "sample_1"])
+def test_full_screened_head_equals_traced_ids(engine, name):
+    """The bench path (screened lm_head + hipGraph loop) gives the oracle's ids over all 512 steps on the bench's
+    synthetic page and on the reference's own assets/sample_1.png."""
+    fx = fixture(name)
+    page = Page(page_image(name), VisionSettings(), engine)
     ids, mask = build_prompt_tokens(SyntheticTokenizer(engine.vocab), PROMPT, [page.n_image_tokens])
     got = engine.generate(ids, mask, page, None, DecodeParameters(max_new_tokens=int(fx["max_new"])), ignore_eos=True)
     s = first_divergence(got, fx["ids"].tolist())
@@ -170,6 +172,26 @@ def test_full_text_batch8_screened_head_equals_oracle(engine):
     fxs = [fixture(n) for n in names]
     n = min(int(f["max_new"]) for f in fxs)
     reqs = [(text_page_prompt(i, vocab=engine.vocab), None, None, None) for i in range(8)]
+    got = engine.generate_batch(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
+    for name, fx, g in zip(names, fxs, got):
+        ref = fx["ids"][:n].tolist()
+        s = first_divergence(g, ref)
+        assert s is None, f"{name}: first divergent step {s}: engine {g[s]} oracle {ref[s]} margin {fx['margin'][s]:.3g}"
+
+
+def test_full_batch8_screened_head_equals_oracle(engine):
+    """The bench path at 8 image pages (no trace: the screened head on the int8 matrix cores + exact rescoring,
+    the replayed step graph) -> every page's oracle ids over all 512 steps (the degenerate image-page streams
+    exercise the head's tie and repeat-penalty paths the text pages rarely reach)."""
+    names = [f"synthetic{i}" for i in range(8)]
+    fxs = [fixture(n) for n in names]
+    n = min(int(f["max_new"]) for f in fxs)
+    tok = SyntheticTokenizer(engine.vocab)
+    reqs = []
+    for name in names:
+        page = Page(page_image(name), VisionSettings(), engine)
+        ids, mask = build_prompt_tokens(tok, PROMPT, [page.n_image_tokens])
+        reqs.append((ids, mask, page, None))
     got = engine.generate_batch(reqs, DecodeParameters(max_new_tokens=n), ignore_eos=True)
     for name, fx, g in zip(names, fxs, got):
         ref = fx["ids"][:n].tolist()
