@@ -2345,12 +2345,23 @@ __global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
     WaveSpan span_(a.span);
     __shared__ float part[NW][RPB];
     constexpr int U = 16 / NW;  // chunks per lane: (topk * I + Is) / 8 / NW waves <= 64 U (= 2)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int j0 = blockIdx.x * RPB;
     const int cpi = a.I >> 3, cps = a.sWd ? (a.Is >> 3) : 0;
     const int nr = a.topk * cpi, nch = nr + cps;
     const int per = (nch + NW - 1) / NW;
     const int c0 = wave * per, c1 = min(nch, c0 + per);
+    // lanes past the wave's range load its last chunk again (dropped below), so a range inside one segment
+    // (the model: 6 x 112 routed + 224 shared chunks over 8 waves of 112) reads one expert id at a uniform
+    // address, issued as the wave's first load: the weight addresses wait for it alone, where the per-lane
+    // id loads sat behind the h loads in the in-order vmcnt.  Same process, one page, 256 tokens: 108.90 vs
+    // 109.08 ms, every one of four alternating rounds (profiles/r06_ab/down_mix_uniform_id_same_process.log)
+    const int glim = c1 > c0 ? c1 - 1 : nch - 1;
+    const int sf = __builtin_amdgcn_readfirstlane(c0 < nr ? c0 / cpi : -1);  // (the division runs on the VALU)
+    const int sl = __builtin_amdgcn_readfirstlane(glim < nr ? glim / cpi : -1);
+    const bool uni = sf == sl;
+    const int e_w = (uni && sf >= 0) ? a.ids[sf] : 0;
     // the residual rows, loaded first (not after the LDS combine: one dependent round trip fewer)
     const float xres = a.out[min(j0 + (int)(threadIdx.x & (RPB - 1)), a.Hout - 1)];
     // 1. h of this wave's chunks (independent of the picks)
@@ -2358,7 +2369,7 @@ __global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
     int seg[U], off[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int g = min(c0 + u * 64 + lane, nch - 1);
+        const int g = min(c0 + u * 64 + lane, glim);
         const bool rt = g < nr;
         seg[u] = rt ? g / cpi : -1;
         off[u] = (rt ? g % cpi : g - nr) << 3;
@@ -2370,7 +2381,7 @@ __global__ __launch_bounds__(512) void moe_down_mix_kernel(MoeDec2Args a) {
     uint4 q[RPB][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int e = seg[u] >= 0 ? a.ids[seg[u]] : 0;  // shared chunks (all of them at topk 0) read no id
+        const int e = uni ? e_w : (seg[u] >= 0 ? a.ids[seg[u]] : 0);  // shared chunks (all at topk 0) read no id
 #pragma unroll
         for (int r = 0; r < RPB; ++r) {
             const int j = min(j0 + r, a.Hout - 1);
